@@ -1,0 +1,159 @@
+"""Benchmark: kube-batch allocate cycles on MI355X (BASELINE.json metric).
+
+metric : pods placed/sec (+ p50 allocate-cycle ms) at 10k nodes x 100k pods (BASELINE.json configs[1], "C2")
+step   : one allocateAction.Execute (actions/allocate/allocate.go:42-193) over the C2 session snapshot:
+         re-open the session from the snapshot already resident in HBM (kb_restore_nodes, device-to-device),
+         then kb_allocate (host ordering plugins + per-job device sweep/argmax/commit). The snapshot is
+         uploaded once before the timed region; value = pods placed / second over the timed steps.
+
+Multi-GPU (torchrun): every rank schedules its own independent C2 cluster partition (weak scaling, no
+data-path collective); torch.distributed is used only for the barrier and the max-over-ranks time.
+
+Extra JSON fields: roofline (dominant kernel, HIP events on the library's stream during the timed region)
+and cpu_baseline (the oracle's C++ restatement of the reference algorithm on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+ROW_BYTES = 76          # algorithmic node-table bytes per (task, node) evaluation at C2
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nodes", type=int, default=10000)
+    ap.add_argument("--jobs", type=int, default=1000)
+    ap.add_argument("--tasks-per-job", type=int, default=100)
+    ap.add_argument("--cpu-sample-tasks", type=int, default=3000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist = dist_mod
+
+    from scheduler_amd import export, runtime, synth
+
+    # each rank: an independent cluster partition of the C2 shape (different seed per rank)
+    cl = synth.c2(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=synth.SEED + rank)
+    snap = export.Snapshot(cl)
+    ctx = runtime.Context(local_rank, timing=True)
+    ctx.upload(snap)
+
+    def step():
+        ctx.restore()
+        return ctx.allocate(snap)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.stats(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    times, placed = [], 0
+    for _ in range(args.steps):
+        s0 = time.perf_counter()
+        out = step()
+        times.append((time.perf_counter() - s0) * 1e3)
+        placed += int(out["n_events"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+
+    total_placed = placed
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        p = torch.tensor([placed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
+        total_placed = int(p.item())
+
+    # roofline: dominant kernel by summed event time
+    k = int(np.argmax(st["kernel_ms"]))
+    launches = max(1, st["launches"][k])
+    avg_ms = st["kernel_ms"][k] / launches
+    bytes_per_launch = st["pairs"][k] * ROW_BYTES / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "kernel": runtime.KERNELS[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_launch_us": round(avg_ms * 1e3, 3), "launches_per_step": round(launches / args.steps, 1),
+                "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
+                "kernel_ms_per_step": {runtime.KERNELS[i]: round(st["kernel_ms"][i] / args.steps, 3)
+                                       for i in range(3)}}
+
+    result = None
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(cl, args.cpu_sample_tasks)
+        result = {
+            "metric": "pods placed/sec + p50 allocate-cycle ms at 10k nodes x 100k pods",
+            "value": round(total_placed / elapsed, 1), "unit": "pods/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "p50_cycle_ms": round(statistics.median(times), 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (seeded C2 generator, SURVEY.md §8 d2)",
+            "config": {"workload": "C2: 10k homogeneous nodes x 100k pods in 1k gang jobs, resource-fit + "
+                                   "LeastRequested/Balanced (default tiers)",
+                       "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
+                       "pods_placed_per_cycle": placed // max(1, args.steps), "parallelism": f"replicas{world}"},
+            "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
+            "job_calls_per_step": st["job_calls"] / args.steps,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cluster, sample_tasks):
+    """The oracle (C++ restatement of the reference, ParallelizeUntil-style pool) on the first
+    `sample_tasks` placements of the same workload."""
+    from oracle import pyoracle
+    cores = min(16, os.cpu_count() or 1)
+    try:
+        aff = len(os.sched_getaffinity(0))
+        cores = min(cores, aff)
+    except AttributeError:
+        pass
+    out = pyoracle.allocate(cluster, workers=cores, max_tasks=sample_tasks)
+    placed = len(out["events"])
+    secs = out["elapsed_ms"] / 1e3
+    return {"value": round(placed / secs, 1) if secs > 0 else None, "unit": "pods/s", "cores": cores,
+            "kind": "port", "sample": f"first {out['attempts']} task placements of the C2 cycle "
+                                      f"({placed} placed in {secs:.2f} s, {cores} worker threads, "
+                                      f"reference-structured full predicate+score sweep per task)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,391 @@
+/*
+ * kbgpu.h — C ABI of the MI355X-native allocate hot path for kube-batch.
+ *
+ * Drop-in boundary. The reference's plugin API stays as it
+ * is: framework.Action / framework.Plugin (pkg/scheduler/framework/interface.go:20-41),
+ * the Session dispatchers (framework/session_plugins.go:25-492) and the helper
+ * trio PredicateNodes / PrioritizeNodes / SelectBestNode
+ * (pkg/scheduler/util/scheduler_helper.go:34,67,147). A kube-batch build binds
+ * this header through cgo and replaces, per pending task, the
+ * three helpers plus Session.Allocate/Pipeline's node-row update with one device
+ * sweep + argmax + in-place commit.
+ *
+ * Two layers:
+ *   1. device layer  — kb_create / kb_upload_* / kb_place_job / kb_eval:
+ *      the snapshot lives on the GPU as a struct-of-arrays node table; the caller
+ *      keeps queue/job/task ordering (allocate.go:95-192) and calls kb_place_job
+ *      once per job pop.
+ *   2. session layer — kb_allocate: the whole allocateAction.Execute
+ *      (actions/allocate/allocate.go:42-193) with the ordering plugins
+ *      (priority, gang, drf, proportion) restated in C++ on the host, driving
+ *      layer 1 per job.
+ *
+ * Conventions: every function returns KB_OK (0) or a negative KB_E_* code and
+ * never throws; kb_last_error() describes the last failure. All pointers passed
+ * in are caller-owned and read only during the call (cgo rule: C keeps no Go
+ * pointers). Device memory is owned by the context. A context is used by one
+ * thread at a time (the action goroutine). Strings never cross the ABI: the
+ * caller interns names into the integer ids below. Node index = canonical node
+ * order (nodes sorted by name), which is also the SelectBestNode tie-break:
+ * among equal best scores the lowest index wins (the reference picks at random,
+ * scheduler_helper.go:157).
+ */
+#ifndef KBGPU_H_
+#define KBGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KBGPU_ABI_VERSION 1
+
+/* ---- return codes ---- */
+#define KB_OK 0
+#define KB_E_INVALID (-1)     /* bad argument / shape mismatch */
+#define KB_E_HIP (-2)         /* HIP runtime failure */
+#define KB_E_UNSUPPORTED (-3) /* input uses a feature the device path does not express */
+#define KB_E_NOMEM (-4)
+#define KB_E_PANIC (-5)       /* the reference would panic: SelectBestNode found no score > -1
+                                 (scheduler_helper.go:147-158) or util/assert fired */
+#define KB_E_STATE (-6)       /* call out of order (e.g. place before upload) */
+
+/* ---- predicate failure reasons: bit i of a reason mask ----
+ * strings: api/unschedule_info.go:11-19, vendor/.../algorithm/predicates/error.go:24-84 */
+#define KB_R_RESOURCE_FIT 0        /* "node(s) resource fit failed" */
+#define KB_R_POD_NUMBER 1          /* "node(s) pod number exceeded" */
+#define KB_R_NOT_READY 2           /* "node(s) were not ready" */
+#define KB_R_OUT_OF_DISK 3         /* "node(s) were out of disk space" */
+#define KB_R_NETWORK_UNAVAILABLE 4 /* "node(s) had unavailable network" */
+#define KB_R_UNSCHEDULABLE 5       /* "node(s) were unschedulable" */
+#define KB_R_NODE_SELECTOR 6       /* "node(s) didn't match node selector" */
+#define KB_R_HOST_PORTS 7          /* "node(s) didn't have free ports for the requested pod ports" */
+#define KB_R_TAINTS 8              /* "node(s) had taints that the pod didn't tolerate" */
+#define KB_R_MEMORY_PRESSURE 9     /* "node(s) had memory pressure" */
+#define KB_R_DISK_PRESSURE 10      /* "node(s) had disk pressure" */
+#define KB_R_PID_PRESSURE 11       /* "node(s) had pid pressure" */
+#define KB_R_POD_AFFINITY 12       /* "node(s) didn't match pod affinity/anti-affinity" */
+#define KB_R_EXISTING_ANTI 13      /* "node(s) didn't satisfy existing pods anti-affinity rules" */
+#define KB_R_AFFINITY_RULES 14     /* "node(s) didn't match pod affinity rules" */
+#define KB_R_ANTI_AFFINITY_RULES 15/* "node(s) didn't match pod anti-affinity rules" */
+#define KB_NUM_REASONS 16
+
+/* ---- node flags (kb_nodes.flags) ---- */
+#define KB_NODE_IDLE_HAS_MAP (1u << 0) /* Idle.ScalarResources != nil (allocatable lists a scalar) */
+#define KB_NODE_REL_HAS_MAP (1u << 1)  /* Releasing.ScalarResources != nil */
+#define KB_NODE_NOT_READY (1u << 2)    /* condition Ready != True            (predicates.go:1582) */
+#define KB_NODE_OUT_OF_DISK (1u << 3)  /* condition OutOfDisk != False       (:1584) */
+#define KB_NODE_NET_UNAVAIL (1u << 4)  /* condition NetworkUnavailable != False (:1586) */
+#define KB_NODE_UNSCHEDULABLE (1u << 5)/* node.Spec.Unschedulable            (:1590) */
+#define KB_NODE_MEM_PRESSURE (1u << 9) /* MemoryPressure == True */
+#define KB_NODE_DISK_PRESSURE (1u << 10)
+#define KB_NODE_PID_PRESSURE (1u << 11)
+
+/*
+ * Node table, struct-of-arrays, n rows in canonical order. Resource quantities
+ * are the reference's integral float64 values as int64: cpu and scalars in
+ * milli-units, memory in bytes (api/resource_info.go:75-93).
+ * Scalar slot s (0 <= s < n_scalar) is a caller-interned scalar resource name;
+ * arrays [n_scalar][n] are slot-major.
+ */
+typedef struct kb_nodes {
+  uint32_t n;
+  uint32_t n_scalar;   /* S */
+  uint32_t n_label;    /* K: label-key slots referenced by any selector / term */
+  uint32_t n_port;     /* P: (protocol, hostPort) slots referenced by any task */
+  const int64_t* idle_cpu;  /* api.NodeInfo.Idle        (node_info.go:35-40) */
+  const int64_t* idle_mem;
+  const int64_t* rel_cpu;   /* api.NodeInfo.Releasing */
+  const int64_t* rel_mem;
+  const int64_t* idle_sc;   /* [S][n] (absent key = 0) */
+  const int64_t* rel_sc;    /* [S][n] */
+  const int64_t* alloc_cpu; /* schedulercache allocatable (cache/node_info.go:611), LR/BRA */
+  const int64_t* alloc_mem;
+  const int64_t* nz_cpu;    /* schedulercache nonzeroRequest (cache/node_info.go:498-520) */
+  const int64_t* nz_mem;
+  const int32_t* pod_count; /* len(nodeInfo.Pods())  (predicates.go:162) */
+  const int32_t* max_pods;  /* Allocatable.MaxTaskNum */
+  const uint32_t* flags;    /* KB_NODE_* */
+  const int32_t* label_val; /* [K][n] interned value id of label key k, -1 when absent */
+  const int64_t* label_int; /* [K][n] strconv.ParseInt of the value (for Gt/Lt) */
+  const uint8_t* label_int_ok; /* [K][n] 1 when the value parsed */
+  const int32_t* taint_set; /* [n] id of the node's NoSchedule/NoExecute taint set (0 = none) */
+  const uint64_t* port_used;/* [P][n] bitmask over the slot's interned host IPs (bit 0 = 0.0.0.0) */
+} kb_nodes;
+
+/* Label requirement program (labels.Requirement, labels/selector.go:185-236). */
+#define KB_OP_IN 0
+#define KB_OP_NOTIN 1
+#define KB_OP_EXISTS 2
+#define KB_OP_DNE 3
+#define KB_OP_GT 4
+#define KB_OP_LT 5
+#define KB_OP_TRUE 6  /* field requirement decided on the host (non-name field key) */
+#define KB_OP_FALSE 7 /* invalid requirement: the term cannot match */
+
+typedef struct kb_req {
+  int32_t key;      /* label-key slot */
+  int32_t op;       /* KB_OP_* */
+  uint32_t val_off; /* into kb_specs.vals */
+  uint32_t val_cnt;
+  int64_t ival;     /* Gt/Lt operand */
+} kb_req;
+
+typedef struct kb_term {
+  uint32_t req_off; /* into kb_specs.reqs; AND of requirements */
+  uint32_t req_cnt; /* 0 => the term matches nothing (helpers.go:308-311, :222-225) */
+  int32_t weight;   /* preferred terms only */
+  int32_t pad;
+} kb_term;
+
+/* spec flags */
+#define KB_SPEC_INIT_HAS_MAP (1u << 0)  /* InitResreq.ScalarResources != nil */
+#define KB_SPEC_REQ_HAS_MAP (1u << 1)
+#define KB_SPEC_BEST_EFFORT (1u << 2)   /* v1qos BestEffort (memory-pressure predicate) */
+#define KB_SPEC_HAS_SELECTOR (1u << 3)  /* len(nodeSelector) > 0 and every pair valid */
+#define KB_SPEC_HAS_REQUIRED (1u << 4)  /* nodeAffinity.RequiredDuringScheduling != nil */
+#define KB_SPEC_NA_ERROR (1u << 5)      /* a preferred term is invalid: map fn errors (node_affinity.go:59-62) */
+#define KB_SPEC_POD_AFFINITY (1u << 6)  /* pod (anti)affinity terms: needs the affinity tables */
+
+/*
+ * Task spec: everything the device needs about a pending pod. Pods of one
+ * job usually share a spec; the caller deduplicates by signature.
+ */
+typedef struct kb_spec {
+  int64_t init_cpu, init_mem; /* InitResreq (pod_info.go:53-63): the predicate request */
+  int64_t req_cpu, req_mem;   /* Resreq (pod_info.go:66-73): what commit subtracts */
+  int64_t nz_cpu, nz_mem;     /* getNonZeroRequests (resource_allocation.go:94-103) */
+  uint64_t init_sc_mask;      /* scalar slots present in InitResreq */
+  uint64_t req_sc_mask;       /* scalar slots present in Resreq */
+  uint32_t flags;             /* KB_SPEC_* */
+  int32_t tol_set;            /* toleration-set id (row of kb_specs.tolerates) */
+  uint32_t sc_off;            /* into kb_specs.sc_init / sc_req: n_scalar values */
+  uint32_t sel_term;          /* nodeSelector as one term (index into terms) */
+  uint32_t req_term_off, req_term_cnt;   /* required node-affinity terms (ORed) */
+  uint32_t pref_term_off, pref_term_cnt; /* preferred node-affinity terms */
+  uint32_t port_off, port_cnt;           /* wanted host ports, into kb_specs.ports */
+  int32_t aff_class;          /* inter-pod affinity class (kb_affinity), -1 none */
+  int32_t pad;
+} kb_spec;
+
+typedef struct kb_port {
+  int32_t slot; /* (protocol, hostPort) slot */
+  int32_t ip;   /* interned host IP within the slot, 0 = 0.0.0.0 */
+} kb_port;
+
+typedef struct kb_specs {
+  uint32_t m;              /* number of specs */
+  const kb_spec* specs;
+  const int64_t* sc_init;  /* [m][n_scalar] */
+  const int64_t* sc_req;   /* [m][n_scalar] */
+  uint32_t n_terms;
+  const kb_term* terms;
+  uint32_t n_reqs;
+  const kb_req* reqs;
+  uint32_t n_vals;
+  const int32_t* vals;     /* interned label-value ids */
+  uint32_t n_ports;
+  const kb_port* ports;
+  uint32_t n_tol_sets, n_taint_sets;
+  const uint8_t* tolerates;/* [n_tol_sets][n_taint_sets]: 1 if the tolerations tolerate every
+                              NoSchedule/NoExecute taint of the set (predicates.go:1489-1518) */
+} kb_specs;
+
+/* Plugin configuration that shapes the predicate chain and the score. */
+typedef struct kb_config {
+  int32_t predicates_enabled; /* "predicates" in tiers with EnabledPredicate (session_plugins.go:372-389) */
+  int32_t nodeorder_enabled;  /* "nodeorder" in tiers with EnabledNodeOrder */
+  int32_t mem_pressure, disk_pressure, pid_pressure; /* predicate.*PressureEnable (predicates.go:72-111) */
+  int32_t w_lr, w_bra, w_na, w_pa;                    /* nodeorder weights (nodeorder.go:96-140) */
+} kb_config;
+
+typedef struct kb_opts {
+  int32_t device; /* HIP device ordinal */
+  uint32_t flags;
+} kb_opts;
+
+typedef struct kb_ctx kb_ctx;
+
+/* ---- layer 1: device ---- */
+kb_ctx* kb_create(const kb_opts* opts);
+void kb_destroy(kb_ctx* ctx);
+const char* kb_last_error(const kb_ctx* ctx);
+int kb_abi_version(void);
+
+int kb_set_config(kb_ctx* ctx, const kb_config* cfg);
+/* Copies the node table to HBM (replaces any previous one). */
+int kb_upload_nodes(kb_ctx* ctx, const kb_nodes* nodes);
+/* Copies the spec tables to HBM. */
+int kb_upload_specs(kb_ctx* ctx, const kb_specs* specs);
+
+/* placement kinds */
+#define KB_PLACE_ALLOCATE 1 /* Session.Allocate (session.go:242) */
+#define KB_PLACE_PIPELINE 2 /* Session.Pipeline (session.go:199) */
+
+/* stop reasons of one job batch (allocate.go:135-188) */
+#define KB_STOP_DONE 0   /* every task placed */
+#define KB_STOP_NO_FIT 1 /* a task fit no node: job leaves the queue (allocate.go:150-153) */
+#define KB_STOP_READY 2  /* ssn.JobReady(job) after a placement: job re-queued (allocate.go:184-187) */
+
+typedef struct kb_job_req {
+  const int32_t* task_specs; /* spec id of each task, in TaskOrderFn order */
+  uint32_t n_tasks;
+  int32_t ready_num;     /* job.ReadyTaskNum() before the batch (job_info.go:367-378) */
+  int32_t min_available; /* job.MinAvailable */
+  int32_t gang_ready;    /* 1: JobReady = ReadyTaskNum >= MinAvailable (gang.go:122-125);
+                            0: no JobReady plugin enabled, JobReady is always true */
+} kb_job_req;
+
+typedef struct kb_job_result {
+  uint32_t n_placed;       /* placements written */
+  int32_t stop;            /* KB_STOP_* */
+  int32_t fail_task;       /* index of the task that fit nowhere (KB_STOP_NO_FIT) */
+  int32_t pad;
+  uint32_t reason_hist[KB_NUM_REASONS]; /* FitErrors histogram over all nodes for fail_task */
+} kb_job_result;
+
+/*
+ * Place one popped job's pending tasks (allocate.go:135-188): for each task in
+ * order, predicate + score every node, pick the best (lowest index on ties),
+ * commit Allocate (InitResreq fits Idle) or Pipeline (fits Releasing) to the
+ * device node table in place, stop on no-fit or when the job becomes ready.
+ * placed_node[i] / placed_kind[i] receive the i-th placement (task i).
+ */
+int kb_place_job(kb_ctx* ctx, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
+                 kb_job_result* result);
+
+/*
+ * Parity / snapshot mode: evaluate t specs against every node at the current
+ * node-table state without committing. reasons[t][n] = reason mask (0 = feasible),
+ * scores[t][n] = total node-order score (PrioritizeNodes' merged score,
+ * scheduler_helper.go:107-127).
+ */
+int kb_eval(kb_ctx* ctx, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores);
+
+/*
+ * Restore the node table to its state at the last kb_upload_nodes (device-to-device copy of the
+ * mutable columns). A fresh allocate cycle over the same cache snapshot re-opens its session this way
+ * without another host upload.
+ */
+int kb_restore_nodes(kb_ctx* ctx);
+
+/* Kernel timing (HIP events on the context's stream), enabled by KB_OPT_TIMING in kb_opts.flags. */
+#define KB_OPT_TIMING (1u << 0)
+#define KB_KERNEL_SWEEP 0
+#define KB_KERNEL_PLACE 1
+#define KB_KERNEL_EVAL 2
+#define KB_NUM_KERNELS 3
+typedef struct kb_stats {
+  uint64_t launches[KB_NUM_KERNELS];
+  double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */
+  uint64_t pairs[KB_NUM_KERNELS];     /* (task, node) evaluations covered by those launches */
+  uint64_t job_calls;
+  double device_ms;                   /* wall time inside kb_place_job */
+} kb_stats;
+int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
+
+/* Read back the mutable node columns (for tests and for the Go side's NodeInfo replay). */
+int kb_read_nodes(kb_ctx* ctx, int64_t* idle_cpu, int64_t* idle_mem, int64_t* rel_cpu, int64_t* rel_mem,
+                  int32_t* pod_count, int64_t* nz_cpu, int64_t* nz_mem);
+
+/* ---- layer 2: session (allocate action + ordering plugins on the host) ---- */
+
+/* plugin bits of a tier entry */
+#define KB_PLUGIN_PRIORITY 0
+#define KB_PLUGIN_GANG 1
+#define KB_PLUGIN_DRF 2
+#define KB_PLUGIN_PROPORTION 3
+#define KB_PLUGIN_PREDICATES 4
+#define KB_PLUGIN_NODEORDER 5
+#define KB_PLUGIN_CONFORMANCE 6
+#define KB_PLUGIN_OTHER 7
+
+/* enable bits (conf.PluginOption, conf/scheduler_conf.go:37-56) */
+#define KB_EN_JOB_ORDER (1u << 0)
+#define KB_EN_JOB_READY (1u << 1)
+#define KB_EN_JOB_PIPELINED (1u << 2)
+#define KB_EN_TASK_ORDER (1u << 3)
+#define KB_EN_PREEMPTABLE (1u << 4)
+#define KB_EN_RECLAIMABLE (1u << 5)
+#define KB_EN_QUEUE_ORDER (1u << 6)
+#define KB_EN_PREDICATE (1u << 7)
+#define KB_EN_NODE_ORDER (1u << 8)
+
+typedef struct kb_tier_plugin {
+  int32_t tier;    /* tier index (order = position in the array) */
+  int32_t plugin;  /* KB_PLUGIN_* */
+  uint32_t enable; /* KB_EN_* */
+  int32_t pad;
+} kb_tier_plugin;
+
+/* task status (api/types.go:23-61) */
+#define KB_ST_PENDING (1 << 0)
+#define KB_ST_ALLOCATED (1 << 1)
+#define KB_ST_PIPELINED (1 << 2)
+#define KB_ST_BINDING (1 << 3)
+#define KB_ST_BOUND (1 << 4)
+#define KB_ST_RUNNING (1 << 5)
+#define KB_ST_RELEASING (1 << 6)
+#define KB_ST_SUCCEEDED (1 << 7)
+#define KB_ST_FAILED (1 << 8)
+#define KB_ST_UNKNOWN (1 << 9)
+
+/*
+ * Resources for drf/proportion accounting use the reference's float64 Resource
+ * with presence semantics: R = 2 + n_rscalar columns (cpu, memory, scalars by
+ * slot) plus a presence mask (bit 63 = map non-nil, bit s = scalar slot s present).
+ */
+typedef struct kb_session {
+  uint32_t n_rscalar;          /* scalar slots used for accounting (<= 62) */
+  /* tasks of session jobs */
+  uint32_t n_tasks;
+  const int32_t* task_job;
+  const int32_t* task_spec;    /* device spec id (pending tasks), -1 otherwise */
+  const int32_t* task_status;  /* KB_ST_* */
+  const int32_t* task_priority;
+  const int64_t* task_ctime;   /* pod creation timestamp */
+  const int32_t* task_uid_rank;/* rank of the task UID in byte order */
+  const double* task_resreq;   /* [n_tasks][2 + n_rscalar] Resreq */
+  const uint64_t* task_resreq_mask;
+  /* jobs */
+  uint32_t n_jobs;
+  const int32_t* job_queue;
+  const int32_t* job_priority;
+  const int32_t* job_min_available;
+  const int64_t* job_ctime;
+  const int32_t* job_uid_rank;
+  const int32_t* job_pg_pending; /* PodGroup phase Pending: skipped (allocate.go:50-52) */
+  /* queues */
+  uint32_t n_queues;
+  const int32_t* queue_weight;
+  const int64_t* queue_ctime;
+  const int32_t* queue_uid_rank;
+  /* sum of session nodes' Allocatable (drf.go:62-64, proportion.go:60-62) */
+  const double* total_alloc;   /* [2 + n_rscalar] */
+  uint64_t total_alloc_mask;
+  /* tiers */
+  uint32_t n_tier_plugins;
+  const kb_tier_plugin* tier_plugins;
+} kb_session;
+
+typedef struct kb_cycle_result {
+  int32_t* task_node;      /* [n_tasks] node index or -1 */
+  int32_t* task_status;    /* [n_tasks] final status */
+  int32_t* job_fail_task;  /* [n_jobs] task index that fit nowhere, -1 */
+  uint32_t* job_reason_hist; /* [n_jobs][KB_NUM_REASONS] */
+  int32_t* event_task;     /* [n_tasks] placement order: task index */
+  uint32_t n_events;       /* out */
+  int32_t pad;
+  double elapsed_ms;       /* out: allocate action wall time */
+  double device_ms;        /* out: time inside kb_place_job calls */
+} kb_cycle_result;
+
+/* allocateAction.Execute (actions/allocate/allocate.go:42-193) over the uploaded node table. */
+int kb_allocate(kb_ctx* ctx, const kb_session* ssn, kb_cycle_result* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KBGPU_H_ */

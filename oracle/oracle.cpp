@@ -1022,11 +1022,12 @@ class Pool {
   int active_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
-  void work() {
+  void work() {  // pieces are handed out in grains of 32 indices
     for (;;) {
-      int i = next_.fetch_add(1);
+      int i = next_.fetch_add(32);
       if (i >= n_) break;
-      (*fn_)(i);
+      int e = std::min(n_, i + 32);
+      for (; i < e; ++i) (*fn_)(i);
     }
   }
   void loop() {
@@ -1697,8 +1698,9 @@ class Session {
     }
     return a;
   }
+  mutable const AffPre* sweep_aff = nullptr;  // set for the duration of one PredicateNodes sweep
   PredResult interpod_affinity_fast(const Task* task, int ni) const {
-    const AffPre& a = aff_pre(task);
+    const AffPre& a = sweep_aff ? *sweep_aff : aff_pre(task);
     if (!a.error.empty()) return interpod_affinity_literal(task, ni);
     const NodeSpec* node = nodes[ni].node;
     for (auto& kv : node->labels)
@@ -1864,7 +1866,9 @@ class Session {
   };
   void predicate_nodes(const Task* task, Sweep* s) const {
     s->pred.assign(nodes.size(), PredResult());
+    sweep_aff = &aff_pre(task);  // the per-task lister scan, hoisted out of the node loop
     pool->run((int)nodes.size(), [&](int i) { s->pred[i] = alloc_predicate(task, i); });
+    sweep_aff = nullptr;
     s->feasible.clear();
     for (size_t i = 0; i < nodes.size(); ++i)
       if (s->pred[i].ok) s->feasible.push_back((int)i);

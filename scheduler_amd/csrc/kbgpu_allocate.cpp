@@ -1,0 +1,480 @@
+// Session layer: allocateAction.Execute (pkg/scheduler/actions/allocate/allocate.go:42-193)
+// with the ordering plugins restated on the host in C++ -- priority (plugins/priority/priority.go),
+// gang (plugins/gang/gang.go), drf (plugins/drf/drf.go), proportion (plugins/proportion/proportion.go)
+// -- dispatched through the tiers exactly as framework/session_plugins.go does. Every job pop hands
+// the job's ordered pending tasks to kb_place_job (device), then replays the placements into the
+// host-side job / share state the ordering reads.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "kbgpu_ctx.h"
+
+namespace {
+
+constexpr double kMinMilliCPU = 10, kMinMemory = 10 * 1024 * 1024, kMinMilliScalar = 10;  // resource_info.go:70-72
+constexpr uint64_t kHasMap = 1ull << 63;
+
+// api.Resource with fixed slots: v[0] cpu, v[1] memory, v[2 + s] scalar slot s; presence mask bit s
+// (+ bit 63 = ScalarResources map non-nil). Restates api/resource_info.go.
+struct Res {
+  int S = 0;
+  double v[64] = {0};
+  uint64_t mask = 0;
+
+  bool has(int s) const { return (mask >> s) & 1; }
+  double sc(int s) const { return has(s) ? v[2 + s] : 0.0; }
+  void add(const Res& r) {  // Add (:131-143)
+    v[0] += r.v[0];
+    v[1] += r.v[1];
+    for (int s = 0; s < S; ++s)
+      if (r.has(s)) {
+        mask |= kHasMap | (1ull << s);
+        v[2 + s] += r.v[2 + s];
+      }
+  }
+  bool less_equal(const Res& rr) const {  // LessEqual (:253-276)
+    bool ok = (v[0] < rr.v[0] || std::fabs(rr.v[0] - v[0]) < kMinMilliCPU) &&
+              (v[1] < rr.v[1] || std::fabs(rr.v[1] - v[1]) < kMinMemory);
+    if (!ok) return false;
+    if (!(mask & kHasMap)) return true;
+    for (int s = 0; s < S; ++s) {
+      if (!has(s)) continue;
+      if (!(rr.mask & kHasMap)) return false;
+      double q = rr.sc(s);
+      if (!(v[2 + s] < q || std::fabs(q - v[2 + s]) < kMinMilliScalar)) return false;
+    }
+    return true;
+  }
+  bool sub(const Res& r) {  // Sub (:145-159); false = util/assert panic
+    if (!r.less_equal(*this)) return false;
+    v[0] -= r.v[0];
+    v[1] -= r.v[1];
+    if (!(mask & kHasMap)) return true;
+    for (int s = 0; s < S; ++s)
+      if (r.has(s)) {
+        mask |= 1ull << s;
+        v[2 + s] -= r.v[2 + s];
+      }
+    return true;
+  }
+  bool less(const Res& rr) const {  // Less (:228-251)
+    if (!(v[0] < rr.v[0] && v[1] < rr.v[1])) return false;
+    if (!(mask & kHasMap)) return (rr.mask & kHasMap) != 0;
+    for (int s = 0; s < S; ++s) {
+      if (!has(s)) continue;
+      if (!(rr.mask & kHasMap)) return false;
+      if (v[2 + s] >= rr.sc(s)) return false;
+    }
+    return true;
+  }
+  bool is_empty() const {  // IsEmpty (:96-108)
+    if (!(v[0] < kMinMilliCPU && v[1] < kMinMemory)) return false;
+    for (int s = 0; s < S; ++s)
+      if (has(s) && v[2 + s] >= kMinMilliScalar) return false;
+    return true;
+  }
+  Res& multi(double ratio) {  // Multi (:218-225)
+    v[0] = v[0] * ratio;
+    v[1] = v[1] * ratio;
+    for (int s = 0; s < S; ++s)
+      if (has(s)) v[2 + s] = v[2 + s] * ratio;
+    return *this;
+  }
+  double get(int col) const { return col < 2 ? v[col] : ((mask & kHasMap) ? sc(col - 2) : 0.0); }
+};
+
+Res res_min(const Res& l, const Res& r) {  // helpers.Min (api/helpers/helpers.go:27-45)
+  Res o;
+  o.S = l.S;
+  o.v[0] = std::min(l.v[0], r.v[0]);
+  o.v[1] = std::min(l.v[1], r.v[1]);
+  if (!(l.mask & kHasMap) || !(r.mask & kHasMap)) return o;
+  o.mask = kHasMap;
+  for (int s = 0; s < l.S; ++s)
+    if (l.has(s)) {
+      o.mask |= 1ull << s;
+      o.v[2 + s] = std::min(l.v[2 + s], r.sc(s));
+    }
+  return o;
+}
+
+double share(double l, double r) {  // helpers.Share (helpers.go:48-63)
+  if (r == 0) return l == 0 ? 0 : 1;
+  return l / r;
+}
+
+// max over ResourceNames() of share(allocated.Get(rn), total.Get(rn)) (drf.go:161-171, proportion.go:265-277)
+double dominant_share(const Res& alloc, const Res& total) {
+  double res = 0;
+  int cols[66];
+  int nc = 0;
+  cols[nc++] = 0;
+  cols[nc++] = 1;
+  if (total.mask & kHasMap)
+    for (int s = 0; s < total.S; ++s)
+      if (total.has(s)) cols[nc++] = 2 + s;
+  for (int i = 0; i < nc; ++i) {
+    double x = share(alloc.get(cols[i]), total.get(cols[i]));
+    if (x > res) res = x;
+  }
+  return res;
+}
+
+bool allocated_status(int s) {  // api/helpers.go:72-79
+  return s == KB_ST_BOUND || s == KB_ST_BINDING || s == KB_ST_RUNNING || s == KB_ST_ALLOCATED;
+}
+
+// Go container/heap (src/container/heap/heap.go) -- Push = append + up, Pop = swap + down.
+template <class T>
+struct GoHeap {
+  std::vector<T> items;
+  std::function<bool(const T&, const T&)> less;
+  void up(int j) {
+    for (;;) {
+      int i = (j - 1) / 2;
+      if (i == j || !less(items[j], items[i])) break;
+      std::swap(items[i], items[j]);
+      j = i;
+    }
+  }
+  void down(int i, int n) {
+    for (;;) {
+      int j1 = 2 * i + 1;
+      if (j1 >= n || j1 < 0) break;
+      int j = j1;
+      if (j1 + 1 < n && less(items[j1 + 1], items[j1])) j = j1 + 1;
+      if (!less(items[j], items[i])) break;
+      std::swap(items[i], items[j]);
+      i = j;
+    }
+  }
+  void push(T x) {
+    items.push_back(x);
+    up((int)items.size() - 1);
+  }
+  T pop() {
+    int n = (int)items.size() - 1;
+    std::swap(items[0], items[n]);
+    down(0, n);
+    T x = items.back();
+    items.pop_back();
+    return x;
+  }
+  bool empty() const { return items.empty(); }
+};
+
+struct JobS {
+  std::vector<int> pending;  // pending tasks in TaskOrderFn order (static during the cycle)
+  size_t cursor = 0;
+  bool pending_built = false;
+  int ready = 0, waiting = 0, valid = 0;
+  Res drf_alloc;
+  double drf_share = 0;
+};
+
+struct QueueS {
+  double share = 0;
+  Res deserved, allocated, request;
+};
+
+struct Driver {
+  kb_ctx* ctx;
+  const kb_session& s;
+  kb_cycle_result* out;
+  int S;
+  std::vector<JobS> jobs;
+  std::vector<QueueS> queues;
+  std::vector<int> task_status;
+  std::vector<std::vector<int>> job_allocated;  // tasks with status Allocated per job (dispatch set)
+  bool has[8] = {false};
+  Res total;
+
+  Driver(kb_ctx* c, const kb_session& ss, kb_cycle_result* o) : ctx(c), s(ss), out(o), S((int)ss.n_rscalar) {}
+
+  Res task_res(int t) const {
+    Res r;
+    r.S = S;
+    const double* p = s.task_resreq + (size_t)t * (2 + S);
+    for (int i = 0; i < 2 + S; ++i) r.v[i] = p[i];
+    r.mask = s.task_resreq_mask[t];
+    return r;
+  }
+  bool enabled(int plugin, uint32_t bit) const {
+    for (uint32_t i = 0; i < s.n_tier_plugins; ++i)
+      if (s.tier_plugins[i].plugin == plugin && (s.tier_plugins[i].enable & bit)) return true;
+    return false;
+  }
+
+  // JobOrderFn (session_plugins.go:281-305)
+  bool job_less(int l, int r) const {
+    for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
+      const kb_tier_plugin& p = s.tier_plugins[i];
+      if (!(p.enable & KB_EN_JOB_ORDER)) continue;
+      int j = 0;
+      if (p.plugin == KB_PLUGIN_PRIORITY) {  // priority.go:60-78
+        int a = s.job_priority[l], b = s.job_priority[r];
+        j = a > b ? -1 : (a < b ? 1 : 0);
+      } else if (p.plugin == KB_PLUGIN_GANG) {  // gang.go:96-119
+        bool lr = jobs[l].ready >= s.job_min_available[l], rr = jobs[r].ready >= s.job_min_available[r];
+        j = (lr && rr) ? 0 : lr ? 1 : rr ? -1 : 0;
+      } else if (p.plugin == KB_PLUGIN_DRF) {  // drf.go:114-130
+        double a = jobs[l].drf_share, b = jobs[r].drf_share;
+        j = a == b ? 0 : (a < b ? -1 : 1);
+      } else {
+        continue;
+      }
+      if (j != 0) return j < 0;
+    }
+    if (s.job_ctime[l] == s.job_ctime[r]) return s.job_uid_rank[l] < s.job_uid_rank[r];
+    return s.job_ctime[l] < s.job_ctime[r];
+  }
+  // QueueOrderFn (session_plugins.go:308-333)
+  bool queue_less(int l, int r) const {
+    for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
+      const kb_tier_plugin& p = s.tier_plugins[i];
+      if (!(p.enable & KB_EN_QUEUE_ORDER) || p.plugin != KB_PLUGIN_PROPORTION) continue;
+      double a = queues[l].share, b = queues[r].share;  // proportion.go:171-184
+      int j = a == b ? 0 : (a < b ? -1 : 1);
+      if (j != 0) return j < 0;
+    }
+    if (s.queue_ctime[l] == s.queue_ctime[r]) return s.queue_uid_rank[l] < s.queue_uid_rank[r];
+    return s.queue_ctime[l] < s.queue_ctime[r];
+  }
+  // TaskOrderFn (session_plugins.go:336-369)
+  bool task_less(int l, int r) const {
+    for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
+      const kb_tier_plugin& p = s.tier_plugins[i];
+      if (!(p.enable & KB_EN_TASK_ORDER) || p.plugin != KB_PLUGIN_PRIORITY) continue;
+      int a = s.task_priority[l], b = s.task_priority[r];  // priority.go:40-56
+      int j = a == b ? 0 : (a > b ? -1 : 1);
+      if (j != 0) return j < 0;
+    }
+    if (s.task_ctime[l] == s.task_ctime[r]) return s.task_uid_rank[l] < s.task_uid_rank[r];
+    return s.task_ctime[l] < s.task_ctime[r];
+  }
+  bool job_ready(int j) const {  // JobReady (session_plugins.go:202-220) -> gang Ready()
+    if (has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY)) return jobs[j].ready >= s.job_min_available[j];
+    return true;
+  }
+  bool overused(int q) const {  // Overused (session_plugins.go:185-199) -> proportion.go:221-233
+    if (!has[KB_PLUGIN_PROPORTION]) return false;
+    return queues[q].deserved.less_equal(queues[q].allocated);
+  }
+
+  int init() {
+    for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
+      int p = s.tier_plugins[i].plugin;
+      if (p >= 0 && p < 8) has[p] = true;
+    }
+    total.S = S;
+    for (int i = 0; i < 2 + S; ++i) total.v[i] = s.total_alloc[i];
+    total.mask = s.total_alloc_mask;
+    jobs.assign(s.n_jobs, JobS());
+    queues.assign(s.n_queues, QueueS());
+    job_allocated.assign(s.n_jobs, {});
+    task_status.assign(s.task_status, s.task_status + s.n_tasks);
+    for (auto& j : jobs) j.drf_alloc.S = S;
+    for (auto& q : queues) {
+      q.deserved.S = q.allocated.S = q.request.S = S;
+    }
+    for (uint32_t t = 0; t < s.n_tasks; ++t) {
+      int j = s.task_job[t], st = task_status[t];
+      if (allocated_status(st) || st == KB_ST_SUCCEEDED) jobs[j].ready++;
+      if (st == KB_ST_PIPELINED) jobs[j].waiting++;
+      if (allocated_status(st) || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
+      if (st == KB_ST_ALLOCATED) job_allocated[j].push_back((int)t);
+      if (allocated_status(st)) jobs[j].drf_alloc.add(task_res(t));
+    }
+    for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
+    if (has[KB_PLUGIN_PROPORTION]) open_proportion();
+    return KB_OK;
+  }
+
+  // proportion.OnSessionOpen (proportion.go:58-169); queues visited in UID order.
+  void open_proportion() {
+    std::vector<char> in_use(s.n_queues, 0);
+    for (uint32_t j = 0; j < s.n_jobs; ++j) in_use[s.job_queue[j]] = 1;
+    for (uint32_t t = 0; t < s.n_tasks; ++t) {
+      QueueS& q = queues[s.job_queue[s.task_job[t]]];
+      int st = task_status[t];
+      if (allocated_status(st)) {
+        q.allocated.add(task_res(t));
+        q.request.add(task_res(t));
+      } else if (st == KB_ST_PENDING) {
+        q.request.add(task_res(t));
+      }
+    }
+    std::vector<int> order;
+    for (uint32_t q = 0; q < s.n_queues; ++q)
+      if (in_use[q]) order.push_back((int)q);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return s.queue_uid_rank[a] < s.queue_uid_rank[b]; });
+    Res remaining = total;
+    std::vector<char> meet(s.n_queues, 0);
+    for (;;) {
+      int32_t tw = 0;
+      for (int q : order)
+        if (!meet[q]) tw += s.queue_weight[q];
+      if (tw == 0) break;
+      Res inc, dec;
+      inc.S = dec.S = S;
+      for (int q : order) {
+        if (meet[q]) continue;
+        QueueS& a = queues[q];
+        Res old = a.deserved;
+        Res part = remaining;
+        a.deserved.add(part.multi((double)s.queue_weight[q] / (double)tw));
+        if (a.request.less(a.deserved)) {
+          a.deserved = res_min(a.deserved, a.request);
+          meet[q] = 1;
+        }
+        a.share = dominant_share(a.allocated, a.deserved);
+        // Resource.Diff (resource_info.go:278-309)
+        Res i2, d2;
+        i2.S = d2.S = S;
+        if (a.deserved.v[0] > old.v[0]) i2.v[0] += a.deserved.v[0] - old.v[0]; else d2.v[0] += old.v[0] - a.deserved.v[0];
+        if (a.deserved.v[1] > old.v[1]) i2.v[1] += a.deserved.v[1] - old.v[1]; else d2.v[1] += old.v[1] - a.deserved.v[1];
+        if (a.deserved.mask & kHasMap)
+          for (int sl = 0; sl < S; ++sl) {
+            if (!a.deserved.has(sl)) continue;
+            double rq = old.sc(sl);
+            if (a.deserved.v[2 + sl] > rq) {
+              i2.mask |= kHasMap | (1ull << sl);
+              i2.v[2 + sl] += a.deserved.v[2 + sl] - rq;
+            } else {
+              d2.mask |= kHasMap | (1ull << sl);
+              d2.v[2 + sl] += rq - a.deserved.v[2 + sl];
+            }
+          }
+        inc.add(i2);
+        dec.add(d2);
+      }
+      remaining.sub(inc);
+      remaining.add(dec);
+      if (remaining.is_empty()) break;
+    }
+  }
+
+  void on_allocate_event(int t) {  // drf.go:135-144, proportion.go:236-246
+    int j = s.task_job[t];
+    Res r = task_res(t);
+    if (has[KB_PLUGIN_DRF]) {
+      jobs[j].drf_alloc.add(r);
+      jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
+    }
+    if (has[KB_PLUGIN_PROPORTION]) {
+      QueueS& q = queues[s.job_queue[j]];
+      q.allocated.add(r);
+      q.share = dominant_share(q.allocated, q.deserved);
+    }
+  }
+
+  int run() {
+    GoHeap<int> qheap;
+    qheap.less = [this](const int& a, const int& b) { return queue_less(a, b); };
+    std::vector<GoHeap<int>> jheaps(s.n_queues);
+    for (auto& h : jheaps) h.less = [this](const int& a, const int& b) { return job_less(a, b); };
+    std::vector<int> jorder(s.n_jobs);
+    for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
+    std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
+    // pending tasks per job
+    std::vector<std::vector<int>> job_pending(s.n_jobs);
+    for (uint32_t t = 0; t < s.n_tasks; ++t)
+      if (task_status[t] == KB_ST_PENDING) job_pending[s.task_job[t]].push_back((int)t);
+    for (int j : jorder) {
+      if (s.job_pg_pending[j]) continue;                                              // allocate.go:50-52
+      if (has[KB_PLUGIN_GANG] && jobs[j].valid < s.job_min_available[j]) continue;  // JobValid, gang.go:48-69
+      int q = s.job_queue[j];
+      if (q < 0 || (uint32_t)q >= s.n_queues) continue;
+      qheap.push(q);
+      jheaps[q].push(j);
+    }
+    std::vector<int32_t> specs, pn, pk;
+    uint32_t n_events = 0;
+    while (!qheap.empty()) {
+      int q = qheap.pop();
+      if (overused(q)) continue;
+      if (jheaps[q].empty()) continue;
+      int j = jheaps[q].pop();
+      JobS& js = jobs[j];
+      if (!js.pending_built) {  // allocate.go:114-129 (BestEffort tasks skipped)
+        for (int t : job_pending[j]) {
+          Res r = task_res(t);
+          if (!r.is_empty()) js.pending.push_back(t);
+        }
+        std::sort(js.pending.begin(), js.pending.end(), [this](int a, int b) { return task_less(a, b); });
+        js.pending_built = true;
+      }
+      if (js.cursor < js.pending.size()) {
+        const size_t nt = js.pending.size() - js.cursor;
+        specs.resize(nt);
+        pn.resize(nt);
+        pk.resize(nt);
+        for (size_t i = 0; i < nt; ++i) {
+          specs[i] = s.task_spec[js.pending[js.cursor + i]];
+          if (specs[i] < 0) return KB_E_INVALID;
+        }
+        kb_job_req req{specs.data(), (uint32_t)nt, js.ready, s.job_min_available[j],
+                       (has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY)) ? 1 : 0};
+        kb_job_result res;
+        int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res);
+        if (rc) return rc;
+        for (uint32_t i = 0; i < res.n_placed; ++i) {
+          int t = js.pending[js.cursor + i];
+          out->task_node[t] = pn[i];
+          out->event_task[n_events++] = t;
+          if (pk[i] == KB_PLACE_ALLOCATE) {  // Session.Allocate (session.go:242-297)
+            task_status[t] = KB_ST_ALLOCATED;
+            js.ready++;
+            job_allocated[j].push_back(t);
+            on_allocate_event(t);
+            if (job_ready(j)) {  // dispatch every Allocated task (session.go:286-294)
+              for (int a : job_allocated[j]) task_status[a] = KB_ST_BINDING;
+              job_allocated[j].clear();
+            }
+          } else {  // Session.Pipeline (session.go:199-239)
+            task_status[t] = KB_ST_PIPELINED;
+            js.waiting++;
+            on_allocate_event(t);
+          }
+        }
+        js.cursor += res.n_placed;
+        if (res.stop == KB_STOP_NO_FIT) {
+          out->job_fail_task[j] = js.pending[js.cursor];
+          memcpy(out->job_reason_hist + (size_t)j * KB_NUM_REASONS, res.reason_hist, sizeof(res.reason_hist));
+        } else if (res.stop == KB_STOP_READY) {
+          jheaps[q].push(j);
+        }
+      }
+      qheap.push(q);
+    }
+    out->n_events = n_events;
+    for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
+    return KB_OK;
+  }
+};
+
+}  // namespace
+
+extern "C" int kb_allocate(kb_ctx* ctx, const kb_session* ssn, kb_cycle_result* out) {
+  if (!ctx || !ssn || !out) return KB_E_INVALID;
+  if (ssn->n_rscalar > 62) {
+    ctx->err = "more than 62 accounting scalar slots";
+    return KB_E_UNSUPPORTED;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  double dev0 = ctx->device_ms;
+  for (uint32_t t = 0; t < ssn->n_tasks; ++t) out->task_node[t] = -1;
+  for (uint32_t j = 0; j < ssn->n_jobs; ++j) out->job_fail_task[j] = -1;
+  memset(out->job_reason_hist, 0, sizeof(uint32_t) * KB_NUM_REASONS * ssn->n_jobs);
+  Driver d(ctx, *ssn, out);
+  int rc = d.init();
+  if (rc == KB_OK) rc = d.run();
+  out->elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  out->device_ms = ctx->device_ms - dev0;
+  return rc;
+}

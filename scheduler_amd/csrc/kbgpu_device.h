@@ -1,0 +1,73 @@
+// Device-side data layout shared by the HIP kernels and the host library.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/kbgpu.h"
+
+namespace kbgpu {
+
+// Packed argmax key:
+//   feasible:   bit 63 = 1 | (score + kScoreBias) << 24 | (2^24 - 1 - node)
+//   infeasible: bit 63 = 0 | reason mask (bits 0..15)
+// max(key) = highest score, then lowest node index (the canonical tie-break).
+constexpr uint64_t kFeasible = 1ull << 63;
+constexpr int64_t kScoreBias = 1ll << 38;
+constexpr uint32_t kIdxMask = (1u << 24) - 1;
+constexpr uint32_t kMaxNodes = 1u << 24;
+
+struct DevNodes {
+  int32_t n, S, K, P;
+  int64_t *idle_cpu, *idle_mem, *rel_cpu, *rel_mem;
+  int64_t *idle_sc, *rel_sc;
+  int64_t *alloc_cpu, *alloc_mem;
+  int64_t *nz_cpu, *nz_mem;
+  int32_t *pod_count, *max_pods;
+  uint32_t* flags;
+  int32_t* label_val;
+  int64_t* label_int;
+  uint8_t* label_int_ok;
+  int32_t* taint_set;
+  uint64_t* port_used;
+};
+
+struct DevSpecs {
+  kb_spec* specs;
+  int64_t *sc_init, *sc_req;
+  kb_term* terms;
+  kb_req* reqs;
+  int32_t* vals;
+  kb_port* ports;
+  uint8_t* tolerates;
+  int32_t n_taint_sets;
+  int32_t m;
+};
+
+struct DevCfg {
+  int32_t predicates, nodeorder, mem_pressure, disk_pressure, pid_pressure;
+  int32_t w_lr, w_bra, w_na, w_pa;
+};
+
+// Per-job device state (one per context), read back after every kb_place_job.
+struct JobState {
+  int32_t stopped;    // 1 once the batch stopped; later kernels of the batch exit at entry
+  int32_t stop;       // KB_STOP_*
+  int32_t fail_task;
+  int32_t n_placed;
+  int32_t ready_num;
+  int32_t min_available;
+  int32_t gang_ready;
+  int32_t panic;      // 1: SelectBestNode would panic (best score <= -1)
+  uint32_t hist[KB_NUM_REASONS];
+};
+
+// Launch wrappers (kbgpu_device.hip).
+void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, uint64_t* keys,
+                       uint64_t* cmax, const JobState* js, void* stream);
+void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                       uint64_t* keys, const uint64_t* cmax, JobState* js, int32_t* out, void* stream);
+void launch_job_init(JobState* js, int ready_num, int min_available, int gang_ready, void* stream);
+void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
+                 uint32_t* reasons, int64_t* scores, void* stream);
+int place_loop_lds_bytes(int n);
+
+}  // namespace kbgpu

@@ -1,0 +1,410 @@
+// Host side of the device layer: context, HBM residency of the node table and
+// spec tables, per-job placement batches, parity evaluation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kbgpu_ctx.h"
+
+using namespace kbgpu;
+
+namespace {
+
+int fail(kb_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIP_OK(ctx, expr)                                                                      \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail(ctx, KB_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int upload(kb_ctx* c, std::vector<void*>& owned, T** dst, const T* src, size_t count, bool required = true) {
+  *dst = nullptr;
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  void* p = nullptr;
+  HIP_OK(c, hipMalloc(&p, bytes));
+  owned.push_back(p);
+  if (count && src) {
+    HIP_OK(c, hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+  } else {
+    if (count && required) return fail(c, KB_E_INVALID, "missing array of %zu elements", count);
+    HIP_OK(c, hipMemset(p, 0, bytes));
+  }
+  *dst = (T*)p;
+  return KB_OK;
+}
+
+void free_all(std::vector<void*>& v) {
+  for (void* p : v) (void)hipFree(p);
+  v.clear();
+}
+
+}  // namespace
+
+hipEvent_t kb_ctx::ev_get() {
+  if (!ev_pool.empty()) {
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+void kb_ctx::ev_begin(hipEvent_t* a) {
+  *a = nullptr;
+  if (!timing) return;
+  *a = ev_get();
+  (void)hipEventRecord(*a, stream);
+}
+void kb_ctx::ev_end(hipEvent_t a, int kind, uint64_t pairs) {
+  if (!timing || !a) return;
+  hipEvent_t b = ev_get();
+  (void)hipEventRecord(b, stream);
+  pending.push_back({a, b, kind, pairs});
+}
+// Called after the stream is synchronised: fold finished event pairs into the stats.
+void kb_ctx::ev_collect() {
+  for (auto& p : pending) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      stats.kernel_ms[p.kind] += ms;
+      stats.launches[p.kind] += 1;
+      stats.pairs[p.kind] += p.pairs;
+    }
+    ev_pool.push_back(p.a);
+    ev_pool.push_back(p.b);
+  }
+  pending.clear();
+}
+
+extern "C" {
+
+int kb_abi_version(void) { return KBGPU_ABI_VERSION; }
+
+kb_ctx* kb_create(const kb_opts* opts) {
+  kb_ctx* c = new kb_ctx();
+  c->device = opts ? opts->device : 0;
+  c->timing = opts && (opts->flags & KB_OPT_TIMING);
+  if (hipSetDevice(c->device) != hipSuccess) {
+    c->err = "hipSetDevice failed";
+    c->broken = true;
+    return c;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    c->err = "hipStreamCreate failed";
+    c->broken = true;
+    return c;
+  }
+  c->cfg = DevCfg{1, 1, 0, 0, 0, 1, 1, 1, 1};
+  return c;
+}
+
+void kb_destroy(kb_ctx* c) {
+  if (!c) return;
+  if (!c->broken) (void)hipSetDevice(c->device);
+  free_all(c->node_mem);
+  free_all(c->spec_mem);
+  free_all(c->work_mem);
+  if (c->h_job) (void)hipHostFree(c->h_job);
+  if (c->h_eval) (void)hipHostFree(c->h_eval);
+  for (auto& p : c->pending) {
+    c->ev_pool.push_back(p.a);
+    c->ev_pool.push_back(p.b);
+  }
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* kb_last_error(const kb_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int kb_set_config(kb_ctx* c, const kb_config* cfg) {
+  if (!c || !cfg) return KB_E_INVALID;
+  c->cfg = DevCfg{cfg->predicates_enabled, cfg->nodeorder_enabled, cfg->mem_pressure, cfg->disk_pressure,
+                  cfg->pid_pressure, cfg->w_lr, cfg->w_bra, cfg->w_na, cfg->w_pa};
+  return kb_check_score_range(c);
+}
+
+int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
+  if (!c || !in) return KB_E_INVALID;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (in->n == 0 || in->n >= kMaxNodes) return fail(c, KB_E_INVALID, "node count %u out of range", in->n);
+  if (in->n_scalar > 64) return fail(c, KB_E_UNSUPPORTED, "more than 64 scalar resource slots");
+  HIP_OK(c, hipSetDevice(c->device));
+  free_all(c->node_mem);
+  free_all(c->work_mem);
+  c->nodes_ok = false;
+  DevNodes& N = c->N;
+  const size_t n = in->n;
+  N.n = (int32_t)in->n;
+  N.S = (int32_t)in->n_scalar;
+  N.K = (int32_t)in->n_label;
+  N.P = (int32_t)in->n_port;
+  int rc;
+#define UP(field, cnt)                                                                   \
+  if ((rc = upload(c, c->node_mem, &N.field, in->field, (cnt))) != KB_OK) return rc;
+  UP(idle_cpu, n) UP(idle_mem, n) UP(rel_cpu, n) UP(rel_mem, n);
+  UP(idle_sc, n * N.S) UP(rel_sc, n * N.S);
+  UP(alloc_cpu, n) UP(alloc_mem, n) UP(nz_cpu, n) UP(nz_mem, n);
+  UP(pod_count, n) UP(max_pods, n) UP(flags, n);
+  UP(label_val, n * N.K) UP(label_int, n * N.K) UP(label_int_ok, n * N.K);
+  UP(taint_set, n) UP(port_used, n * N.P);
+#undef UP
+  // pristine copies of the columns commits mutate
+  c->pristine.clear();
+  auto keep = [&](void* col, size_t bytes) -> int {
+    void* q;
+    HIP_OK(c, hipMalloc(&q, std::max<size_t>(bytes, 1)));
+    c->node_mem.push_back(q);
+    HIP_OK(c, hipMemcpy(q, col, bytes, hipMemcpyDeviceToDevice));
+    c->pristine.push_back({col, q, bytes});
+    return KB_OK;
+  };
+  if ((rc = keep(N.idle_cpu, n * 8)) || (rc = keep(N.idle_mem, n * 8)) || (rc = keep(N.rel_cpu, n * 8)) ||
+      (rc = keep(N.rel_mem, n * 8)) || (rc = keep(N.idle_sc, n * N.S * 8)) || (rc = keep(N.rel_sc, n * N.S * 8)) ||
+      (rc = keep(N.nz_cpu, n * 8)) || (rc = keep(N.nz_mem, n * 8)) || (rc = keep(N.pod_count, n * 4)) ||
+      (rc = keep(N.port_used, n * N.P * 8)))
+    return rc;
+  // work buffers: keys, chunk maxima, job state + placement pairs
+  void* p;
+  HIP_OK(c, hipMalloc(&p, n * sizeof(uint64_t)));
+  c->work_mem.push_back(p);
+  c->keys = (uint64_t*)p;
+  HIP_OK(c, hipMalloc(&p, ((n + 63) / 64 + 2) * sizeof(uint64_t)));
+  c->work_mem.push_back(p);
+  c->cmax = (uint64_t*)p;
+  c->nodes_ok = true;
+  return KB_OK;
+}
+
+int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
+  if (!c || !in) return KB_E_INVALID;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (!c->nodes_ok) return fail(c, KB_E_STATE, "upload nodes before specs");
+  HIP_OK(c, hipSetDevice(c->device));
+  free_all(c->spec_mem);
+  c->specs_ok = false;
+  if (in->n_tol_sets == 0 || in->n_taint_sets == 0) return fail(c, KB_E_INVALID, "empty toleration/taint tables");
+  // host-side validation of every index the kernels will follow (no out-of-bounds device access)
+  const uint32_t S = (uint32_t)c->N.S;
+  for (uint32_t i = 0; i < in->m; ++i) {
+    const kb_spec& s = in->specs[i];
+    if (s.tol_set < 0 || (uint32_t)s.tol_set >= in->n_tol_sets) return fail(c, KB_E_INVALID, "spec %u tol_set", i);
+    if ((s.flags & KB_SPEC_HAS_SELECTOR) && s.sel_term >= in->n_terms) return fail(c, KB_E_INVALID, "spec %u sel", i);
+    if ((uint64_t)s.req_term_off + s.req_term_cnt > in->n_terms) return fail(c, KB_E_INVALID, "spec %u req", i);
+    if ((uint64_t)s.pref_term_off + s.pref_term_cnt > in->n_terms) return fail(c, KB_E_INVALID, "spec %u pref", i);
+    if ((uint64_t)s.port_off + s.port_cnt > in->n_ports) return fail(c, KB_E_INVALID, "spec %u ports", i);
+    if (S < 64 && ((s.init_sc_mask | s.req_sc_mask) >> S)) return fail(c, KB_E_INVALID, "spec %u scalar mask", i);
+    if (s.flags & KB_SPEC_POD_AFFINITY)
+      return fail(c, KB_E_UNSUPPORTED, "spec %u: inter-pod affinity tables not uploaded", i);
+  }
+  for (uint32_t i = 0; i < in->n_terms; ++i)
+    if ((uint64_t)in->terms[i].req_off + in->terms[i].req_cnt > in->n_reqs)
+      return fail(c, KB_E_INVALID, "term %u", i);
+  for (uint32_t i = 0; i < in->n_reqs; ++i) {
+    const kb_req& r = in->reqs[i];
+    if (r.op < KB_OP_IN || r.op > KB_OP_FALSE) return fail(c, KB_E_INVALID, "req %u op", i);
+    if (r.op < KB_OP_TRUE && (r.key < 0 || r.key >= c->N.K)) return fail(c, KB_E_INVALID, "req %u key", i);
+    if ((uint64_t)r.val_off + r.val_cnt > in->n_vals) return fail(c, KB_E_INVALID, "req %u vals", i);
+  }
+  for (uint32_t i = 0; i < in->n_ports; ++i)
+    if (in->ports[i].slot < 0 || in->ports[i].slot >= c->N.P || in->ports[i].ip < 0 || in->ports[i].ip > 63)
+      return fail(c, KB_E_INVALID, "port %u", i);
+  std::vector<int32_t> ts(c->N.n);
+  HIP_OK(c, hipMemcpy(ts.data(), c->N.taint_set, ts.size() * 4, hipMemcpyDeviceToHost));
+  for (int32_t t : ts)
+    if (t < 0 || (uint32_t)t >= in->n_taint_sets) return fail(c, KB_E_INVALID, "node taint_set %d out of range", t);
+
+  DevSpecs& P = c->P;
+  int rc;
+  if ((rc = upload(c, c->spec_mem, &P.specs, in->specs, in->m))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.sc_init, in->sc_init, (size_t)in->m * S))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.sc_req, in->sc_req, (size_t)in->m * S))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.terms, in->terms, in->n_terms))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.reqs, in->reqs, in->n_reqs))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.vals, in->vals, in->n_vals))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.ports, in->ports, in->n_ports))) return rc;
+  if ((rc = upload(c, c->spec_mem, &P.tolerates, in->tolerates, (size_t)in->n_tol_sets * in->n_taint_sets))) return rc;
+  P.n_taint_sets = (int32_t)in->n_taint_sets;
+  P.m = (int32_t)in->m;
+  c->max_pref_weight = 0;
+  for (uint32_t i = 0; i < in->m; ++i) {
+    int64_t sum = 0;
+    for (uint32_t j = 0; j < in->specs[i].pref_term_cnt; ++j)
+      sum += std::llabs((long long)in->terms[in->specs[i].pref_term_off + j].weight);
+    c->max_pref_weight = std::max(c->max_pref_weight, sum);
+  }
+  c->specs_ok = true;
+  return kb_check_score_range(c);
+}
+
+int kb_check_score_range(kb_ctx* c) {
+  // |score| must stay inside the key's 39-bit biased field.
+  const DevCfg& C = c->cfg;
+  long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
+                      (long double)c->max_pref_weight * std::llabs((long long)C.w_na) +
+                      10.0L * std::llabs((long long)C.w_pa);
+  if (bound >= (long double)(kScoreBias / 2)) return fail(c, KB_E_UNSUPPORTED, "score range exceeds 2^37");
+  return KB_OK;
+}
+
+static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
+  if (n_tasks <= c->job_cap && c->d_job) return KB_OK;
+  uint32_t cap = std::max<uint32_t>(n_tasks, 1024);
+  size_t bytes = sizeof(JobState) + (size_t)cap * 2 * sizeof(int32_t);
+  void* p;
+  HIP_OK(c, hipMalloc(&p, bytes));
+  c->work_mem.push_back(p);
+  c->d_job = (char*)p;
+  if (c->h_job) (void)hipHostFree(c->h_job);
+  HIP_OK(c, hipHostMalloc((void**)&c->h_job, bytes, hipHostMallocDefault));
+  c->job_cap = cap;
+  return KB_OK;
+}
+
+int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
+                 kb_job_result* result) {
+  if (!c || !job || !result) return KB_E_INVALID;
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  memset(result, 0, sizeof(*result));
+  result->fail_task = -1;
+  if (job->n_tasks == 0) return KB_OK;
+  for (uint32_t i = 0; i < job->n_tasks; ++i)
+    if (job->task_specs[i] < 0 || job->task_specs[i] >= c->P.m)
+      return fail(c, KB_E_INVALID, "task %u spec %d out of range", i, job->task_specs[i]);
+  int rc = ensure_job_buffers(c, job->n_tasks);
+  if (rc) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  JobState* js = (JobState*)c->d_job;
+  int32_t* out = (int32_t*)(c->d_job + sizeof(JobState));
+  launch_job_init(js, job->ready_num, job->min_available, job->gang_ready, c->stream);
+  uint32_t t = 0;
+  while (t < job->n_tasks) {
+    uint32_t e = t + 1;
+    while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
+    const int spec = job->task_specs[t];
+    hipEvent_t ea;
+    c->ev_begin(&ea);
+    launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, js, c->stream);
+    c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
+    c->ev_begin(&ea);
+    launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, (int)(e - t), c->keys, c->cmax, js, out, c->stream);
+    c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
+    t = e;
+  }
+  HIP_OK(c, hipGetLastError());
+  const size_t bytes = sizeof(JobState) + (size_t)job->n_tasks * 2 * sizeof(int32_t);
+  HIP_OK(c, hipMemcpyAsync(c->h_job, c->d_job, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->device_ms += wall;
+  c->stats.device_ms += wall;
+  c->stats.job_calls += 1;
+  const JobState* hs = (const JobState*)c->h_job;
+  if (c->timing) {
+    // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the batch's launches
+    uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
+    for (auto& p : c->pending)
+      if (p.kind == KB_KERNEL_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
+    c->ev_collect();
+  }
+  const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
+  result->n_placed = (uint32_t)hs->n_placed;
+  result->stop = hs->stop;
+  result->fail_task = hs->fail_task;
+  for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
+  for (int i = 0; i < hs->n_placed; ++i) {
+    if (placed_node) placed_node[i] = ho[2 * i];
+    if (placed_kind) placed_kind[i] = ho[2 * i + 1];
+  }
+  if (hs->panic) return fail(c, KB_E_PANIC, "SelectBestNode: no node scored above -1 (task %d)", hs->fail_task);
+  return KB_OK;
+}
+
+int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
+  if (!c || (!spec_ids && t)) return KB_E_INVALID;
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  for (uint32_t i = 0; i < t; ++i)
+    if (spec_ids[i] < 0 || spec_ids[i] >= c->P.m) return fail(c, KB_E_INVALID, "spec id %d", spec_ids[i]);
+  HIP_OK(c, hipSetDevice(c->device));
+  const size_t n = (size_t)c->N.n;
+  const uint32_t chunk = 8192;
+  int32_t* d_ids;
+  uint32_t* d_r;
+  int64_t* d_s;
+  const uint32_t tc = std::min(t, chunk);
+  HIP_OK(c, hipMalloc(&d_ids, std::max<uint32_t>(tc, 1) * 4));
+  HIP_OK(c, hipMalloc(&d_r, std::max<size_t>(tc * n, 1) * 4));
+  HIP_OK(c, hipMalloc(&d_s, std::max<size_t>(tc * n, 1) * 8));
+  int rc = KB_OK;
+  for (uint32_t b = 0; b < t && rc == KB_OK; b += chunk) {
+    const uint32_t cnt = std::min(chunk, t - b);
+    if (hipMemcpyAsync(d_ids, spec_ids + b, cnt * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = KB_E_HIP;
+    hipEvent_t ea;
+    c->ev_begin(&ea);
+    launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->stream);
+    c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
+    if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
+    if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))
+      rc = KB_E_HIP;
+    if (scores && hipMemcpyAsync(scores + (size_t)b * n, d_s, cnt * n * 8, hipMemcpyDeviceToHost, c->stream))
+      rc = KB_E_HIP;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) rc = KB_E_HIP;
+  }
+  if (c->timing) c->ev_collect();
+  (void)hipFree(d_ids);
+  (void)hipFree(d_r);
+  (void)hipFree(d_s);
+  if (rc) return fail(c, rc, "kb_eval: HIP failure");
+  return KB_OK;
+}
+
+int kb_restore_nodes(kb_ctx* c) {
+  if (!c) return KB_E_INVALID;
+  if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
+  for (auto& col : c->pristine)
+    if (col.bytes) HIP_OK(c, hipMemcpyAsync(col.dst, col.src, col.bytes, hipMemcpyDeviceToDevice, c->stream));
+  return KB_OK;
+}
+
+int kb_get_stats(kb_ctx* c, kb_stats* out, int reset) {
+  if (!c || !out) return KB_E_INVALID;
+  *out = c->stats;
+  if (reset) c->stats = kb_stats{};
+  return KB_OK;
+}
+
+int kb_read_nodes(kb_ctx* c, int64_t* idle_cpu, int64_t* idle_mem, int64_t* rel_cpu, int64_t* rel_mem,
+                  int32_t* pod_count, int64_t* nz_cpu, int64_t* nz_mem) {
+  if (!c) return KB_E_INVALID;
+  if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
+  HIP_OK(c, hipSetDevice(c->device));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  const size_t n = (size_t)c->N.n;
+  if (idle_cpu) HIP_OK(c, hipMemcpy(idle_cpu, c->N.idle_cpu, n * 8, hipMemcpyDeviceToHost));
+  if (idle_mem) HIP_OK(c, hipMemcpy(idle_mem, c->N.idle_mem, n * 8, hipMemcpyDeviceToHost));
+  if (rel_cpu) HIP_OK(c, hipMemcpy(rel_cpu, c->N.rel_cpu, n * 8, hipMemcpyDeviceToHost));
+  if (rel_mem) HIP_OK(c, hipMemcpy(rel_mem, c->N.rel_mem, n * 8, hipMemcpyDeviceToHost));
+  if (pod_count) HIP_OK(c, hipMemcpy(pod_count, c->N.pod_count, n * 4, hipMemcpyDeviceToHost));
+  if (nz_cpu) HIP_OK(c, hipMemcpy(nz_cpu, c->N.nz_cpu, n * 8, hipMemcpyDeviceToHost));
+  if (nz_mem) HIP_OK(c, hipMemcpy(nz_mem, c->N.nz_mem, n * 8, hipMemcpyDeviceToHost));
+  return KB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,280 @@
+"""ctypes binding of libkbgpu.so (include/kbgpu.h) and the high-level allocate call.
+
+The product path: cluster snapshot -> export.Snapshot -> kb_upload_* ->
+kb_allocate (host ordering plugins + per-job device placement) -> binds.
+There is no CPU fallback: if the HIP library or a GPU is missing this raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import export as E
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkbgpu.so")
+
+KB_NUM_REASONS = 16
+KB_OK, KB_E_INVALID, KB_E_HIP, KB_E_UNSUPPORTED, KB_E_NOMEM, KB_E_PANIC, KB_E_STATE = 0, -1, -2, -3, -4, -5, -6
+KB_STOP_DONE, KB_STOP_NO_FIT, KB_STOP_READY = 0, 1, 2
+KB_PLACE_ALLOCATE, KB_PLACE_PIPELINE = 1, 2
+
+P = C.c_void_p
+
+
+class kb_nodes(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_scalar", C.c_uint32), ("n_label", C.c_uint32), ("n_port", C.c_uint32)] + [
+        (f, P) for f in ("idle_cpu", "idle_mem", "rel_cpu", "rel_mem", "idle_sc", "rel_sc", "alloc_cpu", "alloc_mem",
+                         "nz_cpu", "nz_mem", "pod_count", "max_pods", "flags", "label_val", "label_int",
+                         "label_int_ok", "taint_set", "port_used")]
+
+
+class kb_specs(C.Structure):
+    _fields_ = [("m", C.c_uint32), ("specs", P), ("sc_init", P), ("sc_req", P), ("n_terms", C.c_uint32),
+                ("terms", P), ("n_reqs", C.c_uint32), ("reqs", P), ("n_vals", C.c_uint32), ("vals", P),
+                ("n_ports", C.c_uint32), ("ports", P), ("n_tol_sets", C.c_uint32), ("n_taint_sets", C.c_uint32),
+                ("tolerates", P)]
+
+
+class kb_config(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in ("predicates_enabled", "nodeorder_enabled", "mem_pressure", "disk_pressure",
+                                          "pid_pressure", "w_lr", "w_bra", "w_na", "w_pa")]
+
+
+class kb_opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32)]
+
+
+class kb_job_req(C.Structure):
+    _fields_ = [("task_specs", P), ("n_tasks", C.c_uint32), ("ready_num", C.c_int32), ("min_available", C.c_int32),
+                ("gang_ready", C.c_int32)]
+
+
+class kb_job_result(C.Structure):
+    _fields_ = [("n_placed", C.c_uint32), ("stop", C.c_int32), ("fail_task", C.c_int32), ("pad", C.c_int32),
+                ("reason_hist", C.c_uint32 * KB_NUM_REASONS)]
+
+
+class kb_session(C.Structure):
+    _fields_ = [("n_rscalar", C.c_uint32), ("n_tasks", C.c_uint32)] + [
+        (f, P) for f in ("task_job", "task_spec", "task_status", "task_priority", "task_ctime", "task_uid_rank",
+                         "task_resreq", "task_resreq_mask")] + [
+        ("n_jobs", C.c_uint32)] + [(f, P) for f in ("job_queue", "job_priority", "job_min_available", "job_ctime",
+                                                    "job_uid_rank", "job_pg_pending")] + [
+        ("n_queues", C.c_uint32)] + [(f, P) for f in ("queue_weight", "queue_ctime", "queue_uid_rank")] + [
+        ("total_alloc", P), ("total_alloc_mask", C.c_uint64), ("n_tier_plugins", C.c_uint32), ("tier_plugins", P)]
+
+
+class kb_cycle_result(C.Structure):
+    _fields_ = [("task_node", P), ("task_status", P), ("job_fail_task", P), ("job_reason_hist", P),
+                ("event_task", P), ("n_events", C.c_uint32), ("pad", C.c_int32), ("elapsed_ms", C.c_double),
+                ("device_ms", C.c_double)]
+
+
+class kb_stats(C.Structure):
+    _fields_ = [("launches", C.c_uint64 * 3), ("kernel_ms", C.c_double * 3), ("pairs", C.c_uint64 * 3),
+                ("job_calls", C.c_uint64), ("device_ms", C.c_double)]
+
+
+KB_OPT_TIMING = 1
+KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel")
+
+EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
+           "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
+           "kb_get_stats"]
+
+_lib = None
+
+
+class KbError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"kbgpu error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libkbgpu.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: run `make -C scheduler_amd/csrc` (or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    lib.kb_abi_version.restype = C.c_int
+    lib.kb_create.restype = P
+    lib.kb_create.argtypes = [C.POINTER(kb_opts)]
+    lib.kb_destroy.argtypes = [P]
+    lib.kb_last_error.restype = C.c_char_p
+    lib.kb_last_error.argtypes = [P]
+    lib.kb_set_config.argtypes = [P, C.POINTER(kb_config)]
+    lib.kb_upload_nodes.argtypes = [P, C.POINTER(kb_nodes)]
+    lib.kb_upload_specs.argtypes = [P, C.POINTER(kb_specs)]
+    lib.kb_place_job.argtypes = [P, C.POINTER(kb_job_req), P, P, C.POINTER(kb_job_result)]
+    lib.kb_eval.argtypes = [P, P, C.c_uint32, P, P]
+    lib.kb_read_nodes.argtypes = [P] + [P] * 7
+    lib.kb_allocate.argtypes = [P, C.POINTER(kb_session), C.POINTER(kb_cycle_result)]
+    lib.kb_restore_nodes.argtypes = [P]
+    lib.kb_get_stats.argtypes = [P, C.POINTER(kb_stats), C.c_int]
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P) if a is not None and a.size else None
+
+
+class Context:
+    """One device-resident session snapshot (kb_ctx)."""
+
+    def __init__(self, device: int = 0, timing: bool = False):
+        self.lib = load_library()
+        self._keep = []
+        opts = kb_opts(device, KB_OPT_TIMING if timing else 0)
+        self.ctx = self.lib.kb_create(C.byref(opts))
+        if not self.ctx:
+            raise KbError(KB_E_HIP, "kb_create failed")
+        err = self.lib.kb_last_error(self.ctx)
+        if err:  # no HIP device: there is no CPU fallback
+            self.lib.kb_destroy(self.ctx)
+            self.ctx = None
+            raise KbError(KB_E_HIP, err.decode())
+
+    def close(self):
+        if self.ctx:
+            self.lib.kb_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != KB_OK:
+            raise KbError(rc, self.lib.kb_last_error(self.ctx).decode())
+
+    def upload(self, snap: E.Snapshot):
+        self.n_nodes = snap.n_nodes
+        cfg = kb_config(**snap.config)
+        self._check(self.lib.kb_set_config(self.ctx, C.byref(cfg)))
+        c = snap.cols
+        keep = {k: np.ascontiguousarray(v) for k, v in c.items()}
+        self._keep = [keep]
+        nodes = kb_nodes(snap.n_nodes, len(snap.scalars), snap.n_label, snap.n_port,
+                         *[_ptr(keep[f]) for f in ("idle_cpu", "idle_mem", "rel_cpu", "rel_mem", "idle_sc", "rel_sc",
+                                                   "alloc_cpu", "alloc_mem", "nz_cpu", "nz_mem", "pod_count",
+                                                   "max_pods", "flags", "label_val", "label_int", "label_int_ok",
+                                                   "taint_set", "port_used")])
+        self._check(self.lib.kb_upload_nodes(self.ctx, C.byref(nodes)))
+        tol = np.ascontiguousarray(snap.tolerates)
+        specs = kb_specs(len(snap.spec_arr), _ptr(snap.spec_arr), _ptr(snap.sc_init), _ptr(snap.sc_req),
+                         len(snap.term_arr), _ptr(snap.term_arr), len(snap.req_arr), _ptr(snap.req_arr),
+                         len(snap.val_arr), _ptr(snap.val_arr), len(snap.port_arr), _ptr(snap.port_arr),
+                         tol.shape[0], tol.shape[1], _ptr(tol))
+        self._check(self.lib.kb_upload_specs(self.ctx, C.byref(specs)))
+
+    def restore(self):
+        self._check(self.lib.kb_restore_nodes(self.ctx))
+
+    def stats(self, reset=False):
+        st = kb_stats()
+        self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
+        return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
+                "job_calls": st.job_calls, "device_ms": st.device_ms}
+
+    def eval(self, spec_ids):
+        ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
+        n = self.n_nodes
+        reasons = np.zeros((len(ids), n), np.uint32)
+        scores = np.zeros((len(ids), n), np.int64)
+        self._check(self.lib.kb_eval(self.ctx, _ptr(ids), len(ids), _ptr(reasons), _ptr(scores)))
+        return reasons, scores
+
+    def read_nodes(self, n):
+        cols = [np.zeros(n, np.int64) for _ in range(4)] + [np.zeros(n, np.int32)] + [np.zeros(n, np.int64)
+                                                                                       for _ in range(2)]
+        self._check(self.lib.kb_read_nodes(self.ctx, *[_ptr(a) for a in cols]))
+        return dict(zip(("idle_cpu", "idle_mem", "rel_cpu", "rel_mem", "pod_count", "nz_cpu", "nz_mem"), cols))
+
+    def place_job(self, spec_ids, ready_num=0, min_available=0, gang_ready=1):
+        ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
+        nodes = np.zeros(max(len(ids), 1), np.int32)
+        kinds = np.zeros(max(len(ids), 1), np.int32)
+        req = kb_job_req(_ptr(ids), len(ids), ready_num, min_available, gang_ready)
+        res = kb_job_result()
+        self._check(self.lib.kb_place_job(self.ctx, C.byref(req), _ptr(nodes), _ptr(kinds), C.byref(res)))
+        k = res.n_placed
+        return nodes[:k].copy(), kinds[:k].copy(), res
+
+    def allocate(self, snap: E.Snapshot):
+        """kb_allocate: allocateAction.Execute over the uploaded snapshot."""
+        nt, nj = len(snap.session_tasks), len(snap.jobs)
+        arrs = dict(
+            task_job=snap.s_task_job, task_spec=snap.s_task_spec, task_status=snap.s_task_status,
+            task_priority=snap.s_task_priority, task_ctime=snap.s_task_ctime, task_uid_rank=snap.s_task_uid_rank,
+            task_resreq=np.ascontiguousarray(snap.s_task_resreq), task_resreq_mask=snap.s_task_resreq_mask,
+            job_queue=snap.s_job_queue, job_priority=snap.s_job_priority, job_min_available=snap.s_job_min,
+            job_ctime=snap.s_job_ctime, job_uid_rank=snap.s_job_uid_rank, job_pg_pending=snap.s_job_pg_pending,
+            queue_weight=snap.s_queue_weight, queue_ctime=snap.s_queue_ctime, queue_uid_rank=snap.s_queue_uid_rank,
+            total_alloc=snap.s_total, tier_plugins=snap.s_tiers)
+        ssn = kb_session(
+            len(snap.acc_scalars), nt, *[_ptr(arrs[k]) for k in ("task_job", "task_spec", "task_status",
+                                                               "task_priority", "task_ctime", "task_uid_rank",
+                                                               "task_resreq", "task_resreq_mask")],
+            nj, *[_ptr(arrs[k]) for k in ("job_queue", "job_priority", "job_min_available", "job_ctime",
+                                         "job_uid_rank", "job_pg_pending")],
+            len(snap.queues), *[_ptr(arrs[k]) for k in ("queue_weight", "queue_ctime", "queue_uid_rank")],
+            _ptr(arrs["total_alloc"]), snap.s_total_mask, len(snap.s_tiers), _ptr(arrs["tier_plugins"]))
+        out = {"task_node": np.zeros(max(nt, 1), np.int32), "task_status": np.zeros(max(nt, 1), np.int32),
+               "job_fail_task": np.zeros(max(nj, 1), np.int32),
+               "job_reason_hist": np.zeros((max(nj, 1), KB_NUM_REASONS), np.uint32),
+               "event_task": np.zeros(max(nt, 1), np.int32)}
+        res = kb_cycle_result(*[_ptr(out[k]) for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist",
+                                                       "event_task")], 0, 0, 0.0, 0.0)
+        self._check(self.lib.kb_allocate(self.ctx, C.byref(ssn), C.byref(res)))
+        out["n_events"] = res.n_events
+        out["elapsed_ms"] = res.elapsed_ms
+        out["device_ms"] = res.device_ms
+        return out
+
+
+def result_dict(snap: E.Snapshot, out: dict) -> dict:
+    """Map kb_allocate's arrays back to names, in the oracle's output format."""
+    names = snap.node_names()
+    ts = snap.session_tasks
+    events = []
+    for i in range(out["n_events"]):
+        t = ts[out["event_task"][i]]
+        st = out["task_status"][out["event_task"][i]]
+        kind = "pipeline" if st == E.ST["Pipelined"] else "allocate"
+        events.append({"task": t["uid"], "node": names[out["task_node"][out["event_task"][i]]], "kind": kind})
+    binds = {}
+    status = {}
+    for i, t in enumerate(ts):
+        st = int(out["task_status"][i])
+        status[t["uid"]] = E.ST_NAME[st]
+        if st == E.ST["Binding"]:
+            binds[f"{t['pod'].ns}/{t['pod'].name}"] = names[out["task_node"][i]]
+    fit = {}
+    for j, job in enumerate(snap.jobs):
+        ft = int(out["job_fail_task"][j])
+        if ft >= 0:
+            hist = {E.REASONS[b]: int(c) for b, c in enumerate(out["job_reason_hist"][j]) if c}
+            fit[job["uid"]] = {ts[ft]["uid"]: hist}
+    return {"events": events, "binds": binds, "fit_errors": fit, "status": status, "nodes": names,
+            "elapsed_ms": out["elapsed_ms"], "device_ms": out["device_ms"]}
+
+
+def allocate(cluster, device: int = 0) -> dict:
+    """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle."""
+    snap = E.Snapshot(cluster)
+    ctx = Context(device)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+        return result_dict(snap, out)
+    finally:
+        ctx.close()

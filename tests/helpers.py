@@ -1,0 +1,100 @@
+"""Shared fixtures: seeded parity-size clusters of every configuration shape + edge cases."""
+from scheduler_amd import model as m
+from scheduler_amd import synth
+
+GI = 1024 ** 3
+
+
+def parity_clusters():
+    """(name, cluster) pairs small enough for the oracle to finish in seconds."""
+    out = []
+    out.append(("C1-parity", synth.c1(n_nodes=120, n_jobs=24, tasks_per_job=25, seed=1)))
+    out.append(("C2-parity", synth.c2(n_nodes=200, n_jobs=40, tasks_per_job=30, seed=2)))
+    out.append(("C2-fill0.9", synth.c2(n_nodes=150, n_jobs=30, tasks_per_job=40, seed=3, fill=0.9)))
+    out.append(("C3-parity", synth.c3(n_nodes=300, n_jobs=40, tasks_per_job=20, seed=4, n_zones=6, n_racks=30)))
+    out.append(("C2-nogang", _without(synth.c2(n_nodes=80, n_jobs=10, tasks_per_job=12, seed=5), "gang")))
+    out.append(("edge-mixed", edge_cluster()))
+    return out
+
+
+def _without(cl, plugin_name):
+    for t in cl.tiers:
+        t["plugins"] = [p for p in t["plugins"] if p["name"] != plugin_name]
+    return cl
+
+
+def edge_cluster(seed=7):
+    """Small cluster exercising: not-ready / unschedulable / pressure nodes, taints, host ports,
+    Gt/Lt selectors, metadata.name fields, invalid terms, releasing (pipeline) capacity, init containers,
+    pre-placed pods, BestEffort tasks, priorities, a PodGroup in phase Pending and ragged jobs."""
+    import random
+    rng = random.Random(seed)
+    cl = m.Cluster(tiers=m.default_tiers(predicate_args={"predicate.MemoryPressureEnable": "true",
+                                                           "predicate.DiskPressureEnable": "true"}))
+    for i in range(24):
+        labels = {"zone": f"z{i % 3}", "cores": str(8 * (1 + i % 4)), "kubernetes.io/hostname": f"n{i:02d}"}
+        if i % 5 == 0:
+            labels["ssd"] = "true"
+        alloc = {m.CPU: 8000 + 2000 * (i % 3), m.MEMORY: (16 + 8 * (i % 2)) * GI, m.PODS: 6 + i % 3}
+        if i % 4 == 0:
+            alloc["example.com/fpga"] = 2000
+        conds = [{"type": "Ready", "status": "True"}]
+        if i == 3:
+            conds = [{"type": "Ready", "status": "False"}, {"type": "NetworkUnavailable", "status": "True"}]
+        if i == 7:
+            conds.append({"type": "MemoryPressure", "status": "True"})
+        if i == 8:
+            conds.append({"type": "DiskPressure", "status": "True"})
+        taints = []
+        if i % 6 == 1:
+            taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
+        if i == 10:
+            taints.append({"key": "soft", "value": "x", "effect": "PreferNoSchedule"})
+        cl.nodes.append(m.Node(name=f"n{i:02d}", alloc=alloc, labels=labels, conditions=conds, taints=taints,
+                               unschedulable=(i == 5)))
+    # pre-placed pods (running, releasing) incl. one holding host port 8080 on n02
+    for i in range(12):
+        node = f"n{(i * 2) % 24:02d}"
+        if node in ("n03", "n05"):
+            continue
+        p = m.Pod(ns="sys", name=f"run{i}", uid=f"sys-run{i}", node=node, phase="Running",
+                  deleting=(i % 4 == 1), containers=[m.Container(req={m.CPU: 1000 + 500 * (i % 3), m.MEMORY: 2 * GI})])
+        if i == 1:
+            p.containers[0].ports = [{"hostPort": 8080, "protocol": "TCP"}]
+        cl.pods.append(p)
+    cl.queues.append(m.Queue(name="q1", weight=1))
+    specs = [
+        dict(req={m.CPU: 2000, m.MEMORY: 4 * GI}),
+        dict(req={m.CPU: 1500, m.MEMORY: 2 * GI}, sel={"ssd": "true"}),
+        dict(req={m.CPU: 1000, m.MEMORY: GI}, ports=[{"hostPort": 8080}]),
+        dict(req={m.CPU: 3000, m.MEMORY: 3 * GI, "example.com/fpga": 1000}),
+        dict(req={m.CPU: 1000, m.MEMORY: GI}, tol=[{"key": "dedicated", "operator": "Exists"}],
+             aff={"nodeAffinity": {"required": [{"matchExpressions": [{"key": "cores", "operator": "Gt",
+                                                                     "values": ["12"]}]},
+                                                {"matchFields": [{"key": "metadata.name", "operator": "In",
+                                                                  "values": ["n01"]}]}]}}),
+        dict(req={m.CPU: 500, m.MEMORY: GI // 2}, aff={"nodeAffinity": {"preferred": [
+            {"weight": 30, "preference": {"matchExpressions": [{"key": "zone", "operator": "In", "values": ["z1"]}]}},
+            {"weight": 7, "preference": {"matchExpressions": [{"key": "cores", "operator": "Lt", "values": ["20"]}]}},
+            {"weight": 0, "preference": {"matchExpressions": [{"key": "bad key!", "operator": "Exists"}]}}]}}),
+        dict(req={m.CPU: 500, m.MEMORY: GI // 2}, aff={"nodeAffinity": {"preferred": [
+            {"weight": 5, "preference": {"matchExpressions": [{"key": "zone", "operator": "Gt", "values": ["x"]}]}}]}}),
+        dict(req={}, init=[{m.CPU: 6000, m.MEMORY: 2 * GI}]),  # BestEffort by Resreq: skipped by allocate
+        dict(req={m.CPU: 1200, m.MEMORY: GI}, init=[{m.CPU: 6000, m.MEMORY: 6 * GI}]),
+        dict(req={m.CPU: 9000, m.MEMORY: 30 * GI}),  # fits nowhere
+        dict(req={m.CPU: 1000, m.MEMORY: GI}, aff={"nodeAffinity": {"required": [{}]}}),  # empty term
+    ]
+    for j, sp in enumerate(specs):
+        n_tasks = 1 + (j * 3) % 5
+        minm = 1 + j % max(1, n_tasks)
+        phase = "Pending" if j == 6 else ""
+        cl.pod_groups.append(m.PodGroup(ns="e", name=f"g{j:02d}", queue="q1", min_member=minm, phase=phase,
+                                        priority=(j % 3)))
+        for t in range(n_tasks):
+            c = m.Container(req=dict(sp.get("req", {})), ports=[dict(x) for x in sp.get("ports", [])])
+            cl.pods.append(m.Pod(ns="e", name=f"g{j:02d}-{t}", uid=f"e-g{j:02d}-{t}", group=f"g{j:02d}",
+                                 priority=rng.choice([None, 1, 5]), ctime=rng.randint(0, 3), containers=[c],
+                                 init=[m.Container(req=dict(x)) for x in sp.get("init", [])],
+                                 node_selector=dict(sp.get("sel", {})), tolerations=list(sp.get("tol", [])),
+                                 affinity=sp.get("aff")))
+    return cl

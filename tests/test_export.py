@@ -1,0 +1,57 @@
+"""Host-side snapshot export (no GPU): node accounting, spec dedupe, interning."""
+import numpy as np
+
+from scheduler_amd import export as E
+from scheduler_amd import model as m
+from scheduler_amd import synth
+
+from helpers import edge_cluster
+
+GI = 1024 ** 3
+
+
+def test_c2_export_shapes():
+    s = E.Snapshot(synth.c2(n_nodes=64, n_jobs=8, tasks_per_job=5))
+    assert s.n_nodes == 64
+    assert len(s.session_tasks) == 40
+    assert len(s.spec_arr) <= 8
+    assert (s.cols["idle_cpu"] == 64000).all() and (s.cols["max_pods"] == 110).all()
+    assert s.config["predicates_enabled"] == 1 and s.config["nodeorder_enabled"] == 1
+
+
+def test_node_accounting_matches_addtask():
+    # api/node_info.go:165-193: Releasing tasks move capacity to Releasing; Idle drops by Resreq
+    cl = m.Cluster(nodes=[m.Node("n1", alloc={m.CPU: 8000, m.MEMORY: 10 * GI, m.PODS: 10})],
+                   pods=[m.Pod("a", "r", "a-r", node="n1", phase="Running", deleting=True,
+                               containers=[m.Container(req={m.CPU: 1000, m.MEMORY: GI})]),
+                         m.Pod("a", "b", "a-b", node="n1", phase="Running",
+                               containers=[m.Container(req={m.CPU: 2000})])],
+                   queues=[m.Queue("q")])
+    s = E.Snapshot(cl)
+    assert s.cols["idle_cpu"][0] == 5000 and s.cols["idle_mem"][0] == 9 * GI
+    assert s.cols["rel_cpu"][0] == 1000 and s.cols["rel_mem"][0] == GI
+    assert s.cols["pod_count"][0] == 2
+    # non-zero request defaults (non_zero.go:31-52): pod b has no memory key -> 200Mi
+    assert s.cols["nz_cpu"][0] == 3000 and s.cols["nz_mem"][0] == GI + 200 * 1024 * 1024
+
+
+def test_edge_cluster_exports():
+    s = E.Snapshot(edge_cluster())
+    assert s.n_nodes == 24
+    flags = s.cols["flags"]
+    assert flags[3] & E.NODE_NOT_READY and flags[3] & E.NODE_NET_UNAVAIL
+    assert flags[5] & E.NODE_UNSCHEDULABLE and flags[7] & E.NODE_MEM_PRESSURE
+    assert s.config["mem_pressure"] == 1 and s.config["disk_pressure"] == 1
+    # one spec carries an invalid preferred term -> NA_ERROR
+    assert any(f & E.SPEC_NA_ERROR for f in s.spec_arr["flags"])
+    assert s.n_port == 1 and s.cols["port_used"][0].any()
+
+
+def test_invalid_selector_is_everything():
+    # SelectorFromSet: an invalid pair makes the whole nodeSelector match everything (selector.go:849-866)
+    cl = m.Cluster(nodes=[m.Node("n1", alloc={m.CPU: 1000, m.MEMORY: GI, m.PODS: 1})],
+                   pods=[m.Pod("a", "p", "a-p", group="g", node_selector={"bad key!": "x"},
+                               containers=[m.Container(req={m.CPU: 10})])],
+                   pod_groups=[m.PodGroup("a", "g", "q")], queues=[m.Queue("q")])
+    s = E.Snapshot(cl)
+    assert not (s.spec_arr["flags"][0] & E.SPEC_HAS_SELECTOR)

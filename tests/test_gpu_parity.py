@@ -1,0 +1,104 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle on the same seeded snapshots.
+
+Bar: bit-exact. Masks (first-fail reason sets) and scores for every (spec, node) pair, and identical
+allocate outcomes (placement sequence, binds, statuses, FitErrors histograms) under the lowest-index
+tie-break applied to both.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+from scheduler_amd import export as E
+from scheduler_amd import model as m
+from scheduler_amd import runtime, synth
+
+from helpers import parity_clusters
+from test_oracle_kat import allocate_test_cases
+
+pytestmark = pytest.mark.gpu
+
+CLUSTERS = parity_clusters()
+
+
+def _compare(ref, got):
+    assert got["nodes"] == ref["nodes"]
+    assert got["events"] == ref["events"]
+    assert got["binds"] == ref["binds"]
+    assert got["fit_errors"] == ref["fit_errors"]
+    for uid, st in got["status"].items():
+        assert ref["status"][uid] == st, uid
+
+
+@pytest.mark.parametrize("name,cluster", CLUSTERS, ids=[c[0] for c in CLUSTERS])
+def test_allocate_parity(name, cluster):
+    ref = pyoracle.allocate(cluster)
+    got = runtime.allocate(cluster)
+    _compare(ref, got)
+    assert len(got["events"]) > 0
+
+
+@pytest.mark.parametrize("name,cluster,expected", allocate_test_cases(), ids=lambda x: x if isinstance(x, str) else "")
+def test_reference_allocate_cases(name, cluster, expected):  # actions/allocate/allocate_test.go:38-212
+    assert runtime.allocate(cluster)["binds"] == expected
+
+
+@pytest.mark.parametrize("name,cluster", CLUSTERS, ids=[c[0] for c in CLUSTERS])
+def test_eval_masks_and_scores(name, cluster):
+    snap = E.Snapshot(cluster)
+    reps = {}
+    for t in snap.session_tasks:
+        if t["status"] == E.ST["Pending"] and t["spec"] not in reps:
+            reps[t["spec"]] = t["uid"]
+    spec_ids = sorted(reps)
+    ref = pyoracle.evaluate(cluster, [reps[s] for s in spec_ids])
+    assert ref["nodes"] == snap.node_names()
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        reasons, scores = ctx.eval(spec_ids)
+    finally:
+        ctx.close()
+    for i, s in enumerate(spec_ids):
+        rt = ref["tasks"][i]
+        for n in range(snap.n_nodes):
+            want = sorted(rt["reasons"][n])
+            got = sorted(E.REASONS[b] for b in range(16) if (int(reasons[i, n]) >> b) & 1)
+            assert got == want, (s, n, got, want)
+        assert list(scores[i]) == rt["score"], s
+
+
+def test_full_size_c2_properties():
+    """BASELINE configs[1] at full size (10k x 100k): size-independent invariants + determinism."""
+    cl = synth.c2()
+    snap = E.Snapshot(cl)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out1 = ctx.allocate(snap)
+        after = ctx.read_nodes(snap.n_nodes)
+        ctx.restore()
+        out2 = ctx.allocate(snap)
+    finally:
+        ctx.close()
+    assert np.array_equal(out1["task_node"], out2["task_node"])          # deterministic
+    assert np.array_equal(out1["event_task"], out2["event_task"])
+    placed = out1["task_node"][: len(snap.session_tasks)] >= 0
+    assert placed.sum() == out1["n_events"] > 0.9 * len(snap.session_tasks)
+    # conservation: idle = allocatable - sum(resreq of tasks placed there)  (NodeInfo.AddTask)
+    cpu = np.full(snap.n_nodes, snap.cols["idle_cpu"][0])
+    mem = np.full(snap.n_nodes, snap.cols["idle_mem"][0])
+    cnt = np.zeros(snap.n_nodes, np.int64)
+    for t, node in enumerate(out1["task_node"][: len(snap.session_tasks)]):
+        if node >= 0:
+            r = snap.session_tasks[t]["resreq"]
+            cpu[node] -= r.cpu
+            mem[node] -= r.mem
+            cnt[node] += 1
+    assert np.array_equal(after["idle_cpu"], cpu) and np.array_equal(after["idle_mem"], mem)
+    assert np.array_equal(after["pod_count"], cnt) and (cnt <= 110).all()
+    assert (cpu > -10).all() and (mem > -10 * 1024 * 1024).all()  # LessEqual tolerance (resource_info.go:70-72)
+    # gang: every job is either fully placed (minMember = all tasks) or left with a fit error
+    jobs = np.asarray(snap.s_task_job)
+    for j in range(len(snap.jobs)):
+        k = placed[jobs == j].sum()
+        assert k == (jobs == j).sum() or out1["job_fail_task"][j] >= 0
