@@ -22,8 +22,10 @@ struct kb_ctx {
   std::vector<void*> node_mem, spec_mem, work_mem;
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec
   uint64_t* cmax = nullptr;  // [ceil(n/64)] chunk maxima
-  char* d_job = nullptr;     // JobState + placement pairs
-  char* h_job = nullptr;     // pinned mirror
+  uint64_t* stat = nullptr;  // [n] static predicate / NodeAffinity cache of the current spec
+  char* d_job = nullptr;     // device JobState (chains the runs of one job)
+  char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)
+  char* h_job_dev = nullptr; // device address of h_job
   uint32_t job_cap = 0;
   char* h_eval = nullptr;
 

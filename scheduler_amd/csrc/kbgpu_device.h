@@ -62,10 +62,10 @@ struct JobState {
 
 // Launch wrappers (kbgpu_device.hip).
 void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, uint64_t* keys,
-                       uint64_t* cmax, const JobState* js, void* stream);
+                       uint64_t* cmax, uint64_t* stat, const JobState* js, void* stream);
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
-                       uint64_t* keys, const uint64_t* cmax, JobState* js, int32_t* out, void* stream);
-void launch_job_init(JobState* js, int ready_num, int min_available, int gang_ready, void* stream);
+                       uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
+                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, void* stream);
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, void* stream);
 int place_loop_lds_bytes(int n);

@@ -11,7 +11,8 @@
 //
 // Kernels
 //   sweep_keys_kernel : one thread per node; writes the packed argmax key of every
-//                       node and the max key of every 64-node chunk (one wave).
+//                       node, the max key of every 64-node chunk (one wave) and the
+//                       node's static-predicate / NodeAffinity cache for the spec.
 //   place_loop_kernel : ONE wave, persistent for a run of same-spec tasks of a job:
 //                       argmax over chunk maxima (LDS) -> commit the winner's row
 //                       (Session.Allocate/Pipeline -> NodeInfo.AddTask + AddPod) ->
@@ -102,28 +103,117 @@ __device__ bool term_match(const DevNodes& N, const DevSpecs& P, const kb_term& 
   return true;
 }
 
-// The predicate chain; returns the reason mask of the first failing stage (0 = fits).
-__device__ uint32_t node_reasons(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int s,
-                                 int n) {
-  const uint32_t f = N.flags[n];
-  const int64_t* sci = P.sc_init + (size_t)s * N.S;
-  // allocate.go:88: InitResreq <= Idle || InitResreq <= Releasing
-  if (!fits_idle(N, sp, sci, f, n) && !fits_rel(N, sp, sci, f, n)) return 1u << KB_R_RESOURCE_FIT;
-  if (!C.predicates) return 0;
-  // pod number (predicates.go:162-166)
-  if (N.max_pods[n] <= N.pod_count[n]) return 1u << KB_R_POD_NUMBER;
-  // CheckNodeConditionPredicate (vendor/.../predicates.go:1568-1596): one reason per bad condition
-  const uint32_t cond = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
-                             (1u << KB_R_UNSCHEDULABLE));
-  if (cond) return cond;
-  // PodMatchNodeSelector: nodeSelector AND required node affinity (vendor/.../predicates.go:807-863)
-  if ((sp.flags & KB_SPEC_HAS_SELECTOR) && !term_match(N, P, P.terms[sp.sel_term], n))
-    return 1u << KB_R_NODE_SELECTOR;
-  if (sp.flags & KB_SPEC_HAS_REQUIRED) {
-    bool any = false;
-    for (uint32_t i = 0; i < sp.req_term_cnt && !any; ++i) any = term_match(N, P, P.terms[sp.req_term_off + i], n);
-    if (!any) return 1u << KB_R_NODE_SELECTOR;
+// leastRequestedScore (priorities/least_requested.go:36-53): ((cap - req) * 10) / cap, q in [0, 10].
+// The int64 division is replaced by a double estimate corrected with exact int64 products.
+__device__ __forceinline__ int64_t lr_score(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t num = (cap - req) * 10;
+  if (cap > 0 && cap < (1ll << 52) && num >= 0 && num < (1ll << 62)) {
+    int64_t q = (int64_t)((double)num / (double)cap);
+    q = q < 0 ? 0 : (q > 11 ? 11 : q);
+    if (q * cap > num) --q;
+    if ((q + 1) * cap <= num) ++q;
+    return q;
   }
+  return num / cap;
+}
+// fractionOfCapacity (balanced_resource_allocation.go:72-77)
+__device__ __forceinline__ double frac_cap(int64_t req, int64_t cap) {
+  return cap == 0 ? 1.0 : (double)req / (double)cap;
+}
+
+// The mutable + per-node numeric columns one evaluation reads (one batch of independent loads).
+struct Row {
+  uint32_t flags;
+  int32_t pod_count, max_pods;
+  int64_t idle_cpu, idle_mem, rel_cpu, rel_mem, nz_cpu, nz_mem, alloc_cpu, alloc_mem;
+};
+
+__device__ __forceinline__ Row load_row(const DevNodes& N, int n) {
+  Row r;
+  r.flags = N.flags[n];
+  r.pod_count = N.pod_count[n];
+  r.max_pods = N.max_pods[n];
+  r.idle_cpu = N.idle_cpu[n];
+  r.idle_mem = N.idle_mem[n];
+  r.rel_cpu = N.rel_cpu[n];
+  r.rel_mem = N.rel_mem[n];
+  r.nz_cpu = N.nz_cpu[n];
+  r.nz_mem = N.nz_mem[n];
+  r.alloc_cpu = N.alloc_cpu[n];
+  r.alloc_mem = N.alloc_mem[n];
+  return r;
+}
+
+// The columns a commit changes (idle / releasing cpu+mem, pod count, non-zero requests).
+__device__ __forceinline__ void store_row(const DevNodes& N, int n, const Row& r) {
+  N.idle_cpu[n] = r.idle_cpu;
+  N.idle_mem[n] = r.idle_mem;
+  N.rel_cpu[n] = r.rel_cpu;
+  N.rel_mem[n] = r.rel_mem;
+  N.pod_count[n] = r.pod_count;
+  N.nz_cpu[n] = r.nz_cpu;
+  N.nz_mem[n] = r.nz_mem;
+}
+
+// Static part of the predicate chain and score for (spec, node): everything that no commit changes.
+//   bits  0..15: first failing static stage BEFORE the host-port check (conditions, node selector)
+//   bits 16..31: first failing static stage AFTER it (taints, pressure)
+//   bits 32..63: NodeAffinity priority count (node_affinity.go:34-74)
+__device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
+                                uint32_t f, int n) {
+  uint32_t pre = 0, post = 0;
+  if (C.predicates) {
+    // CheckNodeConditionPredicate (vendor/.../predicates.go:1568-1596): one reason per bad condition
+    pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
+               (1u << KB_R_UNSCHEDULABLE));
+    // PodMatchNodeSelector: nodeSelector AND required node affinity (vendor/.../predicates.go:807-863)
+    if (!pre && (sp.flags & KB_SPEC_HAS_SELECTOR) && !term_match(N, P, P.terms[sp.sel_term], n))
+      pre = 1u << KB_R_NODE_SELECTOR;
+    if (!pre && (sp.flags & KB_SPEC_HAS_REQUIRED)) {
+      bool any = false;
+      for (uint32_t i = 0; i < sp.req_term_cnt && !any; ++i) any = term_match(N, P, P.terms[sp.req_term_off + i], n);
+      if (!any) pre = 1u << KB_R_NODE_SELECTOR;
+    }
+    // PodToleratesNodeTaints (vendor/.../predicates.go:1489-1518), then the optional pressure predicates
+    if (!P.tolerates[(size_t)sp.tol_set * P.n_taint_sets + N.taint_set[n]]) post = 1u << KB_R_TAINTS;
+    else if (C.mem_pressure && (sp.flags & KB_SPEC_BEST_EFFORT) && (f & KB_NODE_MEM_PRESSURE))
+      post = 1u << KB_R_MEMORY_PRESSURE;
+    else if (C.disk_pressure && (f & KB_NODE_DISK_PRESSURE)) post = 1u << KB_R_DISK_PRESSURE;
+    else if (C.pid_pressure && (f & KB_NODE_PID_PRESSURE)) post = 1u << KB_R_PID_PRESSURE;
+  }
+  int32_t na = 0;
+  if (C.nodeorder && !(sp.flags & KB_SPEC_NA_ERROR)) {
+    for (uint32_t i = 0; i < sp.pref_term_cnt; ++i) {
+      const kb_term t = P.terms[sp.pref_term_off + i];
+      if (t.weight == 0) continue;
+      if (term_match(N, P, t, n)) na += t.weight;
+    }
+  }
+  return (uint64_t)pre | ((uint64_t)post << 16) | ((uint64_t)(uint32_t)na << 32);
+}
+
+__device__ __forceinline__ bool sc_fit(const DevNodes& N, const kb_spec& sp, const int64_t* sci, bool has_map,
+                                       const int64_t* node_sc, int n) {
+  return scalars_fit(N, sp, sci, has_map, node_sc, n);
+}
+
+// Reason mask of the full chain from a loaded row + the static cache (0 = fits).
+__device__ __forceinline__ uint32_t row_reasons(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
+                                                const kb_spec& sp, const int64_t* sci, const Row& r, uint64_t st,
+                                                int n) {
+  // allocate.go:88: InitResreq <= Idle || InitResreq <= Releasing
+  const bool fi = le_tol(sp.init_cpu, r.idle_cpu, 10) && le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                  sc_fit(N, sp, sci, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, n);
+  if (!fi) {
+    const bool fr = le_tol(sp.init_cpu, r.rel_cpu, 10) && le_tol(sp.init_mem, r.rel_mem, 10ll * 1024 * 1024) &&
+                    sc_fit(N, sp, sci, r.flags & KB_NODE_REL_HAS_MAP, N.rel_sc, n);
+    if (!fr) return 1u << KB_R_RESOURCE_FIT;
+  }
+  if (!C.predicates) return 0;
+  if (r.max_pods <= r.pod_count) return 1u << KB_R_POD_NUMBER;  // predicates.go:162-166
+  const uint32_t pre = (uint32_t)(st & 0xffff);
+  if (pre) return pre;
   // PodFitsHostPorts (vendor/.../predicates.go:1031-1052; cache/host_ports.go:96-125)
   for (uint32_t i = 0; i < sp.port_cnt; ++i) {
     const kb_port p = P.ports[sp.port_off + i];
@@ -131,122 +221,65 @@ __device__ uint32_t node_reasons(const DevNodes& N, const DevSpecs& P, const Dev
     const uint64_t hit = p.ip == 0 ? used : (used & (1ull | (1ull << p.ip)));
     if (hit) return 1u << KB_R_HOST_PORTS;
   }
-  // PodToleratesNodeTaints (vendor/.../predicates.go:1489-1518)
-  if (!P.tolerates[(size_t)sp.tol_set * P.n_taint_sets + N.taint_set[n]]) return 1u << KB_R_TAINTS;
-  // optional pressure predicates (predicates.go:233-276)
-  if (C.mem_pressure && (sp.flags & KB_SPEC_BEST_EFFORT) && (f & KB_NODE_MEM_PRESSURE))
-    return 1u << KB_R_MEMORY_PRESSURE;
-  if (C.disk_pressure && (f & KB_NODE_DISK_PRESSURE)) return 1u << KB_R_DISK_PRESSURE;
-  if (C.pid_pressure && (f & KB_NODE_PID_PRESSURE)) return 1u << KB_R_PID_PRESSURE;
-  return 0;
+  return (uint32_t)((st >> 16) & 0xffff);
 }
 
-// leastRequestedScore (priorities/least_requested.go:36-53)
-__device__ __forceinline__ int64_t lr_score(int64_t req, int64_t cap) {
-  if (cap == 0 || req > cap) return 0;
-  return ((cap - req) * 10) / cap;
-}
-// fractionOfCapacity (balanced_resource_allocation.go:72-77)
-__device__ __forceinline__ double frac_cap(int64_t req, int64_t cap) {
-  return cap == 0 ? 1.0 : (double)req / (double)cap;
-}
-
-// nodeOrderFn (nodeorder.go:188-226) + InterPodAffinity batch score (0 without pod affinity terms).
-// All terms are integers, so the reference's float64 sum is this int64 sum exactly.
-__device__ int64_t node_score(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int n) {
+// nodeOrderFn (nodeorder.go:188-226); InterPodAffinity adds 0 without pod (anti)affinity terms.
+// All terms are integers, so the reference's float64 sum equals this int64 sum.
+__device__ __forceinline__ int64_t row_score(const DevCfg& C, const kb_spec& sp, const Row& r, uint64_t st) {
   if (!C.nodeorder) return 0;
-  if (sp.flags & KB_SPEC_NA_ERROR) return 0;  // map fn error: node keeps only the batch score
-  const int64_t rc = sp.nz_cpu + N.nz_cpu[n], rm = sp.nz_mem + N.nz_mem[n];
-  const int64_t ac = N.alloc_cpu[n], am = N.alloc_mem[n];
-  const int64_t lr = (lr_score(rc, ac) + lr_score(rm, am)) / 2;
-  const double cf = frac_cap(rc, ac), mf = frac_cap(rm, am);
+  if (sp.flags & KB_SPEC_NA_ERROR) return 0;  // map fn error: the node keeps only the batch score
+  const int64_t rc = sp.nz_cpu + r.nz_cpu, rm = sp.nz_mem + r.nz_mem;
+  const int64_t lr = (lr_score(rc, r.alloc_cpu) + lr_score(rm, r.alloc_mem)) / 2;
+  const double cf = frac_cap(rc, r.alloc_cpu), mf = frac_cap(rm, r.alloc_mem);
   const int64_t bra = (cf >= 1.0 || mf >= 1.0) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 10.0);
-  int32_t na = 0;  // CalculateNodeAffinityPriorityMap (priorities/node_affinity.go:34-74)
-  for (uint32_t i = 0; i < sp.pref_term_cnt; ++i) {
-    const kb_term t = P.terms[sp.pref_term_off + i];
-    if (t.weight == 0) continue;
-    if (term_match(N, P, t, n)) na += t.weight;
-  }
+  const int32_t na = (int32_t)(uint32_t)(st >> 32);
   return lr * C.w_lr + bra * C.w_bra + (int64_t)na * C.w_na;
 }
 
-__device__ __forceinline__ uint64_t node_key(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
-                                             const kb_spec& sp, int s, int n) {
-  const uint32_t r = node_reasons(N, P, C, sp, s, n);
-  if (r) return r;
-  const int64_t score = node_score(N, P, C, sp, n);
+__device__ __forceinline__ uint64_t make_key(uint32_t reasons, int64_t score, int n) {
+  if (reasons) return reasons;
   return kFeasible | ((uint64_t)(score + kScoreBias) << 24) | (uint64_t)(kIdxMask - (uint32_t)n);
 }
 
-// Session.Allocate / Session.Pipeline applied to the device row (framework/session.go:199-297):
-// NodeInfo.AddTask (api/node_info.go:165-193) + schedulercache.NodeInfo.AddPod (cache/node_info.go:498-520).
-__device__ int commit_row(const DevNodes& N, const DevSpecs& P, const kb_spec& sp, int s, int w) {
-  const uint32_t f = N.flags[w];
-  const int64_t* sci = P.sc_init + (size_t)s * N.S;
-  const int64_t* scr = P.sc_req + (size_t)s * N.S;
-  int kind;
-  if (fits_idle(N, sp, sci, f, w)) {  // allocate.go:159 -> Idle.Sub(Resreq)
-    N.idle_cpu[w] -= sp.req_cpu;
-    N.idle_mem[w] -= sp.req_mem;
-    if (f & KB_NODE_IDLE_HAS_MAP) {  // Sub leaves a nil map alone (resource_info.go:152-157)
-      uint64_t m = sp.req_sc_mask;
-      while (m) {
-        const int q = __builtin_ctzll(m);
-        m &= m - 1;
-        N.idle_sc[(size_t)q * N.n + w] -= scr[q];
-      }
-    }
-    kind = KB_PLACE_ALLOCATE;
-  } else {  // allocate.go:172 -> Releasing.Sub(Resreq)
-    N.rel_cpu[w] -= sp.req_cpu;
-    N.rel_mem[w] -= sp.req_mem;
-    if (f & KB_NODE_REL_HAS_MAP) {
-      uint64_t m = sp.req_sc_mask;
-      while (m) {
-        const int q = __builtin_ctzll(m);
-        m &= m - 1;
-        N.rel_sc[(size_t)q * N.n + w] -= scr[q];
-      }
-    }
-    kind = KB_PLACE_PIPELINE;
-  }
-  N.pod_count[w] += 1;
-  N.nz_cpu[w] += sp.nz_cpu;
-  N.nz_mem[w] += sp.nz_mem;
-  for (uint32_t i = 0; i < sp.port_cnt; ++i) {  // UpdateUsedPorts (cache/node_info.go:593-606)
-    const kb_port p = P.ports[sp.port_off + i];
-    N.port_used[(size_t)p.slot * N.n + w] |= 1ull << p.ip;
-  }
-  return kind;
+// ---- wave reductions over 64-bit keys with DPP (identity 0 for max) ----
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+// wave-uniform max of v over the 64 lanes (every lane must be active)
+__device__ __forceinline__ uint64_t wave_max_dpp(uint64_t v) {
+  v = umax64(v, dpp_u64<0xb1>(v));   // quad_perm [1,0,3,2]
+  v = umax64(v, dpp_u64<0x4e>(v));   // quad_perm [2,3,0,1]
+  v = umax64(v, dpp_u64<0x124>(v));  // row_ror:4
+  v = umax64(v, dpp_u64<0x128>(v));  // row_ror:8
+  v = umax64(v, dpp_u64<0x142>(v));  // row_bcast:15
+  v = umax64(v, dpp_u64<0x143>(v));  // row_bcast:31
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __global__ __launch_bounds__(256) void sweep_keys_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, uint64_t* keys,
-                                                         uint64_t* cmax, const JobState* js) {
+                                                         uint64_t* cmax, uint64_t* stat, const JobState* js) {
   if (js != nullptr && js->stopped) return;
   const kb_spec sp = P.specs[spec];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t k = 0;
   if (n < N.n) {
-    k = node_key(N, P, C, sp, spec, n);
+    const Row r = load_row(N, n);
+    const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+    stat[n] = st;
+    const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, n);
+    k = make_key(rs, rs ? 0 : row_score(C, sp, r, st), n);
     keys[n] = k;
   }
   const uint64_t m = wave_max_u64(k);
   if ((threadIdx.x & 63) == 0 && (n >> 6) < ((N.n + 63) >> 6)) cmax[n >> 6] = m;
-}
-
-__global__ void job_init_kernel(JobState* js, int ready_num, int min_available, int gang_ready) {
-  const int i = threadIdx.x;
-  if (i == 0) {
-    js->stopped = 0;
-    js->stop = KB_STOP_DONE;
-    js->fail_task = -1;
-    js->n_placed = 0;
-    js->ready_num = ready_num;
-    js->min_available = min_available;
-    js->gang_ready = gang_ready;
-    js->panic = 0;
-  }
-  if (i < KB_NUM_REASONS) js->hist[i] = 0;
 }
 
 // L2-coherent load of a key another lane of this wave may have stored earlier in the launch.
@@ -254,37 +287,84 @@ __device__ __forceinline__ uint64_t load_key_l2(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int stopped, int stop, int fail_task,
+                                              int placed, int ready, int minav, int gang, int panic) {
+  js->stopped = stopped;
+  js->stop = stop;
+  js->fail_task = fail_task;
+  js->n_placed = placed;
+  js->ready_num = ready;
+  js->min_available = minav;
+  js->gang_ready = gang;
+  js->panic = panic;
+  hjs->stopped = stopped;
+  hjs->stop = stop;
+  hjs->fail_task = fail_task;
+  hjs->n_placed = placed;
+  hjs->ready_num = ready;
+  hjs->min_available = minav;
+  hjs->gang_ready = gang;
+  hjs->panic = panic;
+}
+
+// Copy the buffered placements to the caller's pinned host buffer (coalesced, once per run / buffer).
+__device__ __forceinline__ void flush_placements(const uint64_t* pb, int cnt, int base, int32_t* hout, int lane) {
+  __syncthreads();
+  for (int i = lane; i < cnt; i += 64) {
+    const uint64_t v = pb[i];
+    hout[2 * (base + i)] = (int32_t)(uint32_t)v;
+    hout[2 * (base + i) + 1] = (int32_t)(uint32_t)(v >> 32);
+  }
+}
+
+// ONE wave. Runs a job's same-spec tasks: argmax -> commit (Session.Allocate / Pipeline applied to the
+// winner's row: NodeInfo.AddTask, api/node_info.go:165-193, + schedulercache AddPod,
+// cache/node_info.go:498-520) -> re-key the winner from registers -> re-reduce its chunk.
+// The winner's row is read from HBM once per task; the new key needs no reload.
 template <bool KEYS_IN_LDS>
 __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin,
                                                         int t_count, uint64_t* keys, const uint64_t* cmax_g,
-                                                        JobState* js, int32_t* out) {
+                                                        const uint64_t* stat, JobState* js, int first, int ready0,
+                                                        int minav0, int gang0, int32_t* hout, JobState* hjs,
+                                                        int pb_cap) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  if (js->stopped) return;
+  if (!first && js->stopped) return;
   const int lane = threadIdx.x;
   const int n = N.n;
   const int M = (n + 63) >> 6;
-  const int Mp = (M + 1) & ~1;  // keep the key block 16-B aligned
-  uint64_t* cm = lds;
-  uint64_t* lk = lds + Mp;
+  const int Mp = (M + 1) & ~1;
+  uint64_t* cm = lds;                // [Mp] chunk maxima
+  uint64_t* pb = lds + Mp;           // [pb_cap] buffered placements (node | kind << 32)
+  uint64_t* lk = lds + Mp + pb_cap;  // [n] keys (KEYS_IN_LDS)
+  int pb_n = 0, pb_base = t_begin;   // placements buffered since the last flush
   for (int c = lane; c < M; c += 64) cm[c] = cmax_g[c];
   if (KEYS_IN_LDS)
     for (int i = lane; i < n; i += 64) lk[i] = keys[i];
   __syncthreads();
+  uint64_t lmax = 0;  // max over the chunks this lane owns (c = lane + 64 j)
+  for (int c = lane; c < M; c += 64) lmax = umax64(lmax, cm[c]);
 
   const kb_spec sp = P.specs[spec];
-  int ready = js->ready_num;
-  const int minav = js->min_available;
-  const int gang = js->gang_ready;
-  int placed = js->n_placed;
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  int ready, minav, gang, placed;
+  if (first) {
+    ready = ready0;
+    minav = minav0;
+    gang = gang0;
+    placed = 0;
+  } else {
+    ready = js->ready_num;
+    minav = js->min_available;
+    gang = js->gang_ready;
+    placed = js->n_placed;
+  }
 
+  int pw = -1;  // previous winner whose row stores are still pending (lane 0)
+  Row pr{};
+  uint64_t pst = 0;
   for (int t = 0; t < t_count; ++t) {
-    uint64_t best = 0;
-    for (int c = lane; c < M; c += 64) {
-      const uint64_t v = cm[c];
-      best = v > best ? v : best;
-    }
-    best = wave_max_u64(best);
-
+    const uint64_t best = wave_max_dpp(lmax);
     if (!(best & kFeasible)) {
       // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
       uint32_t cnt[KB_NUM_REASONS];
@@ -298,25 +378,21 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
 #pragma unroll
       for (int b = 0; b < KB_NUM_REASONS; ++b) {
         const uint32_t s = wave_sum_u32(cnt[b]);
-        if (lane == 0) js->hist[b] = s;
+        if (lane == 0) {
+          js->hist[b] = s;
+          hjs->hist[b] = s;
+        }
       }
-      if (lane == 0) {
-        js->stop = KB_STOP_NO_FIT;
-        js->fail_task = t_begin + t;
-        js->n_placed = placed;
-        js->ready_num = ready;
-        js->stopped = 1;
-      }
+      if (lane == 0 && pw >= 0) store_row(N, pw, pr);
+      flush_placements(pb, pb_n, pb_base, hout, lane);
+      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_NO_FIT, t_begin + t, placed, ready, minav, gang, 0);
       return;
     }
     const int64_t score = (int64_t)((best >> 24) & ((1ull << 39) - 1)) - kScoreBias;
     if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
-      if (lane == 0) {
-        js->panic = 1;
-        js->fail_task = t_begin + t;
-        js->n_placed = placed;
-        js->stopped = 1;
-      }
+      if (lane == 0 && pw >= 0) store_row(N, pw, pr);
+      flush_placements(pb, pb_n, pb_base, hout, lane);
+      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_DONE, t_begin + t, placed, ready, minav, gang, 1);
       return;
     }
     const int w = (int)(kIdxMask - (uint32_t)(best & kIdxMask));
@@ -324,42 +400,98 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
     uint64_t nk = 0;
     int kind = 0;
     if (lane == 0) {
-      kind = commit_row(N, P, sp, spec, w);
-      nk = node_key(N, P, C, sp, spec, w);
-      if (!KEYS_IN_LDS) keys[w] = nk;
-      out[2 * (t_begin + t)] = w;
-      out[2 * (t_begin + t) + 1] = kind;
+      // The winner's row: from registers when it won the previous task too, else one batch of loads.
+      Row r;
+      uint64_t st;
+      if (w == pw) {
+        r = pr;
+        st = pst;
+      } else {
+        r = load_row(N, w);
+        st = stat[w];
+        // The previous winner's stores are issued only now, after these loads, so waiting on the
+        // loads does not also wait for their acknowledgement (stores and loads share vmcnt).
+        if (pw >= 0) store_row(N, pw, pr);
+      }
+      // allocate.go:159: Allocate when InitResreq fits Idle, else Pipeline onto Releasing (:172)
+      const bool to_idle = le_tol(sp.init_cpu, r.idle_cpu, 10) &&
+                           le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                           scalars_fit(N, sp, sci, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, w);
+      if (to_idle) {
+        r.idle_cpu -= sp.req_cpu;
+        r.idle_mem -= sp.req_mem;
+        if (r.flags & KB_NODE_IDLE_HAS_MAP) {  // Sub leaves a nil map alone (resource_info.go:152-157)
+          uint64_t m = sp.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            N.idle_sc[(size_t)q * n + w] -= scr[q];
+          }
+        }
+        kind = KB_PLACE_ALLOCATE;
+      } else {
+        r.rel_cpu -= sp.req_cpu;
+        r.rel_mem -= sp.req_mem;
+        if (r.flags & KB_NODE_REL_HAS_MAP) {
+          uint64_t m = sp.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            N.rel_sc[(size_t)q * n + w] -= scr[q];
+          }
+        }
+        kind = KB_PLACE_PIPELINE;
+      }
+      r.pod_count += 1;
+      r.nz_cpu += sp.nz_cpu;
+      r.nz_mem += sp.nz_mem;
+      for (uint32_t i = 0; i < sp.port_cnt; ++i) {  // UpdateUsedPorts (cache/node_info.go:593-606)
+        const kb_port p = P.ports[sp.port_off + i];
+        N.port_used[(size_t)p.slot * n + w] |= 1ull << p.ip;
+      }
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, w);
+      nk = make_key(rs, rs ? 0 : row_score(C, sp, r, st), w);
+      pw = w;
+      pr = r;
+      pst = st;
+      pb[pb_n] = (uint32_t)w | ((uint64_t)(uint32_t)kind << 32);
     }
-    nk = __shfl(nk, 0, 64);
-    kind = __shfl(kind, 0, 64);
+    nk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(nk >> 32), 0) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)nk, 0);
+    kind = __builtin_amdgcn_readlane(kind, 0);
     if (!KEYS_IN_LDS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (KEYS_IN_LDS && lane == 0) lk[w] = nk;
 
-    // Re-reduce the winner's chunk.
+    // Re-reduce the winner's chunk; its owner lane refreshes its running max.
     const int c = w >> 6;
     const int i = (c << 6) + lane;
     uint64_t v = 0;
     if (i < n) v = (i == w) ? nk : (KEYS_IN_LDS ? lk[i] : load_key_l2(&keys[i]));
-    v = wave_max_u64(v);
-    if (lane == 0) cm[c] = v;
-    __syncthreads();
+    v = wave_max_dpp(v);
+    if (lane == (c & 63)) {
+      cm[c] = v;
+      uint64_t mx = 0;
+      for (int cc = lane; cc < M; cc += 64) mx = umax64(mx, cm[cc]);
+      lmax = mx;
+    }
 
     ++placed;
+    ++pb_n;
     if (kind == KB_PLACE_ALLOCATE) ++ready;
     if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
-      if (lane == 0) {
-        js->stop = KB_STOP_READY;
-        js->n_placed = placed;
-        js->ready_num = ready;
-        js->stopped = 1;
-      }
+      if (lane == 0 && pw >= 0) store_row(N, pw, pr);
+      flush_placements(pb, pb_n, pb_base, hout, lane);
+      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_READY, -1, placed, ready, minav, gang, 0);
       return;
     }
+    if (pb_n == pb_cap) {
+      flush_placements(pb, pb_n, pb_base, hout, lane);
+      pb_base += pb_n;
+      pb_n = 0;
+    }
   }
-  if (lane == 0) {
-    js->n_placed = placed;
-    js->ready_num = ready;
-  }
+  if (lane == 0 && pw >= 0) store_row(N, pw, pr);
+  flush_placements(pb, pb_n, pb_base, hout, lane);
+  if (lane == 0) publish_state(js, hjs, 0, KB_STOP_DONE, -1, placed, ready, minav, gang, 0);
 }
 
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
@@ -369,52 +501,65 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   if (n >= N.n) return;
   const int s = spec_ids[j];
   const kb_spec sp = P.specs[s];
-  reasons[(size_t)j * N.n + n] = node_reasons(N, P, C, sp, s, n);
-  scores[(size_t)j * N.n + n] = node_score(N, P, C, sp, n);
+  const Row r = load_row(N, n);
+  const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+  reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
+  scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
 }
 
 // ---------------------------------------------------------------------------
-int place_loop_lds_bytes(int n) {
+// LDS plan of one place-loop launch: chunk maxima + placement buffer (+ all keys when they fit).
+static void place_loop_lds_plan(int n, int t_count, int* bytes, int* pb_cap, bool* keys_in_lds) {
   const int M = (n + 63) >> 6;
   const int Mp = (M + 1) & ~1;
-  const size_t keys_bytes = (size_t)(Mp + n) * 8;
-  return keys_bytes <= 160 * 1024 ? (int)keys_bytes : -(Mp * 8);
+  const int limit = 160 * 1024 / 8;  // in u64 words
+  int pb = t_count < 4096 ? t_count : 4096;
+  pb = (pb + 1) & ~1;
+  if (Mp + pb + n <= limit) {
+    *keys_in_lds = true;
+    *pb_cap = pb;
+    *bytes = (Mp + pb + n) * 8;
+    return;
+  }
+  *keys_in_lds = false;
+  if (Mp + pb > limit) pb = (limit - Mp) & ~1;
+  *pb_cap = pb;
+  *bytes = (Mp + pb) * 8;
+}
+int place_loop_lds_bytes(int n) {
+  int bytes, pb;
+  bool in_lds;
+  place_loop_lds_plan(n, 1, &bytes, &pb, &in_lds);
+  return in_lds ? bytes : -bytes;
 }
 
 void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, uint64_t* keys,
-                       uint64_t* cmax, const JobState* js, void* stream) {
+                       uint64_t* cmax, uint64_t* stat, const JobState* js, void* stream) {
   const int blocks = (N.n + 255) / 256;
   hipLaunchKernelGGL(sweep_keys_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, C, spec, keys, cmax,
-                     js);
-}
-
-void launch_job_init(JobState* js, int ready_num, int min_available, int gang_ready, void* stream) {
-  hipLaunchKernelGGL(job_init_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, js, ready_num, min_available,
-                     gang_ready);
+                     stat, js);
 }
 
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
-                       uint64_t* keys, const uint64_t* cmax, JobState* js, int32_t* out, void* stream) {
-  const int lds = place_loop_lds_bytes(N.n);
-  if (lds > 0) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)place_loop_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
-                       t_count, keys, cmax, js, out);
-  } else {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)place_loop_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(64), -lds, (hipStream_t)stream, N, P, C, spec, t_begin,
-                       t_count, keys, cmax, js, out);
+                       uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
+                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, void* stream) {
+  int lds, pb_cap;
+  bool keys_in_lds;
+  place_loop_lds_plan(N.n, t_count, &lds, &pb_cap, &keys_in_lds);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)place_loop_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)place_loop_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
   }
+  if (keys_in_lds)
+    hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
+                       t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+  else
+    hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec,
+                       t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
 }
 
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,

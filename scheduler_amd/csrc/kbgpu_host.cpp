@@ -189,6 +189,9 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, ((n + 63) / 64 + 2) * sizeof(uint64_t)));
   c->work_mem.push_back(p);
   c->cmax = (uint64_t*)p;
+  HIP_OK(c, hipMalloc(&p, n * sizeof(uint64_t)));
+  c->work_mem.push_back(p);
+  c->stat = (uint64_t*)p;
   c->nodes_ok = true;
   return KB_OK;
 }
@@ -265,15 +268,20 @@ int kb_check_score_range(kb_ctx* c) {
 }
 
 static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
-  if (n_tasks <= c->job_cap && c->d_job) return KB_OK;
+  if (!c->d_job) {
+    void* p;
+    HIP_OK(c, hipMalloc(&p, sizeof(JobState)));
+    c->work_mem.push_back(p);
+    c->d_job = (char*)p;
+  }
+  if (n_tasks <= c->job_cap && c->h_job) return KB_OK;
   uint32_t cap = std::max<uint32_t>(n_tasks, 1024);
   size_t bytes = sizeof(JobState) + (size_t)cap * 2 * sizeof(int32_t);
-  void* p;
-  HIP_OK(c, hipMalloc(&p, bytes));
-  c->work_mem.push_back(p);
-  c->d_job = (char*)p;
   if (c->h_job) (void)hipHostFree(c->h_job);
-  HIP_OK(c, hipHostMalloc((void**)&c->h_job, bytes, hipHostMallocDefault));
+  c->h_job = nullptr;
+  // pinned, device-mapped: the place kernel writes placements and the job state straight to host memory
+  HIP_OK(c, hipHostMalloc((void**)&c->h_job, bytes, hipHostMallocMapped));
+  HIP_OK(c, hipHostGetDevicePointer((void**)&c->h_job_dev, c->h_job, 0));
   c->job_cap = cap;
   return KB_OK;
 }
@@ -292,25 +300,25 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
   JobState* js = (JobState*)c->d_job;
-  int32_t* out = (int32_t*)(c->d_job + sizeof(JobState));
-  launch_job_init(js, job->ready_num, job->min_available, job->gang_ready, c->stream);
+  JobState* hjs_dev = (JobState*)c->h_job_dev;
+  int32_t* hout_dev = (int32_t*)(c->h_job_dev + sizeof(JobState));
   uint32_t t = 0;
   while (t < job->n_tasks) {
     uint32_t e = t + 1;
     while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
     const int spec = job->task_specs[t];
+    const int first = t == 0;
     hipEvent_t ea;
     c->ev_begin(&ea);
-    launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, js, c->stream);
+    launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, c->stream);
     c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
     c->ev_begin(&ea);
-    launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, (int)(e - t), c->keys, c->cmax, js, out, c->stream);
+    launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, (int)(e - t), c->keys, c->cmax, c->stat, js, first,
+                      job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, c->stream);
     c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     t = e;
   }
   HIP_OK(c, hipGetLastError());
-  const size_t bytes = sizeof(JobState) + (size_t)job->n_tasks * 2 * sizeof(int32_t);
-  HIP_OK(c, hipMemcpyAsync(c->h_job, c->d_job, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   c->device_ms += wall;
@@ -328,7 +336,8 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   result->n_placed = (uint32_t)hs->n_placed;
   result->stop = hs->stop;
   result->fail_task = hs->fail_task;
-  for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
+  if (hs->stop == KB_STOP_NO_FIT)
+    for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
   for (int i = 0; i < hs->n_placed; ++i) {
     if (placed_node) placed_node[i] = ho[2 * i];
     if (placed_kind) placed_kind[i] = ho[2 * i + 1];
