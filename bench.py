@@ -126,6 +126,7 @@ def main():
                        "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
                        "pods_placed_per_cycle": placed // max(1, args.steps), "parallelism": f"replicas{world}"},
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
+            **({"diag_place_phases": diag_summary(st["diag"], placed)} if any(st["diag"]) else {}),
             "job_calls_per_step": st["job_calls"] / args.steps,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -134,6 +135,14 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def diag_summary(d, tasks):
+    """Per-task shader cycles of each place-loop phase (KB_DIAG builds) and the implied clock."""
+    names = ["argmax", "row_load", "commit", "rescan", "lmax", "loop"]
+    clock_mhz = d[7] and (sum(d[:7]) / (d[7] / 100.0))
+    return {"cycles_per_task": {n: round(d[i] / max(1, tasks), 1) for i, n in enumerate(names)},
+            "clock_mhz": round(clock_mhz, 1) if clock_mhz else None}
 
 
 def cpu_baseline(cluster, sample_tasks):

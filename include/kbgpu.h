@@ -273,6 +273,7 @@ int kb_restore_nodes(kb_ctx* ctx);
 
 /* Kernel timing (HIP events on the context's stream), enabled by KB_OPT_TIMING in kb_opts.flags. */
 #define KB_OPT_TIMING (1u << 0)
+#define KB_OPT_NO_TRAJECTORY (1u << 1) /* force the per-commit re-key loop (testing both device paths) */
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -283,6 +284,7 @@ typedef struct kb_stats {
   uint64_t pairs[KB_NUM_KERNELS];     /* (task, node) evaluations covered by those launches */
   uint64_t job_calls;
   double device_ms;                   /* wall time inside kb_place_job */
+  uint64_t diag[8];                   /* diagnostic builds only: place-loop phase cycles, [7] realtime */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

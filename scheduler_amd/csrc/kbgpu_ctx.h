@@ -23,6 +23,14 @@ struct kb_ctx {
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec
   uint64_t* cmax = nullptr;  // [ceil(n/64)] chunk maxima
   uint64_t* stat = nullptr;  // [n] static predicate / NodeAffinity cache of the current spec
+  // trajectory path
+  uint32_t* traj = nullptr;    // [kTrajMaxJ + 1][n] compressed keys after j commits
+  uint32_t* cmax32 = nullptr;  // [ceil(n/64)]
+  uint32_t* amax = nullptr;    // [n] allocations before Idle stops fitting
+  int idx_bits = 0;
+  std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
+  std::vector<int64_t> spec_pref_weight;
+  bool use_traj = true;
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
   char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)
   char* h_job_dev = nullptr; // device address of h_job
@@ -47,4 +55,6 @@ struct kb_ctx {
   void ev_collect();
 };
 
-extern "C" int kb_check_score_range(kb_ctx* c);
+// internal helpers (defined inside kbgpu_host.cpp's extern "C" block, not part of the ABI)
+extern "C" __attribute__((visibility("hidden"))) int kb_check_score_range(kb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) void kb_update_traj_ok(kb_ctx* c);

@@ -58,6 +58,7 @@ struct JobState {
   int32_t gang_ready;
   int32_t panic;      // 1: SelectBestNode would panic (best score <= -1)
   uint32_t hist[KB_NUM_REASONS];
+  uint64_t diag[8];   // -DKB_DIAG builds: per-phase shader cycles of the place loop, [7] = realtime ticks
 };
 
 // Launch wrappers (kbgpu_device.hip).
@@ -69,5 +70,15 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, void* stream);
 int place_loop_lds_bytes(int n);
+// trajectory path
+constexpr int kTrajMaxJ = 64;
+int traj_lds_bytes(int n, int t_count, int* pb_cap);
+void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
+                       uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,
+                       void* stream);
+void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                       int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
+                       const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                       int32_t* hout, JobState* hjs, void* stream);
 
 }  // namespace kbgpu

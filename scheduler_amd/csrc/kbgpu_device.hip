@@ -287,6 +287,11 @@ __device__ __forceinline__ uint64_t load_key_l2(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void publish_diag(JobState* hjs, const uint64_t* dg, uint64_t rt) {
+  for (int k = 0; k < 7; ++k) hjs->diag[k] += dg[k];
+  hjs->diag[7] += rt;
+}
+
 __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int stopped, int stop, int fail_task,
                                               int placed, int ready, int minav, int gang, int panic) {
   js->stopped = stopped;
@@ -306,6 +311,19 @@ __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int s
   hjs->gang_ready = gang;
   hjs->panic = panic;
 }
+
+#ifdef KB_DIAG
+#define KB_STAMP(k)                                   \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    dg[k] += t_ - dg_last;                            \
+    dg_last = t_;                                     \
+  } while (0)
+#else
+#define KB_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 // Copy the buffered placements to the caller's pinned host buffer (coalesced, once per run / buffer).
 __device__ __forceinline__ void flush_placements(const uint64_t* pb, int cnt, int base, int32_t* hout, int lane) {
@@ -363,8 +381,15 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
   int pw = -1;  // previous winner whose row stores are still pending (lane 0)
   Row pr{};
   uint64_t pst = 0;
+#ifdef KB_DIAG
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int t = 0; t < t_count; ++t) {
+    KB_STAMP(5);
     const uint64_t best = wave_max_dpp(lmax);
+    KB_STAMP(0);
     if (!(best & kFeasible)) {
       // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
       uint32_t cnt[KB_NUM_REASONS];
@@ -385,6 +410,9 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
       }
       if (lane == 0 && pw >= 0) store_row(N, pw, pr);
       flush_placements(pb, pb_n, pb_base, hout, lane);
+#ifdef KB_DIAG
+      if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
       if (lane == 0) publish_state(js, hjs, 1, KB_STOP_NO_FIT, t_begin + t, placed, ready, minav, gang, 0);
       return;
     }
@@ -413,6 +441,10 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
         // loads does not also wait for their acknowledgement (stores and loads share vmcnt).
         if (pw >= 0) store_row(N, pw, pr);
       }
+#ifdef KB_DIAG
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      KB_STAMP(1);
       // allocate.go:159: Allocate when InitResreq fits Idle, else Pipeline onto Releasing (:172)
       const bool to_idle = le_tol(sp.init_cpu, r.idle_cpu, 10) &&
                            le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
@@ -451,10 +483,13 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
       }
       const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, w);
       nk = make_key(rs, rs ? 0 : row_score(C, sp, r, st), w);
+      if (KEYS_IN_LDS) lk[w] = nk;
+      else keys[w] = nk;
       pw = w;
       pr = r;
       pst = st;
       pb[pb_n] = (uint32_t)w | ((uint64_t)(uint32_t)kind << 32);
+      KB_STAMP(2);
     }
     nk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(nk >> 32), 0) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)nk, 0);
@@ -467,12 +502,14 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
     uint64_t v = 0;
     if (i < n) v = (i == w) ? nk : (KEYS_IN_LDS ? lk[i] : load_key_l2(&keys[i]));
     v = wave_max_dpp(v);
+    KB_STAMP(3);
     if (lane == (c & 63)) {
       cm[c] = v;
       uint64_t mx = 0;
       for (int cc = lane; cc < M; cc += 64) mx = umax64(mx, cm[cc]);
       lmax = mx;
     }
+    KB_STAMP(4);
 
     ++placed;
     ++pb_n;
@@ -480,6 +517,9 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
     if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
       if (lane == 0 && pw >= 0) store_row(N, pw, pr);
       flush_placements(pb, pb_n, pb_base, hout, lane);
+#ifdef KB_DIAG
+      if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
       if (lane == 0) publish_state(js, hjs, 1, KB_STOP_READY, -1, placed, ready, minav, gang, 0);
       return;
     }
@@ -491,6 +531,9 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
   }
   if (lane == 0 && pw >= 0) store_row(N, pw, pr);
   flush_placements(pb, pb_n, pb_base, hout, lane);
+#ifdef KB_DIAG
+  if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
   if (lane == 0) publish_state(js, hjs, 0, KB_STOP_DONE, -1, placed, ready, minav, gang, 0);
 }
 
@@ -505,6 +548,338 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
   reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
   scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
+}
+
+// ===========================================================================
+// Trajectory path (N <= kTrajMaxNodes, scores that fit a 32-bit key).
+//
+// Within a run of same-spec tasks only the winner's row changes, and a node's state after j commits of
+// that spec is closed-form: commits Allocate while InitResreq still fits Idle (monotone in the number of
+// allocations A), then Pipeline onto Releasing (allocate.go:159-182; NodeInfo.AddTask, node_info.go:165-193).
+// So the key of every node after 0..J commits is computed in parallel up front (traj_sweep_kernel), and
+// the sequential loop (traj_place_kernel) is pure LDS work: argmax, swap in the precomputed next key,
+// re-reduce one chunk. Rows are written back once per run.
+// ===========================================================================
+constexpr uint32_t kKey32Feasible = 1u << 31;
+constexpr uint32_t kKey32Exhausted = 0x7fffffffu;  // nxt32 sentinel: trajectory ran out, compute on demand
+
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_max32_dpp(uint32_t v) {
+  v = umax32(v, dpp_u32<0xb1>(v));
+  v = umax32(v, dpp_u32<0x4e>(v));
+  v = umax32(v, dpp_u32<0x124>(v));
+  v = umax32(v, dpp_u32<0x128>(v));
+  v = umax32(v, dpp_u32<0x142>(v));
+  v = umax32(v, dpp_u32<0x143>(v));
+  return (uint32_t)__builtin_amdgcn_readlane(v, 63);
+}
+
+// Scalars fit after `mul` subtractions of the spec's Resreq scalars.
+__device__ __forceinline__ bool scalars_fit_after(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+                                                  const int64_t* scr, bool has_map, const int64_t* node_sc, int n,
+                                                  int64_t mul) {
+  if (!(sp.flags & KB_SPEC_INIT_HAS_MAP)) return true;
+  if (!has_map) return false;
+  uint64_t m = sp.init_sc_mask;
+  while (m) {
+    const int q = __builtin_ctzll(m);
+    m &= m - 1;
+    const int64_t avail = node_sc[(size_t)q * N.n + n] - mul * scr[q];
+    if (!le_tol(sci[q], avail, 10)) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool idle_fits_after(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+                                                const int64_t* scr, const Row& r, int n, int64_t a) {
+  return le_tol(sp.init_cpu, r.idle_cpu - a * sp.req_cpu, 10) &&
+         le_tol(sp.init_mem, r.idle_mem - a * sp.req_mem, 10ll * 1024 * 1024) &&
+         scalars_fit_after(N, sp, sci, scr, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, n, a);
+}
+
+// A = number of consecutive Allocates before InitResreq stops fitting Idle (capped at 65535).
+__device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+                                                  const int64_t* scr, const Row& r, int n) {
+  if (!idle_fits_after(N, sp, sci, scr, r, n, 0)) return 0;
+  int lo = 0, hi = 65535;  // fits(lo) holds; find the largest such lo
+  if (idle_fits_after(N, sp, sci, scr, r, n, hi)) return 65535;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (idle_fits_after(N, sp, sci, scr, r, n, mid)) lo = mid;
+    else hi = mid;
+  }
+  return lo + 1;
+}
+
+// Full 64-bit key of node n after j commits of the spec (A allocations at most, the rest pipelined).
+__device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
+                               const int64_t* sci, const int64_t* scr, const Row& r0, uint64_t st, int n, int j,
+                               int A) {
+  const int64_t a = j < A ? j : A;
+  const int64_t p = j - a;
+  Row r = r0;
+  r.idle_cpu -= a * sp.req_cpu;
+  r.idle_mem -= a * sp.req_mem;
+  r.rel_cpu -= p * sp.req_cpu;
+  r.rel_mem -= p * sp.req_mem;
+  r.pod_count += j;
+  r.nz_cpu += (int64_t)j * sp.nz_cpu;
+  r.nz_mem += (int64_t)j * sp.nz_mem;
+  uint32_t reasons = 0;
+  const bool fi = le_tol(sp.init_cpu, r.idle_cpu, 10) && le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                  scalars_fit_after(N, sp, sci, scr, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, n, a);
+  if (!fi) {
+    const bool fr = le_tol(sp.init_cpu, r.rel_cpu, 10) && le_tol(sp.init_mem, r.rel_mem, 10ll * 1024 * 1024) &&
+                    scalars_fit_after(N, sp, sci, scr, r.flags & KB_NODE_REL_HAS_MAP, N.rel_sc, n, p);
+    if (!fr) reasons = 1u << KB_R_RESOURCE_FIT;
+  }
+  if (!reasons && C.predicates) {
+    if (r.max_pods <= r.pod_count) {
+      reasons = 1u << KB_R_POD_NUMBER;
+    } else if (st & 0xffff) {
+      reasons = (uint32_t)(st & 0xffff);
+    } else {
+      for (uint32_t i = 0; i < sp.port_cnt && !reasons; ++i) {
+        const kb_port q = P.ports[sp.port_off + i];
+        uint64_t used = N.port_used[(size_t)q.slot * N.n + n];
+        if (j > 0)  // the spec's own ports were taken by its earlier commits here (UpdateUsedPorts)
+          for (uint32_t k = 0; k < sp.port_cnt; ++k) {
+            const kb_port o = P.ports[sp.port_off + k];
+            if (o.slot == q.slot) used |= 1ull << o.ip;
+          }
+        if (q.ip == 0 ? used : (used & (1ull | (1ull << q.ip)))) reasons = 1u << KB_R_HOST_PORTS;
+      }
+      if (!reasons) reasons = (uint32_t)((st >> 16) & 0xffff);
+    }
+  }
+  if (reasons) return reasons;
+  const int64_t score = row_score(C, sp, r, st);
+  return kFeasible | ((uint64_t)(score + kScoreBias) << 24);
+}
+
+__device__ __forceinline__ uint32_t compress_key(uint64_t k64, int n, int idx_bits) {
+  if (!(k64 & kFeasible)) return (uint32_t)k64;
+  const int64_t score = (int64_t)((k64 >> 24) & ((1ull << 39) - 1)) - kScoreBias;
+  const int64_t bias32 = 1ll << (30 - idx_bits);
+  const uint32_t idx_mask = (1u << idx_bits) - 1;
+  return kKey32Feasible | ((uint32_t)(score + bias32) << idx_bits) | (idx_mask - (uint32_t)n);
+}
+
+// grid (ceil(n/256), J+1): thread (node, j) writes the key after j commits.
+__global__ __launch_bounds__(256) void traj_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
+                                                         uint32_t* traj, uint32_t* cmax32, uint32_t* amax,
+                                                         uint64_t* stat, const JobState* js) {
+  if (js != nullptr && js->stopped) return;
+  const kb_spec sp = P.specs[spec];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y;
+  uint32_t k = 0;
+  if (n < N.n) {
+    const Row r = load_row(N, n);
+    const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+    const int A = allocs_before_full(N, sp, sci, scr, r, n);
+    k = compress_key(traj_key64(N, P, C, sp, sci, scr, r, st, n, j, A), n, idx_bits);
+    traj[(size_t)j * N.n + n] = k;
+    if (j == 0) {
+      stat[n] = st;
+      amax[n] = (uint32_t)A;
+    }
+  }
+  if (j == 0) {
+    const uint32_t m = wave_max32_dpp(k);
+    if ((threadIdx.x & 63) == 0 && (n >> 6) < ((N.n + 63) >> 6)) cmax32[n >> 6] = m;
+  }
+}
+
+// Apply `c` commits (the first min(c, A) Allocate, the rest Pipeline) to node w's row in HBM.
+__device__ void write_back_row(const DevNodes& N, const DevSpecs& P, const kb_spec& sp, const int64_t* scr, int w,
+                               int c, int A) {
+  const int64_t a = c < A ? c : A;
+  const int64_t p = c - a;
+  const uint32_t f = N.flags[w];
+  N.idle_cpu[w] -= a * sp.req_cpu;
+  N.idle_mem[w] -= a * sp.req_mem;
+  N.rel_cpu[w] -= p * sp.req_cpu;
+  N.rel_mem[w] -= p * sp.req_mem;
+  N.pod_count[w] += c;
+  N.nz_cpu[w] += (int64_t)c * sp.nz_cpu;
+  N.nz_mem[w] += (int64_t)c * sp.nz_mem;
+  uint64_t m = sp.req_sc_mask;
+  while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
+    const int q = __builtin_ctzll(m);
+    m &= m - 1;
+    if (a && (f & KB_NODE_IDLE_HAS_MAP)) N.idle_sc[(size_t)q * N.n + w] -= a * scr[q];
+    if (p && (f & KB_NODE_REL_HAS_MAP)) N.rel_sc[(size_t)q * N.n + w] -= p * scr[q];
+  }
+  if (c > 0)
+    for (uint32_t i = 0; i < sp.port_cnt; ++i) {
+      const kb_port q = P.ports[sp.port_off + i];
+      N.port_used[(size_t)q.slot * N.n + w] |= 1ull << q.ip;
+    }
+}
+
+__global__ __launch_bounds__(64) void traj_place_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin,
+                                                        int t_count, int J, int idx_bits, const uint32_t* traj,
+                                                        const uint32_t* cmax32, const uint32_t* amax,
+                                                        const uint64_t* stat, JobState* js, int first, int ready0,
+                                                        int minav0, int gang0, int32_t* hout, JobState* hjs,
+                                                        int pb_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  if (!first && js->stopped) return;
+  const int lane = threadIdx.x;
+  const int n = N.n;
+  const int M = (n + 63) >> 6;
+  const int W = (n + 63) >> 6;           // touched-bitmap words
+  uint64_t* tb = (uint64_t*)lds32;        // [W] nodes committed to in this run
+  uint32_t* cur = lds32 + 2 * W;          // [n] key after the commits so far
+  uint32_t* nxt = cur + n;                // [n] key after one more commit (or kKey32Exhausted)
+  uint32_t* cnt = nxt + n;                // [n] commits so far | A << 16
+  uint32_t* cm = cnt + n;                 // [M] chunk maxima of cur
+  uint32_t* pb = cm + ((M + 3) & ~3);     // [pb_cap] placements: node | kind << 30
+  for (int i = lane; i < W; i += 64) tb[i] = 0;
+  for (int i = lane; i < n; i += 64) {
+    cur[i] = traj[i];
+    nxt[i] = J >= 1 ? traj[(size_t)n + i] : kKey32Exhausted;
+    cnt[i] = amax[i] << 16;
+  }
+  for (int c = lane; c < M; c += 64) cm[c] = cmax32[c];
+  __syncthreads();
+  uint32_t lmax = 0;
+  for (int c = lane; c < M; c += 64) lmax = umax32(lmax, cm[c]);
+
+  const kb_spec sp = P.specs[spec];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const uint32_t idx_mask = (1u << idx_bits) - 1;
+  const int64_t bias32 = 1ll << (30 - idx_bits);
+  int ready, minav, gang, placed;
+  if (first) {
+    ready = ready0;
+    minav = minav0;
+    gang = gang0;
+    placed = 0;
+  } else {
+    ready = js->ready_num;
+    minav = js->min_available;
+    gang = js->gang_ready;
+    placed = js->n_placed;
+  }
+  int pb_n = 0, pb_base = t_begin;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+
+  for (int t = 0; t < t_count; ++t) {
+    const uint32_t best = wave_max32_dpp(lmax);
+    if (!(best & kKey32Feasible)) {
+      // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
+      uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+      for (int i = lane; i < n; i += 64) {
+        const uint32_t k = cur[i];
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k >> b) & 1u;
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) {
+        const uint32_t s = wave_sum_u32(h[b]);
+        if (lane == 0) {
+          js->hist[b] = s;
+          hjs->hist[b] = s;
+        }
+      }
+      stop = KB_STOP_NO_FIT;
+      fail_task = t_begin + t;
+      stopped = 1;
+      break;
+    }
+    const int64_t score = (int64_t)((best >> idx_bits) & ((1u << (31 - idx_bits)) - 1)) - bias32;
+    if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
+      fail_task = t_begin + t;
+      panic = 1;
+      stopped = 1;
+      break;
+    }
+    const int w = (int)(idx_mask - (best & idx_mask));
+
+    uint32_t nk = 0;
+    int kind = 0;
+    uint32_t pf = kKey32Exhausted;
+    if (lane == 0) {
+      const uint32_t s = cnt[w];
+      const int c = (int)(s & 0xffff), A = (int)(s >> 16);
+      kind = c < A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;  // commit c+1 Allocates iff c+1 <= A
+      nk = nxt[w];
+      if (nk == kKey32Exhausted) {  // beyond the precomputed trajectory: compute in place
+        const Row r0 = load_row(N, w);
+        nk = compress_key(traj_key64(N, P, C, sp, sci, scr, r0, stat[w], w, c + 1, A), w, idx_bits);
+      }
+      cur[w] = nk;
+      cnt[w] = (uint32_t)(c + 1) | ((uint32_t)A << 16);
+      if (c == 0) tb[w >> 6] |= 1ull << (w & 63);
+      if (c + 2 <= J) pf = traj[(size_t)(c + 2) * n + w];  // key after c+2 commits (prefetch)
+      pb[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
+    }
+    nk = (uint32_t)__builtin_amdgcn_readlane(nk, 0);
+    kind = __builtin_amdgcn_readlane(kind, 0);
+
+    // Re-reduce the winner's chunk; its owner lane refreshes its running max.
+    const int ch = w >> 6;
+    const int i = (ch << 6) + lane;
+    uint32_t v = 0;
+    if (i < n) v = (i == w) ? nk : cur[i];
+    v = wave_max32_dpp(v);
+    if (lane == (ch & 63)) {
+      cm[ch] = v;
+      uint32_t mx = 0;
+      for (int cc = lane; cc < M; cc += 64) mx = umax32(mx, cm[cc]);
+      lmax = mx;
+    }
+    if (lane == 0) nxt[w] = pf;
+
+    ++placed;
+    ++pb_n;
+    if (kind == KB_PLACE_ALLOCATE) ++ready;
+    if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+      stop = KB_STOP_READY;
+      stopped = 1;
+      break;
+    }
+    if (pb_n == pb_cap) {
+      __syncthreads();
+      for (int k = lane; k < pb_n; k += 64) {
+        const uint32_t e = pb[k];
+        hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+        hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+      }
+      pb_base += pb_n;
+      pb_n = 0;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  // write the run's commits back to the node table (one pass over the touched nodes)
+  for (int wd = lane; wd < W; wd += 64) {
+    uint64_t bits = tb[wd];
+    while (bits) {
+      const int b = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      const int w = (wd << 6) + b;
+      const uint32_t s = cnt[w];
+      write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
+    }
+  }
+  for (int k = lane; k < pb_n; k += 64) {
+    const uint32_t e = pb[k];
+    hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+    hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+  }
+  if (lane == 0) publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic);
 }
 
 // ---------------------------------------------------------------------------
@@ -560,6 +935,42 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
   else
     hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec,
                        t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+}
+
+int traj_lds_bytes(int n, int t_count, int* pb_cap) {
+  const int M = (n + 63) >> 6;
+  const int W = (n + 63) >> 6;
+  const int fixed = 8 * W + 12 * n + 4 * ((M + 3) & ~3);
+  const int limit = 160 * 1024;
+  int pb = t_count;
+  if (fixed + 4 * pb > limit) pb = (limit - fixed) / 4;
+  if (pb < 64) return -1;
+  *pb_cap = pb;
+  return fixed + 4 * pb;
+}
+
+void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
+                       uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,
+                       void* stream) {
+  dim3 grid((N.n + 255) / 256, J + 1);
+  hipLaunchKernelGGL(traj_sweep_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec, idx_bits, traj,
+                     cmax32, amax, stat, js);
+}
+
+void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                       int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
+                       const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                       int32_t* hout, JobState* hjs, void* stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)traj_place_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  int pb_cap = 0;
+  const int lds = traj_lds_bytes(N.n, t_count, &pb_cap);
+  hipLaunchKernelGGL(traj_place_kernel, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec, t_begin, t_count,
+                     J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
 }
 
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,

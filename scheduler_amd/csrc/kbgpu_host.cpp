@@ -101,6 +101,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   kb_ctx* c = new kb_ctx();
   c->device = opts ? opts->device : 0;
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
+  c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   if (hipSetDevice(c->device) != hipSuccess) {
     c->err = "hipSetDevice failed";
     c->broken = true;
@@ -138,6 +139,7 @@ int kb_set_config(kb_ctx* c, const kb_config* cfg) {
   if (!c || !cfg) return KB_E_INVALID;
   c->cfg = DevCfg{cfg->predicates_enabled, cfg->nodeorder_enabled, cfg->mem_pressure, cfg->disk_pressure,
                   cfg->pid_pressure, cfg->w_lr, cfg->w_bra, cfg->w_na, cfg->w_pa};
+  kb_update_traj_ok(c);
   return kb_check_score_range(c);
 }
 
@@ -192,6 +194,22 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, n * sizeof(uint64_t)));
   c->work_mem.push_back(p);
   c->stat = (uint64_t*)p;
+  c->idx_bits = 1;
+  while ((1ull << c->idx_bits) < (unsigned long long)n) ++c->idx_bits;
+  int pbc;
+  if (traj_lds_bytes((int)n, 64, &pbc) > 0) {
+    HIP_OK(c, hipMalloc(&p, (size_t)(kTrajMaxJ + 1) * n * sizeof(uint32_t)));
+    c->work_mem.push_back(p);
+    c->traj = (uint32_t*)p;
+    HIP_OK(c, hipMalloc(&p, ((n + 63) / 64 + 4) * sizeof(uint32_t)));
+    c->work_mem.push_back(p);
+    c->cmax32 = (uint32_t*)p;
+    HIP_OK(c, hipMalloc(&p, n * sizeof(uint32_t)));
+    c->work_mem.push_back(p);
+    c->amax = (uint32_t*)p;
+  } else {
+    c->traj = nullptr;
+  }
   c->nodes_ok = true;
   return KB_OK;
 }
@@ -247,14 +265,30 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   P.n_taint_sets = (int32_t)in->n_taint_sets;
   P.m = (int32_t)in->m;
   c->max_pref_weight = 0;
+  c->spec_pref_weight.assign(in->m, 0);
   for (uint32_t i = 0; i < in->m; ++i) {
     int64_t sum = 0;
     for (uint32_t j = 0; j < in->specs[i].pref_term_cnt; ++j)
       sum += std::llabs((long long)in->terms[in->specs[i].pref_term_off + j].weight);
     c->max_pref_weight = std::max(c->max_pref_weight, sum);
+    c->spec_pref_weight[i] = sum;
   }
+  kb_update_traj_ok(c);
   c->specs_ok = true;
   return kb_check_score_range(c);
+}
+
+// Which specs can use the 32-bit trajectory keys: |score| bound below 2^(30 - idx_bits).
+void kb_update_traj_ok(kb_ctx* c) {
+  const DevCfg& C = c->cfg;
+  const long double bias32 = (long double)(1ll << (30 - c->idx_bits));
+  c->spec_traj_ok.assign(c->spec_pref_weight.size(), 0);
+  for (size_t i = 0; i < c->spec_pref_weight.size(); ++i) {
+    long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
+                        (long double)c->spec_pref_weight[i] * std::llabs((long long)C.w_na) +
+                        10.0L * std::llabs((long long)C.w_pa);
+    c->spec_traj_ok[i] = c->traj != nullptr && bound < bias32 - 1;
+  }
 }
 
 int kb_check_score_range(kb_ctx* c) {
@@ -301,6 +335,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   auto t0 = std::chrono::steady_clock::now();
   JobState* js = (JobState*)c->d_job;
   JobState* hjs_dev = (JobState*)c->h_job_dev;
+  memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
   int32_t* hout_dev = (int32_t*)(c->h_job_dev + sizeof(JobState));
   uint32_t t = 0;
   while (t < job->n_tasks) {
@@ -309,13 +344,29 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     const int spec = job->task_specs[t];
     const int first = t == 0;
     hipEvent_t ea;
-    c->ev_begin(&ea);
-    launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, c->stream);
-    c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
-    c->ev_begin(&ea);
-    launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, (int)(e - t), c->keys, c->cmax, c->stat, js, first,
-                      job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, c->stream);
-    c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
+    int pbc;
+    const int run = (int)(e - t);
+    const bool traj = c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
+    if (traj) {
+      const int J = std::min(run, kTrajMaxJ);
+      c->ev_begin(&ea);
+      launch_traj_sweep(c->N, c->P, c->cfg, spec, J, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
+                        first ? nullptr : js, c->stream);
+      c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
+      c->ev_begin(&ea);
+      launch_traj_place(c->N, c->P, c->cfg, spec, (int)t, run, J, c->idx_bits, c->traj, c->cmax32, c->amax,
+                        c->stat, js, first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev,
+                        c->stream);
+      c->ev_end(ea, KB_KERNEL_PLACE, 0);
+    } else {
+      c->ev_begin(&ea);
+      launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, c->stream);
+      c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
+      c->ev_begin(&ea);
+      launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->cmax, c->stat, js, first,
+                        job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, c->stream);
+      c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
+    }
     t = e;
   }
   HIP_OK(c, hipGetLastError());
@@ -325,6 +376,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   c->stats.device_ms += wall;
   c->stats.job_calls += 1;
   const JobState* hs = (const JobState*)c->h_job;
+  for (int k = 0; k < 8; ++k) c->stats.diag[k] += hs->diag[k];
   if (c->timing) {
     // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the batch's launches
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);

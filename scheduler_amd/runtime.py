@@ -14,7 +14,7 @@ import numpy as np
 from . import export as E
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkbgpu.so")
+LIB_PATH = os.environ.get("KBGPU_LIB", os.path.join(_HERE, "libkbgpu.so"))
 
 KB_NUM_REASONS = 16
 KB_OK, KB_E_INVALID, KB_E_HIP, KB_E_UNSUPPORTED, KB_E_NOMEM, KB_E_PANIC, KB_E_STATE = 0, -1, -2, -3, -4, -5, -6
@@ -75,10 +75,11 @@ class kb_cycle_result(C.Structure):
 
 class kb_stats(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 3), ("kernel_ms", C.c_double * 3), ("pairs", C.c_uint64 * 3),
-                ("job_calls", C.c_uint64), ("device_ms", C.c_double)]
+                ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
 KB_OPT_TIMING = 1
+KB_OPT_NO_TRAJECTORY = 2
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel")
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
@@ -128,10 +129,10 @@ def _ptr(a):
 class Context:
     """One device-resident session snapshot (kb_ctx)."""
 
-    def __init__(self, device: int = 0, timing: bool = False):
+    def __init__(self, device: int = 0, timing: bool = False, trajectory: bool = True):
         self.lib = load_library()
         self._keep = []
-        opts = kb_opts(device, KB_OPT_TIMING if timing else 0)
+        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | (0 if trajectory else KB_OPT_NO_TRAJECTORY))
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
             raise KbError(KB_E_HIP, "kb_create failed")
@@ -183,7 +184,7 @@ class Context:
         st = kb_stats()
         self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
         return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
-                "job_calls": st.job_calls, "device_ms": st.device_ms}
+                "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag)}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
@@ -268,10 +269,10 @@ def result_dict(snap: E.Snapshot, out: dict) -> dict:
             "elapsed_ms": out["elapsed_ms"], "device_ms": out["device_ms"]}
 
 
-def allocate(cluster, device: int = 0) -> dict:
+def allocate(cluster, device: int = 0, trajectory: bool = True) -> dict:
     """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle."""
     snap = E.Snapshot(cluster)
-    ctx = Context(device)
+    ctx = Context(device, trajectory=trajectory)
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)

@@ -29,10 +29,12 @@ def _compare(ref, got):
         assert ref["status"][uid] == st, uid
 
 
+@pytest.mark.parametrize("trajectory", [True, False], ids=["trajectory", "rekey"])
 @pytest.mark.parametrize("name,cluster", CLUSTERS, ids=[c[0] for c in CLUSTERS])
-def test_allocate_parity(name, cluster):
+def test_allocate_parity(name, cluster, trajectory):
+    """Both device paths: precomputed per-node key trajectories, and the per-commit re-key loop."""
     ref = pyoracle.allocate(cluster)
-    got = runtime.allocate(cluster)
+    got = runtime.allocate(cluster, trajectory=trajectory)
     _compare(ref, got)
     assert len(got["events"]) > 0
 
@@ -68,7 +70,8 @@ def test_eval_masks_and_scores(name, cluster):
 
 
 def test_full_size_c2_properties():
-    """BASELINE configs[1] at full size (10k x 100k): size-independent invariants + determinism."""
+    """BASELINE configs[1] at full size (10k x 100k): size-independent invariants, determinism, and
+    identical placements from the two device paths."""
     cl = synth.c2()
     snap = E.Snapshot(cl)
     ctx = runtime.Context(0)
@@ -80,8 +83,16 @@ def test_full_size_c2_properties():
         out2 = ctx.allocate(snap)
     finally:
         ctx.close()
+    ctx = runtime.Context(0, trajectory=False)
+    try:
+        ctx.upload(snap)
+        out3 = ctx.allocate(snap)
+    finally:
+        ctx.close()
     assert np.array_equal(out1["task_node"], out2["task_node"])          # deterministic
     assert np.array_equal(out1["event_task"], out2["event_task"])
+    assert np.array_equal(out1["task_node"], out3["task_node"])          # both device paths agree
+    assert np.array_equal(out1["event_task"], out3["event_task"])
     placed = out1["task_node"][: len(snap.session_tasks)] >= 0
     assert placed.sum() == out1["n_events"] > 0.9 * len(snap.session_tasks)
     # conservation: idle = allocatable - sum(resreq of tasks placed there)  (NodeInfo.AddTask)
