@@ -72,6 +72,7 @@ void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const in
 int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;
+constexpr int kTrajDefaultJ = 16;  // trajectory depth per run; deeper commits are computed in place
 int traj_lds_bytes(int n, int t_count, int* pb_cap);
 void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
                        uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,

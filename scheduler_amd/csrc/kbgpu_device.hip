@@ -335,19 +335,28 @@ __device__ __forceinline__ void flush_placements(const uint64_t* pb, int cnt, in
   }
 }
 
+// Loop-exit state of wave 0, handed to the whole block through LDS.
+struct alignas(16) LoopOut {  // 48 B: keeps the dynamic LDS base 16-B aligned (guide §6 Guideline 17)
+  int32_t stop, fail_task, placed, ready, minav, gang, panic, stopped, pb_n, pb_base, pad0, pad1;
+};
+static_assert(sizeof(LoopOut) % 16 == 0, "static LDS must stay a multiple of 16 B");
+constexpr int kLdsLimit = 160 * 1024 - 256;  // dynamic LDS budget next to the small static block
+
 // ONE wave. Runs a job's same-spec tasks: argmax -> commit (Session.Allocate / Pipeline applied to the
 // winner's row: NodeInfo.AddTask, api/node_info.go:165-193, + schedulercache AddPod,
 // cache/node_info.go:498-520) -> re-key the winner from registers -> re-reduce its chunk.
 // The winner's row is read from HBM once per task; the new key needs no reload.
 template <bool KEYS_IN_LDS>
-__global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin,
+__global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin,
                                                         int t_count, uint64_t* keys, const uint64_t* cmax_g,
                                                         const uint64_t* stat, JobState* js, int first, int ready0,
                                                         int minav0, int gang0, int32_t* hout, JobState* hjs,
                                                         int pb_cap) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  __shared__ LoopOut lo;
   if (!first && js->stopped) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int n = N.n;
   const int M = (n + 63) >> 6;
   const int Mp = (M + 1) & ~1;
@@ -355,10 +364,13 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
   uint64_t* pb = lds + Mp;           // [pb_cap] buffered placements (node | kind << 32)
   uint64_t* lk = lds + Mp + pb_cap;  // [n] keys (KEYS_IN_LDS)
   int pb_n = 0, pb_base = t_begin;   // placements buffered since the last flush
-  for (int c = lane; c < M; c += 64) cm[c] = cmax_g[c];
-  if (KEYS_IN_LDS)
-    for (int i = lane; i < n; i += 64) lk[i] = keys[i];
+  for (int c = tid; c < M; c += 512) cm[c] = cmax_g[c];
+  if (KEYS_IN_LDS) {
+#pragma unroll 4
+    for (int i = tid; i < n; i += 512) lk[i] = keys[i];
+  }
   __syncthreads();
+  if (tid < 64) {  // only wave 0 runs the sequential loop
   uint64_t lmax = 0;  // max over the chunks this lane owns (c = lane + 64 j)
   for (int c = lane; c < M; c += 64) lmax = umax64(lmax, cm[c]);
 
@@ -409,19 +421,17 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
         }
       }
       if (lane == 0 && pw >= 0) store_row(N, pw, pr);
-      flush_placements(pb, pb_n, pb_base, hout, lane);
 #ifdef KB_DIAG
       if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
-      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_NO_FIT, t_begin + t, placed, ready, minav, gang, 0);
-      return;
+      if (lane == 0) lo = LoopOut{KB_STOP_NO_FIT, t_begin + t, placed, ready, minav, gang, 0, 1, pb_n, pb_base, 0, 0};
+      goto done;
     }
     const int64_t score = (int64_t)((best >> 24) & ((1ull << 39) - 1)) - kScoreBias;
     if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
       if (lane == 0 && pw >= 0) store_row(N, pw, pr);
-      flush_placements(pb, pb_n, pb_base, hout, lane);
-      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_DONE, t_begin + t, placed, ready, minav, gang, 1);
-      return;
+      if (lane == 0) lo = LoopOut{KB_STOP_DONE, t_begin + t, placed, ready, minav, gang, 1, 1, pb_n, pb_base, 0, 0};
+      goto done;
     }
     const int w = (int)(kIdxMask - (uint32_t)(best & kIdxMask));
 
@@ -516,25 +526,37 @@ __global__ __launch_bounds__(64) void place_loop_kernel(DevNodes N, DevSpecs P, 
     if (kind == KB_PLACE_ALLOCATE) ++ready;
     if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
       if (lane == 0 && pw >= 0) store_row(N, pw, pr);
-      flush_placements(pb, pb_n, pb_base, hout, lane);
 #ifdef KB_DIAG
       if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
-      if (lane == 0) publish_state(js, hjs, 1, KB_STOP_READY, -1, placed, ready, minav, gang, 0);
-      return;
+      if (lane == 0) lo = LoopOut{KB_STOP_READY, -1, placed, ready, minav, gang, 0, 1, pb_n, pb_base, 0, 0};
+      goto done;
     }
     if (pb_n == pb_cap) {
-      flush_placements(pb, pb_n, pb_base, hout, lane);
+      for (int k = lane; k < pb_n; k += 64) {
+        const uint64_t e = pb[k];
+        hout[2 * (pb_base + k)] = (int32_t)(uint32_t)e;
+        hout[2 * (pb_base + k) + 1] = (int32_t)(uint32_t)(e >> 32);
+      }
       pb_base += pb_n;
       pb_n = 0;
     }
   }
   if (lane == 0 && pw >= 0) store_row(N, pw, pr);
-  flush_placements(pb, pb_n, pb_base, hout, lane);
 #ifdef KB_DIAG
   if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
-  if (lane == 0) publish_state(js, hjs, 0, KB_STOP_DONE, -1, placed, ready, minav, gang, 0);
+  if (lane == 0) lo = LoopOut{KB_STOP_DONE, -1, placed, ready, minav, gang, 0, 0, pb_n, pb_base, 0, 0};
+  }
+done:
+  __syncthreads();
+  for (int k = tid; k < lo.pb_n; k += 512) {
+    const uint64_t v = pb[k];
+    hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
+    hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
+  }
+  if (tid == 0)
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic);
 }
 
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
@@ -724,15 +746,18 @@ __device__ void write_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
     }
 }
 
-__global__ __launch_bounds__(64) void traj_place_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin,
-                                                        int t_count, int J, int idx_bits, const uint32_t* traj,
-                                                        const uint32_t* cmax32, const uint32_t* amax,
-                                                        const uint64_t* stat, JobState* js, int first, int ready0,
-                                                        int minav0, int gang0, int32_t* hout, JobState* hjs,
-                                                        int pb_cap) {
+
+constexpr int kPlaceThreads = 512;
+
+__global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int J, int idx_bits, const uint32_t* traj,
+    const uint32_t* cmax32, const uint32_t* amax, const uint64_t* stat, JobState* js, int first, int ready0,
+    int minav0, int gang0, int32_t* hout, JobState* hjs, int pb_cap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ LoopOut lo;
   if (!first && js->stopped) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int n = N.n;
   const int M = (n + 63) >> 6;
   const int W = (n + 63) >> 6;           // touched-bitmap words
@@ -742,129 +767,132 @@ __global__ __launch_bounds__(64) void traj_place_kernel(DevNodes N, DevSpecs P, 
   uint32_t* cnt = nxt + n;                // [n] commits so far | A << 16
   uint32_t* cm = cnt + n;                 // [M] chunk maxima of cur
   uint32_t* pb = cm + ((M + 3) & ~3);     // [pb_cap] placements: node | kind << 30
-  for (int i = lane; i < W; i += 64) tb[i] = 0;
-  for (int i = lane; i < n; i += 64) {
+  // fill LDS with every thread of the block (independent loads in flight)
+  for (int i = tid; i < W; i += kPlaceThreads) tb[i] = 0;
+#pragma unroll 4
+  for (int i = tid; i < n; i += kPlaceThreads) {
     cur[i] = traj[i];
     nxt[i] = J >= 1 ? traj[(size_t)n + i] : kKey32Exhausted;
     cnt[i] = amax[i] << 16;
   }
-  for (int c = lane; c < M; c += 64) cm[c] = cmax32[c];
+  for (int c = tid; c < M; c += kPlaceThreads) cm[c] = cmax32[c];
   __syncthreads();
-  uint32_t lmax = 0;
-  for (int c = lane; c < M; c += 64) lmax = umax32(lmax, cm[c]);
 
   const kb_spec sp = P.specs[spec];
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
-  const uint32_t idx_mask = (1u << idx_bits) - 1;
-  const int64_t bias32 = 1ll << (30 - idx_bits);
-  int ready, minav, gang, placed;
-  if (first) {
-    ready = ready0;
-    minav = minav0;
-    gang = gang0;
-    placed = 0;
-  } else {
-    ready = js->ready_num;
-    minav = js->min_available;
-    gang = js->gang_ready;
-    placed = js->n_placed;
-  }
-  int pb_n = 0, pb_base = t_begin;
-  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  if (tid < 64) {  // wave 0 runs the sequential placement loop; LDS ops of one wave retire in order
+    uint32_t lmax = 0;
+    for (int c = lane; c < M; c += 64) lmax = umax32(lmax, cm[c]);
+    const uint32_t idx_mask = (1u << idx_bits) - 1;
+    const int64_t bias32 = 1ll << (30 - idx_bits);
+    int ready, minav, gang, placed;
+    if (first) {
+      ready = ready0;
+      minav = minav0;
+      gang = gang0;
+      placed = 0;
+    } else {
+      ready = js->ready_num;
+      minav = js->min_available;
+      gang = js->gang_ready;
+      placed = js->n_placed;
+    }
+    int pb_n = 0, pb_base = t_begin;
+    int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
 
-  for (int t = 0; t < t_count; ++t) {
-    const uint32_t best = wave_max32_dpp(lmax);
-    if (!(best & kKey32Feasible)) {
-      // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
-      uint32_t h[KB_NUM_REASONS];
+    for (int t = 0; t < t_count; ++t) {
+      const uint32_t best = wave_max32_dpp(lmax);
+      if (!(best & kKey32Feasible)) {
+        // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
+        uint32_t h[KB_NUM_REASONS];
 #pragma unroll
-      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
-      for (int i = lane; i < n; i += 64) {
-        const uint32_t k = cur[i];
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+        for (int i = lane; i < n; i += 64) {
+          const uint32_t k = cur[i];
 #pragma unroll
-        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k >> b) & 1u;
-      }
-#pragma unroll
-      for (int b = 0; b < KB_NUM_REASONS; ++b) {
-        const uint32_t s = wave_sum_u32(h[b]);
-        if (lane == 0) {
-          js->hist[b] = s;
-          hjs->hist[b] = s;
+          for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k >> b) & 1u;
         }
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) {
+          const uint32_t s = wave_sum_u32(h[b]);
+          if (lane == 0) {
+            js->hist[b] = s;
+            hjs->hist[b] = s;
+          }
+        }
+        stop = KB_STOP_NO_FIT;
+        fail_task = t_begin + t;
+        stopped = 1;
+        break;
       }
-      stop = KB_STOP_NO_FIT;
-      fail_task = t_begin + t;
-      stopped = 1;
-      break;
-    }
-    const int64_t score = (int64_t)((best >> idx_bits) & ((1u << (31 - idx_bits)) - 1)) - bias32;
-    if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
-      fail_task = t_begin + t;
-      panic = 1;
-      stopped = 1;
-      break;
-    }
-    const int w = (int)(idx_mask - (best & idx_mask));
-
-    uint32_t nk = 0;
-    int kind = 0;
-    uint32_t pf = kKey32Exhausted;
-    if (lane == 0) {
-      const uint32_t s = cnt[w];
-      const int c = (int)(s & 0xffff), A = (int)(s >> 16);
-      kind = c < A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;  // commit c+1 Allocates iff c+1 <= A
-      nk = nxt[w];
-      if (nk == kKey32Exhausted) {  // beyond the precomputed trajectory: compute in place
-        const Row r0 = load_row(N, w);
-        nk = compress_key(traj_key64(N, P, C, sp, sci, scr, r0, stat[w], w, c + 1, A), w, idx_bits);
+      const int64_t score = (int64_t)((best >> idx_bits) & ((1u << (31 - idx_bits)) - 1)) - bias32;
+      if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
+        fail_task = t_begin + t;
+        panic = 1;
+        stopped = 1;
+        break;
       }
-      cur[w] = nk;
-      cnt[w] = (uint32_t)(c + 1) | ((uint32_t)A << 16);
-      if (c == 0) tb[w >> 6] |= 1ull << (w & 63);
-      if (c + 2 <= J) pf = traj[(size_t)(c + 2) * n + w];  // key after c+2 commits (prefetch)
-      pb[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
-    }
-    nk = (uint32_t)__builtin_amdgcn_readlane(nk, 0);
-    kind = __builtin_amdgcn_readlane(kind, 0);
+      const int w = (int)(idx_mask - (best & idx_mask));
 
-    // Re-reduce the winner's chunk; its owner lane refreshes its running max.
-    const int ch = w >> 6;
-    const int i = (ch << 6) + lane;
-    uint32_t v = 0;
-    if (i < n) v = (i == w) ? nk : cur[i];
-    v = wave_max32_dpp(v);
-    if (lane == (ch & 63)) {
-      cm[ch] = v;
-      uint32_t mx = 0;
-      for (int cc = lane; cc < M; cc += 64) mx = umax32(mx, cm[cc]);
-      lmax = mx;
-    }
-    if (lane == 0) nxt[w] = pf;
-
-    ++placed;
-    ++pb_n;
-    if (kind == KB_PLACE_ALLOCATE) ++ready;
-    if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
-      stop = KB_STOP_READY;
-      stopped = 1;
-      break;
-    }
-    if (pb_n == pb_cap) {
-      __syncthreads();
-      for (int k = lane; k < pb_n; k += 64) {
-        const uint32_t e = pb[k];
-        hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-        hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+      uint32_t nk = 0;
+      int kind = 0;
+      uint32_t pf = kKey32Exhausted;
+      if (lane == 0) {
+        const uint32_t s = cnt[w];
+        const int c = (int)(s & 0xffff), A = (int)(s >> 16);
+        kind = c < A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;  // commit c+1 Allocates iff c+1 <= A
+        nk = nxt[w];
+        if (nk == kKey32Exhausted) {  // beyond the precomputed trajectory: compute in place
+          const Row r0 = load_row(N, w);
+          nk = compress_key(traj_key64(N, P, C, sp, sci, scr, r0, stat[w], w, c + 1, A), w, idx_bits);
+        }
+        cur[w] = nk;
+        cnt[w] = (uint32_t)(c + 1) | ((uint32_t)A << 16);
+        if (c == 0) tb[w >> 6] |= 1ull << (w & 63);
+        if (c + 2 <= J) pf = traj[(size_t)(c + 2) * n + w];  // key after c+2 commits (prefetch)
+        pb[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
       }
-      pb_base += pb_n;
-      pb_n = 0;
-      __syncthreads();
+      nk = (uint32_t)__builtin_amdgcn_readlane(nk, 0);
+      kind = __builtin_amdgcn_readlane(kind, 0);
+
+      // Re-reduce the winner's chunk; its owner lane refreshes its running max.
+      const int ch = w >> 6;
+      const int i = (ch << 6) + lane;
+      uint32_t v = 0;
+      if (i < n) v = (i == w) ? nk : cur[i];
+      v = wave_max32_dpp(v);
+      if (lane == (ch & 63)) {
+        cm[ch] = v;
+        uint32_t mx = 0;
+        for (int cc = lane; cc < M; cc += 64) mx = umax32(mx, cm[cc]);
+        lmax = mx;
+      }
+      if (lane == 0) nxt[w] = pf;
+
+      ++placed;
+      ++pb_n;
+      if (kind == KB_PLACE_ALLOCATE) ++ready;
+      if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+        stop = KB_STOP_READY;
+        stopped = 1;
+        break;
+      }
+      if (pb_n == pb_cap) {  // buffer full: hand the placements to the host and keep going
+        for (int k = lane; k < pb_n; k += 64) {
+          const uint32_t e = pb[k];
+          hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+          hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+        }
+        pb_base += pb_n;
+        pb_n = 0;
+      }
     }
+    if (lane == 0) lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, pb_n, pb_base, 0, 0};
   }
   __syncthreads();
-  // write the run's commits back to the node table (one pass over the touched nodes)
-  for (int wd = lane; wd < W; wd += 64) {
+  // write the run's commits back to the node table (one pass over the touched nodes, all threads)
+  for (int wd = tid; wd < W; wd += kPlaceThreads) {
     uint64_t bits = tb[wd];
     while (bits) {
       const int b = __builtin_ctzll(bits);
@@ -874,12 +902,13 @@ __global__ __launch_bounds__(64) void traj_place_kernel(DevNodes N, DevSpecs P, 
       write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
     }
   }
-  for (int k = lane; k < pb_n; k += 64) {
+  for (int k = tid; k < lo.pb_n; k += kPlaceThreads) {
     const uint32_t e = pb[k];
-    hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-    hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+    hout[2 * (lo.pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+    hout[2 * (lo.pb_base + k) + 1] = (int32_t)(e >> 30);
   }
-  if (lane == 0) publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic);
+  if (tid == 0)
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic);
 }
 
 // ---------------------------------------------------------------------------
@@ -887,7 +916,7 @@ __global__ __launch_bounds__(64) void traj_place_kernel(DevNodes N, DevSpecs P, 
 static void place_loop_lds_plan(int n, int t_count, int* bytes, int* pb_cap, bool* keys_in_lds) {
   const int M = (n + 63) >> 6;
   const int Mp = (M + 1) & ~1;
-  const int limit = 160 * 1024 / 8;  // in u64 words
+  const int limit = kLdsLimit / 8;  // in u64 words
   int pb = t_count < 4096 ? t_count : 4096;
   pb = (pb + 1) & ~1;
   if (Mp + pb + n <= limit) {
@@ -930,10 +959,10 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
     attr_set = true;
   }
   if (keys_in_lds)
-    hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
+    hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
                        t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
   else
-    hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec,
+    hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec,
                        t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
 }
 
@@ -941,7 +970,7 @@ int traj_lds_bytes(int n, int t_count, int* pb_cap) {
   const int M = (n + 63) >> 6;
   const int W = (n + 63) >> 6;
   const int fixed = 8 * W + 12 * n + 4 * ((M + 3) & ~3);
-  const int limit = 160 * 1024;
+  const int limit = kLdsLimit;
   int pb = t_count;
   if (fixed + 4 * pb > limit) pb = (limit - fixed) / 4;
   if (pb < 64) return -1;
@@ -969,7 +998,8 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
   }
   int pb_cap = 0;
   const int lds = traj_lds_bytes(N.n, t_count, &pb_cap);
-  hipLaunchKernelGGL(traj_place_kernel, dim3(1), dim3(64), lds, (hipStream_t)stream, N, P, C, spec, t_begin, t_count,
+  hipLaunchKernelGGL(traj_place_kernel, dim3(1), dim3(kPlaceThreads), lds, (hipStream_t)stream, N, P, C, spec,
+                     t_begin, t_count,
                      J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
 }
 

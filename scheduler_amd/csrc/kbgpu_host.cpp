@@ -348,7 +348,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     const int run = (int)(e - t);
     const bool traj = c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
     if (traj) {
-      const int J = std::min(run, kTrajMaxJ);
+      const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
       launch_traj_sweep(c->N, c->P, c->cfg, spec, J, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
                         first ? nullptr : js, c->stream);
