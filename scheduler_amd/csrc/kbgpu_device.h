@@ -73,6 +73,8 @@ int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;
 constexpr int kTrajDefaultJ = 16;  // trajectory depth per run; deeper commits are computed in place
+// Opt the place kernels into the dynamic LDS they need; returns 0 or the hipError_t.
+int configure_kernels();
 int traj_lds_bytes(int n, int t_count, int* pb_cap);
 void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
                        uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,

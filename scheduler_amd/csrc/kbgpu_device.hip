@@ -950,20 +950,23 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
   int lds, pb_cap;
   bool keys_in_lds;
   place_loop_lds_plan(N.n, t_count, &lds, &pb_cap, &keys_in_lds);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)place_loop_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)place_loop_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set = true;
-  }
   if (keys_in_lds)
     hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
                        t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
   else
     hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec,
                        t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+}
+
+int configure_kernels() {
+  // dynamic LDS opt-in for the single-workgroup place kernels; kLdsLimit leaves room for their static block
+  const void* fns[] = {(const void*)place_loop_kernel<true>, (const void*)place_loop_kernel<false>,
+                       (const void*)traj_place_kernel};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 
 int traj_lds_bytes(int n, int t_count, int* pb_cap) {
@@ -990,12 +993,6 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
                        const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
                        int32_t* hout, JobState* hjs, void* stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)traj_place_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set = true;
-  }
   int pb_cap = 0;
   const int lds = traj_lds_bytes(N.n, t_count, &pb_cap);
   hipLaunchKernelGGL(traj_place_kernel, dim3(1), dim3(kPlaceThreads), lds, (hipStream_t)stream, N, P, C, spec,

@@ -112,6 +112,11 @@ kb_ctx* kb_create(const kb_opts* opts) {
     c->broken = true;
     return c;
   }
+  if (int e = kbgpu::configure_kernels()) {
+    c->err = std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString((hipError_t)e);
+    c->broken = true;
+    return c;
+  }
   c->cfg = DevCfg{1, 1, 0, 0, 0, 1, 1, 1, 1};
   return c;
 }
