@@ -103,11 +103,16 @@ def main():
     bytes_per_launch = st["pairs"][k] * ROW_BYTES / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": "hbm", "kernel": runtime.KERNELS[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None, "traffic_source": None,
                 "avg_launch_us": round(avg_ms * 1e3, 3), "launches_per_step": round(launches / args.steps, 1),
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
                 "kernel_ms_per_step": {runtime.KERNELS[i]: round(st["kernel_ms"][i] / args.steps, 3)
-                                       for i in range(3)}}
+                                       for i in range(len(runtime.KERNELS))}}
+
+    tr = pmc_traffic(runtime.KERNELS[k])
+    if tr is not None:
+        roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
 
     result = None
     if rank == 0:
@@ -135,6 +140,21 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md HBM section), or None when no summary for it is committed."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*prof_summary.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                e = json.load(fh)["kernels"].get(kernel, {})
+        except (OSError, ValueError, KeyError):
+            continue
+        if "hbm_bytes_per_launch" in e:
+            return {"bytes_per_launch": e["hbm_bytes_per_launch"], "source": os.path.relpath(f, ROOT)}
+    return None
 
 
 def diag_summary(d, tasks):

@@ -277,7 +277,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
-#define KB_NUM_KERNELS 3
+#define KB_KERNEL_TRAJ_SWEEP 3
+#define KB_KERNEL_TRAJ_PLACE 4
+#define KB_NUM_KERNELS 5
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */

@@ -357,12 +357,12 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_begin(&ea);
       launch_traj_sweep(c->N, c->P, c->cfg, spec, J, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
                         first ? nullptr : js, c->stream);
-      c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
+      c->ev_end(ea, KB_KERNEL_TRAJ_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_traj_place(c->N, c->P, c->cfg, spec, (int)t, run, J, c->idx_bits, c->traj, c->cmax32, c->amax,
                         c->stat, js, first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev,
                         c->stream);
-      c->ev_end(ea, KB_KERNEL_PLACE, 0);
+      c->ev_end(ea, KB_KERNEL_TRAJ_PLACE, 0);
     } else {
       c->ev_begin(&ea);
       launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, c->stream);
@@ -386,7 +386,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the batch's launches
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
     for (auto& p : c->pending)
-      if (p.kind == KB_KERNEL_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
+      if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
     c->ev_collect();
   }
   const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));

@@ -74,13 +74,13 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 3), ("kernel_ms", C.c_double * 3), ("pairs", C.c_uint64 * 3),
+    _fields_ = [("launches", C.c_uint64 * 5), ("kernel_ms", C.c_double * 5), ("pairs", C.c_uint64 * 5),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
 KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
-KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel")
+KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel")
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
