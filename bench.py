@@ -159,9 +159,10 @@ def pmc_traffic(kernel):
 
 def diag_summary(d, tasks):
     """Per-task shader cycles of each place-loop phase (KB_DIAG builds) and the implied clock."""
-    names = ["argmax", "row_load", "commit", "rescan", "lmax", "loop"]
+    names = ["argmax", "commit", "rereduce", "lmax", "prefetch_store", "loop", "fill"]  # traj_place_kernel
     clock_mhz = d[7] and (sum(d[:7]) / (d[7] / 100.0))
     return {"cycles_per_task": {n: round(d[i] / max(1, tasks), 1) for i, n in enumerate(names)},
+            "fill_cycles_total": d[6],
             "clock_mhz": round(clock_mhz, 1) if clock_mhz else None}
 
 

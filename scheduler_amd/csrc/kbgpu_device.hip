@@ -748,7 +748,12 @@ __device__ void write_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 
 
 constexpr int kPlaceThreads = 512;
+static_assert(kTrajDefaultJ <= kTrajMaxJ, "trajectory buffer depth");
 
+// The sequential loop keeps the LDS reads of one task independent of each other (issued together) and
+// the chunk maxima in registers (lane l owns chunks l, l+64, l+128, l+192). A node's first commit in the
+// run takes its key from nxt[] in LDS; a repeat commit (about 1 in 7 on C2) reads its trajectory level
+// from global memory.
 __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int J, int idx_bits, const uint32_t* traj,
     const uint32_t* cmax32, const uint32_t* amax, const uint64_t* stat, JobState* js, int first, int ready0,
@@ -756,34 +761,57 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ LoopOut lo;
   if (!first && js->stopped) return;
+#ifdef KB_DIAG
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int n = N.n;
-  const int M = (n + 63) >> 6;
-  const int W = (n + 63) >> 6;           // touched-bitmap words
+  const int M = (n + 63) >> 6;            // <= 256 (checked by traj_lds_bytes)
+  const int W = (n + 63) >> 6;            // touched-bitmap words
   uint64_t* tb = (uint64_t*)lds32;        // [W] nodes committed to in this run
   uint32_t* cur = lds32 + 2 * W;          // [n] key after the commits so far
-  uint32_t* nxt = cur + n;                // [n] key after one more commit (or kKey32Exhausted)
-  uint32_t* cnt = nxt + n;                // [n] commits so far | A << 16
-  uint32_t* cm = cnt + n;                 // [M] chunk maxima of cur
-  uint32_t* pb = cm + ((M + 3) & ~3);     // [pb_cap] placements: node | kind << 30
+  // [n] {key after the node's first commit of the run, commits so far | A << 16}: one 8-B read per task
+  uint2* nc = (uint2*)(cur + ((n + 1) & ~1));
+  uint32_t* pb = (uint32_t*)(nc + n);     // [pb_cap] placements: node | kind << 30
   // fill LDS with every thread of the block (independent loads in flight)
   for (int i = tid; i < W; i += kPlaceThreads) tb[i] = 0;
-#pragma unroll 4
-  for (int i = tid; i < n; i += kPlaceThreads) {
-    cur[i] = traj[i];
-    nxt[i] = J >= 1 ? traj[(size_t)n + i] : kKey32Exhausted;
-    cnt[i] = amax[i] << 16;
+  {
+    // batches of 8 nodes per thread: all 24 loads are issued before the first LDS store
+    constexpr int kB = 8;
+    const uint32_t* t1 = J >= 1 ? traj + n : traj;
+    for (int base = 0; base < n; base += kB * kPlaceThreads) {
+      uint32_t a[kB], b[kB], m[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int i = base + u * kPlaceThreads + tid;
+        const int ic = i < n ? i : n - 1;  // clamped: unconditional loads keep them all in flight
+        a[u] = traj[ic];
+        b[u] = t1[ic];
+        m[u] = amax[ic];
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int i = base + u * kPlaceThreads + tid;
+        if (i < n) {
+          cur[i] = a[u];
+          nc[i] = make_uint2(J >= 1 ? b[u] : kKey32Exhausted, m[u] << 16);
+        }
+      }
+    }
   }
-  for (int c = tid; c < M; c += kPlaceThreads) cm[c] = cmax32[c];
   __syncthreads();
 
   const kb_spec sp = P.specs[spec];
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
   if (tid < 64) {  // wave 0 runs the sequential placement loop; LDS ops of one wave retire in order
-    uint32_t lmax = 0;
-    for (int c = lane; c < M; c += 64) lmax = umax32(lmax, cm[c]);
+    uint32_t cm0 = lane < M ? cmax32[lane] : 0u;
+    uint32_t cm1 = lane + 64 < M ? cmax32[lane + 64] : 0u;
+    uint32_t cm2 = lane + 128 < M ? cmax32[lane + 128] : 0u;
+    uint32_t cm3 = lane + 192 < M ? cmax32[lane + 192] : 0u;
+    uint32_t lmax = umax32(umax32(cm0, cm1), umax32(cm2, cm3));
     const uint32_t idx_mask = (1u << idx_bits) - 1;
     const int64_t bias32 = 1ll << (30 - idx_bits);
     int ready, minav, gang, placed;
@@ -800,9 +828,17 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
     }
     int pb_n = 0, pb_base = t_begin;
     int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+#ifdef KB_DIAG
+    // phases: 0 argmax, 1 commit, 2 chunk re-reduce, 3 chunk-max update, 4 unused, 5 loop, 6 fill
+    uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t dg_last = __builtin_amdgcn_s_memtime();
+    dg[6] = dg_last - t_start;
+#endif
 
     for (int t = 0; t < t_count; ++t) {
+      KB_STAMP(5);
       const uint32_t best = wave_max32_dpp(lmax);
+      KB_STAMP(0);
       if (!(best & kKey32Feasible)) {
         // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
         uint32_t h[KB_NUM_REASONS];
@@ -834,41 +870,45 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
         break;
       }
       const int w = (int)(idx_mask - (best & idx_mask));
-
-      uint32_t nk = 0;
-      int kind = 0;
-      uint32_t pf = kKey32Exhausted;
-      if (lane == 0) {
-        const uint32_t s = cnt[w];
-        const int c = (int)(s & 0xffff), A = (int)(s >> 16);
-        kind = c < A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;  // commit c+1 Allocates iff c+1 <= A
-        nk = nxt[w];
-        if (nk == kKey32Exhausted) {  // beyond the precomputed trajectory: compute in place
-          const Row r0 = load_row(N, w);
-          nk = compress_key(traj_key64(N, P, C, sp, sci, scr, r0, stat[w], w, c + 1, A), w, idx_bits);
-        }
-        cur[w] = nk;
-        cnt[w] = (uint32_t)(c + 1) | ((uint32_t)A << 16);
-        if (c == 0) tb[w >> 6] |= 1ull << (w & 63);
-        if (c + 2 <= J) pf = traj[(size_t)(c + 2) * n + w];  // key after c+2 commits (prefetch)
-        pb[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
-      }
-      nk = (uint32_t)__builtin_amdgcn_readlane(nk, 0);
-      kind = __builtin_amdgcn_readlane(kind, 0);
-
-      // Re-reduce the winner's chunk; its owner lane refreshes its running max.
       const int ch = w >> 6;
       const int i = (ch << 6) + lane;
-      uint32_t v = 0;
-      if (i < n) v = (i == w) ? nk : cur[i];
-      v = wave_max32_dpp(v);
-      if (lane == (ch & 63)) {
-        cm[ch] = v;
-        uint32_t mx = 0;
-        for (int cc = lane; cc < M; cc += 64) mx = umax32(mx, cm[cc]);
-        lmax = mx;
+      // the three LDS reads of this task, issued together (uniform addresses broadcast)
+      const uint32_t cv = i < n ? cur[i] : 0u;
+      const uint2 ncw = nc[w];
+      const uint32_t s = ncw.y, nx = ncw.x;
+      const int c = (int)(s & 0xffff), A = (int)(s >> 16);
+      const int kind = c < A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;  // commit c+1 Allocates iff c+1 <= A
+
+      // key after c+1 commits: level 1 is in LDS, deeper levels in the trajectory buffer
+      uint32_t nk = nx;
+      if (c >= 1) nk = c + 1 <= J ? traj[(size_t)(c + 1) * n + w] : kKey32Exhausted;
+      if (nk == kKey32Exhausted) {  // beyond the precomputed trajectory: compute in place (rare)
+        uint32_t k = 0;
+        if (lane == 0) {
+          const Row r0 = load_row(N, w);
+          k = compress_key(traj_key64(N, P, C, sp, sci, scr, r0, stat[w], w, c + 1, A), w, idx_bits);
+        }
+        nk = (uint32_t)__builtin_amdgcn_readlane((int)k, 0);
       }
-      if (lane == 0) nxt[w] = pf;
+      KB_STAMP(1);
+      if (lane == 0) {  // fire-and-forget LDS updates
+        cur[w] = nk;
+        nc[w].y = (uint32_t)(c + 1) | ((uint32_t)A << 16);
+        if (c == 0) atomicOr((unsigned long long*)&tb[w >> 6], 1ull << (w & 63));
+        pb[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
+      }
+
+      // Re-reduce the winner's chunk; its owner lane refreshes its running max (registers only).
+      const uint32_t v = wave_max32_dpp(i == w ? nk : cv);
+      KB_STAMP(2);
+      const bool own = lane == (ch & 63);
+      const int jj = ch >> 6;
+      cm0 = (own && jj == 0) ? v : cm0;
+      cm1 = (own && jj == 1) ? v : cm1;
+      cm2 = (own && jj == 2) ? v : cm2;
+      cm3 = (own && jj == 3) ? v : cm3;
+      lmax = umax32(umax32(cm0, cm1), umax32(cm2, cm3));
+      KB_STAMP(3);
 
       ++placed;
       ++pb_n;
@@ -888,19 +928,18 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
         pb_n = 0;
       }
     }
+#ifdef KB_DIAG
+    if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
     if (lane == 0) lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, pb_n, pb_base, 0, 0};
   }
   __syncthreads();
-  // write the run's commits back to the node table (one pass over the touched nodes, all threads)
-  for (int wd = tid; wd < W; wd += kPlaceThreads) {
-    uint64_t bits = tb[wd];
-    while (bits) {
-      const int b = __builtin_ctzll(bits);
-      bits &= bits - 1;
-      const int w = (wd << 6) + b;
-      const uint32_t s = cnt[w];
-      write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
-    }
+  // write the run's commits back to the node table: one node per thread (touched nodes cluster at low
+  // indices, so a per-bitmap-word walk would serialise their load->store chains on a few threads)
+  for (int w = tid; w < n; w += kPlaceThreads) {
+    if (!((tb[w >> 6] >> (w & 63)) & 1)) continue;
+    const uint32_t s = nc[w].y;
+    write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
   }
   for (int k = tid; k < lo.pb_n; k += kPlaceThreads) {
     const uint32_t e = pb[k];
@@ -971,8 +1010,9 @@ int configure_kernels() {
 
 int traj_lds_bytes(int n, int t_count, int* pb_cap) {
   const int M = (n + 63) >> 6;
+  if (M > 256) return -1;  // chunk maxima live in 4 registers per lane
   const int W = (n + 63) >> 6;
-  const int fixed = 8 * W + 12 * n + 4 * ((M + 3) & ~3);
+  const int fixed = 8 * W + 4 * ((n + 1) & ~1) + 8 * n;  // tb | cur | nc
   const int limit = kLdsLimit;
   int pb = t_count;
   if (fixed + 4 * pb > limit) pb = (limit - fixed) / 4;
