@@ -32,6 +32,7 @@ struct kb_ctx {
   std::vector<int64_t> spec_pref_weight;
   bool use_traj = true;
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
+  uint32_t seq = 0;           // place launches issued (JobState::seq)
   char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)
   char* h_job_dev = nullptr; // device address of h_job
   uint32_t job_cap = 0;
@@ -52,7 +53,8 @@ struct kb_ctx {
   hipEvent_t ev_get();
   void ev_begin(hipEvent_t* a);
   void ev_end(hipEvent_t a, int kind, uint64_t pairs);
-  void ev_collect();
+  void ev_collect(bool all);
+  size_t pending_job_begin = 0;  // first pending event pair of the current kb_place_job call
 };
 
 // internal helpers (defined inside kbgpu_host.cpp's extern "C" block, not part of the ABI)

@@ -59,6 +59,8 @@ struct JobState {
   int32_t panic;      // 1: SelectBestNode would panic (best score <= -1)
   uint32_t hist[KB_NUM_REASONS];
   uint64_t diag[8];   // -DKB_DIAG builds: per-phase shader cycles of the place loop, [7] = realtime ticks
+  uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
+  uint32_t pad;
 };
 
 // Launch wrappers (kbgpu_device.hip).
@@ -66,7 +68,7 @@ void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        uint64_t* cmax, uint64_t* stat, const JobState* js, void* stream);
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
-                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, void* stream);
+                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, void* stream);
 int place_loop_lds_bytes(int n);
@@ -82,6 +84,6 @@ void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
                        const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
-                       int32_t* hout, JobState* hjs, void* stream);
+                       int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 
 }  // namespace kbgpu

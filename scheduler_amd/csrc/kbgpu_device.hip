@@ -292,8 +292,10 @@ __device__ __forceinline__ void publish_diag(JobState* hjs, const uint64_t* dg, 
   hjs->diag[7] += rt;
 }
 
+// Thread 0, after a block barrier that follows every thread's host-buffer writes and system fence.
 __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int stopped, int stop, int fail_task,
-                                              int placed, int ready, int minav, int gang, int panic) {
+                                              int placed, int ready, int minav, int gang, int panic,
+                                              uint32_t seq) {
   js->stopped = stopped;
   js->stop = stop;
   js->fail_task = fail_task;
@@ -310,6 +312,13 @@ __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int s
   hjs->min_available = minav;
   hjs->gang_ready = gang;
   hjs->panic = panic;
+  __threadfence_system();
+  __hip_atomic_store(&hjs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host spins on this
+}
+
+// A launch that finds its batch already stopped still reports completion.
+__device__ __forceinline__ void signal_skip(JobState* hjs, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(&hjs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef KB_DIAG
@@ -351,10 +360,13 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
                                                         int t_count, uint64_t* keys, const uint64_t* cmax_g,
                                                         const uint64_t* stat, JobState* js, int first, int ready0,
                                                         int minav0, int gang0, int32_t* hout, JobState* hjs,
-                                                        int pb_cap) {
+                                                        int pb_cap, uint32_t seq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   __shared__ LoopOut lo;
-  if (!first && js->stopped) return;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int n = N.n;
@@ -555,8 +567,11 @@ done:
     hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
     hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
   }
+  __threadfence_system();
+  __syncthreads();
   if (tid == 0)
-    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic);
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic,
+                  seq);
 }
 
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
@@ -757,10 +772,13 @@ static_assert(kTrajDefaultJ <= kTrajMaxJ, "trajectory buffer depth");
 __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int J, int idx_bits, const uint32_t* traj,
     const uint32_t* cmax32, const uint32_t* amax, const uint64_t* stat, JobState* js, int first, int ready0,
-    int minav0, int gang0, int32_t* hout, JobState* hjs, int pb_cap) {
+    int minav0, int gang0, int32_t* hout, JobState* hjs, int pb_cap, uint32_t seq) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ LoopOut lo;
-  if (!first && js->stopped) return;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
 #ifdef KB_DIAG
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -946,8 +964,11 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
     hout[2 * (lo.pb_base + k)] = (int32_t)(e & 0x3fffffffu);
     hout[2 * (lo.pb_base + k) + 1] = (int32_t)(e >> 30);
   }
+  __threadfence_system();
+  __syncthreads();
   if (tid == 0)
-    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic);
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic,
+                  seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -985,16 +1006,17 @@ void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
-                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, void* stream) {
+                       int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq,
+                       void* stream) {
   int lds, pb_cap;
   bool keys_in_lds;
   place_loop_lds_plan(N.n, t_count, &lds, &pb_cap, &keys_in_lds);
   if (keys_in_lds)
     hipLaunchKernelGGL(place_loop_kernel<true>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec, t_begin,
-                       t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+                       t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
   else
     hipLaunchKernelGGL(place_loop_kernel<false>, dim3(1), dim3(512), lds, (hipStream_t)stream, N, P, C, spec,
-                       t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+                       t_begin, t_count, keys, cmax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
 int configure_kernels() {
@@ -1032,12 +1054,12 @@ void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
                        const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
-                       int32_t* hout, JobState* hjs, void* stream) {
+                       int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
   int pb_cap = 0;
   const int lds = traj_lds_bytes(N.n, t_count, &pb_cap);
   hipLaunchKernelGGL(traj_place_kernel, dim3(1), dim3(kPlaceThreads), lds, (hipStream_t)stream, N, P, C, spec,
                      t_begin, t_count,
-                     J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap);
+                     J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,

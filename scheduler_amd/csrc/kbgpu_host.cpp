@@ -78,9 +78,14 @@ void kb_ctx::ev_end(hipEvent_t a, int kind, uint64_t pairs) {
   (void)hipEventRecord(b, stream);
   pending.push_back({a, b, kind, pairs});
 }
-// Called after the stream is synchronised: fold finished event pairs into the stats.
-void kb_ctx::ev_collect() {
-  for (auto& p : pending) {
+// Fold finished event pairs into the stats, oldest first. `all`: wait for the stream first; otherwise
+// stop at the first pair still in flight (it is collected by a later call, off the job's critical path).
+void kb_ctx::ev_collect(bool all) {
+  if (all && !pending.empty()) (void)hipStreamSynchronize(stream);
+  size_t k = 0;
+  for (; k < pending.size(); ++k) {
+    Pending& p = pending[k];
+    if (!all && hipEventQuery(p.b) != hipSuccess) break;
     float ms = 0;
     if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       stats.kernel_ms[p.kind] += ms;
@@ -90,7 +95,7 @@ void kb_ctx::ev_collect() {
     ev_pool.push_back(p.a);
     ev_pool.push_back(p.b);
   }
-  pending.clear();
+  pending.erase(pending.begin(), pending.begin() + k);
 }
 
 extern "C" {
@@ -306,6 +311,29 @@ int kb_check_score_range(kb_ctx* c) {
   return KB_OK;
 }
 
+// Wait for the last place launch of a job: spin on the sequence number it writes to pinned host memory
+// (cheaper than a stream synchronisation's wake-up), checking the stream now and then so a failed launch
+// is reported instead of waited on. Kernel timing events are then complete or nearly so.
+static int wait_seq(kb_ctx* c) {
+  const JobState* hs = (const JobState*)c->h_job;
+  const uint32_t want = c->seq;
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 0;; ++spin) {
+    if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == want) break;
+    if ((spin & 4095) == 4095) {
+      hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == want) break;
+        return fail(c, KB_E_HIP, "place kernel finished without reporting (seq %u, want %u)", hs->seq, want);
+      }
+      if (q != hipErrorNotReady) return fail(c, KB_E_HIP, "place kernel failed: %s", hipGetErrorString(q));
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        return fail(c, KB_E_HIP, "place kernel did not finish within 120 s");
+    }
+  }
+  return KB_OK;
+}
+
 static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
   if (!c->d_job) {
     void* p;
@@ -319,8 +347,10 @@ static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
   if (c->h_job) (void)hipHostFree(c->h_job);
   c->h_job = nullptr;
   // pinned, device-mapped: the place kernel writes placements and the job state straight to host memory
-  HIP_OK(c, hipHostMalloc((void**)&c->h_job, bytes, hipHostMallocMapped));
+  HIP_OK(c, hipHostMalloc((void**)&c->h_job, bytes, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_OK(c, hipHostGetDevicePointer((void**)&c->h_job_dev, c->h_job, 0));
+  memset(c->h_job, 0, bytes);
+  ((JobState*)c->h_job)->seq = c->seq;
   c->job_cap = cap;
   return KB_OK;
 }
@@ -338,6 +368,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   int rc = ensure_job_buffers(c, job->n_tasks);
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
+  c->pending_job_begin = c->pending.size();
   JobState* js = (JobState*)c->d_job;
   JobState* hjs_dev = (JobState*)c->h_job_dev;
   memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
@@ -361,7 +392,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_begin(&ea);
       launch_traj_place(c->N, c->P, c->cfg, spec, (int)t, run, J, c->idx_bits, c->traj, c->cmax32, c->amax,
                         c->stat, js, first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev,
-                        c->stream);
+                        ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_TRAJ_PLACE, 0);
     } else {
       c->ev_begin(&ea);
@@ -369,13 +400,17 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->cmax, c->stat, js, first,
-                        job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, c->stream);
+                        job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq,
+                        c->stream);
       c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     }
     t = e;
   }
   HIP_OK(c, hipGetLastError());
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  {
+    int rc2 = wait_seq(c);
+    if (rc2) return rc2;
+  }
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   c->device_ms += wall;
   c->stats.device_ms += wall;
@@ -385,9 +420,11 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   if (c->timing) {
     // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the batch's launches
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
-    for (auto& p : c->pending)
+    for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
+      auto& p = c->pending[k];
       if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
-    c->ev_collect();
+    }
+    c->ev_collect(false);
   }
   const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
   result->n_placed = (uint32_t)hs->n_placed;
@@ -433,7 +470,7 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
       rc = KB_E_HIP;
     if (hipStreamSynchronize(c->stream) != hipSuccess) rc = KB_E_HIP;
   }
-  if (c->timing) c->ev_collect();
+  if (c->timing) c->ev_collect(true);
   (void)hipFree(d_ids);
   (void)hipFree(d_r);
   (void)hipFree(d_s);
@@ -451,6 +488,7 @@ int kb_restore_nodes(kb_ctx* c) {
 
 int kb_get_stats(kb_ctx* c, kb_stats* out, int reset) {
   if (!c || !out) return KB_E_INVALID;
+  if (c->timing && !c->broken) c->ev_collect(true);
   *out = c->stats;
   if (reset) c->stats = kb_stats{};
   return KB_OK;
