@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 1
+#define KBGPU_ABI_VERSION 2
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -202,8 +202,9 @@ typedef struct kb_config {
 } kb_config;
 
 typedef struct kb_opts {
-  int32_t device; /* HIP device ordinal */
+  int32_t device;        /* HIP device ordinal */
   uint32_t flags;
+  uint32_t timing_every; /* KB_OPT_TIMING: time the launches of every Nth kb_place_job call (0 or 1: all) */
 } kb_opts;
 
 typedef struct kb_ctx kb_ctx;

@@ -46,6 +46,8 @@ struct kb_ctx {
 
   // kernel timing (KB_OPT_TIMING)
   bool timing = false;
+  uint32_t timing_every = 1;  // sample the launches of every Nth kb_place_job call
+  bool timing_now = false;
   std::vector<hipEvent_t> ev_pool;
   struct Pending { hipEvent_t a, b; int kind; uint64_t pairs; };
   std::vector<Pending> pending;

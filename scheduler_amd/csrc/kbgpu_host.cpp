@@ -68,7 +68,7 @@ hipEvent_t kb_ctx::ev_get() {
 }
 void kb_ctx::ev_begin(hipEvent_t* a) {
   *a = nullptr;
-  if (!timing) return;
+  if (!timing_now) return;
   *a = ev_get();
   (void)hipEventRecord(*a, stream);
 }
@@ -106,6 +106,8 @@ kb_ctx* kb_create(const kb_opts* opts) {
   kb_ctx* c = new kb_ctx();
   c->device = opts ? opts->device : 0;
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
+  c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
+  c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   if (hipSetDevice(c->device) != hipSuccess) {
     c->err = "hipSetDevice failed";
@@ -369,6 +371,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
   c->pending_job_begin = c->pending.size();
+  c->timing_now = c->timing && (c->stats.job_calls % c->timing_every == 0);
   JobState* js = (JobState*)c->d_job;
   JobState* hjs_dev = (JobState*)c->h_job_dev;
   memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
@@ -441,6 +444,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
 }
 
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
+  if (c) c->timing_now = c->timing;
   if (!c || (!spec_ids && t)) return KB_E_INVALID;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
   for (uint32_t i = 0; i < t; ++i)

@@ -44,7 +44,7 @@ class kb_config(C.Structure):
 
 
 class kb_opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32)]
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("timing_every", C.c_uint32)]
 
 
 class kb_job_req(C.Structure):
@@ -82,6 +82,8 @@ KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel")
 
+ABI_VERSION = 2  # include/kbgpu.h KBGPU_ABI_VERSION
+
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
            "kb_get_stats"]
@@ -104,6 +106,8 @@ def load_library(path: str = LIB_PATH):
         raise RuntimeError(f"{path} missing: run `make -C scheduler_amd/csrc` (or __graft_entry__.build())")
     lib = C.CDLL(path)
     lib.kb_abi_version.restype = C.c_int
+    if lib.kb_abi_version() != ABI_VERSION:
+        raise KbError(KB_E_INVALID, f"libkbgpu ABI {lib.kb_abi_version()} != binding ABI {ABI_VERSION}")
     lib.kb_create.restype = P
     lib.kb_create.argtypes = [C.POINTER(kb_opts)]
     lib.kb_destroy.argtypes = [P]
@@ -129,10 +133,11 @@ def _ptr(a):
 class Context:
     """One device-resident session snapshot (kb_ctx)."""
 
-    def __init__(self, device: int = 0, timing: bool = False, trajectory: bool = True):
+    def __init__(self, device: int = 0, timing: bool = False, trajectory: bool = True, timing_every: int = 1):
         self.lib = load_library()
         self._keep = []
-        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | (0 if trajectory else KB_OPT_NO_TRAJECTORY))
+        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | (0 if trajectory else KB_OPT_NO_TRAJECTORY),
+                       timing_every)
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
             raise KbError(KB_E_HIP, "kb_create failed")
