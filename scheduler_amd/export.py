@@ -252,6 +252,10 @@ class Snapshot:
         self._config()
         self._specs()
         self._node_table()
+        self.aff = None
+        if self.aff_in_play:
+            from .affinity import Tables
+            self.aff = Tables(self, Unsupported).build()
         self._session_arrays()
 
     # ---------------- cache.Snapshot + session open ----------------
@@ -319,9 +323,9 @@ class Snapshot:
                     nz_c += a
                     nz_m += b
             n["nz"] = (nz_c, nz_m)
-        for t in self.tasks:
-            if has_pod_affinity(t["pod"]) and (t["pod"].node in self.node_index or "sidx" in t):
-                raise Unsupported("pod (anti)affinity: device affinity tables are not built yet")
+        # pod (anti)affinity anywhere the predicate or the score can see it: build the affinity tables
+        self.aff_in_play = any(has_pod_affinity(t["pod"]) for t in self.session_tasks) or \
+            any(has_pod_affinity(t["pod"]) for nd in self.nodes for t in nd["tasks"])
 
     # ---------------- plugin configuration ----------------
     def _config(self):
@@ -450,6 +454,9 @@ class Snapshot:
                    rr.cpu, rr.mem, tuple(sorted((rr.sc or {}).items())) if rr.sc is not None else None,
                    nzc, nzm, tuple(sorted(p.node_selector.items())), repr(nodeaff), tols, tuple(port_list),
                    best_effort)
+            if self.aff_in_play:  # selectors and terms see the pod's namespace, labels and own terms
+                sig = sig + (p.ns, tuple(sorted(p.labels.items())), repr(aff.get("podAffinity")),
+                             repr(aff.get("podAntiAffinity")))
             if sig in sig_index:
                 t["spec"] = sig_index[sig]
                 continue
@@ -460,6 +467,8 @@ class Snapshot:
                 flags |= SPEC_REQ_HAS_MAP
             if best_effort:
                 flags |= SPEC_BEST_EFFORT
+            if self.aff_in_play:
+                flags |= SPEC_POD_AFFINITY
             imask = sum(1 << slot[k] for k in (ir.sc or {}))
             rmask = sum(1 << slot[k] for k in (rr.sc or {}))
             si = [0] * len(self.scalars)
@@ -539,7 +548,7 @@ class Snapshot:
                 ports.append((s_id, ipi(ip)))
             specs.append((ir.cpu, ir.mem, rr.cpu, rr.mem, nzc, nzm, imask, rmask, flags, tol_id,
                           len(sc_init) * len(self.scalars), sel_term, req_off, req_cnt, pref_off, len(pref_rows),
-                          port_off, len(ports) - port_off, -1, 0))
+                          port_off, len(ports) - port_off, len(specs) if self.aff_in_play else -1, 0))
             sc_init.extend(si)
             sc_req.extend(sr)
             sig_index[sig] = len(specs) - 1

@@ -3,8 +3,8 @@
 C1  1k nodes x 5k pods: 100 gang jobs x 50, gang+drf+predicates+nodeorder (the reference's CPU path)
 C2  10k homogeneous nodes x 100k pods: 1k gang jobs x 100, resource fit + LeastRequested/Balanced
 C3  20k heterogeneous nodes x 200k pods: GPU scalars, taints/tolerations, node selector/affinity
+C4  10k nodes x 100k pods with inter-pod (anti)affinity over hostname / zone / rack domains
 C5  50k nodes x 1M pods: the C2 shape scaled (the 8-GPU configuration)
-(C4, inter-pod affinity, is generated by `c4` once the device affinity tables land.)
 
 Every generator takes explicit sizes so tests can run "parity variants" (<= 1k x 5k) of the
 same shapes. There is no network: all data is synthetic.
@@ -116,4 +116,70 @@ def c3(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_r
     return cl
 
 
-CONFIGS = {"C1": c1, "C2": c2, "C3": c3}
+def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_racks=100, n_pre=None,
+       pre_job_size=100) -> M.Cluster:
+    """C4: nodes {64 cores, 256Gi, 110 pods} in n_zones zones x n_racks racks (contiguous), plus n_pre
+    running pods (default n_nodes) in running gang jobs labelled job=<name>, app=svc|web. Services (app=svc)
+    run only in the first 30% of the zones; the first service also carries required anti-affinity
+    (hostname) and preferred anti-affinity (zone, w=10) against noisy=true pods.
+    Pending jobs: 30% required podAntiAffinity (hostname) to their own job label, 30% preferred
+    podAffinity (rack, w=50) to their own job label, 20% required podAffinity (zone) to app=svc, 20% plain;
+    10% of the jobs are noisy=true."""
+    rng = np.random.default_rng(seed)
+    n_pre = n_nodes if n_pre is None else n_pre
+    cl = M.Cluster()
+    racks_per_zone = max(1, n_racks // n_zones)
+    for i in range(n_nodes):
+        rack = i * n_racks // n_nodes
+        cl.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: 64000, M.MEMORY: 256 * GI, M.PODS: 110},
+                               labels={"kubernetes.io/hostname": f"node-{i:05d}",
+                                       "zone": f"z{min(n_zones - 1, rack // racks_per_zone)}",
+                                       "rack": f"r{rack}"}))
+    cl.queues.append(M.Queue(name="default", weight=1))
+    # running jobs (lister pods)
+    n_pre_jobs = max(1, n_pre // pre_job_size)
+    svc_nodes = max(1, int(n_nodes * 0.3))
+    for j in range(n_pre_jobs):
+        name = f"pre{j:04d}"
+        svc = j % 5 == 0
+        cl.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=pre_job_size,
+                                        phase="Running"))
+        aff = None
+        if j == 0:
+            noisy = {"labelSelector": {"matchLabels": {"noisy": "true"}}}
+            aff = {"podAntiAffinity": {
+                "required": [dict(noisy, topologyKey="kubernetes.io/hostname")],
+                "preferred": [{"weight": 10, "podAffinityTerm": dict(noisy, topologyKey="zone")}]}}
+        for t in range(pre_job_size):
+            node = int(rng.integers(0, svc_nodes if svc else n_nodes))
+            cl.pods.append(M.Pod(ns="ns", name=f"{name}-{t:04d}", uid=f"ns-{name}-{t:04d}", group=name,
+                                 node=f"node-{node:05d}", phase="Running",
+                                 labels={"job": name, "app": "svc" if svc else "web"},
+                                 containers=[M.Container(req={M.CPU: 1000, M.MEMORY: 2 * GI})],
+                                 affinity=aff))
+    # pending jobs
+    for j in range(n_jobs):
+        name = f"job{j:05d}"
+        cl.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=tasks_per_job))
+        req = {M.CPU: int(rng.integers(1, 9)) * 250, M.MEMORY: int(rng.integers(1, 9)) * (GI // 2)}
+        labels = {"job": name}
+        if rng.random() < 0.1:
+            labels["noisy"] = "true"
+        own = {"labelSelector": {"matchLabels": {"job": name}}}
+        kind = rng.random()
+        aff = None
+        if kind < 0.3:
+            aff = {"podAntiAffinity": {"required": [dict(own, topologyKey="kubernetes.io/hostname")]}}
+        elif kind < 0.6:
+            aff = {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": dict(own, topologyKey="rack")}]}}
+        elif kind < 0.8:
+            aff = {"podAffinity": {"required": [{"labelSelector": {"matchLabels": {"app": "svc"}},
+                                                 "topologyKey": "zone"}]}}
+        for t in range(tasks_per_job):
+            cl.pods.append(M.Pod(ns="ns", name=f"{name}-{t:04d}", uid=f"ns-{name}-{t:04d}", group=name,
+                                 labels=dict(labels), containers=[M.Container(req=dict(req))],
+                                 affinity=None if aff is None else aff))
+    return cl
+
+
+CONFIGS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4}

@@ -98,3 +98,89 @@ def edge_cluster(seed=7):
                                  node_selector=dict(sp.get("sel", {})), tolerations=list(sp.get("tol", [])),
                                  affinity=sp.get("aff")))
     return cl
+
+
+def affinity_edge_cluster(seed=11, n_nodes=40):
+    """Inter-pod (anti)affinity edge cases: nodes missing topology labels, two namespaces, existing pods
+    with required/preferred anti terms (NotIn / Exists / DoesNotExist selectors, explicit namespaces),
+    pods outside any PodGroup on nodes (scored, not listed), pending jobs with composite required
+    affinity (zone+rack), multi-term anti-affinity, self-matching affinity with no existing match,
+    affinity nothing can satisfy, preferred terms with empty topology keys and mixed weights."""
+    import random
+    rng = random.Random(seed)
+    cl = m.Cluster(tiers=m.default_tiers())
+    for i in range(n_nodes):
+        labels = {"kubernetes.io/hostname": f"n{i:02d}", "zone": f"z{i % 4}"}
+        if i % 7 != 3:
+            labels["rack"] = f"r{i % 10}"
+        cl.nodes.append(m.Node(name=f"n{i:02d}", alloc={m.CPU: 16000, m.MEMORY: 64 * GI, m.PODS: 20},
+                               labels=labels))
+    cl.queues.append(m.Queue(name="q", weight=1))
+    sel = lambda **kv: {"labelSelector": {"matchLabels": dict(kv)}}
+    exprs = lambda *e: {"labelSelector": {"matchExpressions": [dict(key=k, operator=o, values=list(v)) if v
+                                                               else dict(key=k, operator=o) for k, o, v in e]}}
+    # running jobs (lister pods)
+    running = [
+        ("db", {"app": "db", "tier": "data"}, {"podAntiAffinity": {
+            "required": [dict(sel(app="cache"), topologyKey="kubernetes.io/hostname")],
+            "preferred": [{"weight": 7, "podAffinityTerm": dict(exprs(("tier", "Exists", ())), topologyKey="zone")}]}}),
+        ("web", {"app": "web"}, {"podAffinity": {
+            "preferred": [{"weight": 3, "podAffinityTerm": dict(sel(app="db"), topologyKey="rack")},
+                          {"weight": 9, "podAffinityTerm": dict(sel(app="db"), topologyKey="")}]}}),
+        ("ops", {"app": "ops"}, {"podAntiAffinity": {
+            "required": [dict(exprs(("app", "NotIn", ("ops", "db")), ("batch", "DoesNotExist", ())),
+                              namespaces=["other"], topologyKey="zone")]}}),
+        ("svc", {"app": "svc", "tier": "front"}, {"podAffinity": {
+            "required": [dict(sel(app="db"), topologyKey="zone")]}}),
+    ]
+    for j, (name, labels, aff) in enumerate(running):
+        cl.pod_groups.append(m.PodGroup(ns="ns", name=name, queue="q", min_member=3, phase="Running"))
+        for t in range(3):
+            node = rng.randrange(n_nodes)
+            cl.pods.append(m.Pod(ns="ns", name=f"{name}-{t}", uid=f"ns-{name}-{t}", group=name, node=f"n{node:02d}",
+                                 phase="Running", labels=dict(labels), affinity=aff,
+                                 containers=[m.Container(req={m.CPU: 500, m.MEMORY: GI})]))
+    for t in range(2):  # pods outside any PodGroup: on nodes (score), not in the lister
+        cl.pods.append(m.Pod(ns="ns", name=f"loose-{t}", uid=f"ns-loose-{t}", node=f"n{rng.randrange(n_nodes):02d}",
+                             phase="Running", labels={"app": "loose"}, containers=[m.Container(req={m.CPU: 100})],
+                             affinity={"podAffinity": {"preferred": [
+                                 {"weight": 4, "podAffinityTerm": dict(sel(role="batch"), topologyKey="zone")}]}}))
+    pending = [
+        ("cache", "ns", {"app": "cache"}, None),
+        ("b-anti", "ns", {"role": "batch", "job": "b-anti"}, {"podAntiAffinity": {
+            "required": [dict(sel(job="b-anti"), topologyKey="kubernetes.io/hostname"),
+                         dict(sel(role="batch"), topologyKey="rack")]}}),
+        ("b-comp", "ns", {"role": "batch", "job": "b-comp"}, {"podAffinity": {
+            "required": [dict(sel(app="db"), topologyKey="zone"), dict(sel(tier="data"), topologyKey="rack")]}}),
+        ("self", "ns", {"job": "self"}, {"podAffinity": {
+            "required": [dict(sel(job="self"), topologyKey="rack")]}}),
+        ("never", "ns", {"job": "never"}, {"podAffinity": {
+            "required": [dict(sel(app="nothing-here"), topologyKey="zone")]}}),
+        ("pref", "ns", {"job": "pref", "batch": "1"}, {"podAffinity": {
+            "preferred": [{"weight": 50, "podAffinityTerm": dict(sel(job="pref"), topologyKey="rack")},
+                          {"weight": 20, "podAffinityTerm": dict(exprs(("app", "In", ("web", "svc"))),
+                                                                 topologyKey="zone")}]},
+            "podAntiAffinity": {"preferred": [
+                {"weight": 30, "podAffinityTerm": dict(sel(app="db"), topologyKey="kubernetes.io/hostname")}]}}),
+        ("other-ns", "other", {"app": "x"}, None),
+        ("plain", "ns", {"job": "plain"}, None),
+    ]
+    for name, ns, labels, aff in pending:
+        cl.pod_groups.append(m.PodGroup(ns=ns, name=name, queue="q", min_member=1))
+        for t in range(5):
+            cl.pods.append(m.Pod(ns=ns, name=f"{name}-{t}", uid=f"{ns}-{name}-{t}", group=name,
+                                 labels=dict(labels), affinity=aff,
+                                 containers=[m.Container(req={m.CPU: 1000, m.MEMORY: 2 * GI})]))
+    return cl
+
+
+def affinity_clusters():
+    """(name, cluster) pairs with inter-pod (anti)affinity for parity tests."""
+    return [
+        ("C4-parity", synth.c4(n_nodes=300, n_jobs=30, tasks_per_job=10, n_zones=5, n_racks=25, n_pre=300,
+                               pre_job_size=20, seed=21)),
+        ("C4-tight", synth.c4(n_nodes=60, n_jobs=12, tasks_per_job=8, n_zones=3, n_racks=6, n_pre=120,
+                              pre_job_size=20, seed=22)),
+        ("aff-edge", affinity_edge_cluster()),
+        ("aff-edge-b", affinity_edge_cluster(seed=12, n_nodes=25)),
+    ]
