@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 2
+#define KBGPU_ABI_VERSION 3
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -221,6 +221,80 @@ int kb_upload_nodes(kb_ctx* ctx, const kb_nodes* nodes);
 /* Copies the spec tables to HBM. */
 int kb_upload_specs(kb_ctx* ctx, const kb_specs* specs);
 
+/*
+ * Inter-pod (anti)affinity as counts per topology domain (scheduler_amd/affinity.py has the derivation).
+ * Replaces the lister scans of InterPodAffinityMatches (vendor/.../predicates/predicates.go:1155-1465,
+ * called from plugins/predicates/predicates.go:278-296) and the per-node loops of
+ * CalculateInterPodAffinityPriority (vendor/.../priorities/interpod_affinity.go:119-241, called from
+ * plugins/nodeorder/nodeorder.go:229-246).
+ *
+ * A topology slot is a tuple of label keys; topo_dom[slot][node] is the node's domain id (-1: a key is
+ * missing). A count table holds, per domain of its slot, the lister pods that carry one required
+ * anti-affinity term (EXISTING_ANTI) or match all required (anti-)affinity terms of a spec (ANTI /
+ * AFFINITY), plus a total. A spec checks its tables in order (existing anti, anti, affinity: the
+ * reference's order) and keeps InterPodAffinity histograms H[h_off + domain] per topology key.
+ * Commits apply the committed spec's increment lists: lister tables on Allocate only (Pipelined tasks
+ * are not listed, plugins/util/util.go:108-130), histogram increments on every commit.
+ * Counts are int32.
+ */
+#define KB_AFF_EXISTING_ANTI 0 /* fail if count > 0: "didn't satisfy existing pods anti-affinity rules" */
+#define KB_AFF_ANTI 1          /* fail if count > 0: "didn't match pod anti-affinity rules" */
+#define KB_AFF_AFFINITY 2      /* fail if count == 0 and (total > 0 or !self_match): "...affinity rules" */
+#define KB_AFF_SELF_DYNAMIC (1u << 0) /* the spec's own commits change its checks or histograms */
+
+typedef struct kb_aff_table {
+  int32_t slot;
+  uint32_t cnt_off; /* into counters: one entry per domain of the slot */
+} kb_aff_table;
+typedef struct kb_aff_check {
+  int32_t table;
+  int32_t kind; /* KB_AFF_* */
+} kb_aff_check;
+typedef struct kb_ipa_hist {
+  int32_t slot;   /* single-key slot */
+  uint32_t h_off; /* into h: one entry per domain */
+} kb_ipa_hist;
+typedef struct kb_ipa_incr {
+  int32_t slot;
+  uint32_t h_off;
+  int32_t weight; /* added at the committed node's domain, per commit */
+  int32_t pad;
+} kb_ipa_incr;
+typedef struct kb_aff_spec {
+  uint32_t check_off, check_cnt;   /* into checks */
+  uint32_t lister_off, lister_cnt; /* into lister: tables a committed (Allocated) task of this spec joins */
+  uint32_t hist_off, hist_cnt;     /* into hists: this spec's InterPodAffinity histograms */
+  uint32_t incr_off, incr_cnt;     /* into incr: histogram updates of one commit of this spec */
+  int32_t self_match;              /* targetPodMatchesAffinityOfPod(pod, pod) (metadata.go:498-510) */
+  uint32_t flags;                  /* KB_AFF_SELF_DYNAMIC */
+} kb_aff_spec;
+
+typedef struct kb_affinity {
+  uint32_t n_slots;
+  const int32_t* topo_dom; /* [n_slots][n] */
+  uint32_t n_tables;
+  const kb_aff_table* tables;
+  const int32_t* totals;   /* [n_tables] */
+  uint32_t n_counters;
+  const int32_t* counters;
+  uint32_t m;              /* must equal kb_specs.m; kb_spec.aff_class indexes specs */
+  const kb_aff_spec* specs;
+  uint32_t n_checks;
+  const kb_aff_check* checks;
+  uint32_t n_lister;
+  const int32_t* lister;   /* table ids */
+  uint32_t n_hists;
+  const kb_ipa_hist* hists;
+  uint32_t n_h;
+  const int32_t* h;
+  uint32_t n_incr;
+  const kb_ipa_incr* incr;
+} kb_affinity;
+
+/* Copies the affinity tables to HBM (after kb_upload_nodes and kb_upload_specs). Specs flagged
+ * KB_SPEC_POD_AFFINITY are refused by kb_place_job / kb_eval until this is called. */
+int kb_upload_affinity(kb_ctx* ctx, const kb_affinity* aff);
+
 /* placement kinds */
 #define KB_PLACE_ALLOCATE 1 /* Session.Allocate (session.go:242) */
 #define KB_PLACE_PIPELINE 2 /* Session.Pipeline (session.go:199) */
@@ -280,7 +354,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_EVAL 2
 #define KB_KERNEL_TRAJ_SWEEP 3
 #define KB_KERNEL_TRAJ_PLACE 4
-#define KB_NUM_KERNELS 5
+#define KB_KERNEL_AFF_PLACE 5 /* block-wide re-sweep loop (specs with self-dependent pod affinity) */
+#define KB_KERNEL_IPA_MINMAX 6
+#define KB_NUM_KERNELS 7
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */

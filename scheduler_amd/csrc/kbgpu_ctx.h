@@ -19,7 +19,14 @@ struct kb_ctx {
   bool nodes_ok = false, specs_ok = false;
   int64_t max_pref_weight = 0;
 
-  std::vector<void*> node_mem, spec_mem, work_mem;
+  std::vector<void*> node_mem, spec_mem, work_mem, aff_mem;
+  // inter-pod affinity (kb_upload_affinity)
+  bool aff_ok = false;
+  std::vector<char> spec_needs_aff;  // per spec: KB_SPEC_POD_AFFINITY / aff_class set
+  std::vector<char> spec_dyn;   // per spec: KB_AFF_SELF_DYNAMIC -> block-wide re-sweep loop
+  std::vector<char> spec_hist;  // per spec: has InterPodAffinity histograms
+  int64_t* mm_eval = nullptr;   // [2 * chunk] per-spec IPA min / max for kb_eval
+  uint32_t mm_eval_cap = 0;
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec
   uint64_t* cmax = nullptr;  // [ceil(n/64)] chunk maxima
   uint64_t* stat = nullptr;  // [n] static predicate / NodeAffinity cache of the current spec
@@ -42,7 +49,7 @@ struct kb_ctx {
 
   // pristine copies of the mutable node columns (kb_restore_nodes)
   struct Col { void* dst; void* src; size_t bytes; };
-  std::vector<Col> pristine;
+  std::vector<Col> pristine, aff_pristine;
 
   // kernel timing (KB_OPT_TIMING)
   bool timing = false;

@@ -30,7 +30,25 @@ struct DevNodes {
   uint64_t* port_used;
 };
 
+// Inter-pod affinity tables (kb_affinity). enabled == 0: none uploaded (no spec refers to them).
+struct DevAff {
+  int32_t enabled;
+  int32_t n;            // nodes (topo_dom row length)
+  int32_t* topo_dom;    // [slots][n]
+  kb_aff_table* tables;
+  int32_t* totals;      // mutable
+  int32_t* counters;    // mutable
+  kb_aff_spec* specs;
+  kb_aff_check* checks;
+  int32_t* lister;
+  kb_ipa_hist* hists;
+  int32_t* h;           // mutable
+  kb_ipa_incr* incr;
+  int64_t* mm;          // [2] InterPodAffinity min / max count of the current run's spec
+};
+
 struct DevSpecs {
+  DevAff A;
   kb_spec* specs;
   int64_t *sc_init, *sc_req;
   kb_term* terms;
@@ -70,11 +88,20 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, void* stream);
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream);
 int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;
 constexpr int kTrajDefaultJ = 16;  // trajectory depth per run; deeper commits are computed in place
+// Inter-pod affinity (kbgpu_device.hip): min / max InterPodAffinity count over all nodes for each of
+// `count` specs (spec_ids, or the single `spec` when spec_ids is null) into mm[2 * i], and the
+// block-wide re-sweep place loop for specs whose own commits change their affinity inputs.
+void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec_ids, int spec, int count,
+                       int64_t* mm, const JobState* js, void* stream);
+void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                      uint64_t* base, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                      int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+
 // Opt the place kernels into the dynamic LDS they need; returns 0 or the hipError_t.
 int configure_kernels();
 int traj_lds_bytes(int n, int t_count, int* pb_cap);

@@ -156,13 +156,94 @@ __device__ __forceinline__ void store_row(const DevNodes& N, int n, const Row& r
   N.nz_mem[n] = r.nz_mem;
 }
 
+// ---- inter-pod (anti)affinity lookups (kb_affinity; scheduler_amd/affinity.py) ----
+constexpr uint32_t kAffExistingAnti = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_EXISTING_ANTI);
+constexpr uint32_t kAffAntiRules = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_ANTI_AFFINITY_RULES);
+constexpr uint32_t kAffAffinityRules = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_AFFINITY_RULES);
+
+// InterPodAffinityMatches (vendor/.../predicates.go:1155-1185) through the count tables, in the
+// reference's order: existing pods' anti-affinity (:1293-1333), then the pod's own anti-affinity and
+// affinity (satisfiesPodsAffinityAntiAffinity, :1367-1465).
+// Mutable table entries: COH = true reads at L2 (the block-wide place loop updates them with atomics,
+// which do not refresh this CU's L1).
+template <bool COH>
+__device__ __forceinline__ int32_t ld_cnt(const int32_t* p) {
+  if (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+template <bool COH = false>
+__device__ uint32_t aff_reasons(const DevAff& A, const kb_aff_spec& as, int n) {
+  for (uint32_t i = 0; i < as.check_cnt; ++i) {
+    const kb_aff_check c = A.checks[as.check_off + i];
+    const kb_aff_table t = A.tables[c.table];
+    const int32_t d = A.topo_dom[(size_t)t.slot * A.n + n];
+    const int32_t cnt = d >= 0 ? ld_cnt<COH>(&A.counters[t.cnt_off + d]) : 0;
+    if (c.kind == KB_AFF_EXISTING_ANTI) {
+      if (cnt > 0) return kAffExistingAnti;
+    } else if (c.kind == KB_AFF_ANTI) {
+      if (cnt > 0) return kAffAntiRules;
+    } else if (cnt == 0 && (ld_cnt<COH>(&A.totals[c.table]) > 0 || !as.self_match)) {
+      return kAffAffinityRules;
+    }
+  }
+  return 0;
+}
+
+// counts[node] of CalculateInterPodAffinityPriority (interpod_affinity.go:119-219) as the sum of the
+// spec's per-key domain histograms.
+template <bool COH = false>
+__device__ __forceinline__ int64_t ipa_count(const DevAff& A, const kb_aff_spec& as, int n) {
+  int64_t c = 0;
+  for (uint32_t i = 0; i < as.hist_cnt; ++i) {
+    const kb_ipa_hist h = A.hists[as.hist_off + i];
+    const int32_t d = A.topo_dom[(size_t)h.slot * A.n + n];
+    if (d >= 0) c += ld_cnt<COH>(&A.h[h.h_off + d]);
+  }
+  return c;
+}
+
+// fScore = MaxPriority * ((count - min) / (max - min)), HostPriority.Score = int(fScore) (:221-238);
+// min and max start at 0 and run over every node. Counts are integers, exact in float64.
+__device__ __forceinline__ int32_t ipa_score(int64_t c, int64_t mn, int64_t mx) {
+  if (mx - mn <= 0) return 0;
+  const double f = 10.0 * ((double)(c - mn) / (double)(mx - mn));
+  return (int32_t)f;
+}
+
+// The table updates of commits of `sp` on node w: n_alloc Allocates join the lister tables
+// (PodLister.UpdateTask, plugins/util/util.go:108-130), every commit adds the pod to the node for the
+// score (nodeorder.go:161-172).
+__device__ void apply_commit_tables(const DevAff& A, const kb_spec& sp, int w, int n_alloc, int n_commit) {
+  if (!A.enabled || sp.aff_class < 0) return;
+  const kb_aff_spec as = A.specs[sp.aff_class];
+  if (n_alloc > 0)
+    for (uint32_t i = 0; i < as.lister_cnt; ++i) {
+      const int32_t t = A.lister[as.lister_off + i];
+      const kb_aff_table tb = A.tables[t];
+      const int32_t d = A.topo_dom[(size_t)tb.slot * A.n + w];
+      if (d >= 0) atomicAdd(&A.counters[tb.cnt_off + d], n_alloc);
+      atomicAdd(&A.totals[t], n_alloc);
+    }
+  if (n_commit > 0)
+    for (uint32_t i = 0; i < as.incr_cnt; ++i) {
+      const kb_ipa_incr e = A.incr[as.incr_off + i];
+      const int32_t d = A.topo_dom[(size_t)e.slot * A.n + w];
+      if (d >= 0) atomicAdd(&A.h[e.h_off + d], e.weight * n_commit);
+    }
+}
+
 // Static part of the predicate chain and score for (spec, node): everything that no commit changes.
 //   bits  0..15: first failing static stage BEFORE the host-port check (conditions, node selector)
-//   bits 16..31: first failing static stage AFTER it (taints, pressure)
-//   bits 32..63: NodeAffinity priority count (node_affinity.go:34-74)
+//   bits 16..31: first failing static stage AFTER it (taints, pressure, then inter-pod affinity)
+//   bits 32..59: NodeAffinity priority count (node_affinity.go:34-74), signed 28-bit
+//   bits 60..63: InterPodAffinity priority (0..10)
+// `mm` (this spec's InterPodAffinity min / max) non-null: the spec's affinity inputs do not change
+// during its run, so the affinity predicate and priority are folded in here too.
 __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
-                                uint32_t f, int n) {
+                                uint32_t f, int n, const int64_t* mm) {
   uint32_t pre = 0, post = 0;
+  const bool aff = mm != nullptr && sp.aff_class >= 0;
   if (C.predicates) {
     // CheckNodeConditionPredicate (vendor/.../predicates.go:1568-1596): one reason per bad condition
     pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
@@ -181,17 +262,29 @@ __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevC
       post = 1u << KB_R_MEMORY_PRESSURE;
     else if (C.disk_pressure && (f & KB_NODE_DISK_PRESSURE)) post = 1u << KB_R_DISK_PRESSURE;
     else if (C.pid_pressure && (f & KB_NODE_PID_PRESSURE)) post = 1u << KB_R_PID_PRESSURE;
+    // InterPodAffinityMatches, the last predicate (plugins/predicates/predicates.go:278-296)
+    if (aff && !pre && !post) post = aff_reasons(P.A, P.A.specs[sp.aff_class], n);
   }
   int32_t na = 0;
-  if (C.nodeorder && !(sp.flags & KB_SPEC_NA_ERROR)) {
-    for (uint32_t i = 0; i < sp.pref_term_cnt; ++i) {
-      const kb_term t = P.terms[sp.pref_term_off + i];
-      if (t.weight == 0) continue;
-      if (term_match(N, P, t, n)) na += t.weight;
+  uint32_t ipa = 0;
+  if (C.nodeorder) {
+    if (!(sp.flags & KB_SPEC_NA_ERROR))
+      for (uint32_t i = 0; i < sp.pref_term_cnt; ++i) {
+        const kb_term t = P.terms[sp.pref_term_off + i];
+        if (t.weight == 0) continue;
+        if (term_match(N, P, t, n)) na += t.weight;
+      }
+    if (aff) {
+      const kb_aff_spec as = P.A.specs[sp.aff_class];
+      if (as.hist_cnt) ipa = (uint32_t)ipa_score(ipa_count(P.A, as, n), mm[0], mm[1]);
     }
   }
-  return (uint64_t)pre | ((uint64_t)post << 16) | ((uint64_t)(uint32_t)na << 32);
+  return (uint64_t)pre | ((uint64_t)post << 16) | ((uint64_t)((uint32_t)na & 0x0fffffffu) << 32) |
+         ((uint64_t)ipa << 60);
 }
+
+__device__ __forceinline__ int32_t stat_na(uint64_t st) { return (int32_t)((uint32_t)(st >> 32) << 4) >> 4; }
+__device__ __forceinline__ int32_t stat_ipa(uint64_t st) { return (int32_t)(st >> 60); }
 
 __device__ __forceinline__ bool sc_fit(const DevNodes& N, const kb_spec& sp, const int64_t* sci, bool has_map,
                                        const int64_t* node_sc, int n) {
@@ -224,17 +317,17 @@ __device__ __forceinline__ uint32_t row_reasons(const DevNodes& N, const DevSpec
   return (uint32_t)((st >> 16) & 0xffff);
 }
 
-// nodeOrderFn (nodeorder.go:188-226); InterPodAffinity adds 0 without pod (anti)affinity terms.
+// nodeOrderFn (nodeorder.go:188-226) + the InterPodAffinity batch score (:229-246) from the static cache.
 // All terms are integers, so the reference's float64 sum equals this int64 sum.
 __device__ __forceinline__ int64_t row_score(const DevCfg& C, const kb_spec& sp, const Row& r, uint64_t st) {
   if (!C.nodeorder) return 0;
-  if (sp.flags & KB_SPEC_NA_ERROR) return 0;  // map fn error: the node keeps only the batch score
+  const int64_t batch = (int64_t)stat_ipa(st) * C.w_pa;
+  if (sp.flags & KB_SPEC_NA_ERROR) return batch;  // map fn error: the node keeps only the batch score
   const int64_t rc = sp.nz_cpu + r.nz_cpu, rm = sp.nz_mem + r.nz_mem;
   const int64_t lr = (lr_score(rc, r.alloc_cpu) + lr_score(rm, r.alloc_mem)) / 2;
   const double cf = frac_cap(rc, r.alloc_cpu), mf = frac_cap(rm, r.alloc_mem);
   const int64_t bra = (cf >= 1.0 || mf >= 1.0) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 10.0);
-  const int32_t na = (int32_t)(uint32_t)(st >> 32);
-  return lr * C.w_lr + bra * C.w_bra + (int64_t)na * C.w_na;
+  return lr * C.w_lr + bra * C.w_bra + (int64_t)stat_na(st) * C.w_na + batch;
 }
 
 __device__ __forceinline__ uint64_t make_key(uint32_t reasons, int64_t score, int n) {
@@ -272,7 +365,7 @@ __global__ __launch_bounds__(256) void sweep_keys_kernel(DevNodes N, DevSpecs P,
   uint64_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+    const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? P.A.mm : nullptr);
     stat[n] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, n);
     k = make_key(rs, rs ? 0 : row_score(C, sp, r, st), n);
@@ -549,6 +642,7 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
         const uint64_t e = pb[k];
         hout[2 * (pb_base + k)] = (int32_t)(uint32_t)e;
         hout[2 * (pb_base + k) + 1] = (int32_t)(uint32_t)(e >> 32);
+        apply_commit_tables(P.A, sp, (int)(uint32_t)e, (uint32_t)(e >> 32) == KB_PLACE_ALLOCATE, 1);
       }
       pb_base += pb_n;
       pb_n = 0;
@@ -562,10 +656,14 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
   }
 done:
   __syncthreads();
-  for (int k = tid; k < lo.pb_n; k += 512) {
-    const uint64_t v = pb[k];
-    hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
-    hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
+  {
+    const kb_spec spb = P.specs[spec];
+    for (int k = tid; k < lo.pb_n; k += 512) {
+      const uint64_t v = pb[k];
+      hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
+      hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
+      apply_commit_tables(P.A, spb, (int)(uint32_t)v, (uint32_t)(v >> 32) == KB_PLACE_ALLOCATE, 1);
+    }
   }
   __threadfence_system();
   __syncthreads();
@@ -575,14 +673,14 @@ done:
 }
 
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
-                                                   uint32_t* reasons, int64_t* scores) {
+                                                   uint32_t* reasons, int64_t* scores, const int64_t* mm) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = blockIdx.y;
   if (n >= N.n) return;
   const int s = spec_ids[j];
   const kb_spec sp = P.specs[s];
   const Row r = load_row(N, n);
-  const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+  const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? mm + 2 * j : nullptr);
   reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
   scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
 }
@@ -719,7 +817,7 @@ __global__ __launch_bounds__(256) void traj_sweep_kernel(DevNodes N, DevSpecs P,
   uint32_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval(N, P, C, sp, r.flags, n);
+    const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? P.A.mm : nullptr);
     const int A = allocs_before_full(N, sp, sci, scr, r, n);
     k = compress_key(traj_key64(N, P, C, sp, sci, scr, r, st, n, j, A), n, idx_bits);
     traj[(size_t)j * N.n + n] = k;
@@ -957,7 +1055,9 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
   for (int w = tid; w < n; w += kPlaceThreads) {
     if (!((tb[w >> 6] >> (w & 63)) & 1)) continue;
     const uint32_t s = nc[w].y;
-    write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
+    const int c = (int)(s & 0xffff), A = (int)(s >> 16);
+    write_back_row(N, P, sp, scr, w, c, A);
+    apply_commit_tables(P.A, sp, w, c < A ? c : A, c);  // the run's affinity inputs were static
   }
   for (int k = tid; k < lo.pb_n; k += kPlaceThreads) {
     const uint32_t e = pb[k];
@@ -972,6 +1072,286 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// ===========================================================================
+// Inter-pod affinity kernels.
+// ===========================================================================
+constexpr int kAffThreads = 1024;
+
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t x = __shfl_xor(v, o, 64);
+    v = x < v ? x : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t x = __shfl_xor(v, o, 64);
+    v = x > v ? x : v;
+  }
+  return v;
+}
+
+// Block-wide min / max (starting at 0, as the reference's do) of the InterPodAffinity counts of a spec.
+template <bool COH>
+__device__ void block_ipa_minmax(const DevAff& A, const kb_aff_spec& as, int n, int64_t* rmin, int64_t* rmax,
+                                 int64_t* mn_out, int64_t* mx_out) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  int64_t mn = 0, mx = 0;
+  for (int i = tid; i < n; i += nthr) {
+    const int64_t c = ipa_count<COH>(A, as, i);
+    mn = c < mn ? c : mn;
+    mx = c > mx ? c : mx;
+  }
+  mn = wave_min_i64(mn);
+  mx = wave_max_i64(mx);
+  if ((tid & 63) == 0) {
+    rmin[tid >> 6] = mn;
+    rmax[tid >> 6] = mx;
+  }
+  __syncthreads();
+  mn = 0, mx = 0;
+  for (int w = 0; w < (nthr + 63) / 64; ++w) {
+    mn = rmin[w] < mn ? rmin[w] : mn;
+    mx = rmax[w] > mx ? rmax[w] : mx;
+  }
+  __syncthreads();  // rmin / rmax reusable
+  *mn_out = mn;
+  *mx_out = mx;
+}
+
+// One block per spec: min / max of its InterPodAffinity counts over all nodes into mm[2 * block].
+__global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, DevSpecs P, const int32_t* spec_ids,
+                                                                 int spec, int64_t* mm, const JobState* js) {
+  __shared__ int64_t rmin[16], rmax[16];
+  if (js != nullptr && js->stopped) return;
+  const int s = spec_ids ? spec_ids[blockIdx.x] : spec;
+  const kb_spec sp = P.specs[s];
+  int64_t mn = 0, mx = 0;
+  if (sp.aff_class >= 0) {
+    const kb_aff_spec as = P.A.specs[sp.aff_class];
+    if (as.hist_cnt) block_ipa_minmax<false>(P.A, as, N.n, rmin, rmax, &mn, &mx);
+  }
+  if (threadIdx.x == 0) {
+    mm[2 * blockIdx.x] = mn;
+    mm[2 * blockIdx.x + 1] = mx;
+  }
+}
+
+// Key of node i for a spec whose affinity inputs move with its own commits: the cached base key (row
+// + static predicates + LR/BRA/NodeAffinity), then the inter-pod affinity predicate (the last one) and
+// the InterPodAffinity batch score from the live tables.
+__device__ __forceinline__ uint64_t aff_key(const DevAff& A, const kb_aff_spec& as, const DevCfg& C, uint64_t b,
+                                            int i, int64_t mn, int64_t mx) {
+  if (!(b & kFeasible)) return b;
+  if (C.predicates) {
+    const uint32_t ar = aff_reasons<true>(A, as, i);
+    if (ar) return ar;
+  }
+  if (!C.nodeorder || !as.hist_cnt) return b;
+  const int64_t score = (int64_t)((b >> 24) & ((1ull << 39) - 1)) - kScoreBias +
+                        (int64_t)ipa_score(ipa_count<true>(A, as, i), mn, mx) * C.w_pa;
+  return make_key(0, score, i);
+}
+
+// Block-wide place loop for a run of a spec whose own commits change its affinity inputs (e.g.
+// anti-affinity to its own job on hostname, or preferred affinity to its own job): per task every node
+// is re-keyed from the live tables (the reference's full PredicateNodes + PrioritizeNodes sweep,
+// scheduler_helper.go:34-129), the block reduces the argmax, thread 0 commits the row, and the block
+// applies the commit's table increments before the next task.
+__global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, uint64_t* base, uint64_t* stat,
+    JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, int pb_cap,
+    uint32_t seq) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t pbs[];  // [pb_cap] placements: node | kind << 30
+  __shared__ uint64_t red[16];
+  __shared__ int64_t rmin[16], rmax[16];
+  __shared__ uint32_t hist_s[KB_NUM_REASONS];
+  __shared__ int32_t sh_kind;
+  __shared__ LoopOut lo;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = N.n;
+  const kb_spec sp = P.specs[spec];
+  const kb_aff_spec as = P.A.specs[sp.aff_class];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  for (int i = tid; i < n; i += kAffThreads) {  // base keys (no inter-pod affinity)
+    const Row r = load_row(N, i);
+    const uint64_t st = static_eval(N, P, C, sp, r.flags, i, nullptr);
+    stat[i] = st;
+    const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
+    base[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
+  }
+  int ready = first ? ready0 : js->ready_num;
+  int minav = first ? minav0 : js->min_available;
+  int gang = first ? gang0 : js->gang_ready;
+  int placed = first ? 0 : js->n_placed;
+  int pb_n = 0, pb_base = t_begin;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  const bool ipa = C.nodeorder && as.hist_cnt;
+  __syncthreads();
+  for (int t = 0; t < t_count; ++t) {
+    int64_t mn = 0, mx = 0;
+    if (ipa) block_ipa_minmax<true>(P.A, as, n, rmin, rmax, &mn, &mx);
+    uint64_t best = 0;
+    for (int i = tid; i < n; i += kAffThreads) best = umax64(best, aff_key(P.A, as, C, base[i], i, mn, mx));
+    best = wave_max_u64(best);
+    if (lane == 0) red[wv] = best;
+    __syncthreads();
+    best = 0;
+    for (int k = 0; k < kAffThreads / 64; ++k) best = umax64(best, red[k]);
+    if (!(best & kFeasible)) {
+      // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
+      if (tid < KB_NUM_REASONS) hist_s[tid] = 0;
+      __syncthreads();
+      uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+      for (int i = tid; i < n; i += kAffThreads) {
+        const uint64_t k = aff_key(P.A, as, C, base[i], i, mn, mx);
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (uint32_t)(k >> b) & 1u;
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) {
+        const uint32_t v = wave_sum_u32(h[b]);
+        if (lane == 0 && v) atomicAdd(&hist_s[b], v);
+      }
+      __syncthreads();
+      if (tid < KB_NUM_REASONS) {
+        js->hist[tid] = hist_s[tid];
+        hjs->hist[tid] = hist_s[tid];
+      }
+      stop = KB_STOP_NO_FIT;
+      fail_task = t_begin + t;
+      stopped = 1;
+      break;
+    }
+    const int64_t score = (int64_t)((best >> 24) & ((1ull << 39) - 1)) - kScoreBias;
+    if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
+      fail_task = t_begin + t;
+      panic = 1;
+      stopped = 1;
+      break;
+    }
+    const int w = (int)(kIdxMask - (uint32_t)(best & kIdxMask));
+    if (tid == 0) {  // commit: Session.Allocate / Pipeline on the winner's row (allocate.go:159-182)
+      Row r = load_row(N, w);
+      const uint64_t st = stat[w];
+      const bool to_idle = le_tol(sp.init_cpu, r.idle_cpu, 10) && le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                           scalars_fit(N, sp, sci, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, w);
+      int kind;
+      if (to_idle) {
+        r.idle_cpu -= sp.req_cpu;
+        r.idle_mem -= sp.req_mem;
+        if (r.flags & KB_NODE_IDLE_HAS_MAP) {
+          uint64_t m = sp.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            N.idle_sc[(size_t)q * n + w] -= scr[q];
+          }
+        }
+        kind = KB_PLACE_ALLOCATE;
+      } else {
+        r.rel_cpu -= sp.req_cpu;
+        r.rel_mem -= sp.req_mem;
+        if (r.flags & KB_NODE_REL_HAS_MAP) {
+          uint64_t m = sp.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            N.rel_sc[(size_t)q * n + w] -= scr[q];
+          }
+        }
+        kind = KB_PLACE_PIPELINE;
+      }
+      r.pod_count += 1;
+      r.nz_cpu += sp.nz_cpu;
+      r.nz_mem += sp.nz_mem;
+      for (uint32_t i = 0; i < sp.port_cnt; ++i) {
+        const kb_port p = P.ports[sp.port_off + i];
+        N.port_used[(size_t)p.slot * n + w] |= 1ull << p.ip;
+      }
+      store_row(N, w, r);
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, w);
+      base[w] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), w);
+      pbs[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
+      sh_kind = kind;
+    }
+    __syncthreads();
+    const int kind = sh_kind;
+    // this commit's table increments, in parallel (distinct counters per entry)
+    const int nl = kind == KB_PLACE_ALLOCATE ? (int)as.lister_cnt : 0;
+    for (int i = tid; i < nl + (int)as.incr_cnt; i += kAffThreads) {
+      if (i < nl) {
+        const int32_t tb = P.A.lister[as.lister_off + i];
+        const kb_aff_table ta = P.A.tables[tb];
+        const int32_t d = P.A.topo_dom[(size_t)ta.slot * n + w];
+        if (d >= 0) atomicAdd(&P.A.counters[ta.cnt_off + d], 1);
+        atomicAdd(&P.A.totals[tb], 1);
+      } else {
+        const kb_ipa_incr e = P.A.incr[as.incr_off + (i - nl)];
+        const int32_t d = P.A.topo_dom[(size_t)e.slot * n + w];
+        if (d >= 0) atomicAdd(&P.A.h[e.h_off + d], e.weight);
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    ++placed;
+    ++pb_n;
+    if (kind == KB_PLACE_ALLOCATE) ++ready;
+    if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+      stop = KB_STOP_READY;
+      stopped = 1;
+      break;
+    }
+    if (pb_n == pb_cap) {
+      for (int k = tid; k < pb_n; k += kAffThreads) {
+        const uint32_t e = pbs[k];
+        hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+        hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+      }
+      __syncthreads();
+      pb_base += pb_n;
+      pb_n = 0;
+    }
+  }
+  for (int k = tid; k < pb_n; k += kAffThreads) {
+    const uint32_t e = pbs[k];
+    hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+    hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+  }
+  if (tid == 0) lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, pb_n, pb_base, 0, 0};
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0)
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic,
+                  seq);
+}
+
+int aff_pb_cap(int t_count) { return t_count < 8192 ? (t_count < 1 ? 1 : t_count) : 8192; }
+
+void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec_ids, int spec, int count,
+                       int64_t* mm, const JobState* js, void* stream) {
+  hipLaunchKernelGGL(ipa_minmax_kernel, dim3(count), dim3(kAffThreads), 0, (hipStream_t)stream, N, P, spec_ids, spec,
+                     mm, js);
+}
+
+void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                      uint64_t* base, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                      int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+  const int pb_cap = aff_pb_cap(t_count);
+  hipLaunchKernelGGL(aff_place_kernel, dim3(1), dim3(kAffThreads), (size_t)pb_cap * 4, (hipStream_t)stream, N, P, C,
+                     spec, t_begin, t_count, base, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
+}
+
 // LDS plan of one place-loop launch: chunk maxima + placement buffer (+ all keys when they fit).
 static void place_loop_lds_plan(int n, int t_count, int* bytes, int* pb_cap, bool* keys_in_lds) {
   const int M = (n + 63) >> 6;
@@ -1063,9 +1443,9 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 }
 
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, void* stream) {
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
   dim3 grid((N.n + 255) / 256, t);
-  hipLaunchKernelGGL(eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons, scores);
+  hipLaunchKernelGGL(eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons, scores, mm);
 }
 
 }  // namespace kbgpu

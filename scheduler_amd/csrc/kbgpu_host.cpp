@@ -54,6 +54,17 @@ void free_all(std::vector<void*>& v) {
   v.clear();
 }
 
+void drop_affinity(kb_ctx* c) {
+  free_all(c->aff_mem);
+  c->aff_pristine.clear();
+  c->aff_ok = false;
+  c->P.A = kbgpu::DevAff{};
+  c->spec_dyn.clear();
+  c->spec_hist.clear();
+  c->mm_eval = nullptr;
+  c->mm_eval_cap = 0;
+}
+
 }  // namespace
 
 hipEvent_t kb_ctx::ev_get() {
@@ -133,6 +144,7 @@ void kb_destroy(kb_ctx* c) {
   if (!c->broken) (void)hipSetDevice(c->device);
   free_all(c->node_mem);
   free_all(c->spec_mem);
+  free_all(c->aff_mem);
   free_all(c->work_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
@@ -163,6 +175,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipSetDevice(c->device));
   free_all(c->node_mem);
   free_all(c->work_mem);
+  drop_affinity(c);
   c->nodes_ok = false;
   DevNodes& N = c->N;
   const size_t n = in->n;
@@ -233,6 +246,7 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   HIP_OK(c, hipSetDevice(c->device));
   free_all(c->spec_mem);
   c->specs_ok = false;
+  drop_affinity(c);
   if (in->n_tol_sets == 0 || in->n_taint_sets == 0) return fail(c, KB_E_INVALID, "empty toleration/taint tables");
   // host-side validation of every index the kernels will follow (no out-of-bounds device access)
   const uint32_t S = (uint32_t)c->N.S;
@@ -244,8 +258,6 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
     if ((uint64_t)s.pref_term_off + s.pref_term_cnt > in->n_terms) return fail(c, KB_E_INVALID, "spec %u pref", i);
     if ((uint64_t)s.port_off + s.port_cnt > in->n_ports) return fail(c, KB_E_INVALID, "spec %u ports", i);
     if (S < 64 && ((s.init_sc_mask | s.req_sc_mask) >> S)) return fail(c, KB_E_INVALID, "spec %u scalar mask", i);
-    if (s.flags & KB_SPEC_POD_AFFINITY)
-      return fail(c, KB_E_UNSUPPORTED, "spec %u: inter-pod affinity tables not uploaded", i);
   }
   for (uint32_t i = 0; i < in->n_terms; ++i)
     if ((uint64_t)in->terms[i].req_off + in->terms[i].req_cnt > in->n_reqs)
@@ -278,6 +290,9 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   P.m = (int32_t)in->m;
   c->max_pref_weight = 0;
   c->spec_pref_weight.assign(in->m, 0);
+  c->spec_needs_aff.assign(in->m, 0);
+  for (uint32_t i = 0; i < in->m; ++i)
+    c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
   for (uint32_t i = 0; i < in->m; ++i) {
     int64_t sum = 0;
     for (uint32_t j = 0; j < in->specs[i].pref_term_cnt; ++j)
@@ -288,6 +303,91 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   kb_update_traj_ok(c);
   c->specs_ok = true;
   return kb_check_score_range(c);
+}
+
+int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
+  if (!c || !a) return KB_E_INVALID;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs before affinity");
+  HIP_OK(c, hipSetDevice(c->device));
+  drop_affinity(c);
+  const size_t n = (size_t)c->N.n;
+  if (a->m != (uint32_t)c->P.m) return fail(c, KB_E_INVALID, "affinity specs %u != specs %d", a->m, c->P.m);
+  // every index the kernels follow is checked here (no out-of-bounds device access)
+  std::vector<int64_t> D(a->n_slots, 0);  // domains per slot
+  for (uint32_t sl = 0; sl < a->n_slots; ++sl)
+    for (size_t i = 0; i < n; ++i) {
+      const int32_t d = a->topo_dom[sl * n + i];
+      if (d < -1) return fail(c, KB_E_INVALID, "topo_dom[%u][%zu] = %d", sl, i, d);
+      D[sl] = std::max<int64_t>(D[sl], (int64_t)d + 1);
+    }
+  auto slot_ok = [&](int32_t sl) { return sl >= 0 && (uint32_t)sl < a->n_slots; };
+  for (uint32_t t = 0; t < a->n_tables; ++t) {
+    const kb_aff_table& tb = a->tables[t];
+    if (!slot_ok(tb.slot) || (int64_t)tb.cnt_off + D[tb.slot] > (int64_t)a->n_counters)
+      return fail(c, KB_E_INVALID, "affinity table %u", t);
+  }
+  for (uint32_t i = 0; i < a->n_checks; ++i)
+    if (a->checks[i].table < 0 || (uint32_t)a->checks[i].table >= a->n_tables || a->checks[i].kind < 0 ||
+        a->checks[i].kind > KB_AFF_AFFINITY)
+      return fail(c, KB_E_INVALID, "affinity check %u", i);
+  for (uint32_t i = 0; i < a->n_lister; ++i)
+    if (a->lister[i] < 0 || (uint32_t)a->lister[i] >= a->n_tables) return fail(c, KB_E_INVALID, "lister %u", i);
+  for (uint32_t i = 0; i < a->n_hists; ++i)
+    if (!slot_ok(a->hists[i].slot) || (int64_t)a->hists[i].h_off + D[a->hists[i].slot] > (int64_t)a->n_h)
+      return fail(c, KB_E_INVALID, "ipa hist %u", i);
+  for (uint32_t i = 0; i < a->n_incr; ++i)
+    if (!slot_ok(a->incr[i].slot) || (int64_t)a->incr[i].h_off + D[a->incr[i].slot] > (int64_t)a->n_h)
+      return fail(c, KB_E_INVALID, "ipa incr %u", i);
+  for (uint32_t s = 0; s < a->m; ++s) {
+    const kb_aff_spec& e = a->specs[s];
+    if ((uint64_t)e.check_off + e.check_cnt > a->n_checks || (uint64_t)e.lister_off + e.lister_cnt > a->n_lister ||
+        (uint64_t)e.hist_off + e.hist_cnt > a->n_hists || (uint64_t)e.incr_off + e.incr_cnt > a->n_incr)
+      return fail(c, KB_E_INVALID, "affinity spec %u offsets", s);
+  }
+  std::vector<kb_spec> specs(a->m);
+  if (a->m) HIP_OK(c, hipMemcpy(specs.data(), c->P.specs, a->m * sizeof(kb_spec), hipMemcpyDeviceToHost));
+  c->spec_dyn.assign(a->m, 0);
+  c->spec_hist.assign(a->m, 0);
+  for (uint32_t s = 0; s < a->m; ++s) {
+    const int32_t ac = specs[s].aff_class;
+    if (ac < -1 || ac >= (int32_t)a->m) return fail(c, KB_E_INVALID, "spec %u aff_class %d", s, ac);
+    if (ac >= 0) {
+      c->spec_dyn[s] = (a->specs[ac].flags & KB_AFF_SELF_DYNAMIC) != 0;
+      c->spec_hist[s] = a->specs[ac].hist_cnt > 0;
+    }
+  }
+  DevAff& A = c->P.A;
+  int rc;
+  if ((rc = upload(c, c->aff_mem, &A.topo_dom, a->topo_dom, (size_t)a->n_slots * n))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.tables, a->tables, a->n_tables))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.totals, a->totals, a->n_tables))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.counters, a->counters, a->n_counters))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.specs, a->specs, a->m))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.checks, a->checks, a->n_checks))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.lister, a->lister, a->n_lister))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.hists, a->hists, a->n_hists))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.h, a->h, a->n_h))) return rc;
+  if ((rc = upload(c, c->aff_mem, &A.incr, a->incr, a->n_incr))) return rc;
+  int64_t* mm = nullptr;
+  if ((rc = upload(c, c->aff_mem, &mm, (const int64_t*)nullptr, 2, false))) return rc;
+  A.mm = mm;
+  A.n = (int32_t)n;
+  // pristine copies of the mutable tables (kb_restore_nodes re-opens the session)
+  auto keep = [&](void* col, size_t bytes) -> int {
+    void* q;
+    HIP_OK(c, hipMalloc(&q, std::max<size_t>(bytes, 1)));
+    c->aff_mem.push_back(q);
+    HIP_OK(c, hipMemcpy(q, col, bytes, hipMemcpyDeviceToDevice));
+    c->aff_pristine.push_back({col, q, bytes});
+    return KB_OK;
+  };
+  if ((rc = keep(A.totals, a->n_tables * 4)) || (rc = keep(A.counters, a->n_counters * 4)) ||
+      (rc = keep(A.h, a->n_h * 4)))
+    return rc;
+  A.enabled = 1;
+  c->aff_ok = true;
+  return KB_OK;
 }
 
 // Which specs can use the 32-bit trajectory keys: |score| bound below 2^(30 - idx_bits).
@@ -364,9 +464,13 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   memset(result, 0, sizeof(*result));
   result->fail_task = -1;
   if (job->n_tasks == 0) return KB_OK;
-  for (uint32_t i = 0; i < job->n_tasks; ++i)
+  for (uint32_t i = 0; i < job->n_tasks; ++i) {
     if (job->task_specs[i] < 0 || job->task_specs[i] >= c->P.m)
       return fail(c, KB_E_INVALID, "task %u spec %d out of range", i, job->task_specs[i]);
+    if (c->spec_needs_aff[job->task_specs[i]] && !c->aff_ok)
+      return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first",
+                  job->task_specs[i]);
+  }
   int rc = ensure_job_buffers(c, job->n_tasks);
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
@@ -385,8 +489,19 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     hipEvent_t ea;
     int pbc;
     const int run = (int)(e - t);
-    const bool traj = c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
-    if (traj) {
+    const bool dyn = c->aff_ok && c->spec_dyn[spec];
+    const bool traj = !dyn && c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
+    if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
+      c->ev_begin(&ea);
+      launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->P.A.mm, first ? nullptr : js, c->stream);
+      c->ev_end(ea, KB_KERNEL_IPA_MINMAX, (uint64_t)c->N.n);
+    }
+    if (dyn) {
+      c->ev_begin(&ea);
+      launch_aff_place(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->stat, js, first, job->ready_num,
+                       job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
+      c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
+    } else if (traj) {
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
       launch_traj_sweep(c->N, c->P, c->cfg, spec, J, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
@@ -425,7 +540,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
     for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
       auto& p = c->pending[k];
-      if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
+      if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
     }
     c->ev_collect(false);
   }
@@ -447,8 +562,12 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
   if (c) c->timing_now = c->timing;
   if (!c || (!spec_ids && t)) return KB_E_INVALID;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
-  for (uint32_t i = 0; i < t; ++i)
+  for (uint32_t i = 0; i < t; ++i) {
     if (spec_ids[i] < 0 || spec_ids[i] >= c->P.m) return fail(c, KB_E_INVALID, "spec id %d", spec_ids[i]);
+    if (c->spec_needs_aff[spec_ids[i]] && !c->aff_ok)
+      return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first",
+                  spec_ids[i]);
+  }
   HIP_OK(c, hipSetDevice(c->device));
   const size_t n = (size_t)c->N.n;
   const uint32_t chunk = 8192;
@@ -464,8 +583,18 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
     const uint32_t cnt = std::min(chunk, t - b);
     if (hipMemcpyAsync(d_ids, spec_ids + b, cnt * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = KB_E_HIP;
     hipEvent_t ea;
+    if (c->aff_ok) {  // per-spec InterPodAffinity min / max first
+      if (c->mm_eval_cap < cnt) {
+        void* q;
+        if (hipMalloc(&q, (size_t)cnt * 2 * sizeof(int64_t)) != hipSuccess) { rc = KB_E_HIP; break; }
+        c->aff_mem.push_back(q);
+        c->mm_eval = (int64_t*)q;
+        c->mm_eval_cap = cnt;
+      }
+      launch_ipa_minmax(c->N, c->P, d_ids, 0, (int)cnt, c->mm_eval, nullptr, c->stream);
+    }
     c->ev_begin(&ea);
-    launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->stream);
+    launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
     c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
     if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
     if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))
@@ -486,6 +615,8 @@ int kb_restore_nodes(kb_ctx* c) {
   if (!c) return KB_E_INVALID;
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
   for (auto& col : c->pristine)
+    if (col.bytes) HIP_OK(c, hipMemcpyAsync(col.dst, col.src, col.bytes, hipMemcpyDeviceToDevice, c->stream));
+  for (auto& col : c->aff_pristine)
     if (col.bytes) HIP_OK(c, hipMemcpyAsync(col.dst, col.src, col.bytes, hipMemcpyDeviceToDevice, c->stream));
   return KB_OK;
 }

@@ -38,6 +38,14 @@ class kb_specs(C.Structure):
                 ("tolerates", P)]
 
 
+class kb_affinity(C.Structure):
+    _fields_ = [("n_slots", C.c_uint32), ("topo_dom", P), ("n_tables", C.c_uint32), ("tables", P), ("totals", P),
+                ("n_counters", C.c_uint32), ("counters", P), ("m", C.c_uint32), ("specs", P),
+                ("n_checks", C.c_uint32), ("checks", P), ("n_lister", C.c_uint32), ("lister", P),
+                ("n_hists", C.c_uint32), ("hists", P), ("n_h", C.c_uint32), ("h", P), ("n_incr", C.c_uint32),
+                ("incr", P)]
+
+
 class kb_config(C.Structure):
     _fields_ = [(f, C.c_int32) for f in ("predicates_enabled", "nodeorder_enabled", "mem_pressure", "disk_pressure",
                                           "pid_pressure", "w_lr", "w_bra", "w_na", "w_pa")]
@@ -74,19 +82,20 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 5), ("kernel_ms", C.c_double * 5), ("pairs", C.c_uint64 * 5),
+    _fields_ = [("launches", C.c_uint64 * 7), ("kernel_ms", C.c_double * 7), ("pairs", C.c_uint64 * 7),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
 KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
-KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel")
+KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
+           "aff_place_kernel", "ipa_minmax_kernel")
 
-ABI_VERSION = 2  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 3  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
-           "kb_get_stats"]
+           "kb_get_stats", "kb_upload_affinity"]
 
 _lib = None
 
@@ -116,6 +125,7 @@ def load_library(path: str = LIB_PATH):
     lib.kb_set_config.argtypes = [P, C.POINTER(kb_config)]
     lib.kb_upload_nodes.argtypes = [P, C.POINTER(kb_nodes)]
     lib.kb_upload_specs.argtypes = [P, C.POINTER(kb_specs)]
+    lib.kb_upload_affinity.argtypes = [P, C.POINTER(kb_affinity)]
     lib.kb_place_job.argtypes = [P, C.POINTER(kb_job_req), P, P, C.POINTER(kb_job_result)]
     lib.kb_eval.argtypes = [P, P, C.c_uint32, P, P]
     lib.kb_read_nodes.argtypes = [P] + [P] * 7
@@ -181,6 +191,16 @@ class Context:
                          len(snap.val_arr), _ptr(snap.val_arr), len(snap.port_arr), _ptr(snap.port_arr),
                          tol.shape[0], tol.shape[1], _ptr(tol))
         self._check(self.lib.kb_upload_specs(self.ctx, C.byref(specs)))
+        if snap.aff is not None:
+            a = snap.aff
+            arrs = [np.ascontiguousarray(x) for x in (a.topo_dom, a.table_arr, a.totals, a.counters, a.spec_arr,
+                                                      a.check_arr, a.lister_arr, a.hist_arr, a.h, a.incr_arr)]
+            self._keep.append(arrs)
+            td, tb, tot, cnt, sp, ck, ls, hs, h, inc = arrs
+            aff = kb_affinity(td.shape[0], _ptr(td), len(tb), _ptr(tb), _ptr(tot), len(cnt), _ptr(cnt), len(sp),
+                              _ptr(sp), len(ck), _ptr(ck), len(ls), _ptr(ls), len(hs), _ptr(hs), len(h), _ptr(h),
+                              len(inc), _ptr(inc))
+            self._check(self.lib.kb_upload_affinity(self.ctx, C.byref(aff)))
 
     def restore(self):
         self._check(self.lib.kb_restore_nodes(self.ctx))

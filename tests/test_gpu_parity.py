@@ -12,12 +12,12 @@ from scheduler_amd import export as E
 from scheduler_amd import model as m
 from scheduler_amd import runtime, synth
 
-from helpers import parity_clusters
+from helpers import affinity_clusters, parity_clusters
 from test_oracle_kat import allocate_test_cases
 
 pytestmark = pytest.mark.gpu
 
-CLUSTERS = parity_clusters()
+CLUSTERS = parity_clusters() + affinity_clusters()
 
 
 def _compare(ref, got):
@@ -113,3 +113,54 @@ def test_full_size_c2_properties():
     for j in range(len(snap.jobs)):
         k = placed[jobs == j].sum()
         assert k == (jobs == j).sum() or out1["job_fail_task"][j] >= 0
+
+
+def test_affinity_restore_reopens_tables():
+    """kb_restore_nodes also restores the affinity tables: two cycles from one upload agree."""
+    cl = affinity_clusters()[0][1]
+    snap = E.Snapshot(cl)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        a = ctx.allocate(snap)
+        ctx.restore()
+        b = ctx.allocate(snap)
+    finally:
+        ctx.close()
+    assert np.array_equal(a["task_node"], b["task_node"]) and np.array_equal(a["event_task"], b["event_task"])
+
+
+def test_c4_full_size_properties():
+    """BASELINE configs[3] (C4, 10k x 100k) at full size: hard inter-pod constraints hold in the result
+    (no two pods of a hostname-anti-affinity job share a node; svc-affinity pods land in svc zones) and
+    both device paths agree."""
+    cl = synth.c4()
+    snap = E.Snapshot(cl)
+    outs = []
+    for traj in (True, False):
+        ctx = runtime.Context(0, trajectory=traj)
+        try:
+            ctx.upload(snap)
+            outs.append(ctx.allocate(snap))
+        finally:
+            ctx.close()
+    assert np.array_equal(outs[0]["task_node"], outs[1]["task_node"])
+    tn = outs[0]["task_node"][: len(snap.session_tasks)]
+    assert (tn >= 0).sum() > 0.5 * len(snap.session_tasks)
+    names = snap.node_names()
+    svc_zones = {cl_node.labels["zone"] for p in cl.pods if p.labels.get("app") == "svc"
+                 for cl_node in [next(n for n in cl.nodes if n.name == p.node)]}
+    by_job = {}
+    for t, node in zip(snap.session_tasks, tn):
+        if node < 0 or t["status"] != E.ST["Pending"]:
+            continue
+        by_job.setdefault(t["pod"].group, []).append(node)
+        aff = t["pod"].affinity or {}
+        if "podAffinity" in aff and aff["podAffinity"].get("required"):
+            zone = next(n for n in cl.nodes if n.name == names[node]).labels["zone"]
+            assert zone in svc_zones
+    for t in snap.session_tasks:
+        aff = t["pod"].affinity or {}
+        if t["status"] == E.ST["Pending"] and "podAntiAffinity" in aff:
+            nodes = by_job.get(t["pod"].group, [])
+            assert len(nodes) == len(set(nodes)), t["pod"].group
