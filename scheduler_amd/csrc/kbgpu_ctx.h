@@ -25,6 +25,7 @@ struct kb_ctx {
   std::vector<char> spec_needs_aff;  // per spec: KB_SPEC_POD_AFFINITY / aff_class set
   std::vector<char> spec_dyn;   // per spec: KB_AFF_SELF_DYNAMIC -> block-wide re-sweep loop
   std::vector<char> spec_hist;  // per spec: has InterPodAffinity histograms
+  std::vector<char> spec_incr;  // per spec: its commits update affinity tables
   int64_t* mm_eval = nullptr;   // [2 * chunk] per-spec IPA min / max for kb_eval
   uint32_t mm_eval_cap = 0;
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec

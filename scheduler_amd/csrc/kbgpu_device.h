@@ -83,7 +83,7 @@ struct JobState {
 
 // Launch wrappers (kbgpu_device.hip).
 void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, uint64_t* keys,
-                       uint64_t* cmax, uint64_t* stat, const JobState* js, void* stream);
+                       uint64_t* cmax, uint64_t* stat, const JobState* js, bool aff, void* stream);
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
@@ -107,6 +107,9 @@ int configure_kernels();
 int traj_lds_bytes(int n, int t_count, int* pb_cap);
 void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
                        uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,
+                       bool aff, void* stream);
+// Table increments of a run placed by the trajectory / re-key loops (affinity specs with increments).
+void launch_aff_commit(const DevSpecs& P, int spec, int t_begin, int run, const JobState* js, const int32_t* hout,
                        void* stream);
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,

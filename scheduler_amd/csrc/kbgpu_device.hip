@@ -240,10 +240,12 @@ __device__ void apply_commit_tables(const DevAff& A, const kb_spec& sp, int w, i
 //   bits 60..63: InterPodAffinity priority (0..10)
 // `mm` (this spec's InterPodAffinity min / max) non-null: the spec's affinity inputs do not change
 // during its run, so the affinity predicate and priority are folded in here too.
+// AFF = false compiles the affinity lookups out (specs without inter-pod affinity: fewer live registers).
+template <bool AFF>
 __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
                                 uint32_t f, int n, const int64_t* mm) {
   uint32_t pre = 0, post = 0;
-  const bool aff = mm != nullptr && sp.aff_class >= 0;
+  const bool aff = AFF && mm != nullptr && sp.aff_class >= 0;
   if (C.predicates) {
     // CheckNodeConditionPredicate (vendor/.../predicates.go:1568-1596): one reason per bad condition
     pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
@@ -356,6 +358,7 @@ __device__ __forceinline__ uint64_t wave_max_dpp(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+template <bool AFF>
 __global__ __launch_bounds__(256) void sweep_keys_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, uint64_t* keys,
                                                          uint64_t* cmax, uint64_t* stat, const JobState* js) {
   if (js != nullptr && js->stopped) return;
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(256) void sweep_keys_kernel(DevNodes N, DevSpecs P,
   uint64_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? P.A.mm : nullptr);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
     stat[n] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, n);
     k = make_key(rs, rs ? 0 : row_score(C, sp, r, st), n);
@@ -642,7 +645,6 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
         const uint64_t e = pb[k];
         hout[2 * (pb_base + k)] = (int32_t)(uint32_t)e;
         hout[2 * (pb_base + k) + 1] = (int32_t)(uint32_t)(e >> 32);
-        apply_commit_tables(P.A, sp, (int)(uint32_t)e, (uint32_t)(e >> 32) == KB_PLACE_ALLOCATE, 1);
       }
       pb_base += pb_n;
       pb_n = 0;
@@ -656,14 +658,10 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
   }
 done:
   __syncthreads();
-  {
-    const kb_spec spb = P.specs[spec];
-    for (int k = tid; k < lo.pb_n; k += 512) {
-      const uint64_t v = pb[k];
-      hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
-      hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
-      apply_commit_tables(P.A, spb, (int)(uint32_t)v, (uint32_t)(v >> 32) == KB_PLACE_ALLOCATE, 1);
-    }
+  for (int k = tid; k < lo.pb_n; k += 512) {
+    const uint64_t v = pb[k];
+    hout[2 * (lo.pb_base + k)] = (int32_t)(uint32_t)v;
+    hout[2 * (lo.pb_base + k) + 1] = (int32_t)(uint32_t)(v >> 32);
   }
   __threadfence_system();
   __syncthreads();
@@ -672,6 +670,7 @@ done:
                   seq);
 }
 
+template <bool AFF>
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
                                                    uint32_t* reasons, int64_t* scores, const int64_t* mm) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -680,7 +679,7 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   const int s = spec_ids[j];
   const kb_spec sp = P.specs[s];
   const Row r = load_row(N, n);
-  const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? mm + 2 * j : nullptr);
+  const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, AFF ? mm + 2 * j : nullptr);
   reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
   scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
 }
@@ -805,6 +804,7 @@ __device__ __forceinline__ uint32_t compress_key(uint64_t k64, int n, int idx_bi
 }
 
 // grid (ceil(n/256), J+1): thread (node, j) writes the key after j commits.
+template <bool AFF>
 __global__ __launch_bounds__(256) void traj_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
                                                          uint32_t* traj, uint32_t* cmax32, uint32_t* amax,
                                                          uint64_t* stat, const JobState* js) {
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(256) void traj_sweep_kernel(DevNodes N, DevSpecs P,
   uint32_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval(N, P, C, sp, r.flags, n, P.A.enabled ? P.A.mm : nullptr);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
     const int A = allocs_before_full(N, sp, sci, scr, r, n);
     k = compress_key(traj_key64(N, P, C, sp, sci, scr, r, st, n, j, A), n, idx_bits);
     traj[(size_t)j * N.n + n] = k;
@@ -1055,9 +1055,7 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
   for (int w = tid; w < n; w += kPlaceThreads) {
     if (!((tb[w >> 6] >> (w & 63)) & 1)) continue;
     const uint32_t s = nc[w].y;
-    const int c = (int)(s & 0xffff), A = (int)(s >> 16);
-    write_back_row(N, P, sp, scr, w, c, A);
-    apply_commit_tables(P.A, sp, w, c < A ? c : A, c);  // the run's affinity inputs were static
+    write_back_row(N, P, sp, scr, w, (int)(s & 0xffff), (int)(s >> 16));
   }
   for (int k = tid; k < lo.pb_n; k += kPlaceThreads) {
     const uint32_t e = pb[k];
@@ -1140,6 +1138,18 @@ __global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, Dev
   }
 }
 
+// The table increments of a run placed by the trajectory / re-key loops (whose spec's own affinity
+// inputs do not move): one thread per placement of the run, read back from the placement buffer.
+__global__ __launch_bounds__(256) void aff_commit_kernel(DevSpecs P, int spec, int t_begin, int run,
+                                                         const JobState* js, const int32_t* hout) {
+  const int placed = js->n_placed - t_begin;  // placements of this run (tasks t_begin .. t_begin + run)
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= run || k >= placed) return;
+  const int w = hout[2 * (t_begin + k)];
+  const int kind = hout[2 * (t_begin + k) + 1];
+  apply_commit_tables(P.A, P.specs[spec], w, kind == KB_PLACE_ALLOCATE, 1);
+}
+
 // Key of node i for a spec whose affinity inputs move with its own commits: the cached base key (row
 // + static predicates + LR/BRA/NodeAffinity), then the inter-pod affinity predicate (the last one) and
 // the InterPodAffinity batch score from the live tables.
@@ -1183,7 +1193,7 @@ __global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
   for (int i = tid; i < n; i += kAffThreads) {  // base keys (no inter-pod affinity)
     const Row r = load_row(N, i);
-    const uint64_t st = static_eval(N, P, C, sp, r.flags, i, nullptr);
+    const uint64_t st = static_eval<false>(N, P, C, sp, r.flags, i, nullptr);
     stat[i] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
     base[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
@@ -1378,10 +1388,14 @@ int place_loop_lds_bytes(int n) {
 }
 
 void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, uint64_t* keys,
-                       uint64_t* cmax, uint64_t* stat, const JobState* js, void* stream) {
+                       uint64_t* cmax, uint64_t* stat, const JobState* js, bool aff, void* stream) {
   const int blocks = (N.n + 255) / 256;
-  hipLaunchKernelGGL(sweep_keys_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, C, spec, keys, cmax,
-                     stat, js);
+  if (aff)
+    hipLaunchKernelGGL(sweep_keys_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, C, spec, keys,
+                       cmax, stat, js);
+  else
+    hipLaunchKernelGGL(sweep_keys_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, C, spec, keys,
+                       cmax, stat, js);
 }
 
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
@@ -1425,10 +1439,20 @@ int traj_lds_bytes(int n, int t_count, int* pb_cap) {
 
 void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int J, int idx_bits,
                        uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,
-                       void* stream) {
+                       bool aff, void* stream) {
   dim3 grid((N.n + 255) / 256, J + 1);
-  hipLaunchKernelGGL(traj_sweep_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec, idx_bits, traj,
-                     cmax32, amax, stat, js);
+  if (aff)
+    hipLaunchKernelGGL(traj_sweep_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
+                       traj, cmax32, amax, stat, js);
+  else
+    hipLaunchKernelGGL(traj_sweep_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
+                       traj, cmax32, amax, stat, js);
+}
+
+void launch_aff_commit(const DevSpecs& P, int spec, int t_begin, int run, const JobState* js, const int32_t* hout,
+                       void* stream) {
+  hipLaunchKernelGGL(aff_commit_kernel, dim3((run + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, spec, t_begin,
+                     run, js, hout);
 }
 
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
@@ -1445,7 +1469,12 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
   dim3 grid((N.n + 255) / 256, t);
-  hipLaunchKernelGGL(eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons, scores, mm);
+  if (mm)
+    hipLaunchKernelGGL(eval_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons, scores,
+                       mm);
+  else
+    hipLaunchKernelGGL(eval_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons,
+                       scores, mm);
 }
 
 }  // namespace kbgpu

@@ -61,6 +61,7 @@ void drop_affinity(kb_ctx* c) {
   c->P.A = kbgpu::DevAff{};
   c->spec_dyn.clear();
   c->spec_hist.clear();
+  c->spec_incr.clear();
   c->mm_eval = nullptr;
   c->mm_eval_cap = 0;
 }
@@ -349,12 +350,14 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   if (a->m) HIP_OK(c, hipMemcpy(specs.data(), c->P.specs, a->m * sizeof(kb_spec), hipMemcpyDeviceToHost));
   c->spec_dyn.assign(a->m, 0);
   c->spec_hist.assign(a->m, 0);
+  c->spec_incr.assign(a->m, 0);
   for (uint32_t s = 0; s < a->m; ++s) {
     const int32_t ac = specs[s].aff_class;
     if (ac < -1 || ac >= (int32_t)a->m) return fail(c, KB_E_INVALID, "spec %u aff_class %d", s, ac);
     if (ac >= 0) {
       c->spec_dyn[s] = (a->specs[ac].flags & KB_AFF_SELF_DYNAMIC) != 0;
       c->spec_hist[s] = a->specs[ac].hist_cnt > 0;
+      c->spec_incr[s] = a->specs[ac].lister_cnt > 0 || a->specs[ac].incr_cnt > 0;
     }
   }
   DevAff& A = c->P.A;
@@ -489,7 +492,8 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     hipEvent_t ea;
     int pbc;
     const int run = (int)(e - t);
-    const bool dyn = c->aff_ok && c->spec_dyn[spec];
+    const bool aff = c->aff_ok && c->spec_needs_aff[spec];
+    const bool dyn = aff && c->spec_dyn[spec];
     const bool traj = !dyn && c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
     if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
       c->ev_begin(&ea);
@@ -505,7 +509,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
       launch_traj_sweep(c->N, c->P, c->cfg, spec, J, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
-                        first ? nullptr : js, c->stream);
+                        first ? nullptr : js, aff, c->stream);
       c->ev_end(ea, KB_KERNEL_TRAJ_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_traj_place(c->N, c->P, c->cfg, spec, (int)t, run, J, c->idx_bits, c->traj, c->cmax32, c->amax,
@@ -514,7 +518,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_end(ea, KB_KERNEL_TRAJ_PLACE, 0);
     } else {
       c->ev_begin(&ea);
-      launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, c->stream);
+      launch_sweep_keys(c->N, c->P, c->cfg, spec, c->keys, c->cmax, c->stat, first ? nullptr : js, aff, c->stream);
       c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_place_loop(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->cmax, c->stat, js, first,
@@ -522,6 +526,8 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
                         c->stream);
       c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     }
+    if (aff && !dyn && c->spec_incr[spec])  // this run's commits update other specs' affinity tables
+      launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, c->stream);
     t = e;
   }
   HIP_OK(c, hipGetLastError());
