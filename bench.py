@@ -27,7 +27,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-ROW_BYTES = 76          # algorithmic node-table bytes per (task, node) evaluation at C2
+# per configuration: generator defaults, algorithmic node-table bytes per (task, node) evaluation
+# (the row bytes the enabled predicate / score stages read) and the workload line
+CONFIGS = {
+    "C1": dict(nodes=1000, jobs=100, tasks=50, row_bytes=76,
+               workload="C1: 1k nodes x 5k pods in 100 gang jobs (the reference's CPU-runnable case)"),
+    "C2": dict(nodes=10000, jobs=1000, tasks=100, row_bytes=76,
+               workload="C2: 10k homogeneous nodes x 100k pods in 1k gang jobs, resource-fit + "
+                        "LeastRequested/Balanced (default tiers)"),
+    "C3": dict(nodes=20000, jobs=2000, tasks=100, row_bytes=124,
+               workload="C3: 20k heterogeneous nodes x 200k pods, GPU scalars, taints/tolerations, node affinity"),
+    "C4": dict(nodes=10000, jobs=1000, tasks=100, row_bytes=88,
+               workload="C4: 10k nodes x 100k pods, inter-pod (anti)affinity over hostname / zone / rack"),
+}
 
 
 def main():
@@ -35,9 +47,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nodes", type=int, default=10000)
-    ap.add_argument("--jobs", type=int, default=1000)
-    ap.add_argument("--tasks-per-job", type=int, default=100)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE.json configuration (C2 = the headline metric's)")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--tasks-per-job", type=int, default=None)
     ap.add_argument("--cpu-sample-tasks", type=int, default=3000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
@@ -45,6 +59,10 @@ def main():
                     help="HIP events around the launches of every Nth job call of the timed region")
     args = ap.parse_args()
 
+    cfg = CONFIGS[args.config]
+    args.nodes = args.nodes or cfg["nodes"]
+    args.jobs = args.jobs or cfg["jobs"]
+    args.tasks_per_job = args.tasks_per_job or cfg["tasks"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -59,7 +77,8 @@ def main():
     from scheduler_amd import export, runtime, synth
 
     # each rank: an independent cluster partition of the C2 shape (different seed per rank)
-    cl = synth.c2(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=synth.SEED + rank)
+    gen = synth.CONFIGS[args.config]
+    cl = gen(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=synth.SEED + rank)
     snap = export.Snapshot(cl)
     ctx = runtime.Context(local_rank, timing=not args.no_timing, timing_every=args.timing_every)
     ctx.upload(snap)
@@ -103,7 +122,7 @@ def main():
     k = int(np.argmax(st["kernel_ms"])) if any(st["kernel_ms"]) else 0
     launches = max(1, st["launches"][k])
     avg_ms = st["kernel_ms"][k] / launches
-    bytes_per_launch = st["pairs"][k] * ROW_BYTES / launches
+    bytes_per_launch = st["pairs"][k] * cfg["row_bytes"] / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": "hbm", "kernel": runtime.KERNELS[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -119,6 +138,9 @@ def main():
     if tr is not None:
         roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
 
+    workload = cfg["workload"]
+    if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
+        workload = f"{args.config} shape at {args.nodes} nodes x {args.jobs * args.tasks_per_job} pods"
     result = None
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -131,8 +153,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "p50_cycle_ms": round(statistics.median(times), 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (seeded C2 generator, SURVEY.md §8 d2)",
-            "config": {"workload": "C2: 10k homogeneous nodes x 100k pods in 1k gang jobs, resource-fit + "
-                                   "LeastRequested/Balanced (default tiers)",
+            "config": {"workload": workload,
                        "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
                        "pods_placed_per_cycle": placed // max(1, args.steps), "parallelism": f"replicas{world}"},
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
