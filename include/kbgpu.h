@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 3
+#define KBGPU_ABI_VERSION 4
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -348,7 +348,8 @@ int kb_restore_nodes(kb_ctx* ctx);
 
 /* Kernel timing (HIP events on the context's stream), enabled by KB_OPT_TIMING in kb_opts.flags. */
 #define KB_OPT_TIMING (1u << 0)
-#define KB_OPT_NO_TRAJECTORY (1u << 1) /* force the per-commit re-key loop (testing both device paths) */
+#define KB_OPT_NO_TRAJECTORY (1u << 1) /* no trajectory loop: the per-commit re-key loop (testing the device paths) */
+#define KB_OPT_NO_SELECT (1u << 2)     /* no top-T selection path: the trajectory loop (testing the device paths) */
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -356,7 +357,8 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_TRAJ_PLACE 4
 #define KB_KERNEL_AFF_PLACE 5 /* block-wide re-sweep loop (specs with self-dependent pod affinity) */
 #define KB_KERNEL_IPA_MINMAX 6
-#define KB_NUM_KERNELS 7
+#define KB_KERNEL_SEL_PLACE 7 /* a run as one parallel top-T selection (32-bit keys) */
+#define KB_NUM_KERNELS 8
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */

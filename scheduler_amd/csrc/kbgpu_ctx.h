@@ -38,7 +38,9 @@ struct kb_ctx {
   int idx_bits = 0;
   std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
   std::vector<int64_t> spec_pref_weight;
-  bool use_traj = true;
+  bool use_traj = true, use_sel = true;
+  bool traj_full = false;  // trajectory buffers (kTrajMaxJ + 1 levels): chunk maxima fit the place loop
+  bool sel_ok = false;     // the node count fits the selection kernel's LDS plan (level-0 keys buffer)
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
   uint32_t seq = 0;           // place launches issued (JobState::seq)
   char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)

@@ -1069,6 +1069,503 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
                   seq);
 }
 
+// ===========================================================================
+// Selection path (32-bit keys, sel_lds_bytes(n) >= 0): a run of same-spec tasks as a parallel top-T
+// selection instead of T dependent argmax steps.
+//
+// Within the run node x's key after j commits of the spec is k_x(j) (closed form, traj_key64), and the
+// reference's loop (SelectBestNode + commit, repeated: scheduler_helper.go:147-158, allocate.go:135-188)
+// is a greedy merge: take the largest current key, advance that node. Let e_x(j) = min_{i<=j} k_x(i).
+// The e-values of the successive picks never increase (DESIGN.md §3 has the argument), so the picks are
+// exactly the elements (x, j) in descending (e, then node ascending, then j ascending) order — node
+// indices are part of the key, so e-values of different nodes never tie. Per segment of T <= kSegMax
+// tasks the kernel therefore
+//   1. takes S = the T nodes with the largest current key (binary search on the score field, lowest
+//      index first on the threshold score): an element (x, j) ranks at least j + rank_S(x), so no node
+//      outside S and no level j >= T - rank_S(x) can be among the first T picks;
+//   2. generates every S node's e-sequence over those levels, in parallel rounds;
+//   3. finds the T-th largest element (binary search again), orders the T winners, and applies the
+//      stop rules in that order: panic (score <= -1), gang ready (allocate.go:184-187), no fit;
+//   4. writes the placements and the touched rows back and re-keys the touched nodes for the next
+//      segment.
+// ===========================================================================
+constexpr int kSelThreads = 1024;
+constexpr int kSelWaves = kSelThreads / 64;
+constexpr int kSegMax = 127;                           // slot and level fit 7-bit fields
+constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
+
+struct SelShared {
+  Row row[128];            // segment-start rows of the selected nodes
+  uint64_t stat[128];
+  uint64_t comp[128];      // (e << 14 | (127 - slot) << 7 | (127 - level)) of the taken elements
+  uint64_t ord[128];       // the same, in pick order
+  int32_t node[128];
+  uint32_t key0[128];      // current key of the selected node
+  int32_t A[128];          // Allocates before InitResreq stops fitting Idle
+  int32_t lmax[128];       // levels that can rank below T: T - rank
+  int32_t off[128];        // into the candidate array
+  int32_t cnt[128];        // e-values kept (all feasible, and >= the cut-off when S fills the segment)
+  int32_t gen[128];        // levels examined
+  uint32_t emin[128];      // running prefix minimum
+  int32_t done[128];
+  int32_t fin[128];        // commits of this node in the segment
+  int32_t act[128];        // active slots of a generation round
+  uint32_t raw[kSelThreads];
+  uint32_t red[3][kSelWaves];
+  uint32_t hist[KB_NUM_REASONS];
+  uint32_t theta0;
+  int32_t n_act, s_count, cut, stop_kind, n_alloc;
+  LoopOut lo;
+};
+constexpr int kSelDynLimit = 160 * 1024 - (int)sizeof(SelShared) - 64;
+
+__device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = umax32(v, (uint32_t)__shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = (uint32_t)__shfl_xor(v, o, 64);
+    v = x < v ? x : v;
+  }
+  return v;
+}
+
+// Block-wide sum / max / min (every thread gets the three results).
+__device__ __forceinline__ void sel_reduce3(SelShared& sh, uint32_t& s, uint32_t& mx, uint32_t& mn) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  s = wave_sum_u32(s);
+  mx = wave_max_u32(mx);
+  mn = wave_min_u32(mn);
+  if (lane == 0) {
+    sh.red[0][wv] = s;
+    sh.red[1][wv] = mx;
+    sh.red[2][wv] = mn;
+  }
+  __syncthreads();
+  s = 0, mx = 0, mn = 0xffffffffu;
+  for (int w = 0; w < kSelWaves; ++w) {
+    s += sh.red[0][w];
+    mx = umax32(mx, sh.red[1][w]);
+    mn = sh.red[2][w] < mn ? sh.red[2][w] : mn;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ uint32_t sel_sum(SelShared& sh, uint32_t v) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_sum_u32(v);
+  if (lane == 0) sh.red[0][wv] = v;
+  __syncthreads();
+  uint32_t s = 0;
+  for (int w = 0; w < kSelWaves; ++w) s += sh.red[0][w];
+  __syncthreads();
+  return s;
+}
+// Block-wide exclusive prefix sum in thread order; *total = the sum over the block.
+__device__ __forceinline__ uint32_t sel_excl_scan(SelShared& sh, uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t x = wave_excl_scan_u32(v, lane);
+  if (lane == 63) sh.red[0][wv] = x + v;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (int w = 0; w < kSelWaves; ++w) {
+    const uint32_t r = sh.red[0][w];
+    base += w < wv ? r : 0;
+    tot += r;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x;
+}
+
+// Elements of slot s's candidate list whose score field is >= v (the list is non-increasing).
+__device__ __forceinline__ uint32_t sel_cnt_ge(const SelShared& sh, const uint32_t* cand, int s, int S, uint32_t v,
+                                               int idx_bits) {
+  if (s >= S) return 0;
+  uint32_t lo = 0, hi = (uint32_t)sh.cnt[s];
+  const uint32_t* c = cand + sh.off[s];
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((c[mid] >> idx_bits) >= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int sel_slot(uint64_t o) { return 127 - (int)((o >> 7) & 127); }
+__device__ __forceinline__ int sel_level(uint64_t o) { return 127 - (int)(o & 127); }
+
+__global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
+    const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
+    uint32_t seq) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ SelShared sh;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = N.n;
+  uint32_t* k32 = lds32;       // [n] current key of every node
+  uint32_t* cand = lds32 + n;  // [kCandMax] e-values, one contiguous list per selected node
+  const kb_spec sp = P.specs[spec];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const int64_t bias32 = 1ll << (30 - idx_bits);
+  const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
+  for (int i = tid; i < n; i += kSelThreads) k32[i] = keys32[i];
+  int ready = first ? ready0 : js->ready_num;
+  const int minav = first ? minav0 : js->min_available;
+  const int gang = first ? gang0 : js->gang_ready;
+  int placed = first ? 0 : js->n_placed;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  // contiguous node range per thread: index order decides the lowest-index tie-break
+  const int Q = (n + kSelThreads - 1) / kSelThreads;
+  const int i0 = tid * Q < n ? tid * Q : n, i1 = i0 + Q < n ? i0 + Q : n;
+  const uint64_t lt = (1ull << lane) - 1;
+  __syncthreads();
+
+  int done_tasks = 0;
+  while (done_tasks < t_count) {
+    const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
+    // ---- 1. S = the T best nodes by current key ----
+    uint32_t F = 0, MX = 0, MN = 0xffffffffu;
+    for (int i = i0; i < i1; ++i) {
+      const uint32_t k = k32[i];
+      if (k >> 31) {
+        ++F;
+        const uint32_t h = k >> idx_bits;
+        MX = umax32(MX, h);
+        MN = h < MN ? h : MN;
+      }
+    }
+    sel_reduce3(sh, F, MX, MN);
+    bool no_fit = F == 0;
+    if (!no_fit) {
+      // infeasible keys have a score field below every feasible one: never counted below
+      uint32_t sstar = MN, R = 0xffffffffu;  // F <= T: every feasible node
+      if (F > T) {
+        uint32_t lo = MN, hi = MX;
+        while (lo < hi) {
+          const uint32_t mid = lo + (hi - lo + 1) / 2;
+          uint32_t c = 0;
+          for (int i = i0; i < i1; ++i) c += (k32[i] >> idx_bits) >= mid;
+          if (sel_sum(sh, c) >= T) lo = mid;
+          else hi = mid - 1;
+        }
+        sstar = lo;
+        uint32_t gt = 0;
+        for (int i = i0; i < i1; ++i) gt += (k32[i] >> idx_bits) > sstar;
+        R = T - sel_sum(sh, gt);
+      }
+      uint32_t g = 0, e = 0, tot, S;
+      for (int i = i0; i < i1; ++i) {
+        const uint32_t h = k32[i] >> idx_bits;
+        g += h > sstar;
+        e += h == sstar;
+      }
+      const uint32_t E = sel_excl_scan(sh, e, &tot);
+      const uint32_t selE = R > E ? (R - E < e ? R - E : e) : 0u;
+      uint32_t slot = sel_excl_scan(sh, g + selE, &S);
+      uint32_t le = 0;
+      for (int i = i0; i < i1; ++i) {
+        const uint32_t k = k32[i];
+        const uint32_t h = k >> idx_bits;
+        bool take = h > sstar;
+        if (h == sstar) take = le++ < selE;
+        if (take) {
+          sh.node[slot] = i;
+          sh.key0[slot] = k;
+          ++slot;
+        }
+      }
+      __syncthreads();
+      // ---- 2. selected nodes: rows, A, rank, candidate offsets ----
+      if (tid < (int)S) {
+        const int w = sh.node[tid];
+        const Row r = load_row(N, w);
+        sh.row[tid] = r;
+        sh.stat[tid] = stat[w];
+        sh.A[tid] = allocs_before_full(N, sp, sci, scr, r, w);
+        sh.cnt[tid] = 0;
+        sh.gen[tid] = 0;
+        sh.emin[tid] = 0xffffffffu;
+        sh.fin[tid] = 0;
+        sh.done[tid] = 0;
+        const uint32_t k = sh.key0[tid];
+        uint32_t rk = 0;
+        for (uint32_t q = 0; q < S; ++q) rk += sh.key0[q] > k;
+        sh.lmax[tid] = (int)(T - rk);
+        if (rk == S - 1) sh.theta0 = k;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        const uint32_t a = lane < (int)S ? (uint32_t)sh.lmax[lane] : 0u;
+        const uint32_t b = lane + 64 < (int)S ? (uint32_t)sh.lmax[lane + 64] : 0u;
+        const uint32_t ea = wave_excl_scan_u32(a, lane), ta = wave_sum_u32(a);
+        const uint32_t eb = wave_excl_scan_u32(b, lane);
+        sh.off[lane] = (int32_t)ea;
+        sh.off[lane + 64] = (int32_t)(ta + eb);
+      }
+      // ---- 3. e-sequences of the selected nodes: rounds of 8 levels per node (64 once <= 16 remain) ----
+      const bool cut0 = S == T;  // level 0 of S fills the segment: elements below theta0 cannot rank < T
+      for (;;) {
+        __syncthreads();
+        if (wv == 0) {
+          const bool a0 = lane < (int)S && !sh.done[lane];
+          const bool a1 = lane + 64 < (int)S && !sh.done[lane + 64];
+          const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+          const int c0 = __popcll(m0);
+          if (a0) sh.act[__popcll(m0 & lt)] = lane;
+          if (a1) sh.act[c0 + __popcll(m1 & lt)] = lane + 64;
+          if (lane == 0) sh.n_act = c0 + __popcll(m1);
+        }
+        __syncthreads();
+        const int na = sh.n_act;
+        if (na == 0) break;
+        const int shift = na <= 16 ? 6 : 3;
+        const int q = tid >> shift, u = tid & ((1 << shift) - 1);
+        if (q < na) {
+          const int s = sh.act[q];
+          const int j = sh.gen[s] + u;
+          if (j < sh.lmax[s]) {
+            uint32_t raw = sh.key0[s];
+            if (j > 0) {
+              const int w = sh.node[s];
+              raw = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w,
+                                 idx_bits);
+            }
+            sh.raw[tid] = raw;
+          }
+        }
+        __syncthreads();
+        if (tid < na) {  // thread q scans the new levels of active node q in order
+          const int s = sh.act[tid];
+          const int L = 1 << shift;
+          const uint32_t* rw = sh.raw + (tid << shift);
+          int j = sh.gen[s], c = sh.cnt[s], fin = 0;
+          uint32_t em = sh.emin[s];
+          const int lm = sh.lmax[s];
+          uint32_t* out = cand + sh.off[s];
+          const uint32_t th = sh.theta0;
+          for (int v = 0; v < L; ++v, ++j) {
+            if (j >= lm) {
+              fin = 1;
+              break;
+            }
+            const uint32_t r = rw[v];
+            const uint32_t ee = r < em ? r : em;
+            if (!(ee >> 31) || (cut0 && ee < th)) {  // e never increases: the node is finished
+              fin = 1;
+              break;
+            }
+            out[c++] = ee;
+            em = ee;
+          }
+          sh.gen[s] = j;
+          sh.cnt[s] = c;
+          sh.emin[s] = em;
+          if (fin) sh.done[s] = 1;
+        }
+      }
+      // ---- 4. the T winners, in pick order ----
+      if (wv == 0) {
+        const int a = lane, b = lane + 64;
+        const uint32_t ca = a < (int)S ? (uint32_t)sh.cnt[a] : 0u, cb = b < (int)S ? (uint32_t)sh.cnt[b] : 0u;
+        const uint32_t K = wave_sum_u32(ca + cb);
+        uint32_t ta = ca, tb = cb;
+        if (K > T) {
+          uint32_t hmax = 0, hmin = 0xffffffffu;
+          if (ca) {
+            hmax = cand[sh.off[a]] >> idx_bits;
+            hmin = cand[sh.off[a] + ca - 1] >> idx_bits;
+          }
+          if (cb) {
+            hmax = umax32(hmax, cand[sh.off[b]] >> idx_bits);
+            const uint32_t x = cand[sh.off[b] + cb - 1] >> idx_bits;
+            hmin = x < hmin ? x : hmin;
+          }
+          uint32_t lo = wave_min_u32(hmin), hi = wave_max_u32(hmax);
+          while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo + 1) / 2;
+            const uint32_t c = wave_sum_u32(sel_cnt_ge(sh, cand, a, S, mid, idx_bits) +
+                                            sel_cnt_ge(sh, cand, b, S, mid, idx_bits));
+            if (c >= T) lo = mid;
+            else hi = mid - 1;
+          }
+          const uint32_t ga = sel_cnt_ge(sh, cand, a, S, lo + 1, idx_bits);
+          const uint32_t gb = sel_cnt_ge(sh, cand, b, S, lo + 1, idx_bits);
+          const uint32_t qa = sel_cnt_ge(sh, cand, a, S, lo, idx_bits) - ga;
+          const uint32_t qb = sel_cnt_ge(sh, cand, b, S, lo, idx_bits) - gb;
+          const uint32_t R2 = T - wave_sum_u32(ga + gb);
+          // ties on the threshold score: lower slot (= lower node index) first, then lower level
+          const uint32_t Ea = wave_excl_scan_u32(qa, lane), Qa = wave_sum_u32(qa);
+          const uint32_t Eb = Qa + wave_excl_scan_u32(qb, lane);
+          ta = ga + (R2 > Ea ? (R2 - Ea < qa ? R2 - Ea : qa) : 0u);
+          tb = gb + (R2 > Eb ? (R2 - Eb < qb ? R2 - Eb : qb) : 0u);
+        }
+        const uint32_t pa = wave_excl_scan_u32(ta, lane), Ta = wave_sum_u32(ta);
+        const uint32_t pb = Ta + wave_excl_scan_u32(tb, lane);
+        for (uint32_t j = 0; j < ta; ++j)
+          sh.comp[pa + j] = ((uint64_t)cand[sh.off[a] + j] << 14) | ((uint64_t)(127 - a) << 7) | (127 - j);
+        for (uint32_t j = 0; j < tb; ++j)
+          sh.comp[pb + j] = ((uint64_t)cand[sh.off[b] + j] << 14) | ((uint64_t)(127 - b) << 7) | (127 - j);
+        const uint32_t Kp = K < T ? K : T;
+        for (uint32_t p = Kp + lane; p < 128; p += 64) sh.comp[p] = 0;
+        if (lane == 0) sh.s_count = (int)Kp;
+      }
+      __syncthreads();
+      {  // rank of every taken element, 8 threads per element (composites are distinct and nonzero)
+        const int e2 = tid >> 3, part = tid & 7;
+        const uint64_t v = sh.comp[e2];
+        uint32_t c = 0;
+        for (int q2 = part * 16; q2 < part * 16 + 16; ++q2) c += sh.comp[q2] > v;
+        c += __shfl_xor(c, 1, 64);
+        c += __shfl_xor(c, 2, 64);
+        c += __shfl_xor(c, 4, 64);
+        if (part == 0 && e2 < sh.s_count) sh.ord[c] = v;
+      }
+      __syncthreads();
+      // ---- stop rules in pick order (wave 0) ----
+      if (wv == 0) {
+        const int Kp = sh.s_count;
+        const bool va = lane < Kp, vb = lane + 64 < Kp;
+        const uint64_t oa = sh.ord[lane], ob = sh.ord[lane + 64];
+        const bool aa = va && sel_level(oa) < sh.A[sel_slot(oa)];
+        const bool ab = vb && sel_level(ob) < sh.A[sel_slot(ob)];
+        const auto neg = [&](uint64_t o) {
+          const uint32_t e32 = (uint32_t)(o >> 14);
+          return (int64_t)((e32 >> idx_bits) & score_mask) - bias32 <= -1;
+        };
+        const uint64_t le_mask = lt | (1ull << lane);
+        const uint64_t ma = __ballot(aa), mb = __ballot(ab);
+        const int ra = ready + __popcll(ma & le_mask);
+        const int rb = ready + __popcll(ma) + __popcll(mb & le_mask);
+        const uint64_t sta = __ballot(va && (!gang || ra >= minav));
+        const uint64_t stb = __ballot(vb && (!gang || rb >= minav));
+        const uint64_t nga = __ballot(va && neg(oa)), ngb = __ballot(vb && neg(ob));
+        const int first_stop = sta ? __builtin_ctzll(sta) : (stb ? 64 + __builtin_ctzll(stb) : 128);
+        const int first_neg = nga ? __builtin_ctzll(nga) : (ngb ? 64 + __builtin_ctzll(ngb) : 128);
+        int cut, kind;
+        if (first_neg < Kp && first_neg <= first_stop) {
+          cut = first_neg;  // SelectBestNode finds no score > -1 there: the reference panics
+          kind = 3;
+        } else if (first_stop < Kp) {
+          cut = first_stop + 1;
+          kind = KB_STOP_READY;
+        } else if (Kp < (int)T) {
+          cut = Kp;
+          kind = KB_STOP_NO_FIT;
+        } else {
+          cut = (int)T;
+          kind = -1;  // segment done, the run goes on
+        }
+        const int al = __popcll(cut >= 64 ? ma : (ma & ((1ull << cut) - 1))) +
+                       (cut > 64 ? __popcll(mb & ((1ull << (cut - 64)) - 1)) : 0);
+        if (lane == 0) {
+          sh.cut = cut;
+          sh.stop_kind = kind;
+          sh.n_alloc = al;
+        }
+      }
+      __syncthreads();
+      // ---- commit: placements, rows, keys ----
+      const int cut = sh.cut;
+      if (tid < cut) {
+        const uint64_t o = sh.ord[tid];
+        const int s = sel_slot(o), j = sel_level(o);
+        atomicAdd(&sh.fin[s], 1);
+        const int at = t_begin + done_tasks + tid;
+        hout[2 * at] = sh.node[s];
+        hout[2 * at + 1] = j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+      }
+      __syncthreads();
+      if (tid < (int)S && sh.fin[tid] > 0) {
+        const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
+        write_back_row(N, P, sp, scr, w, c, A);
+        k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w, idx_bits);
+      }
+      __syncthreads();
+      ready += sh.n_alloc;
+      placed += cut;
+      done_tasks += cut;
+      const int kind = sh.stop_kind;
+      if (kind == 3) {
+        fail_task = t_begin + done_tasks;
+        panic = 1;
+        stopped = 1;
+        break;
+      }
+      if (kind == KB_STOP_READY) {
+        stop = KB_STOP_READY;
+        stopped = 1;
+        break;
+      }
+      no_fit = kind == KB_STOP_NO_FIT;
+    }
+    if (no_fit) {
+      // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes at their
+      // current keys (an infeasible key is its reason mask).
+      if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
+      __syncthreads();
+      uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+      for (int i = i0; i < i1; ++i) {
+        const uint32_t k = k32[i];
+        if (k >> 31) continue;
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k >> b) & 1u;
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) {
+        const uint32_t v = wave_sum_u32(h[b]);
+        if (lane == 0 && v) atomicAdd(&sh.hist[b], v);
+      }
+      __syncthreads();
+      if (tid < KB_NUM_REASONS) {
+        js->hist[tid] = sh.hist[tid];
+        hjs->hist[tid] = sh.hist[tid];
+      }
+      stop = KB_STOP_NO_FIT;
+      fail_task = t_begin + done_tasks;
+      stopped = 1;
+      break;
+    }
+  }
+  if (tid == 0) sh.lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, 0, 0, 0, 0};
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0)
+    publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
+                  sh.lo.gang, sh.lo.panic, seq);
+}
+
+int sel_lds_bytes(int n) {
+  const long bytes = 4l * ((long)n + kCandMax);
+  return bytes <= kSelDynLimit ? (int)bytes : -1;
+}
+
+void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                      int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
+                      int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+  hipLaunchKernelGGL(sel_place_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P, C,
+                     spec, t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs,
+                     seq);
+}
+
 // ---------------------------------------------------------------------------
 // ===========================================================================
 // Inter-pod affinity kernels.
@@ -1421,6 +1918,9 @@ int configure_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit);
     if (e != hipSuccess) return (int)e;
   }
+  hipError_t e = hipFuncSetAttribute((const void*)sel_place_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kSelDynLimit);
+  if (e != hipSuccess) return (int)e;
   return 0;
 }
 

@@ -121,6 +121,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
+  c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
   if (hipSetDevice(c->device) != hipSuccess) {
     c->err = "hipSetDevice failed";
     c->broken = true;
@@ -223,8 +224,11 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   c->idx_bits = 1;
   while ((1ull << c->idx_bits) < (unsigned long long)n) ++c->idx_bits;
   int pbc;
-  if (traj_lds_bytes((int)n, 64, &pbc) > 0) {
-    HIP_OK(c, hipMalloc(&p, (size_t)(kTrajMaxJ + 1) * n * sizeof(uint32_t)));
+  c->traj_full = traj_lds_bytes((int)n, 64, &pbc) > 0;
+  c->sel_ok = sel_lds_bytes((int)n) >= 0;
+  if (c->traj_full || c->sel_ok) {  // trajectory levels, or level 0 only (the selection path's keys)
+    const size_t levels = c->traj_full ? (size_t)kTrajMaxJ + 1 : 1;
+    HIP_OK(c, hipMalloc(&p, levels * n * sizeof(uint32_t)));
     c->work_mem.push_back(p);
     c->traj = (uint32_t*)p;
     HIP_OK(c, hipMalloc(&p, ((n + 63) / 64 + 4) * sizeof(uint32_t)));
@@ -237,6 +241,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
     c->traj = nullptr;
   }
   c->nodes_ok = true;
+  kb_update_traj_ok(c);  // key widths depend on the node count
   return KB_OK;
 }
 
@@ -402,7 +407,7 @@ void kb_update_traj_ok(kb_ctx* c) {
     long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
                         (long double)c->spec_pref_weight[i] * std::llabs((long long)C.w_na) +
                         10.0L * std::llabs((long long)C.w_pa);
-    c->spec_traj_ok[i] = c->traj != nullptr && bound < bias32 - 1;
+    c->spec_traj_ok[i] = bound < bias32 - 1;
   }
 }
 
@@ -494,7 +499,9 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     const int run = (int)(e - t);
     const bool aff = c->aff_ok && c->spec_needs_aff[spec];
     const bool dyn = aff && c->spec_dyn[spec];
-    const bool traj = !dyn && c->use_traj && c->spec_traj_ok[spec] && traj_lds_bytes(c->N.n, run, &pbc) > 0;
+    const bool key32 = c->spec_traj_ok[spec] && c->traj != nullptr;
+    const bool sel = !dyn && c->use_sel && key32 && c->sel_ok;
+    const bool traj = !sel && !dyn && c->use_traj && key32 && c->traj_full && traj_lds_bytes(c->N.n, run, &pbc) > 0;
     if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
       c->ev_begin(&ea);
       launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->P.A.mm, first ? nullptr : js, c->stream);
@@ -505,6 +512,15 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       launch_aff_place(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->stat, js, first, job->ready_num,
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
+    } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
+      c->ev_begin(&ea);
+      launch_traj_sweep(c->N, c->P, c->cfg, spec, 0, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
+                        first ? nullptr : js, aff, c->stream);
+      c->ev_end(ea, KB_KERNEL_TRAJ_SWEEP, (uint64_t)c->N.n);
+      c->ev_begin(&ea);
+      launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, c->traj, c->stat, js, first,
+                       job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
+      c->ev_end(ea, KB_KERNEL_SEL_PLACE, 0);
     } else if (traj) {
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
@@ -546,7 +562,11 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
     for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
       auto& p = c->pending[k];
-      if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE) { p.pairs = tasks * (uint64_t)c->N.n; tasks = 0; }
+      if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE ||
+          p.kind == KB_KERNEL_SEL_PLACE) {
+        p.pairs = tasks * (uint64_t)c->N.n;
+        tasks = 0;
+      }
     }
     c->ev_collect(false);
   }

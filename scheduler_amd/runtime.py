@@ -82,16 +82,22 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 7), ("kernel_ms", C.c_double * 7), ("pairs", C.c_uint64 * 7),
+    _fields_ = [("launches", C.c_uint64 * 8), ("kernel_ms", C.c_double * 8), ("pairs", C.c_uint64 * 8),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
 KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
+KB_OPT_NO_SELECT = 4
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
-           "aff_place_kernel", "ipa_minmax_kernel")
+           "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel")
+# device paths for a run of same-spec tasks (kb_place_job picks the first one that applies):
+#   select     - one parallel top-T selection per run (sel_place_kernel)
+#   trajectory - precomputed per-node key trajectories + a one-wave argmax loop (traj_place_kernel)
+#   rekey      - 64-bit keys, per-commit re-key + one-wave argmax loop (place_loop_kernel)
+PATHS = {"select": 0, "trajectory": KB_OPT_NO_SELECT, "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 3  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 4  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -143,11 +149,10 @@ def _ptr(a):
 class Context:
     """One device-resident session snapshot (kb_ctx)."""
 
-    def __init__(self, device: int = 0, timing: bool = False, trajectory: bool = True, timing_every: int = 1):
+    def __init__(self, device: int = 0, timing: bool = False, path: str = "select", timing_every: int = 1):
         self.lib = load_library()
         self._keep = []
-        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | (0 if trajectory else KB_OPT_NO_TRAJECTORY),
-                       timing_every)
+        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | PATHS[path], timing_every)
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
             raise KbError(KB_E_HIP, "kb_create failed")
@@ -294,10 +299,10 @@ def result_dict(snap: E.Snapshot, out: dict) -> dict:
             "elapsed_ms": out["elapsed_ms"], "device_ms": out["device_ms"]}
 
 
-def allocate(cluster, device: int = 0, trajectory: bool = True) -> dict:
+def allocate(cluster, device: int = 0, path: str = "select") -> dict:
     """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle."""
     snap = E.Snapshot(cluster)
-    ctx = Context(device, trajectory=trajectory)
+    ctx = Context(device, path=path)
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)

@@ -17,7 +17,7 @@ step() {  # step <name> <timeout-seconds> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step gpu_tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then

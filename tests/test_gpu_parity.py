@@ -29,12 +29,13 @@ def _compare(ref, got):
         assert ref["status"][uid] == st, uid
 
 
-@pytest.mark.parametrize("trajectory", [True, False], ids=["trajectory", "rekey"])
+@pytest.mark.parametrize("path", list(runtime.PATHS))
 @pytest.mark.parametrize("name,cluster", CLUSTERS, ids=[c[0] for c in CLUSTERS])
-def test_allocate_parity(name, cluster, trajectory):
-    """Both device paths: precomputed per-node key trajectories, and the per-commit re-key loop."""
+def test_allocate_parity(name, cluster, path):
+    """Every device path: the top-T selection, precomputed per-node key trajectories with a one-wave
+    argmax loop, and the per-commit re-key loop."""
     ref = pyoracle.allocate(cluster)
-    got = runtime.allocate(cluster, trajectory=trajectory)
+    got = runtime.allocate(cluster, path=path)
     _compare(ref, got)
     assert len(got["events"]) > 0
 
@@ -83,16 +84,19 @@ def test_full_size_c2_properties():
         out2 = ctx.allocate(snap)
     finally:
         ctx.close()
-    ctx = runtime.Context(0, trajectory=False)
-    try:
-        ctx.upload(snap)
-        out3 = ctx.allocate(snap)
-    finally:
-        ctx.close()
+    others = []
+    for path in ("trajectory", "rekey"):
+        ctx = runtime.Context(0, path=path)
+        try:
+            ctx.upload(snap)
+            others.append(ctx.allocate(snap))
+        finally:
+            ctx.close()
     assert np.array_equal(out1["task_node"], out2["task_node"])          # deterministic
     assert np.array_equal(out1["event_task"], out2["event_task"])
-    assert np.array_equal(out1["task_node"], out3["task_node"])          # both device paths agree
-    assert np.array_equal(out1["event_task"], out3["event_task"])
+    for out3 in others:                                                  # every device path agrees
+        assert np.array_equal(out1["task_node"], out3["task_node"])
+        assert np.array_equal(out1["event_task"], out3["event_task"])
     placed = out1["task_node"][: len(snap.session_tasks)] >= 0
     assert placed.sum() == out1["n_events"] > 0.9 * len(snap.session_tasks)
     # conservation: idle = allocatable - sum(resreq of tasks placed there)  (NodeInfo.AddTask)
@@ -137,14 +141,15 @@ def test_c4_full_size_properties():
     cl = synth.c4()
     snap = E.Snapshot(cl)
     outs = []
-    for traj in (True, False):
-        ctx = runtime.Context(0, trajectory=traj)
+    for path in runtime.PATHS:
+        ctx = runtime.Context(0, path=path)
         try:
             ctx.upload(snap)
             outs.append(ctx.allocate(snap))
         finally:
             ctx.close()
-    assert np.array_equal(outs[0]["task_node"], outs[1]["task_node"])
+    for o in outs[1:]:
+        assert np.array_equal(outs[0]["task_node"], o["task_node"])
     tn = outs[0]["task_node"][: len(snap.session_tasks)]
     assert (tn >= 0).sum() > 0.5 * len(snap.session_tasks)
     names = snap.node_names()
