@@ -157,7 +157,8 @@ def main():
                        "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
                        "pods_placed_per_cycle": placed // max(1, args.steps), "parallelism": f"replicas{world}"},
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
-            **({"diag_place_phases": diag_summary(st["diag"], placed)} if any(st["diag"]) else {}),
+            **({"diag_place_phases": diag_summary(st["diag"], placed, runtime.KERNELS[k])}
+               if any(st["diag"]) else {}),
             "job_calls_per_step": st["job_calls"] / args.steps,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -183,9 +184,16 @@ def pmc_traffic(kernel):
     return None
 
 
-def diag_summary(d, tasks):
-    """Per-task shader cycles of each place-loop phase (KB_DIAG builds) and the implied clock."""
-    names = ["argmax", "commit", "rereduce", "lmax", "prefetch_store", "loop", "fill"]  # traj_place_kernel
+DIAG_PHASES = {
+    "traj_place_kernel": ["argmax", "commit", "rereduce", "lmax", "prefetch_store", "loop", "fill"],
+    "sel_place_kernel": ["key_load", "node_select", "node_setup", "e_sequences", "winners_order", "stop_commit",
+                         "nofit_hist"],
+}
+
+
+def diag_summary(d, tasks, kernel):
+    """Per-task shader cycles of each place-kernel phase (KB_DIAG builds) and the implied clock."""
+    names = DIAG_PHASES.get(kernel, [f"phase{i}" for i in range(7)])
     clock_mhz = d[7] and (sum(d[:7]) / (d[7] / 100.0))
     return {"cycles_per_task": {n: round(d[i] / max(1, tasks), 1) for i, n in enumerate(names)},
             "fill_cycles_total": d[6],

@@ -103,8 +103,10 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                       int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
-// keys of launch_traj_sweep(J = 0). sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.
+// keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.
 int sel_lds_bytes(int n);
+void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
+                      uint64_t* stat, const JobState* js, bool aff, void* stream);
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);

@@ -430,6 +430,19 @@ __device__ __forceinline__ void signal_skip(JobState* hjs, uint32_t seq) {
   } while (0)
 #endif
 
+
+// Selection-kernel stamps: KB_DIAG gives its 7 phases; KB_DIAG_SEL splits node selection finer
+// (0 key load, 1 reduce, 2 threshold search, 3 scans, 4 compaction, 5 the rest of the segment).
+#if defined(KB_DIAG_SEL)
+#define KB_SEL_PH(k) KB_STAMP((k) == 0 ? 0 : (k) == 1 ? 4 : (k) == 6 ? 6 : 5)
+#define KB_SEL_FINE(k) KB_STAMP(k)
+#else
+#define KB_SEL_PH(k) KB_STAMP(k)
+#define KB_SEL_FINE(k) \
+  do {                 \
+  } while (0)
+#endif
+
 // Copy the buffered placements to the caller's pinned host buffer (coalesced, once per run / buffer).
 __device__ __forceinline__ void flush_placements(const uint64_t* pb, int cnt, int base, int32_t* hout, int lane) {
   __syncthreads();
@@ -1093,6 +1106,9 @@ constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kSegMax = 127;                           // slot and level fit 7-bit fields
 constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
+constexpr int kCandCap = 8192;                         // candidate array: 8 per thread, two uint4 reads
+constexpr int kSelQ4 = 6;                              // uint4 key groups per thread: n <= 1024 * 24
+static_assert(kCandMax <= kCandCap && kCandCap == 8 * kSelThreads, "candidate layout");
 
 struct SelShared {
   Row row[128];            // segment-start rows of the selected nodes
@@ -1110,8 +1126,7 @@ struct SelShared {
   int32_t done[128];
   int32_t fin[128];        // commits of this node in the segment
   int32_t act[128];        // active slots of a generation round
-  uint32_t raw[kSelThreads];
-  uint32_t red[3][kSelWaves];
+  uint32_t red[2][3][kSelWaves];  // reduction scratch, alternating halves: one barrier per reduction
   uint32_t hist[KB_NUM_REASONS];
   uint32_t theta0;
   int32_t n_act, s_count, cut, stop_kind, n_alloc;
@@ -1142,51 +1157,66 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
-// Block-wide sum / max / min (every thread gets the three results).
-__device__ __forceinline__ void sel_reduce3(SelShared& sh, uint32_t& s, uint32_t& mx, uint32_t& mn) {
+// Block-wide reductions with one barrier each: the scratch half alternates between calls, and the
+// barrier of call k+1 separates call k's reads from call k+2's writes. `rp` is block-uniform.
+__device__ __forceinline__ void sel_reduce3(SelShared& sh, int& rp, uint32_t& s, uint32_t& mx, uint32_t& mn) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   s = wave_sum_u32(s);
   mx = wave_max_u32(mx);
   mn = wave_min_u32(mn);
+  uint32_t(*r)[kSelWaves] = sh.red[rp];
+  rp ^= 1;
   if (lane == 0) {
-    sh.red[0][wv] = s;
-    sh.red[1][wv] = mx;
-    sh.red[2][wv] = mn;
+    r[0][wv] = s;
+    r[1][wv] = mx;
+    r[2][wv] = mn;
   }
   __syncthreads();
   s = 0, mx = 0, mn = 0xffffffffu;
+#pragma unroll
   for (int w = 0; w < kSelWaves; ++w) {
-    s += sh.red[0][w];
-    mx = umax32(mx, sh.red[1][w]);
-    mn = sh.red[2][w] < mn ? sh.red[2][w] : mn;
+    s += r[0][w];
+    mx = umax32(mx, r[1][w]);
+    mn = r[2][w] < mn ? r[2][w] : mn;
   }
-  __syncthreads();
 }
-__device__ __forceinline__ uint32_t sel_sum(SelShared& sh, uint32_t v) {
+__device__ __forceinline__ uint32_t sel_sum(SelShared& sh, int& rp, uint32_t v) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   v = wave_sum_u32(v);
-  if (lane == 0) sh.red[0][wv] = v;
+  uint32_t* r = sh.red[rp][0];
+  rp ^= 1;
+  if (lane == 0) r[wv] = v;
   __syncthreads();
   uint32_t s = 0;
-  for (int w = 0; w < kSelWaves; ++w) s += sh.red[0][w];
-  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) s += r[w];
   return s;
 }
-// Block-wide exclusive prefix sum in thread order; *total = the sum over the block.
-__device__ __forceinline__ uint32_t sel_excl_scan(SelShared& sh, uint32_t v, uint32_t* total) {
+// Two block-wide exclusive prefix sums in thread order at once; totals in *ta / *tb.
+__device__ __forceinline__ void sel_excl_scan2(SelShared& sh, int& rp, uint32_t& a, uint32_t& b, uint32_t* ta,
+                                               uint32_t* tb) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t x = wave_excl_scan_u32(v, lane);
-  if (lane == 63) sh.red[0][wv] = x + v;
-  __syncthreads();
-  uint32_t base = 0, tot = 0;
-  for (int w = 0; w < kSelWaves; ++w) {
-    const uint32_t r = sh.red[0][w];
-    base += w < wv ? r : 0;
-    tot += r;
+  const uint32_t xa = wave_excl_scan_u32(a, lane), xb = wave_excl_scan_u32(b, lane);
+  uint32_t(*r)[kSelWaves] = sh.red[rp];
+  rp ^= 1;
+  if (lane == 63) {
+    r[0][wv] = xa + a;
+    r[1][wv] = xb + b;
   }
   __syncthreads();
-  *total = tot;
-  return base + x;
+  uint32_t ba = 0, bb = 0, sa = 0, sb = 0;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) {
+    const uint32_t ra = r[0][w], rb = r[1][w];
+    ba += w < wv ? ra : 0;
+    bb += w < wv ? rb : 0;
+    sa += ra;
+    sb += rb;
+  }
+  a = ba + xa;
+  b = bb + xb;
+  *ta = sa;
+  *tb = sb;
 }
 
 // Elements of slot s's candidate list whose score field is >= v (the list is non-increasing).
@@ -1206,6 +1236,34 @@ __device__ __forceinline__ uint32_t sel_cnt_ge(const SelShared& sh, const uint32
 __device__ __forceinline__ int sel_slot(uint64_t o) { return 127 - (int)((o >> 7) & 127); }
 __device__ __forceinline__ int sel_level(uint64_t o) { return 127 - (int)(o & 127); }
 
+// The row after c commits of the spec from its segment-start state r0 (min(c, A) Allocates, the rest
+// Pipelines): stores only, no read-modify-write of the main columns (scalars and ports as
+// write_back_row does them).
+__device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_spec& sp, const int64_t* scr, int w,
+                               int c, int A, const Row& r0) {
+  const int64_t a = c < A ? c : A;
+  const int64_t p = c - a;
+  N.idle_cpu[w] = r0.idle_cpu - a * sp.req_cpu;
+  N.idle_mem[w] = r0.idle_mem - a * sp.req_mem;
+  N.rel_cpu[w] = r0.rel_cpu - p * sp.req_cpu;
+  N.rel_mem[w] = r0.rel_mem - p * sp.req_mem;
+  N.pod_count[w] = r0.pod_count + c;
+  N.nz_cpu[w] = r0.nz_cpu + (int64_t)c * sp.nz_cpu;
+  N.nz_mem[w] = r0.nz_mem + (int64_t)c * sp.nz_mem;
+  uint64_t m = sp.req_sc_mask;
+  while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
+    const int q = __builtin_ctzll(m);
+    m &= m - 1;
+    if (a && (r0.flags & KB_NODE_IDLE_HAS_MAP)) N.idle_sc[(size_t)q * N.n + w] -= a * scr[q];
+    if (p && (r0.flags & KB_NODE_REL_HAS_MAP)) N.rel_sc[(size_t)q * N.n + w] -= p * scr[q];
+  }
+  if (c > 0)
+    for (uint32_t i = 0; i < sp.port_cnt; ++i) {
+      const kb_port q = P.ports[sp.port_off + i];
+      N.port_used[(size_t)q.slot * N.n + w] |= 1ull << q.ip;
+    }
+}
+
 __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
@@ -1218,81 +1276,116 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
-  uint32_t* k32 = lds32;       // [n] current key of every node
-  uint32_t* cand = lds32 + n;  // [kCandMax] e-values, one contiguous list per selected node
+  // node keys in contiguous groups of 4 per thread (index order decides the lowest-index tie-break);
+  // the padding past n holds 0, an infeasible key with no reason bits
+  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  uint32_t* k32 = lds32;           // [n_pad] current key of every node
+  uint32_t* cand = lds32 + n_pad;  // [kCandCap] e-values, one contiguous list per selected node
+  uint4* k32v = (uint4*)k32;
   const kb_spec sp = P.specs[spec];
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
   const int64_t bias32 = 1ll << (30 - idx_bits);
   const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
-  for (int i = tid; i < n; i += kSelThreads) k32[i] = keys32[i];
+  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
   int ready = first ? ready0 : js->ready_num;
   const int minav = first ? minav0 : js->min_available;
   const int gang = first ? gang0 : js->gang_ready;
   int placed = first ? 0 : js->n_placed;
   int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
-  // contiguous node range per thread: index order decides the lowest-index tie-break
-  const int Q = (n + kSelThreads - 1) / kSelThreads;
-  const int i0 = tid * Q < n ? tid * Q : n, i1 = i0 + Q < n ? i0 + Q : n;
   const uint64_t lt = (1ull << lane) - 1;
+  int rp = 0;
+#ifdef KB_DIAG
+  // phases: 0 key load, 1 node selection, 2 selected-node setup, 3 e-sequences, 4 winners + order,
+  // 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after the block barriers)
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __syncthreads();
+  KB_SEL_PH(0);
 
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
-    // ---- 1. S = the T best nodes by current key ----
+    // ---- 1. S = the T best nodes by current key (keys in registers for this phase) ----
+    uint4 kv[kSelQ4];
+#pragma unroll
+    for (int c = 0; c < kSelQ4; ++c) kv[c] = c < Q4 ? k32v[tid * Q4 + c] : make_uint4(0u, 0u, 0u, 0u);
+#define SEL_EACH_KEY(BODY)                                       \
+  _Pragma("unroll") for (int c_ = 0; c_ < kSelQ4; ++c_) {       \
+    const uint32_t ks_[4] = {kv[c_].x, kv[c_].y, kv[c_].z, kv[c_].w}; \
+    _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {           \
+      const uint32_t k = ks_[q_];                                \
+      const int ki = (tid * Q4 + c_) * 4 + q_;                   \
+      (void)ki;                                                  \
+      BODY                                                       \
+    }                                                            \
+  }
     uint32_t F = 0, MX = 0, MN = 0xffffffffu;
-    for (int i = i0; i < i1; ++i) {
-      const uint32_t k = k32[i];
+    SEL_EACH_KEY({
       if (k >> 31) {
         ++F;
         const uint32_t h = k >> idx_bits;
         MX = umax32(MX, h);
         MN = h < MN ? h : MN;
       }
-    }
-    sel_reduce3(sh, F, MX, MN);
+    })
+    sel_reduce3(sh, rp, F, MX, MN);
+    KB_SEL_FINE(1);
     bool no_fit = F == 0;
     if (!no_fit) {
-      // infeasible keys have a score field below every feasible one: never counted below
+      // infeasible keys (and padding) have a score field below every feasible one: never counted below
       uint32_t sstar = MN, R = 0xffffffffu;  // F <= T: every feasible node
       if (F > T) {
         uint32_t lo = MN, hi = MX;
         while (lo < hi) {
-          const uint32_t mid = lo + (hi - lo + 1) / 2;
+          // the first probe is the top score itself (often enough nodes share it)
+          const uint32_t mid = hi == MX && lo < hi ? hi : lo + (hi - lo + 1) / 2;
           uint32_t c = 0;
-          for (int i = i0; i < i1; ++i) c += (k32[i] >> idx_bits) >= mid;
-          if (sel_sum(sh, c) >= T) lo = mid;
+          SEL_EACH_KEY({ c += (k >> idx_bits) >= mid; })
+          if (sel_sum(sh, rp, c) >= T) lo = mid;
           else hi = mid - 1;
         }
         sstar = lo;
-        uint32_t gt = 0;
-        for (int i = i0; i < i1; ++i) gt += (k32[i] >> idx_bits) > sstar;
-        R = T - sel_sum(sh, gt);
       }
-      uint32_t g = 0, e = 0, tot, S;
-      for (int i = i0; i < i1; ++i) {
-        const uint32_t h = k32[i] >> idx_bits;
+      KB_SEL_FINE(2);
+      uint32_t g = 0, e = 0, tg, te;
+      SEL_EACH_KEY({
+        const uint32_t h = k >> idx_bits;
         g += h > sstar;
         e += h == sstar;
-      }
-      const uint32_t E = sel_excl_scan(sh, e, &tot);
+      })
+      uint32_t G = g, E = e;
+      sel_excl_scan2(sh, rp, G, E, &tg, &te);
+      KB_SEL_FINE(3);
+      if (F > T) R = T - tg;
       const uint32_t selE = R > E ? (R - E < e ? R - E : e) : 0u;
-      uint32_t slot = sel_excl_scan(sh, g + selE, &S);
+      // slot of this thread's first selected node: selected nodes before it in index order
+      uint32_t slot = G + (R > E ? E : R);
+      const uint32_t S = tg + (R < te ? R : te);
       uint32_t le = 0;
-      for (int i = i0; i < i1; ++i) {
-        const uint32_t k = k32[i];
+      SEL_EACH_KEY({
         const uint32_t h = k >> idx_bits;
         bool take = h > sstar;
         if (h == sstar) take = le++ < selE;
         if (take) {
-          sh.node[slot] = i;
+          sh.node[slot] = ki;
           sh.key0[slot] = k;
           ++slot;
         }
+      })
+#undef SEL_EACH_KEY
+      // zero the candidate lists (an unused entry reads as 0: infeasible, never counted)
+      {
+        uint4* cv = (uint4*)cand;
+        cv[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
+        cv[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
       }
       __syncthreads();
-      // ---- 2. selected nodes: rows, A, rank, candidate offsets ----
+      KB_SEL_PH(1);
+      // ---- 2. selected nodes: rows, A; rank by key (8 threads per node) ----
       if (tid < (int)S) {
         const int w = sh.node[tid];
         const Row r = load_row(N, w);
@@ -1304,11 +1397,23 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         sh.emin[tid] = 0xffffffffu;
         sh.fin[tid] = 0;
         sh.done[tid] = 0;
-        const uint32_t k = sh.key0[tid];
+      }
+      {
+        const int s = tid >> 3, part = tid & 7;
+        const uint32_t k = s < (int)S ? sh.key0[s] : 0u;
         uint32_t rk = 0;
-        for (uint32_t q = 0; q < S; ++q) rk += sh.key0[q] > k;
-        sh.lmax[tid] = (int)(T - rk);
-        if (rk == S - 1) sh.theta0 = k;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int o = part * 16 + q;
+          rk += o < (int)S && sh.key0[o] > k;
+        }
+        rk += __shfl_xor(rk, 1, 64);
+        rk += __shfl_xor(rk, 2, 64);
+        rk += __shfl_xor(rk, 4, 64);
+        if (part == 0 && s < (int)S) {
+          sh.lmax[s] = (int)(T - rk);
+          if (rk == S - 1) sh.theta0 = k;
+        }
       }
       __syncthreads();
       if (wv == 0) {
@@ -1319,10 +1424,12 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         sh.off[lane] = (int32_t)ea;
         sh.off[lane + 64] = (int32_t)(ta + eb);
       }
-      // ---- 3. e-sequences of the selected nodes: rounds of 8 levels per node (64 once <= 16 remain) ----
+      // ---- 3. e-sequences: rounds of 8 levels per node (64 once <= 16 remain), one lane per level,
+      //         segmented prefix-min across the node's lanes ----
       const bool cut0 = S == T;  // level 0 of S fills the segment: elements below theta0 cannot rank < T
+      __syncthreads();
+      KB_SEL_PH(2);
       for (;;) {
-        __syncthreads();
         if (wv == 0) {
           const bool a0 = lane < (int)S && !sh.done[lane];
           const bool a1 = lane + 64 < (int)S && !sh.done[lane + 64];
@@ -1336,79 +1443,85 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         const int na = sh.n_act;
         if (na == 0) break;
         const int shift = na <= 16 ? 6 : 3;
-        const int q = tid >> shift, u = tid & ((1 << shift) - 1);
-        if (q < na) {
-          const int s = sh.act[q];
-          const int j = sh.gen[s] + u;
-          if (j < sh.lmax[s]) {
-            uint32_t raw = sh.key0[s];
-            if (j > 0) {
-              const int w = sh.node[s];
-              raw = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w,
-                                 idx_bits);
-            }
-            sh.raw[tid] = raw;
+        const int L = 1 << shift;
+        const int q = tid >> shift, u = tid & (L - 1);
+        // whole lane groups of L share q; groups with q >= na idle (wave-uniform when L = 64)
+        const bool live = q < na;
+        const int s = live ? sh.act[q] : 0;
+        const int j = live ? sh.gen[s] + u : 0;
+        const int lm = live ? sh.lmax[s] : 0;
+        uint32_t x = 0xffffffffu;
+        if (live && j < lm) {
+          x = sh.key0[s];
+          if (j > 0) {
+            const int w = sh.node[s];
+            x = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w, idx_bits);
           }
+        }
+        // segmented inclusive prefix minimum over the group's lanes (levels in order)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          if (o >= L) break;
+          const uint32_t y = __shfl_up(x, o, L);
+          if (u >= o) x = y < x ? y : x;
+        }
+        const uint32_t em = live ? sh.emin[s] : 0u;
+        const uint32_t ee = x < em ? x : em;
+        const bool valid = live && j < lm && (ee >> 31) && (!cut0 || ee >= sh.theta0);
+        const uint64_t vm = __ballot(valid);
+        const int gbase = lane & ~(L - 1) & 63;
+        const uint32_t gm = L == 64 ? (uint32_t)__popcll(vm) : (uint32_t)__popcll((vm >> gbase) & ((1ull << L) - 1));
+        // validity is a prefix of the group: e never increases, levels only grow
+        const int c0 = live ? sh.cnt[s] : 0;
+        if (valid) cand[sh.off[s] + c0 + u] = ee;
+        const uint32_t elast = __shfl(ee, gbase + (gm ? gm - 1 : 0), 64);
+        __syncthreads();  // every lane of the group has read the node's state
+        if (live && u == 0) {
+          sh.cnt[s] = c0 + (int)gm;
+          if (gm) sh.emin[s] = elast;
+          sh.gen[s] = sh.gen[s] + L;
+          if ((int)gm < L || sh.gen[s] >= lm) sh.done[s] = 1;
         }
         __syncthreads();
-        if (tid < na) {  // thread q scans the new levels of active node q in order
-          const int s = sh.act[tid];
-          const int L = 1 << shift;
-          const uint32_t* rw = sh.raw + (tid << shift);
-          int j = sh.gen[s], c = sh.cnt[s], fin = 0;
-          uint32_t em = sh.emin[s];
-          const int lm = sh.lmax[s];
-          uint32_t* out = cand + sh.off[s];
-          const uint32_t th = sh.theta0;
-          for (int v = 0; v < L; ++v, ++j) {
-            if (j >= lm) {
-              fin = 1;
-              break;
-            }
-            const uint32_t r = rw[v];
-            const uint32_t ee = r < em ? r : em;
-            if (!(ee >> 31) || (cut0 && ee < th)) {  // e never increases: the node is finished
-              fin = 1;
-              break;
-            }
-            out[c++] = ee;
-            em = ee;
-          }
-          sh.gen[s] = j;
-          sh.cnt[s] = c;
-          sh.emin[s] = em;
-          if (fin) sh.done[s] = 1;
-        }
       }
-      // ---- 4. the T winners, in pick order ----
+      KB_SEL_PH(3);
+      // ---- 4. the T winners: threshold on the score field over all candidates, then per-slot takes ----
+      uint4 cv0 = ((const uint4*)cand)[2 * tid], cv1 = ((const uint4*)cand)[2 * tid + 1];
+      uint32_t K = 0, HX = 0, HN = 0xffffffffu;
+      {
+        const uint32_t cs[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (cs[q]) {
+            ++K;
+            const uint32_t h = cs[q] >> idx_bits;
+            HX = umax32(HX, h);
+            HN = h < HN ? h : HN;
+          }
+      }
+      sel_reduce3(sh, rp, K, HX, HN);
+      uint32_t thr = 0;  // score field of the T-th winner (0: take every candidate)
+      if (K > T) {
+        uint32_t lo = HN, hi = HX;
+        while (lo < hi) {
+          const uint32_t mid = lo + (hi - lo + 1) / 2;
+          const uint32_t cs[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+          uint32_t c = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) c += cs[q] && (cs[q] >> idx_bits) >= mid;
+          if (sel_sum(sh, rp, c) >= T) lo = mid;
+          else hi = mid - 1;
+        }
+        thr = lo;
+      }
       if (wv == 0) {
         const int a = lane, b = lane + 64;
-        const uint32_t ca = a < (int)S ? (uint32_t)sh.cnt[a] : 0u, cb = b < (int)S ? (uint32_t)sh.cnt[b] : 0u;
-        const uint32_t K = wave_sum_u32(ca + cb);
-        uint32_t ta = ca, tb = cb;
+        uint32_t ta = a < (int)S ? (uint32_t)sh.cnt[a] : 0u, tb = b < (int)S ? (uint32_t)sh.cnt[b] : 0u;
         if (K > T) {
-          uint32_t hmax = 0, hmin = 0xffffffffu;
-          if (ca) {
-            hmax = cand[sh.off[a]] >> idx_bits;
-            hmin = cand[sh.off[a] + ca - 1] >> idx_bits;
-          }
-          if (cb) {
-            hmax = umax32(hmax, cand[sh.off[b]] >> idx_bits);
-            const uint32_t x = cand[sh.off[b] + cb - 1] >> idx_bits;
-            hmin = x < hmin ? x : hmin;
-          }
-          uint32_t lo = wave_min_u32(hmin), hi = wave_max_u32(hmax);
-          while (lo < hi) {
-            const uint32_t mid = lo + (hi - lo + 1) / 2;
-            const uint32_t c = wave_sum_u32(sel_cnt_ge(sh, cand, a, S, mid, idx_bits) +
-                                            sel_cnt_ge(sh, cand, b, S, mid, idx_bits));
-            if (c >= T) lo = mid;
-            else hi = mid - 1;
-          }
-          const uint32_t ga = sel_cnt_ge(sh, cand, a, S, lo + 1, idx_bits);
-          const uint32_t gb = sel_cnt_ge(sh, cand, b, S, lo + 1, idx_bits);
-          const uint32_t qa = sel_cnt_ge(sh, cand, a, S, lo, idx_bits) - ga;
-          const uint32_t qb = sel_cnt_ge(sh, cand, b, S, lo, idx_bits) - gb;
+          const uint32_t ga = sel_cnt_ge(sh, cand, a, S, thr + 1, idx_bits);
+          const uint32_t gb = sel_cnt_ge(sh, cand, b, S, thr + 1, idx_bits);
+          const uint32_t qa = sel_cnt_ge(sh, cand, a, S, thr, idx_bits) - ga;
+          const uint32_t qb = sel_cnt_ge(sh, cand, b, S, thr, idx_bits) - gb;
           const uint32_t R2 = T - wave_sum_u32(ga + gb);
           // ties on the threshold score: lower slot (= lower node index) first, then lower level
           const uint32_t Ea = wave_excl_scan_u32(qa, lane), Qa = wave_sum_u32(qa);
@@ -1431,13 +1544,15 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         const int e2 = tid >> 3, part = tid & 7;
         const uint64_t v = sh.comp[e2];
         uint32_t c = 0;
-        for (int q2 = part * 16; q2 < part * 16 + 16; ++q2) c += sh.comp[q2] > v;
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) c += sh.comp[part * 16 + q2] > v;
         c += __shfl_xor(c, 1, 64);
         c += __shfl_xor(c, 2, 64);
         c += __shfl_xor(c, 4, 64);
         if (part == 0 && e2 < sh.s_count) sh.ord[c] = v;
       }
       __syncthreads();
+      KB_SEL_PH(4);
       // ---- stop rules in pick order (wave 0) ----
       if (wv == 0) {
         const int Kp = sh.s_count;
@@ -1483,6 +1598,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
       __syncthreads();
       // ---- commit: placements, rows, keys ----
       const int cut = sh.cut;
+      const int kind = sh.stop_kind;
       if (tid < cut) {
         const uint64_t o = sh.ord[tid];
         const int s = sel_slot(o), j = sel_level(o);
@@ -1492,16 +1608,19 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         hout[2 * at + 1] = j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
       }
       __syncthreads();
+      // the touched nodes' keys matter only to a later segment or to the no-fit histogram
+      const bool rekey = kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count);
       if (tid < (int)S && sh.fin[tid] > 0) {
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
-        write_back_row(N, P, sp, scr, w, c, A);
-        k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w, idx_bits);
+        store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
+        if (rekey)
+          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w, idx_bits);
       }
       __syncthreads();
+      KB_SEL_PH(5);
       ready += sh.n_alloc;
       placed += cut;
       done_tasks += cut;
-      const int kind = sh.stop_kind;
       if (kind == 3) {
         fail_task = t_begin + done_tasks;
         panic = 1;
@@ -1517,17 +1636,21 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     }
     if (no_fit) {
       // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes at their
-      // current keys (an infeasible key is its reason mask).
+      // current keys (an infeasible key is its reason mask; padding keys are 0).
       if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
       __syncthreads();
       uint32_t h[KB_NUM_REASONS];
 #pragma unroll
       for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
-      for (int i = i0; i < i1; ++i) {
-        const uint32_t k = k32[i];
-        if (k >> 31) continue;
+      for (int c = 0; c < Q4; ++c) {
+        const uint4 v = k32v[tid * Q4 + c];
+        const uint32_t ks[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k >> b) & 1u;
+        for (int q = 0; q < 4; ++q) {
+          if (ks[q] >> 31) continue;
+#pragma unroll
+          for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (ks[q] >> b) & 1u;
+        }
       }
 #pragma unroll
       for (int b = 0; b < KB_NUM_REASONS; ++b) {
@@ -1539,23 +1662,59 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         js->hist[tid] = sh.hist[tid];
         hjs->hist[tid] = sh.hist[tid];
       }
+      KB_SEL_PH(6);
       stop = KB_STOP_NO_FIT;
       fail_task = t_begin + done_tasks;
       stopped = 1;
       break;
     }
   }
+#ifdef KB_DIAG
+  if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
   if (tid == 0) sh.lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, 0, 0, 0, 0};
-  __threadfence_system();
+  // every wave's host-buffer and row stores are complete before the barrier; one lane then releases
+  // at system scope and publishes (the host spins on the sequence number)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0)
+  if (tid == 0) {
+    __threadfence_system();
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
+  }
+}
+
+// Level-0 keys for the selection path: one node per thread, 64-thread blocks (a 10k-node table is
+// ~160 workgroups, spread over the chip), no trajectory levels.
+template <bool AFF>
+__global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
+                                                      uint32_t* keys32, uint64_t* stat, const JobState* js) {
+  if (js != nullptr && js->stopped) return;
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  if (n >= N.n) return;
+  const kb_spec sp = P.specs[spec];
+  const Row r = load_row(N, n);
+  const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+  stat[n] = st;
+  const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
+  keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n, idx_bits);
+}
+
+void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
+                      uint64_t* stat, const JobState* js, bool aff, void* stream) {
+  const int blocks = (N.n + 63) / 64;
+  if (aff)
+    hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
+                       keys32, stat, js);
+  else
+    hipLaunchKernelGGL(sel_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec,
+                       idx_bits, keys32, stat, js);
 }
 
 int sel_lds_bytes(int n) {
-  const long bytes = 4l * ((long)n + kCandMax);
-  return bytes <= kSelDynLimit ? (int)bytes : -1;
+  const long q4 = ((long)n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const long bytes = 4l * (4 * kSelThreads * q4 + kCandCap);
+  return q4 <= kSelQ4 && bytes <= kSelDynLimit ? (int)bytes : -1;
 }
 
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,

@@ -514,9 +514,9 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
     } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
       c->ev_begin(&ea);
-      launch_traj_sweep(c->N, c->P, c->cfg, spec, 0, c->idx_bits, c->traj, c->cmax32, c->amax, c->stat,
-                        first ? nullptr : js, aff, c->stream);
-      c->ev_end(ea, KB_KERNEL_TRAJ_SWEEP, (uint64_t)c->N.n);
+      launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, aff,
+                       c->stream);
+      c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, c->traj, c->stat, js, first,
                        job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
