@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--cpu-sample-tasks", type=int, default=3000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
+    ap.add_argument("--path", default="select", choices=["select", "engine", "trajectory", "rekey"],
+                    help="device path for the runs (scheduler_amd.runtime.PATHS)")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP events around the launches of every Nth job call of the timed region")
     args = ap.parse_args()
@@ -80,7 +82,7 @@ def main():
     gen = synth.CONFIGS[args.config]
     cl = gen(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=synth.SEED + rank)
     snap = export.Snapshot(cl)
-    ctx = runtime.Context(local_rank, timing=not args.no_timing, timing_every=args.timing_every)
+    ctx = runtime.Context(local_rank, timing=not args.no_timing, timing_every=args.timing_every, path=args.path)
     ctx.upload(snap)
 
     def step():

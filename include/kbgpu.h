@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 4
+#define KBGPU_ABI_VERSION 5
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -350,6 +350,7 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_OPT_TIMING (1u << 0)
 #define KB_OPT_NO_TRAJECTORY (1u << 1) /* no trajectory loop: the per-commit re-key loop (testing the device paths) */
 #define KB_OPT_NO_SELECT (1u << 2)     /* no top-T selection path: the trajectory loop (testing the device paths) */
+#define KB_OPT_ENGINE (1u << 3)        /* serve selection-path jobs from the persistent placement engine */
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -358,7 +359,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_AFF_PLACE 5 /* block-wide re-sweep loop (specs with self-dependent pod affinity) */
 #define KB_KERNEL_IPA_MINMAX 6
 #define KB_KERNEL_SEL_PLACE 7 /* a run as one parallel top-T selection (32-bit keys) */
-#define KB_NUM_KERNELS 8
+#define KB_KERNEL_ENGINE 8    /* persistent placement engine: device time per served job */
+#define KB_KERNEL_SEL_SWEEP 9 /* level-0 keys of every node for the selection path */
+#define KB_NUM_KERNELS 10
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */

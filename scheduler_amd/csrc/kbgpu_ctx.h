@@ -38,7 +38,14 @@ struct kb_ctx {
   int idx_bits = 0;
   std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
   std::vector<int64_t> spec_pref_weight;
-  bool use_traj = true, use_sel = true;
+  bool use_traj = true, use_sel = true, use_engine = false;
+  // persistent placement engine (the selection path as one resident workgroup)
+  bool eng_running = false;
+  hipStream_t eng_stream = nullptr;
+  hipEvent_t eng_dep = nullptr;  // orders the engine after work already queued on `stream`
+  char* h_cmd = nullptr;         // pinned mailbox: EngineCmd + EngineRun[cmd_cap]
+  char* h_cmd_dev = nullptr;
+  uint32_t cmd_cap = 0;
   bool traj_full = false;  // trajectory buffers (kTrajMaxJ + 1 levels): chunk maxima fit the place loop
   bool sel_ok = false;     // the node count fits the selection kernel's LDS plan (level-0 keys buffer)
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
@@ -72,3 +79,5 @@ struct kb_ctx {
 // internal helpers (defined inside kbgpu_host.cpp's extern "C" block, not part of the ABI)
 extern "C" __attribute__((visibility("hidden"))) int kb_check_score_range(kb_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) void kb_update_traj_ok(kb_ctx* c);
+// stops the placement engine (if running) before other work touches the device state
+extern "C" __attribute__((visibility("hidden"))) int kb_engine_stop(kb_ctx* c);

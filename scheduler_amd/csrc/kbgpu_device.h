@@ -77,8 +77,24 @@ struct JobState {
   int32_t panic;      // 1: SelectBestNode would panic (best score <= -1)
   uint32_t hist[KB_NUM_REASONS];
   uint64_t diag[8];   // -DKB_DIAG builds: per-phase shader cycles of the place loop, [7] = realtime ticks
+  uint64_t t_recv, t_done;  // placement engine: s_memrealtime (100 MHz) at command receipt / completion
+  uint32_t exit_seq;  // placement engine: the command it was waiting for when it exited idle (0: none)
   uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
-  uint32_t pad;
+};
+
+// Placement engine mailbox (pinned host memory, written by the host): one command per kb_place_job.
+#define KB_ENG_RUN 1
+#define KB_ENG_EXIT 2
+#define KB_ENG_EXIT_IDLE 3
+struct EngineRun {
+  int32_t spec, t_begin, t_count, pad;
+};
+struct EngineCmd {
+  uint32_t seq;  // written last (release): the engine starts on seq == the number it waits for
+  int32_t op;    // KB_ENG_RUN / KB_ENG_EXIT
+  int32_t n_runs, ready0, minav0, gang0;
+  int32_t pad[2];
+  // EngineRun runs[n_runs] follow
 };
 
 // Launch wrappers (kbgpu_device.hip).
@@ -110,6 +126,13 @@ void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+
+// Placement engine (kbgpu_device.hip): the selection path as one persistent workgroup serving the
+// commands posted to `cmd` from sequence number seq0 on; exits on KB_ENG_EXIT or after idle_ticks
+// (s_memrealtime, 100 MHz) without a command.
+void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint64_t* stat,
+                   const EngineCmd* cmd, JobState* js, JobState* hjs, int32_t* hout, uint32_t seq0,
+                   uint64_t idle_ticks, void* stream);
 
 // Opt the place kernels into the dynamic LDS they need; returns 0 or the hipError_t.
 int configure_kernels();

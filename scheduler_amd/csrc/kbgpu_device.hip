@@ -35,10 +35,29 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+// ---- wave-wide scans / reductions on DPP (row shifts + row broadcasts: a few cycles per step, where a
+// ds_bpermute shuffle butterfly waits on LDS latency six times). Lanes whose DPP source is out of range
+// keep `ident`. Every lane of the wave must be active.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t ident, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+// inclusive prefix combine over the 64 lanes
+template <class Op>
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x, uint32_t ident, Op op) {
+  x = op(x, dpp_src<0x111>(ident, x));        // row_shr:1
+  x = op(x, dpp_src<0x112>(ident, x));        // row_shr:2
+  x = op(x, dpp_src<0x114>(ident, x));        // row_shr:4
+  x = op(x, dpp_src<0x118>(ident, x));        // row_shr:8
+  x = op(x, dpp_src<0x142, 0xa>(ident, x));   // row_bcast:15 -> rows 1, 3
+  x = op(x, dpp_src<0x143, 0xc>(ident, x));   // row_bcast:31 -> rows 2, 3
+  return x;
+}
+struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMax { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };
+struct OpMin { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(v, 0u, OpAdd{}), 63);
 }
 
 // Resource.LessEqual per dimension for integral values: r < rr || |rr - r| < tol  <=>  r - rr < tol
@@ -1102,19 +1121,21 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
 //   4. writes the placements and the touched rows back and re-keys the touched nodes for the next
 //      segment.
 // ===========================================================================
-constexpr int kSelThreads = 1024;
+constexpr int kSelThreads = 512;   // 8 waves: up to 256 VGPRs per lane, no spills
 constexpr int kSelWaves = kSelThreads / 64;
-constexpr int kSegMax = 127;                           // slot and level fit 7-bit fields
+constexpr int kSegMax = 100;                           // tasks per segment (slot and level fit 7-bit fields)
 constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
-constexpr int kCandCap = 8192;                         // candidate array: 8 per thread, two uint4 reads
-constexpr int kSelQ4 = 6;                              // uint4 key groups per thread: n <= 1024 * 24
-static_assert(kCandMax <= kCandCap && kCandCap == 8 * kSelThreads, "candidate layout");
+constexpr int kCandCap = 5120;                         // candidate composites: 10 per thread, five uint4 reads
+constexpr int kCandV = kCandCap / 2 / kSelThreads;     // uint4 (two composites) groups per thread
+constexpr int kSelQ4 = 12;                             // uint4 key groups per thread: n <= 512 * 48
+static_assert(kCandMax <= kCandCap && kCandCap == 2 * kCandV * kSelThreads, "candidate layout");
 
 struct SelShared {
   Row row[128];            // segment-start rows of the selected nodes
   uint64_t stat[128];
-  uint64_t comp[128];      // (e << 14 | (127 - slot) << 7 | (127 - level)) of the taken elements
+  uint64_t comp[128];      // composites (e << 14 | (127 - slot) << 7 | (127 - level)) of the taken elements
   uint64_t ord[128];       // the same, in pick order
+  uint64_t dense[kSelThreads];  // the candidates, compacted (when there are at most one per thread)
   int32_t node[128];
   uint32_t key0[128];      // current key of the selected node
   int32_t A[128];          // Allocates before InitResreq stops fitting Idle
@@ -1131,30 +1152,21 @@ struct SelShared {
   uint32_t theta0;
   int32_t n_act, s_count, cut, stop_kind, n_alloc;
   LoopOut lo;
+  EngineCmd cmd;  // placement engine: the command being served and its current run
+  EngineRun run;
+  uint64_t t_recv;
 };
 constexpr int kSelDynLimit = 160 * 1024 - (int)sizeof(SelShared) - 64;
 
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x - v;
+  (void)lane;
+  return wave_incl_scan_dpp(v, 0u, OpAdd{}) - v;
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = umax32(v, (uint32_t)__shfl_xor(v, o, 64));
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(v, 0u, OpMax{}), 63);
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t x = (uint32_t)__shfl_xor(v, o, 64);
-    v = x < v ? x : v;
-  }
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(v, 0xffffffffu, OpMin{}), 63);
 }
 
 // Block-wide reductions with one barrier each: the scratch half alternates between calls, and the
@@ -1220,14 +1232,14 @@ __device__ __forceinline__ void sel_excl_scan2(SelShared& sh, int& rp, uint32_t&
 }
 
 // Elements of slot s's candidate list whose score field is >= v (the list is non-increasing).
-__device__ __forceinline__ uint32_t sel_cnt_ge(const SelShared& sh, const uint32_t* cand, int s, int S, uint32_t v,
+__device__ __forceinline__ uint32_t sel_cnt_ge(const SelShared& sh, const uint64_t* cand, int s, int S, uint32_t v,
                                                int idx_bits) {
   if (s >= S) return 0;
   uint32_t lo = 0, hi = (uint32_t)sh.cnt[s];
-  const uint32_t* c = cand + sh.off[s];
+  const uint64_t* c = cand + sh.off[s];
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if ((c[mid] >> idx_bits) >= v) lo = mid + 1;
+    if ((uint32_t)(c[mid] >> (14 + idx_bits)) >= v) lo = mid + 1;
     else hi = mid;
   }
   return lo;
@@ -1264,48 +1276,33 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
     }
 }
 
-__global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
-    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
-    const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
-    uint32_t seq) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
-  __shared__ SelShared sh;
-  if (!first && js->stopped) {
-    signal_skip(hjs, seq);
-    return;
-  }
+#ifdef KB_DIAG
+#define SEL_DIAG_PARAMS , uint64_t *dg, uint64_t &dg_last
+#define SEL_DIAG_ARGS , dg, dg_last
+#else
+#define SEL_DIAG_PARAMS
+#define SEL_DIAG_ARGS
+#endif
+
+// One run of same-spec tasks inside a 1024-thread workgroup (the selection algorithm above).
+// k32 (LDS, n_pad entries, zero past n) holds every node's current key at entry and is kept current;
+// cand (LDS, kCandCap) is scratch; stat is the run's static cache. Placements go to hout[2 * task];
+// ready / placed advance, and the stop state is set when the run stops the job.
+__device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* cand, const DevNodes& N,
+                                        const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
+                                        int t_begin, int t_count,
+                                        int idx_bits, const uint64_t* stat, int& ready, int minav, int gang,
+                                        int& placed, int& stop, int& fail_task, int& panic, int& stopped,
+                                        int32_t* hout, JobState* js, JobState* hjs, int& rp SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
-  // node keys in contiguous groups of 4 per thread (index order decides the lowest-index tie-break);
-  // the padding past n holds 0, an infeasible key with no reason bits
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
-  const int n_pad = 4 * kSelThreads * Q4;
-  uint32_t* k32 = lds32;           // [n_pad] current key of every node
-  uint32_t* cand = lds32 + n_pad;  // [kCandCap] e-values, one contiguous list per selected node
-  uint4* k32v = (uint4*)k32;
-  const kb_spec sp = P.specs[spec];
+  const uint4* k32v = (const uint4*)k32;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
   const int64_t bias32 = 1ll << (30 - idx_bits);
   const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
-  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
-  int ready = first ? ready0 : js->ready_num;
-  const int minav = first ? minav0 : js->min_available;
-  const int gang = first ? gang0 : js->gang_ready;
-  int placed = first ? 0 : js->n_placed;
-  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
   const uint64_t lt = (1ull << lane) - 1;
-  int rp = 0;
-#ifdef KB_DIAG
-  // phases: 0 key load, 1 node selection, 2 selected-node setup, 3 e-sequences, 4 winners + order,
-  // 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after the block barriers)
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t dg_last = __builtin_amdgcn_s_memtime();
-  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  __syncthreads();
-  KB_SEL_PH(0);
-
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
@@ -1365,23 +1362,25 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
       // slot of this thread's first selected node: selected nodes before it in index order
       uint32_t slot = G + (R > E ? E : R);
       const uint32_t S = tg + (R < te ? R : te);
-      uint32_t le = 0;
-      SEL_EACH_KEY({
-        const uint32_t h = k >> idx_bits;
-        bool take = h > sstar;
-        if (h == sstar) take = le++ < selE;
-        if (take) {
-          sh.node[slot] = ki;
-          sh.key0[slot] = k;
-          ++slot;
-        }
-      })
+      if (g + selE) {  // most threads hold no selected node
+        uint32_t le = 0;
+        SEL_EACH_KEY({
+          const uint32_t h = k >> idx_bits;
+          bool take = h > sstar;
+          if (h == sstar) take = le++ < selE;
+          if (take) {
+            sh.node[slot] = ki;
+            sh.key0[slot] = k;
+            ++slot;
+          }
+        })
+      }
 #undef SEL_EACH_KEY
-      // zero the candidate lists (an unused entry reads as 0: infeasible, never counted)
+      // zero the candidate lists (an unused entry reads as 0: never counted)
       {
         uint4* cv = (uint4*)cand;
-        cv[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
-        cv[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int q = 0; q < kCandV; ++q) cv[kCandV * tid + q] = make_uint4(0u, 0u, 0u, 0u);
       }
       __syncthreads();
       KB_SEL_PH(1);
@@ -1399,17 +1398,18 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         sh.done[tid] = 0;
       }
       {
-        const int s = tid >> 3, part = tid & 7;
+        constexpr int kPer = 32;  // keys compared per thread: 4 threads per node, 128 nodes
+        static_assert(kSelThreads == 4 * 128, "rank layout");
+        const int s = tid >> 2, part = tid & 3;
         const uint32_t k = s < (int)S ? sh.key0[s] : 0u;
         uint32_t rk = 0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int o = part * 16 + q;
+        for (int q = 0; q < kPer; ++q) {
+          const int o = part * kPer + q;
           rk += o < (int)S && sh.key0[o] > k;
         }
-        rk += __shfl_xor(rk, 1, 64);
-        rk += __shfl_xor(rk, 2, 64);
-        rk += __shfl_xor(rk, 4, 64);
+        rk += dpp_src<0xb1>(0u, rk);  // quad_perm [1,0,3,2]
+        rk += dpp_src<0x4e>(0u, rk);  // quad_perm [2,3,0,1]
         if (part == 0 && s < (int)S) {
           sh.lmax[s] = (int)(T - rk);
           if (rk == S - 1) sh.theta0 = k;
@@ -1442,7 +1442,9 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         __syncthreads();
         const int na = sh.n_act;
         if (na == 0) break;
-        const int shift = na <= 16 ? 6 : 3;
+        // levels per active node this round: the largest power of two with na * L <= threads, at most 64
+        int shift = 6;
+        while (shift > 2 && (na << shift) > kSelThreads) --shift;
         const int L = 1 << shift;
         const int q = tid >> shift, u = tid & (L - 1);
         // whole lane groups of L share q; groups with q >= na idle (wave-uniform when L = 64)
@@ -1473,7 +1475,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         const uint32_t gm = L == 64 ? (uint32_t)__popcll(vm) : (uint32_t)__popcll((vm >> gbase) & ((1ull << L) - 1));
         // validity is a prefix of the group: e never increases, levels only grow
         const int c0 = live ? sh.cnt[s] : 0;
-        if (valid) cand[sh.off[s] + c0 + u] = ee;
+        if (valid) cand[sh.off[s] + c0 + u] = ((uint64_t)ee << 14) | ((uint64_t)(127 - s) << 7) | (uint64_t)(127 - j);
         const uint32_t elast = __shfl(ee, gbase + (gm ? gm - 1 : 0), 64);
         __syncthreads();  // every lane of the group has read the node's state
         if (live && u == 0) {
@@ -1485,39 +1487,56 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
         __syncthreads();
       }
       KB_SEL_PH(3);
-      // ---- 4. the T winners: threshold on the score field over all candidates, then per-slot takes ----
-      uint4 cv0 = ((const uint4*)cand)[2 * tid], cv1 = ((const uint4*)cand)[2 * tid + 1];
-      uint32_t K = 0, HX = 0, HN = 0xffffffffu;
-      {
-        const uint32_t cs[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+      // ---- 4. the T winners in pick order: rank every candidate when they fit one per thread, else a
+      //         threshold on the score field plus per-slot takes, then rank the T taken ones ----
+      uint64_t cs[2 * kCandV];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < kCandV; ++q) {
+        const uint4 v = ((const uint4*)cand)[kCandV * tid + q];
+        cs[2 * q] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        cs[2 * q + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      }
+      uint32_t kc = 0;
+#pragma unroll
+      for (int q = 0; q < 2 * kCandV; ++q) kc += cs[q] != 0;
+      uint32_t K, zero = 0, ztot;
+      uint32_t pos = kc;
+      sel_excl_scan2(sh, rp, pos, zero, &K, &ztot);
+      if (K <= (uint32_t)kSelThreads) {
+#pragma unroll
+        for (int q = 0; q < 2 * kCandV; ++q)
+          if (cs[q]) sh.dense[pos++] = cs[q];
+        __syncthreads();
+        if (tid < (int)K) {  // composites are distinct: rank = number of larger ones
+          const uint64_t v = sh.dense[tid];
+          uint32_t r = 0;
+          for (uint32_t q = 0; q < K; ++q) r += sh.dense[q] > v;
+          if (r < T) sh.ord[r] = v;
+        }
+        if (tid == 0) sh.s_count = (int)(K < T ? K : T);
+      } else {
+        const int fs = 14 + idx_bits;  // score field of a composite
+        uint32_t HX = 0, HN = 0xffffffffu, kk = kc;
+#pragma unroll
+        for (int q = 0; q < 2 * kCandV; ++q)
           if (cs[q]) {
-            ++K;
-            const uint32_t h = cs[q] >> idx_bits;
+            const uint32_t h = (uint32_t)(cs[q] >> fs);
             HX = umax32(HX, h);
             HN = h < HN ? h : HN;
           }
-      }
-      sel_reduce3(sh, rp, K, HX, HN);
-      uint32_t thr = 0;  // score field of the T-th winner (0: take every candidate)
-      if (K > T) {
-        uint32_t lo = HN, hi = HX;
+        sel_reduce3(sh, rp, kk, HX, HN);
+        uint32_t lo = HN, hi = HX;  // K > T here
         while (lo < hi) {
           const uint32_t mid = lo + (hi - lo + 1) / 2;
-          const uint32_t cs[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
           uint32_t c = 0;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) c += cs[q] && (cs[q] >> idx_bits) >= mid;
+          for (int q = 0; q < 2 * kCandV; ++q) c += cs[q] && (uint32_t)(cs[q] >> fs) >= mid;
           if (sel_sum(sh, rp, c) >= T) lo = mid;
           else hi = mid - 1;
         }
-        thr = lo;
-      }
-      if (wv == 0) {
-        const int a = lane, b = lane + 64;
-        uint32_t ta = a < (int)S ? (uint32_t)sh.cnt[a] : 0u, tb = b < (int)S ? (uint32_t)sh.cnt[b] : 0u;
-        if (K > T) {
+        const uint32_t thr = lo;
+        if (wv == 0) {
+          const int a = lane, b = lane + 64;
           const uint32_t ga = sel_cnt_ge(sh, cand, a, S, thr + 1, idx_bits);
           const uint32_t gb = sel_cnt_ge(sh, cand, b, S, thr + 1, idx_bits);
           const uint32_t qa = sel_cnt_ge(sh, cand, a, S, thr, idx_bits) - ga;
@@ -1526,30 +1545,26 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
           // ties on the threshold score: lower slot (= lower node index) first, then lower level
           const uint32_t Ea = wave_excl_scan_u32(qa, lane), Qa = wave_sum_u32(qa);
           const uint32_t Eb = Qa + wave_excl_scan_u32(qb, lane);
-          ta = ga + (R2 > Ea ? (R2 - Ea < qa ? R2 - Ea : qa) : 0u);
-          tb = gb + (R2 > Eb ? (R2 - Eb < qb ? R2 - Eb : qb) : 0u);
+          const uint32_t ta = ga + (R2 > Ea ? (R2 - Ea < qa ? R2 - Ea : qa) : 0u);
+          const uint32_t tb = gb + (R2 > Eb ? (R2 - Eb < qb ? R2 - Eb : qb) : 0u);
+          const uint32_t pa = wave_excl_scan_u32(ta, lane), Ta = wave_sum_u32(ta);
+          const uint32_t pb = Ta + wave_excl_scan_u32(tb, lane);
+          for (uint32_t j = 0; j < ta; ++j) sh.comp[pa + j] = cand[sh.off[a] + j];
+          for (uint32_t j = 0; j < tb; ++j) sh.comp[pb + j] = cand[sh.off[b] + j];
+          for (uint32_t p = T + lane; p < 128; p += 64) sh.comp[p] = 0;
+          if (lane == 0) sh.s_count = (int)T;
         }
-        const uint32_t pa = wave_excl_scan_u32(ta, lane), Ta = wave_sum_u32(ta);
-        const uint32_t pb = Ta + wave_excl_scan_u32(tb, lane);
-        for (uint32_t j = 0; j < ta; ++j)
-          sh.comp[pa + j] = ((uint64_t)cand[sh.off[a] + j] << 14) | ((uint64_t)(127 - a) << 7) | (127 - j);
-        for (uint32_t j = 0; j < tb; ++j)
-          sh.comp[pb + j] = ((uint64_t)cand[sh.off[b] + j] << 14) | ((uint64_t)(127 - b) << 7) | (127 - j);
-        const uint32_t Kp = K < T ? K : T;
-        for (uint32_t p = Kp + lane; p < 128; p += 64) sh.comp[p] = 0;
-        if (lane == 0) sh.s_count = (int)Kp;
-      }
-      __syncthreads();
-      {  // rank of every taken element, 8 threads per element (composites are distinct and nonzero)
-        const int e2 = tid >> 3, part = tid & 7;
-        const uint64_t v = sh.comp[e2];
-        uint32_t c = 0;
+        __syncthreads();
+        {  // rank of every taken element, 4 threads per element
+          const int e2 = tid >> 2, part = tid & 3;
+          const uint64_t v = sh.comp[e2];
+          uint32_t c = 0;
 #pragma unroll
-        for (int q2 = 0; q2 < 16; ++q2) c += sh.comp[part * 16 + q2] > v;
-        c += __shfl_xor(c, 1, 64);
-        c += __shfl_xor(c, 2, 64);
-        c += __shfl_xor(c, 4, 64);
-        if (part == 0 && e2 < sh.s_count) sh.ord[c] = v;
+          for (int q2 = 0; q2 < 32; ++q2) c += sh.comp[part * 32 + q2] > v;
+          c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
+          c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
+          if (part == 0 && e2 < sh.s_count) sh.ord[c] = v;
+        }
       }
       __syncthreads();
       KB_SEL_PH(4);
@@ -1669,6 +1684,46 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
       break;
     }
   }
+}
+
+__global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
+    const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
+    uint32_t seq) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ SelShared sh;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x;
+  const int n = N.n;
+  // node keys in contiguous groups of 4 per thread (index order decides the lowest-index tie-break);
+  // the padding past n holds 0, an infeasible key with no reason bits
+  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  uint32_t* k32 = lds32;           // [n_pad] current key of every node
+  uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap] candidate composites, a list per selected node
+  const kb_spec sp = P.specs[spec];
+  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
+  int ready = first ? ready0 : js->ready_num;
+  const int minav = first ? minav0 : js->min_available;
+  const int gang = first ? gang0 : js->gang_ready;
+  int placed = first ? 0 : js->n_placed;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  int rp = 0;
+#ifdef KB_DIAG
+  // phases: 0 key load, 1 node selection, 2 selected-node setup, 3 e-sequences, 4 winners + order,
+  // 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after the block barriers)
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  __syncthreads();
+  KB_SEL_PH(0);
+
+  sel_run(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
+          panic, stopped, hout, js, hjs, rp SEL_DIAG_ARGS);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
@@ -1682,6 +1737,122 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
   }
+}
+
+// ===========================================================================
+// Placement engine: the selection path as ONE persistent workgroup serving kb_place_job calls.
+// A per-job launch pays a cold instruction cache on whichever CU it lands on (the selection kernel's
+// first pass over a phase ran 2.6x slower than a repeat of the same code) plus two launch latencies
+// (level-0 sweep, selection). The engine keeps its code and the node table hot on one CU and takes
+// each job from a mailbox in pinned host memory: per run it sweeps every node for the run's spec
+// (keys straight into LDS), then runs the selection. It exits on an EXIT command, or by itself after
+// idle_ticks without a command (recording which command it was waiting for in exit_seq), so a host
+// that stops talking to it never leaves a kernel running.
+// ===========================================================================
+__device__ __forceinline__ uint32_t load_sys_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kSelThreads) void engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
+                                                             uint64_t* stat, const EngineCmd* cmd, JobState* js,
+                                                             JobState* hjs, int32_t* hout, uint32_t seq0,
+                                                             uint64_t idle_ticks) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ SelShared sh;
+  const int tid = threadIdx.x;
+  const int n = N.n;
+  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  uint32_t* k32 = lds32;           // [n_pad] keys of the current run's spec
+  uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap]
+  const EngineRun* runs = (const EngineRun*)(cmd + 1);
+  for (int i = n + tid; i < n_pad; i += kSelThreads) k32[i] = 0u;  // padding: infeasible, no reasons
+  int rp = 0;
+#ifdef KB_DIAG
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+#endif
+  for (uint32_t want = seq0;; ++want) {
+    if (tid == 0) {  // one lane polls the mailbox
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int op = KB_ENG_EXIT_IDLE;
+      for (;;) {
+        if (load_sys_u32(&cmd->seq) == want) {
+          op = cmd->op;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      sh.cmd.op = op;
+      if (op == KB_ENG_RUN) {
+        sh.cmd.n_runs = cmd->n_runs;
+        sh.cmd.ready0 = cmd->ready0;
+        sh.cmd.minav0 = cmd->minav0;
+        sh.cmd.gang0 = cmd->gang0;
+      }
+      sh.t_recv = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    const int op = sh.cmd.op;
+    if (op != KB_ENG_RUN) {
+      if (tid == 0 && op == KB_ENG_EXIT_IDLE)
+        __hip_atomic_store(&hjs->exit_seq, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+#ifdef KB_DIAG
+    for (int k = 0; k < 7; ++k) dg[k] = 0;
+    dg_last = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    int ready = sh.cmd.ready0, placed = 0;
+    const int minav = sh.cmd.minav0, gang = sh.cmd.gang0, n_runs = sh.cmd.n_runs;
+    int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+    for (int r = 0; r < n_runs && !stopped; ++r) {
+      if (tid == 0) sh.run = runs[r];
+      __syncthreads();
+      const int spec = sh.run.spec;
+      {  // level-0 keys of the run's spec (every node) into LDS, its static cache into `stat`
+        const kb_spec sp = P.specs[spec];
+        const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+        for (int i = tid; i < n; i += kSelThreads) {
+          const Row row = load_row(N, i);
+          const uint64_t st = static_eval<false>(N, P, C, sp, row.flags, i, nullptr);
+          stat[i] = st;
+          const uint32_t rs = row_reasons(N, P, C, sp, sci, row, st, i);
+          k32[i] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, row, st), i), i, idx_bits);
+        }
+      }
+      __syncthreads();
+      KB_SEL_PH(0);
+      const kb_spec sp = P.specs[spec];
+      sel_run(sh, k32, cand, N, P, C, sp, spec, sh.run.t_begin, sh.run.t_count, idx_bits, stat, ready, minav, gang, placed,
+              stop, fail_task, panic, stopped, hout, js, hjs, rp SEL_DIAG_ARGS);
+    }
+#ifdef KB_DIAG
+    if (tid == 0) {
+      for (int k = 0; k < 7; ++k) hjs->diag[k] = dg[k];
+      hjs->diag[7] = __builtin_amdgcn_s_memrealtime() - rt0;
+    }
+#endif
+    // every wave's placement and row stores are complete before the barrier; one lane then releases at
+    // system scope and publishes the job state (the host spins on the sequence number)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      hjs->t_recv = sh.t_recv;
+      hjs->t_done = __builtin_amdgcn_s_memrealtime();
+      __threadfence_system();
+      publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, want);
+    }
+  }
+}
+
+void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint64_t* stat,
+                   const EngineCmd* cmd, JobState* js, JobState* hjs, int32_t* hout, uint32_t seq0,
+                   uint64_t idle_ticks, void* stream) {
+  hipLaunchKernelGGL(engine_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P, C,
+                     idx_bits, stat, cmd, js, hjs, hout, seq0, idle_ticks);
 }
 
 // Level-0 keys for the selection path: one node per thread, 64-thread blocks (a 10k-node table is
@@ -1713,7 +1884,7 @@ void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 
 int sel_lds_bytes(int n) {
   const long q4 = ((long)n + 4 * kSelThreads - 1) / (4 * kSelThreads);
-  const long bytes = 4l * (4 * kSelThreads * q4 + kCandCap);
+  const long bytes = 4l * (4 * kSelThreads * q4) + 8l * kCandCap;
   return q4 <= kSelQ4 && bytes <= kSelDynLimit ? (int)bytes : -1;
 }
 
@@ -2077,9 +2248,10 @@ int configure_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit);
     if (e != hipSuccess) return (int)e;
   }
-  hipError_t e = hipFuncSetAttribute((const void*)sel_place_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kSelDynLimit);
-  if (e != hipSuccess) return (int)e;
+  for (const void* f : {(const void*)sel_place_kernel, (const void*)engine_kernel}) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit);
+    if (e != hipSuccess) return (int)e;
+  }
   return 0;
 }
 

@@ -122,6 +122,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
+  c->use_engine = opts && (opts->flags & KB_OPT_ENGINE);
   if (hipSetDevice(c->device) != hipSuccess) {
     c->err = "hipSetDevice failed";
     c->broken = true;
@@ -129,6 +130,12 @@ kb_ctx* kb_create(const kb_opts* opts) {
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->err = "hipStreamCreate failed";
+    c->broken = true;
+    return c;
+  }
+  if (hipStreamCreateWithFlags(&c->eng_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->eng_dep, hipEventDisableTiming) != hipSuccess) {
+    c->err = "hipStreamCreate (engine) failed";
     c->broken = true;
     return c;
   }
@@ -143,13 +150,19 @@ kb_ctx* kb_create(const kb_opts* opts) {
 
 void kb_destroy(kb_ctx* c) {
   if (!c) return;
-  if (!c->broken) (void)hipSetDevice(c->device);
+  if (!c->broken) {
+    (void)hipSetDevice(c->device);
+    (void)kb_engine_stop(c);
+  }
   free_all(c->node_mem);
   free_all(c->spec_mem);
   free_all(c->aff_mem);
   free_all(c->work_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
+  if (c->h_cmd) (void)hipHostFree(c->h_cmd);
+  if (c->eng_dep) (void)hipEventDestroy(c->eng_dep);
+  if (c->eng_stream) (void)hipStreamDestroy(c->eng_stream);
   for (auto& p : c->pending) {
     c->ev_pool.push_back(p.a);
     c->ev_pool.push_back(p.b);
@@ -163,6 +176,7 @@ const char* kb_last_error(const kb_ctx* c) { return c ? c->err.c_str() : "null c
 
 int kb_set_config(kb_ctx* c, const kb_config* cfg) {
   if (!c || !cfg) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   c->cfg = DevCfg{cfg->predicates_enabled, cfg->nodeorder_enabled, cfg->mem_pressure, cfg->disk_pressure,
                   cfg->pid_pressure, cfg->w_lr, cfg->w_bra, cfg->w_na, cfg->w_pa};
   kb_update_traj_ok(c);
@@ -171,6 +185,7 @@ int kb_set_config(kb_ctx* c, const kb_config* cfg) {
 
 int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   if (!c || !in) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (in->n == 0 || in->n >= kMaxNodes) return fail(c, KB_E_INVALID, "node count %u out of range", in->n);
   if (in->n_scalar > 64) return fail(c, KB_E_UNSUPPORTED, "more than 64 scalar resource slots");
@@ -247,6 +262,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
 
 int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   if (!c || !in) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "upload nodes before specs");
   HIP_OK(c, hipSetDevice(c->device));
@@ -313,6 +329,7 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
 
 int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   if (!c || !a) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs before affinity");
   HIP_OK(c, hipSetDevice(c->device));
@@ -465,6 +482,138 @@ static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
   return KB_OK;
 }
 
+// ---- persistent placement engine (kbgpu_device.hip engine_kernel) ----
+constexpr uint64_t kEngineIdleTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz) without a command
+
+int kb_engine_stop(kb_ctx* c) {
+  if (!c || !c->eng_running) return KB_OK;
+  EngineCmd* cm = (EngineCmd*)c->h_cmd;
+  cm->op = KB_ENG_EXIT;
+  __atomic_store_n(&cm->seq, ++c->seq, __ATOMIC_RELEASE);
+  c->eng_running = false;
+  const hipError_t e = hipStreamSynchronize(c->eng_stream);  // bounded: EXIT or the idle timeout ends it
+  if (e != hipSuccess) return fail(c, KB_E_HIP, "placement engine: %s", hipGetErrorString(e));
+  return KB_OK;
+}
+
+// Launch the engine so that it serves commands from seq0 on, after everything queued on c->stream.
+static int engine_launch(kb_ctx* c, uint32_t seq0) {
+  HIP_OK(c, hipEventRecord(c->eng_dep, c->stream));
+  HIP_OK(c, hipStreamWaitEvent(c->eng_stream, c->eng_dep, 0));
+  launch_engine(c->N, c->P, c->cfg, c->idx_bits, c->stat, (const EngineCmd*)c->h_cmd_dev, (JobState*)c->d_job,
+                (JobState*)c->h_job_dev, (int32_t*)(c->h_job_dev + sizeof(JobState)), seq0, kEngineIdleTicks,
+                c->eng_stream);
+  HIP_OK(c, hipGetLastError());
+  c->eng_running = true;
+  return KB_OK;
+}
+
+// Every task of the job goes through the selection path: 32-bit keys, no inter-pod affinity, LDS fit.
+static bool engine_ok(const kb_ctx* c, const kb_job_req* job) {
+  if (!c->use_engine || !c->use_sel || !c->sel_ok) return false;
+  for (uint32_t i = 0; i < job->n_tasks; ++i) {
+    const int s = job->task_specs[i];
+    if (!c->spec_traj_ok[s] || c->spec_needs_aff[s]) return false;
+  }
+  return true;
+}
+
+static int engine_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
+                            kb_job_result* result) {
+  uint32_t n_runs = 0;
+  for (uint32_t t = 0; t < job->n_tasks; ++t)
+    if (t == 0 || job->task_specs[t] != job->task_specs[t - 1]) ++n_runs;
+  // buffers the engine holds pointers to: grow them only while it is stopped
+  if (n_runs > c->cmd_cap || job->n_tasks > c->job_cap || !c->h_job) {
+    if (int rc = kb_engine_stop(c)) return rc;
+    if (int rc = ensure_job_buffers(c, job->n_tasks)) return rc;
+    if (n_runs > c->cmd_cap || !c->h_cmd) {
+      const uint32_t cap = std::max<uint32_t>(n_runs, 256);
+      if (c->h_cmd) (void)hipHostFree(c->h_cmd);
+      c->h_cmd = nullptr;
+      HIP_OK(c, hipHostMalloc((void**)&c->h_cmd, sizeof(EngineCmd) + (size_t)cap * sizeof(EngineRun),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_OK(c, hipHostGetDevicePointer((void**)&c->h_cmd_dev, c->h_cmd, 0));
+      memset(c->h_cmd, 0, sizeof(EngineCmd));
+      ((EngineCmd*)c->h_cmd)->seq = c->seq;
+      c->cmd_cap = cap;
+    }
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  EngineCmd* cm = (EngineCmd*)c->h_cmd;
+  EngineRun* runs = (EngineRun*)(cm + 1);
+  uint32_t r = 0;
+  for (uint32_t t = 0; t < job->n_tasks;) {
+    uint32_t e = t + 1;
+    while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
+    runs[r++] = EngineRun{job->task_specs[t], (int32_t)t, (int32_t)(e - t), 0};
+    t = e;
+  }
+  // an engine that exited (idle timeout) is relaunched below
+  if (c->eng_running) {
+    const hipError_t q = hipStreamQuery(c->eng_stream);
+    if (q == hipSuccess) c->eng_running = false;
+    else if (q != hipErrorNotReady) {
+      c->eng_running = false;
+      return fail(c, KB_E_HIP, "placement engine failed: %s", hipGetErrorString(q));
+    }
+  }
+  cm->op = KB_ENG_RUN;
+  cm->n_runs = (int32_t)n_runs;
+  cm->ready0 = job->ready_num;
+  cm->minav0 = job->min_available;
+  cm->gang0 = job->gang_ready;
+  const uint32_t want = ++c->seq;
+  __atomic_store_n(&cm->seq, want, __ATOMIC_RELEASE);
+  if (!c->eng_running)
+    if (int rc = engine_launch(c, want)) return rc;
+  const JobState* hs = (const JobState*)c->h_job;
+  for (uint64_t spin = 0;; ++spin) {
+    if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == want) break;
+    if ((spin & 1023) == 1023) {
+      if (__atomic_load_n(&hs->exit_seq, __ATOMIC_ACQUIRE) == want) {  // it timed out just before our post
+        (void)hipStreamSynchronize(c->eng_stream);
+        c->eng_running = false;
+        if (int rc = engine_launch(c, want)) return rc;
+        continue;
+      }
+      const hipError_t q = hipStreamQuery(c->eng_stream);
+      if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != want &&
+          __atomic_load_n(&hs->exit_seq, __ATOMIC_ACQUIRE) != want) {
+        c->eng_running = false;
+        return fail(c, KB_E_HIP, "placement engine exited without serving command %u", want);
+      }
+      if (q != hipSuccess && q != hipErrorNotReady) {
+        c->eng_running = false;
+        return fail(c, KB_E_HIP, "placement engine failed: %s", hipGetErrorString(q));
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        return fail(c, KB_E_HIP, "placement engine did not answer command %u within 120 s", want);
+    }
+  }
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->device_ms += wall;
+  c->stats.device_ms += wall;
+  c->stats.job_calls += 1;
+  for (int k = 0; k < 8; ++k) c->stats.diag[k] += hs->diag[k];
+  const uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
+  c->stats.launches[KB_KERNEL_ENGINE] += 1;
+  c->stats.kernel_ms[KB_KERNEL_ENGINE] += (double)(hs->t_done - hs->t_recv) * 1e-5;  // 100 MHz ticks
+  c->stats.pairs[KB_KERNEL_ENGINE] += tasks * (uint64_t)c->N.n;
+  const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
+  result->n_placed = (uint32_t)hs->n_placed;
+  result->stop = hs->stop;
+  result->fail_task = hs->fail_task;
+  if (hs->stop == KB_STOP_NO_FIT)
+    for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
+  for (int i = 0; i < hs->n_placed; ++i) {
+    if (placed_node) placed_node[i] = ho[2 * i];
+    if (placed_kind) placed_kind[i] = ho[2 * i + 1];
+  }
+  if (hs->panic) return fail(c, KB_E_PANIC, "SelectBestNode: no node scored above -1 (task %d)", hs->fail_task);
+  return KB_OK;
+}
+
 int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
                  kb_job_result* result) {
   if (!c || !job || !result) return KB_E_INVALID;
@@ -479,6 +628,8 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first",
                   job->task_specs[i]);
   }
+  if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
+  if (int rc = kb_engine_stop(c)) return rc;
   int rc = ensure_job_buffers(c, job->n_tasks);
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
@@ -516,7 +667,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       c->ev_begin(&ea);
       launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, aff,
                        c->stream);
-      c->ev_end(ea, KB_KERNEL_SWEEP, (uint64_t)c->N.n);
+      c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
       launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, c->traj, c->stat, js, first,
                        job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
@@ -587,6 +738,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   if (c) c->timing_now = c->timing;
   if (!c || (!spec_ids && t)) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
   for (uint32_t i = 0; i < t; ++i) {
     if (spec_ids[i] < 0 || spec_ids[i] >= c->P.m) return fail(c, KB_E_INVALID, "spec id %d", spec_ids[i]);
@@ -639,6 +791,7 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
 
 int kb_restore_nodes(kb_ctx* c) {
   if (!c) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
   for (auto& col : c->pristine)
     if (col.bytes) HIP_OK(c, hipMemcpyAsync(col.dst, col.src, col.bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -658,6 +811,7 @@ int kb_get_stats(kb_ctx* c, kb_stats* out, int reset) {
 int kb_read_nodes(kb_ctx* c, int64_t* idle_cpu, int64_t* idle_mem, int64_t* rel_cpu, int64_t* rel_mem,
                   int32_t* pod_count, int64_t* nz_cpu, int64_t* nz_mem) {
   if (!c) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
   HIP_OK(c, hipSetDevice(c->device));
   HIP_OK(c, hipStreamSynchronize(c->stream));

@@ -82,22 +82,25 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 8), ("kernel_ms", C.c_double * 8), ("pairs", C.c_uint64 * 8),
+    _fields_ = [("launches", C.c_uint64 * 10), ("kernel_ms", C.c_double * 10), ("pairs", C.c_uint64 * 10),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
 KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
 KB_OPT_NO_SELECT = 4
+KB_OPT_ENGINE = 8
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
-           "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel")
+           "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel")
 # device paths for a run of same-spec tasks (kb_place_job picks the first one that applies):
-#   select     - one parallel top-T selection per run (sel_place_kernel)
+#   select     - per-job launches of the level-0 sweep + the top-T selection kernel (default)
+#   engine     - the same selection served by one persistent workgroup (no launches; single-CU sweep)
 #   trajectory - precomputed per-node key trajectories + a one-wave argmax loop (traj_place_kernel)
 #   rekey      - 64-bit keys, per-commit re-key + one-wave argmax loop (place_loop_kernel)
-PATHS = {"select": 0, "trajectory": KB_OPT_NO_SELECT, "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
+PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
+         "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 4  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 5  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",

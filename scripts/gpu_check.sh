@@ -27,7 +27,7 @@ if [ "$MODE" = diag ]; then  # phase cycle counts of the place loop (KB_DIAG bui
   KBGPU_LIB=scheduler_amd/libkbgpu_diag.so step bench_diag 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline
 fi
 if [ "$MODE" = diagsel ]; then  # node-selection sub-phases of the selection kernel (KB_DIAG_SEL build)
-  KBGPU_LIB=scheduler_amd/libkbgpu_diagsel.so step bench_diagsel 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+  KBGPU_LIB=scheduler_amd/libkbgpu_diagsel.so step bench_diagsel 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --path select
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   export TMPDIR=/tmp

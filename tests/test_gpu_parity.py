@@ -85,7 +85,7 @@ def test_full_size_c2_properties():
     finally:
         ctx.close()
     others = []
-    for path in ("trajectory", "rekey"):
+    for path in ("engine", "trajectory", "rekey"):
         ctx = runtime.Context(0, path=path)
         try:
             ctx.upload(snap)
@@ -169,3 +169,26 @@ def test_c4_full_size_properties():
         if t["status"] == E.ST["Pending"] and "podAntiAffinity" in aff:
             nodes = by_job.get(t["pod"].group, [])
             assert len(nodes) == len(set(nodes)), t["pod"].group
+
+
+def test_engine_idle_exit_and_relaunch():
+    """The placement engine exits by itself after 1 s without a command; the next kb_place_job relaunches
+    it and the session goes on with the same results as the launch-per-job path."""
+    import time
+    cl = synth.c2(n_nodes=300, n_jobs=20, tasks_per_job=20, seed=9)
+    snap = E.Snapshot(cl)
+    outs = []
+    for path in ("engine", "select"):
+        ctx = runtime.Context(0, path=path)
+        try:
+            ctx.upload(snap)
+            first = ctx.allocate(snap)
+            time.sleep(1.5)  # engine idles out
+            spec = int(snap.s_task_spec[0])
+            nodes, kinds, res = ctx.place_job([spec] * 7, ready_num=0, min_available=7, gang_ready=1)
+            outs.append((first, nodes, kinds, res.stop, res.n_placed))
+        finally:
+            ctx.close()
+    (a, na, ka, sa, pa), (b, nb, kb, sb, pb) = outs
+    assert np.array_equal(a["task_node"], b["task_node"]) and np.array_equal(a["event_task"], b["event_task"])
+    assert np.array_equal(na, nb) and np.array_equal(ka, kb) and (sa, pa) == (sb, pb)
