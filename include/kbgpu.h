@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 5
+#define KBGPU_ABI_VERSION 6
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -361,7 +361,10 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_SEL_PLACE 7 /* a run as one parallel top-T selection (32-bit keys) */
 #define KB_KERNEL_ENGINE 8    /* persistent placement engine: device time per served job */
 #define KB_KERNEL_SEL_SWEEP 9 /* level-0 keys of every node for the selection path */
-#define KB_NUM_KERNELS 10
+#define KB_KERNEL_SHARD_PROPOSE 10 /* node sharding: the rank's proposal for a segment */
+#define KB_KERNEL_SHARD_EXCHANGE 11 /* node sharding: the all-gather of the proposals (RCCL) */
+#define KB_KERNEL_SHARD_COMMIT 12  /* node sharding: global merge, stop rules, own commits */
+#define KB_NUM_KERNELS 13
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */
@@ -375,6 +378,30 @@ int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 /* Read back the mutable node columns (for tests and for the Go side's NodeInfo replay). */
 int kb_read_nodes(kb_ctx* ctx, int64_t* idle_cpu, int64_t* idle_mem, int64_t* rel_cpu, int64_t* rel_mem,
                   int32_t* pod_count, int64_t* nz_cpu, int64_t* nz_mem);
+
+/*
+ * ---- node sharding across GPUs ----
+ * The canonical node table is split into contiguous blocks, one per rank (one process per GPU). Every
+ * rank uploads only its block (kb_upload_nodes with those rows) plus every spec, and every rank runs the
+ * same allocate loop. Per run segment (<= 100 tasks of one spec) each rank proposes its own best picks
+ * (the selection path), the ranks exchange the proposals with ONE all-gather (1280 B per rank), and every
+ * rank merges them into the same global pick order, applies the stop rules and commits the picks that
+ * land on its own rows -- the same placements as one GPU holding the whole table. Node indices in
+ * placements are global. Only selection-path jobs (32-bit keys, no inter-pod affinity) run sharded;
+ * others return KB_E_UNSUPPORTED. Call before kb_upload_nodes.
+ */
+typedef struct kb_shard {
+  uint32_t n_total;    /* nodes in the whole session */
+  uint32_t node_begin; /* this rank's first canonical node */
+  int32_t rank, world; /* world <= 16 */
+} kb_shard;
+/* Host-staged exchange: copy `bytes` from send into recv + r * bytes for every rank r (host memory). */
+typedef int (*kb_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+int kb_set_shard(kb_ctx* ctx, const kb_shard* shard, kb_allgather_fn fn, void* user);
+/* Device exchange over RCCL (xGMI): rank 0 makes the id, every rank passes the same bytes. */
+#define KB_COMM_ID_BYTES 128
+int kb_comm_unique_id(uint8_t id[KB_COMM_ID_BYTES]);
+int kb_set_shard_rccl(kb_ctx* ctx, const kb_shard* shard, const uint8_t id[KB_COMM_ID_BYTES]);
 
 /* ---- layer 2: session (allocate action + ordering plugins on the host) ---- */
 

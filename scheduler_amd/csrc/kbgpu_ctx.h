@@ -46,6 +46,15 @@ struct kb_ctx {
   char* h_cmd = nullptr;         // pinned mailbox: EngineCmd + EngineRun[cmd_cap]
   char* h_cmd_dev = nullptr;
   uint32_t cmd_cap = 0;
+  // node sharding (kb_set_shard / kb_set_shard_rccl)
+  bool sharded = false;
+  kb_shard shard{};
+  kb_allgather_fn ag_fn = nullptr;
+  void* ag_user = nullptr;
+  void* comm = nullptr;            // ncclComm_t when the exchange is RCCL
+  kbgpu::ShardRec* d_rec = nullptr;     // this rank's proposal
+  kbgpu::ShardRec* d_rec_all = nullptr; // [world] all proposals
+  kbgpu::ShardRec* h_rec = nullptr;     // host staging (host exchange): [1 + world]
   bool traj_full = false;  // trajectory buffers (kTrajMaxJ + 1 levels): chunk maxima fit the place loop
   bool sel_ok = false;     // the node count fits the selection kernel's LDS plan (level-0 keys buffer)
   char* d_job = nullptr;     // device JobState (chains the runs of one job)

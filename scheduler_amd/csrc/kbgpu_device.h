@@ -17,6 +17,8 @@ constexpr uint32_t kMaxNodes = 1u << 24;
 
 struct DevNodes {
   int32_t n, S, K, P;
+  int32_t base;  // canonical index of row 0 (node sharding across GPUs; 0 on one GPU)
+  int32_t pad;
   int64_t *idle_cpu, *idle_mem, *rel_cpu, *rel_mem;
   int64_t *idle_sc, *rel_sc;
   int64_t *alloc_cpu, *alloc_mem;
@@ -82,6 +84,18 @@ struct JobState {
   uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
 };
 
+// Node sharding (kb_set_shard): one rank's proposal for a run segment, exchanged by an all-gather.
+constexpr int kShardSegMax = 100;  // == the selection path's segment length (kSegMax)
+struct ShardRec {
+  int32_t kp;                      // proposals (feasible picks, best first)
+  int32_t pad;
+  uint32_t hist[KB_NUM_REASONS];   // reason histogram of this rank's rows after all kp picks (kp < T only)
+  uint64_t comp[kShardSegMax];     // pick-order composites (global node index inside)
+  int32_t node_kind[kShardSegMax]; // global node | kind << 30
+  int32_t pad2[2];
+};
+static_assert(sizeof(ShardRec) % 16 == 0, "ShardRec is exchanged as raw bytes");
+
 // Placement engine mailbox (pinned host memory, written by the host): one command per kb_place_job.
 #define KB_ENG_RUN 1
 #define KB_ENG_EXIT 2
@@ -133,6 +147,15 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint64_t* stat,
                    const EngineCmd* cmd, JobState* js, JobState* hjs, int32_t* hout, uint32_t seq0,
                    uint64_t idle_ticks, void* stream);
+
+// Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
+// all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.
+void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
+                          int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
+                          ShardRec* rec, void* stream);
+void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                         int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
+                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 
 // Opt the place kernels into the dynamic LDS they need; returns 0 or the hipError_t.
 int configure_kernels();

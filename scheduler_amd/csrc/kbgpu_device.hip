@@ -1288,12 +1288,16 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 // k32 (LDS, n_pad entries, zero past n) holds every node's current key at entry and is kept current;
 // cand (LDS, kCandCap) is scratch; stat is the run's static cache. Placements go to hout[2 * task];
 // ready / placed advance, and the stop state is set when the run stops the job.
+// PROPOSE (node sharding): one segment of t_count <= kSegMax tasks, no commit; the rank's best picks go
+// to `rec` instead (launch_shard_propose).
+template <bool PROPOSE = false>
 __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* cand, const DevNodes& N,
                                         const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
                                         int t_begin, int t_count,
                                         int idx_bits, const uint64_t* stat, int& ready, int minav, int gang,
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
-                                        int32_t* hout, JobState* js, JobState* hjs, int& rp SEL_DIAG_PARAMS) {
+                                        int32_t* hout, JobState* js, JobState* hjs, int& rp,
+                                        ShardRec* rec SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -1303,6 +1307,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   const int64_t bias32 = 1ll << (30 - idx_bits);
   const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
   const uint64_t lt = (1ull << lane) - 1;
+  if (PROPOSE && tid == 0) rec->kp = 0;
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
@@ -1457,7 +1462,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           x = sh.key0[s];
           if (j > 0) {
             const int w = sh.node[s];
-            x = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w, idx_bits);
+            x = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w + N.base,
+                             idx_bits);
           }
         }
         // segmented inclusive prefix minimum over the group's lanes (levels in order)
@@ -1568,6 +1574,31 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
       __syncthreads();
       KB_SEL_PH(4);
+      if constexpr (PROPOSE) {
+        // the rank's proposal: its best picks in order with their global nodes and commit kinds; when it runs
+        // out of feasible picks, the reason histogram of its rows after all of them (the no-fit case)
+        const int Kp = sh.s_count;
+        if (tid < Kp) {
+          const uint64_t o = sh.ord[tid];
+          const int s = sel_slot(o), j = sel_level(o);
+          rec->comp[tid] = o;
+          rec->node_kind[tid] = (sh.node[s] + N.base) | ((j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE) << 30);
+          if (Kp < (int)T) atomicAdd(&sh.fin[s], 1);
+        }
+        if (tid == 0) rec->kp = Kp;
+        __syncthreads();
+        if (Kp == (int)T) {
+          if (tid < KB_NUM_REASONS) rec->hist[tid] = 0;
+          break;
+        }
+        if (tid < (int)S && sh.fin[tid] > 0) {
+          const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
+          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
+                                idx_bits);
+        }
+        __syncthreads();
+        no_fit = true;
+      } else {
       // ---- stop rules in pick order (wave 0) ----
       if (wv == 0) {
         const int Kp = sh.s_count;
@@ -1619,7 +1650,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         const int s = sel_slot(o), j = sel_level(o);
         atomicAdd(&sh.fin[s], 1);
         const int at = t_begin + done_tasks + tid;
-        hout[2 * at] = sh.node[s];
+        hout[2 * at] = sh.node[s] + N.base;
         hout[2 * at + 1] = j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
       }
       __syncthreads();
@@ -1629,7 +1660,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
         store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
         if (rekey)
-          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w, idx_bits);
+          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
+                                idx_bits);
       }
       __syncthreads();
       KB_SEL_PH(5);
@@ -1648,6 +1680,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         break;
       }
       no_fit = kind == KB_STOP_NO_FIT;
+      }
     }
     if (no_fit) {
       // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes at their
@@ -1673,6 +1706,10 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         if (lane == 0 && v) atomicAdd(&sh.hist[b], v);
       }
       __syncthreads();
+      if (PROPOSE) {
+        if (tid < KB_NUM_REASONS) rec->hist[tid] = sh.hist[tid];
+        break;
+      }
       if (tid < KB_NUM_REASONS) {
         js->hist[tid] = sh.hist[tid];
         hjs->hist[tid] = sh.hist[tid];
@@ -1723,7 +1760,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   KB_SEL_PH(0);
 
   sel_run(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
-          panic, stopped, hout, js, hjs, rp SEL_DIAG_ARGS);
+          panic, stopped, hout, js, hjs, rp, nullptr SEL_DIAG_ARGS);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
@@ -1820,14 +1857,14 @@ __global__ __launch_bounds__(kSelThreads) void engine_kernel(DevNodes N, DevSpec
           const uint64_t st = static_eval<false>(N, P, C, sp, row.flags, i, nullptr);
           stat[i] = st;
           const uint32_t rs = row_reasons(N, P, C, sp, sci, row, st, i);
-          k32[i] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, row, st), i), i, idx_bits);
+          k32[i] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, row, st), i), i + N.base, idx_bits);
         }
       }
       __syncthreads();
       KB_SEL_PH(0);
       const kb_spec sp = P.specs[spec];
       sel_run(sh, k32, cand, N, P, C, sp, spec, sh.run.t_begin, sh.run.t_count, idx_bits, stat, ready, minav, gang, placed,
-              stop, fail_task, panic, stopped, hout, js, hjs, rp SEL_DIAG_ARGS);
+              stop, fail_task, panic, stopped, hout, js, hjs, rp, nullptr SEL_DIAG_ARGS);
     }
 #ifdef KB_DIAG
     if (tid == 0) {
@@ -1868,7 +1905,7 @@ __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, D
   const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
   stat[n] = st;
   const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
-  keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n, idx_bits);
+  keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
 }
 
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
@@ -1880,6 +1917,209 @@ void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   else
     hipLaunchKernelGGL(sel_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec,
                        idx_bits, keys32, stat, js);
+}
+
+// ===========================================================================
+// Node sharding across GPUs. Every rank holds a contiguous block of the canonical node
+// table. Because the picks of a run come out in descending composite order (the selection argument
+// above), the global first-T picks are the T largest of the union of every rank's own first-T picks:
+// one all-gather of the ranks' proposals per segment replaces a collective per task. Each rank then
+// merges the same proposals into the same global order, applies the stop rules, and commits the picks
+// that land on its own rows.
+// ===========================================================================
+static_assert(kShardSegMax == kSegMax, "ShardRec holds one segment");
+
+__global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec,
+                                                                    int t_count, int idx_bits,
+                                                                    const uint32_t* keys32, const uint64_t* stat,
+                                                                    const JobState* js, int first, ShardRec* rec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ SelShared sh;
+  if (!first && js->stopped) return;  // the segment's commit kernel skips too
+  const int tid = threadIdx.x;
+  const int n = N.n;
+  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  uint32_t* k32 = lds32;
+  uint64_t* cand = (uint64_t*)(lds32 + n_pad);
+  const kb_spec sp = P.specs[spec];
+  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
+  int ready = 0, placed = 0, stop = 0, fail_task = -1, panic = 0, stopped = 0, rp = 0;
+#ifdef KB_DIAG
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+#endif
+  __syncthreads();
+  sel_run<true>(sh, k32, cand, N, P, C, sp, spec, 0, t_count, idx_bits, stat, ready, 0, 0, placed, stop, fail_task,
+                panic, stopped, nullptr, nullptr, nullptr, rp, rec SEL_DIAG_ARGS);
+}
+
+// Elements of a proposal list (descending) greater than v.
+__device__ __forceinline__ int shard_count_gt(const uint64_t* list, int len, uint64_t v) {
+  int lo = 0, hi = len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (list[mid] > v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+constexpr int kShardMaxWorld = 16;
+
+__global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec,
+                                                                   int t_begin, int t_count, int idx_bits,
+                                                                   const ShardRec* recs, int world, JobState* js,
+                                                                   int first, int ready0, int minav0, int gang0,
+                                                                   int32_t* hout, JobState* hjs, uint32_t seq) {
+  __shared__ ShardRec r[kShardMaxWorld];
+  __shared__ uint64_t ord[128];
+  __shared__ int32_t ordnk[128];
+  __shared__ int32_t fin[128], fin_node[128];
+  __shared__ int32_t s_cut, s_kind, s_alloc;
+  __shared__ LoopOut lo;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t T = (uint32_t)t_count;
+  const int64_t bias32 = 1ll << (30 - idx_bits);
+  const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
+  const uint64_t lt = (1ull << lane) - 1;
+  {  // every rank's proposal into LDS
+    const uint4* src = (const uint4*)recs;
+    uint4* dst = (uint4*)r;
+    const int words = world * (int)(sizeof(ShardRec) / 16);
+    for (int i = tid; i < words; i += kSelThreads) dst[i] = src[i];
+  }
+  if (tid < 128) fin[tid] = 0;
+  const int ready_in = first ? ready0 : js->ready_num;
+  const int minav = first ? minav0 : js->min_available;
+  const int gang = first ? gang0 : js->gang_ready;
+  const int placed_in = first ? 0 : js->n_placed;
+  __syncthreads();
+  // global pick order: rank of proposal i of rank g = i + the larger proposals of every other rank
+  int K = 0;
+  for (int g = 0; g < world; ++g) K += r[g].kp;
+  for (int e = tid; e < world * kShardSegMax; e += kSelThreads) {
+    const int g = e / kShardSegMax, i = e % kShardSegMax;
+    if (i >= r[g].kp) continue;
+    const uint64_t v = r[g].comp[i];
+    int rank = i;
+    for (int h = 0; h < world; ++h)
+      if (h != g) rank += shard_count_gt(r[h].comp, r[h].kp, v);
+    if (rank < (int)T) {
+      ord[rank] = v;
+      ordnk[rank] = r[g].node_kind[i];
+    }
+  }
+  __syncthreads();
+  const int Kp = K < (int)T ? K : (int)T;
+  if (wv == 0) {  // stop rules in pick order (as the one-GPU selection kernel applies them)
+    const bool va = lane < Kp, vb = lane + 64 < Kp;
+    const uint64_t oa = va ? ord[lane] : 0, ob = vb ? ord[lane + 64] : 0;
+    const bool aa = va && (ordnk[lane] >> 30) == KB_PLACE_ALLOCATE;
+    const bool ab = vb && (ordnk[lane + 64] >> 30) == KB_PLACE_ALLOCATE;
+    const auto neg = [&](uint64_t o) {
+      const uint32_t e32 = (uint32_t)(o >> 14);
+      return (int64_t)((e32 >> idx_bits) & score_mask) - bias32 <= -1;
+    };
+    const uint64_t le_mask = lt | (1ull << lane);
+    const uint64_t ma = __ballot(aa), mb = __ballot(ab);
+    const int ra = ready_in + __popcll(ma & le_mask);
+    const int rb = ready_in + __popcll(ma) + __popcll(mb & le_mask);
+    const uint64_t sta = __ballot(va && (!gang || ra >= minav));
+    const uint64_t stb = __ballot(vb && (!gang || rb >= minav));
+    const uint64_t nga = __ballot(va && neg(oa)), ngb = __ballot(vb && neg(ob));
+    const int first_stop = sta ? __builtin_ctzll(sta) : (stb ? 64 + __builtin_ctzll(stb) : 128);
+    const int first_neg = nga ? __builtin_ctzll(nga) : (ngb ? 64 + __builtin_ctzll(ngb) : 128);
+    int cut, kind;
+    if (first_neg < Kp && first_neg <= first_stop) {
+      cut = first_neg;
+      kind = 3;
+    } else if (first_stop < Kp) {
+      cut = first_stop + 1;
+      kind = KB_STOP_READY;
+    } else if (Kp < (int)T) {
+      cut = Kp;
+      kind = KB_STOP_NO_FIT;
+    } else {
+      cut = (int)T;
+      kind = -1;
+    }
+    const int al = __popcll(cut >= 64 ? ma : (ma & ((1ull << cut) - 1))) +
+                   (cut > 64 ? __popcll(mb & ((1ull << (cut - 64)) - 1)) : 0);
+    if (lane == 0) {
+      s_cut = cut;
+      s_kind = kind;
+      s_alloc = al;
+    }
+  }
+  __syncthreads();
+  const int cut = s_cut, kind = s_kind;
+  // placements (every rank writes the whole sequence) and this rank's commits, counted per local slot
+  if (tid < cut) {
+    const int nk = ordnk[tid];
+    const int node = nk & 0x3fffffff;
+    hout[2 * (t_begin + tid)] = node;
+    hout[2 * (t_begin + tid) + 1] = nk >> 30;
+    if (node >= N.base && node < N.base + N.n) {
+      const int s = sel_slot(ord[tid]);
+      atomicAdd(&fin[s], 1);
+      fin_node[s] = node - N.base;
+    }
+  }
+  __syncthreads();
+  if (tid < 128 && fin[tid] > 0) {  // NodeInfo.AddTask x c on the rank's own row
+    const kb_spec sp = P.specs[spec];
+    const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+    const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+    const int w = fin_node[tid];
+    const Row row = load_row(N, w);
+    store_back_row(N, P, sp, scr, w, fin[tid], allocs_before_full(N, sp, sci, scr, row, w), row);
+  }
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  if (kind == 3) {
+    fail_task = t_begin + cut;
+    panic = 1;
+    stopped = 1;
+  } else if (kind == KB_STOP_READY) {
+    stop = KB_STOP_READY;
+    stopped = 1;
+  } else if (kind == KB_STOP_NO_FIT) {  // FitErrors over all ranks' rows
+    if (tid < KB_NUM_REASONS) {
+      uint32_t h = 0;
+      for (int g = 0; g < world; ++g) h += r[g].hist[tid];
+      js->hist[tid] = h;
+      hjs->hist[tid] = h;
+    }
+    stop = KB_STOP_NO_FIT;
+    fail_task = t_begin + cut;
+    stopped = 1;
+  }
+  if (tid == 0)
+    lo = LoopOut{stop, fail_task, placed_in + cut, ready_in + s_alloc, minav, gang, panic, stopped, 0, 0, 0, 0};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence_system();
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic, seq);
+  }
+}
+
+void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
+                          int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
+                          ShardRec* rec, void* stream) {
+  hipLaunchKernelGGL(shard_propose_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P,
+                     C, spec, t_count, idx_bits, keys32, stat, js, first, rec);
+}
+
+void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
+                         int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
+                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(kSelThreads), 0, (hipStream_t)stream, N, P, C, spec, t_begin,
+                     t_count, idx_bits, recs, world, js, first, ready0, minav0, gang0, hout, hjs, seq);
 }
 
 int sel_lds_bytes(int n) {
@@ -2248,7 +2488,7 @@ int configure_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit);
     if (e != hipSuccess) return (int)e;
   }
-  for (const void* f : {(const void*)sel_place_kernel, (const void*)engine_kernel}) {
+  for (const void* f : {(const void*)sel_place_kernel, (const void*)engine_kernel, (const void*)shard_propose_kernel}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit);
     if (e != hipSuccess) return (int)e;
   }

@@ -1,6 +1,7 @@
 // Host side of the device layer: context, HBM residency of the node table and
 // spec tables, per-job placement batches, parity evaluation.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -161,6 +162,10 @@ void kb_destroy(kb_ctx* c) {
   if (c->h_job) (void)hipHostFree(c->h_job);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
+  if (c->h_rec) (void)hipHostFree(c->h_rec);
+  if (c->d_rec) (void)hipFree(c->d_rec);
+  if (c->d_rec_all) (void)hipFree(c->d_rec_all);
+  if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   if (c->eng_dep) (void)hipEventDestroy(c->eng_dep);
   if (c->eng_stream) (void)hipStreamDestroy(c->eng_stream);
   for (auto& p : c->pending) {
@@ -197,6 +202,13 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   DevNodes& N = c->N;
   const size_t n = in->n;
   N.n = (int32_t)in->n;
+  N.base = 0;
+  if (c->sharded) {
+    if ((uint64_t)c->shard.node_begin + in->n > c->shard.n_total)
+      return fail(c, KB_E_INVALID, "shard rows [%u, %u) exceed n_total %u", c->shard.node_begin,
+                  c->shard.node_begin + in->n, c->shard.n_total);
+    N.base = (int32_t)c->shard.node_begin;
+  }
   N.S = (int32_t)in->n_scalar;
   N.K = (int32_t)in->n_label;
   N.P = (int32_t)in->n_port;
@@ -236,8 +248,9 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, n * sizeof(uint64_t)));
   c->work_mem.push_back(p);
   c->stat = (uint64_t*)p;
-  c->idx_bits = 1;
-  while ((1ull << c->idx_bits) < (unsigned long long)n) ++c->idx_bits;
+  c->idx_bits = 1;  // key index field: global node indices when sharded
+  const unsigned long long n_keys = c->sharded ? c->shard.n_total : n;
+  while ((1ull << c->idx_bits) < n_keys) ++c->idx_bits;
   int pbc;
   c->traj_full = traj_lds_bytes((int)n, 64, &pbc) > 0;
   c->sel_ok = sel_lds_bytes((int)n) >= 0;
@@ -332,6 +345,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs before affinity");
+  if (c->sharded) return fail(c, KB_E_UNSUPPORTED, "inter-pod affinity tables do not run node-sharded");
   HIP_OK(c, hipSetDevice(c->device));
   drop_affinity(c);
   const size_t n = (size_t)c->N.n;
@@ -614,6 +628,151 @@ static int engine_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_no
   return KB_OK;
 }
 
+// ---- node sharding across GPUs ----
+static int shard_common(kb_ctx* c, const kb_shard* sh) {
+  if (!c || !sh) return KB_E_INVALID;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (sh->world < 1 || sh->world > 16 || sh->rank < 0 || sh->rank >= sh->world || sh->n_total == 0 ||
+      sh->n_total >= kMaxNodes || sh->node_begin >= sh->n_total)
+    return fail(c, KB_E_INVALID, "bad shard (rank %d of %d, begin %u of %u)", sh->rank, sh->world, sh->node_begin,
+                sh->n_total);
+  if (c->nodes_ok) return fail(c, KB_E_STATE, "kb_set_shard comes before kb_upload_nodes");
+  HIP_OK(c, hipSetDevice(c->device));
+  if (!c->d_rec) {
+    HIP_OK(c, hipMalloc((void**)&c->d_rec, sizeof(ShardRec)));
+    HIP_OK(c, hipMemset(c->d_rec, 0, sizeof(ShardRec)));
+  }
+  if (c->d_rec_all) (void)hipFree(c->d_rec_all);
+  c->d_rec_all = nullptr;
+  HIP_OK(c, hipMalloc((void**)&c->d_rec_all, sizeof(ShardRec) * (size_t)sh->world));
+  HIP_OK(c, hipMemset(c->d_rec_all, 0, sizeof(ShardRec) * (size_t)sh->world));
+  c->shard = *sh;
+  c->sharded = true;
+  return KB_OK;
+}
+
+int kb_set_shard(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) {
+  if (!c) return KB_E_INVALID;
+  if (!fn) return fail(c, KB_E_INVALID, "kb_set_shard needs an all-gather function");
+  if (int rc = shard_common(c, sh)) return rc;
+  if (c->h_rec) (void)hipHostFree(c->h_rec);
+  c->h_rec = nullptr;
+  HIP_OK(c, hipHostMalloc((void**)&c->h_rec, sizeof(ShardRec) * (size_t)(1 + sh->world), hipHostMallocDefault));
+  c->ag_fn = fn;
+  c->ag_user = user;
+  return KB_OK;
+}
+
+int kb_comm_unique_id(uint8_t id[KB_COMM_ID_BYTES]) {
+  if (!id) return KB_E_INVALID;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return KB_E_HIP;
+  memcpy(id, &u, sizeof(u) < KB_COMM_ID_BYTES ? sizeof(u) : KB_COMM_ID_BYTES);
+  return KB_OK;
+}
+
+int kb_set_shard_rccl(kb_ctx* c, const kb_shard* sh, const uint8_t id[KB_COMM_ID_BYTES]) {
+  if (!c) return KB_E_INVALID;
+  if (!id) return fail(c, KB_E_INVALID, "missing RCCL id");
+  if (int rc = shard_common(c, sh)) return rc;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t comm;
+  const ncclResult_t r = ncclCommInitRank(&comm, sh->world, u, sh->rank);
+  if (r != ncclSuccess) return fail(c, KB_E_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
+  c->comm = comm;
+  c->ag_fn = nullptr;
+  return KB_OK;
+}
+
+// One job on a node-sharded table: per run segment, sweep + local proposal, one all-gather, merge + commit.
+static int shard_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
+                           kb_job_result* result) {
+  if (!c->sel_ok || !c->traj) return fail(c, KB_E_UNSUPPORTED, "sharded table does not fit the selection path");
+  for (uint32_t i = 0; i < job->n_tasks; ++i) {
+    const int s = job->task_specs[i];
+    if (!c->spec_traj_ok[s] || c->spec_needs_aff[s])
+      return fail(c, KB_E_UNSUPPORTED, "spec %d needs a path that does not run sharded", s);
+  }
+  if (int rc = ensure_job_buffers(c, job->n_tasks)) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  c->pending_job_begin = c->pending.size();
+  c->timing_now = c->timing && (c->stats.job_calls % c->timing_every == 0);
+  memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
+  JobState* js = (JobState*)c->d_job;
+  JobState* hjs_dev = (JobState*)c->h_job_dev;
+  int32_t* hout_dev = (int32_t*)(c->h_job_dev + sizeof(JobState));
+  const size_t rb = sizeof(ShardRec);
+  for (uint32_t t = 0; t < job->n_tasks;) {
+    uint32_t e = t + 1;
+    while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
+    const int spec = job->task_specs[t];
+    for (uint32_t seg = t; seg < e; seg += kShardSegMax) {
+      const int T = (int)std::min<uint32_t>(kShardSegMax, e - seg);
+      const int first = seg == 0;
+      hipEvent_t ea;
+      c->ev_begin(&ea);
+      launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, false,
+                       c->stream);
+      c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
+      c->ev_begin(&ea);
+      launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, c->traj, c->stat, js, first, c->d_rec,
+                           c->stream);
+      c->ev_end(ea, KB_KERNEL_SHARD_PROPOSE, 0);
+      c->ev_begin(&ea);
+      if (c->comm) {
+        const ncclResult_t r = ncclAllGather(c->d_rec, c->d_rec_all, rb, ncclUint8, (ncclComm_t)c->comm, c->stream);
+        if (r != ncclSuccess) return fail(c, KB_E_HIP, "ncclAllGather: %s", ncclGetErrorString(r));
+      } else {  // host-staged: every rank calls the exchange for every segment, stopped or not
+        HIP_OK(c, hipMemcpyAsync(c->h_rec, c->d_rec, rb, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+        if (int rc = c->ag_fn(c->ag_user, c->h_rec, c->h_rec + 1, rb))
+          return fail(c, KB_E_HIP, "all-gather callback failed (%d)", rc);
+        HIP_OK(c, hipMemcpyAsync(c->d_rec_all, c->h_rec + 1, rb * (size_t)c->shard.world, hipMemcpyHostToDevice,
+                                 c->stream));
+      }
+      c->ev_end(ea, KB_KERNEL_SHARD_EXCHANGE, 0);
+      c->ev_begin(&ea);
+      launch_shard_commit(c->N, c->P, c->cfg, spec, (int)seg, T, c->idx_bits, c->d_rec_all, c->shard.world, js,
+                          first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq,
+                          c->stream);
+      c->ev_end(ea, KB_KERNEL_SHARD_COMMIT, 0);
+    }
+    t = e;
+  }
+  HIP_OK(c, hipGetLastError());
+  if (int rc = wait_seq(c)) return rc;
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->device_ms += wall;
+  c->stats.device_ms += wall;
+  c->stats.job_calls += 1;
+  const JobState* hs = (const JobState*)c->h_job;
+  if (c->timing) {
+    uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
+    for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
+      auto& p = c->pending[k];
+      if (p.kind == KB_KERNEL_SHARD_PROPOSE) {
+        p.pairs = tasks * (uint64_t)c->N.n;
+        tasks = 0;
+      }
+    }
+    c->ev_collect(false);
+  }
+  const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
+  result->n_placed = (uint32_t)hs->n_placed;
+  result->stop = hs->stop;
+  result->fail_task = hs->fail_task;
+  if (hs->stop == KB_STOP_NO_FIT)
+    for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
+  for (int i = 0; i < hs->n_placed; ++i) {
+    if (placed_node) placed_node[i] = ho[2 * i];
+    if (placed_kind) placed_kind[i] = ho[2 * i + 1];
+  }
+  if (hs->panic) return fail(c, KB_E_PANIC, "SelectBestNode: no node scored above -1 (task %d)", hs->fail_task);
+  return KB_OK;
+}
+
 int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
                  kb_job_result* result) {
   if (!c || !job || !result) return KB_E_INVALID;
@@ -628,6 +787,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first",
                   job->task_specs[i]);
   }
+  if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
   if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
   if (int rc = kb_engine_stop(c)) return rc;
   int rc = ensure_job_buffers(c, job->n_tasks);

@@ -51,6 +51,21 @@ class kb_config(C.Structure):
                                           "pid_pressure", "w_lr", "w_bra", "w_na", "w_pa")]
 
 
+class kb_shard(C.Structure):
+    _fields_ = [("n_total", C.c_uint32), ("node_begin", C.c_uint32), ("rank", C.c_int32), ("world", C.c_int32)]
+
+
+# kb_allgather_fn: int (*)(void* user, const void* send, void* recv, size_t bytes)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
+def shard_range(n_total: int, rank: int, world: int):
+    """Contiguous block of canonical nodes held by `rank` (the first n_total % world ranks get one more)."""
+    q, r = divmod(n_total, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
 class kb_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("timing_every", C.c_uint32)]
 
@@ -82,7 +97,7 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 10), ("kernel_ms", C.c_double * 10), ("pairs", C.c_uint64 * 10),
+    _fields_ = [("launches", C.c_uint64 * 13), ("kernel_ms", C.c_double * 13), ("pairs", C.c_uint64 * 13),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
@@ -91,7 +106,8 @@ KB_OPT_NO_TRAJECTORY = 2
 KB_OPT_NO_SELECT = 4
 KB_OPT_ENGINE = 8
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
-           "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel")
+           "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
+           "shard_propose_kernel", "shard_exchange", "shard_commit_kernel")
 # device paths for a run of same-spec tasks (kb_place_job picks the first one that applies):
 #   select     - per-job launches of the level-0 sweep + the top-T selection kernel (default)
 #   engine     - the same selection served by one persistent workgroup (no launches; single-CU sweep)
@@ -100,11 +116,11 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 5  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 6  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
-           "kb_get_stats", "kb_upload_affinity"]
+           "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl"]
 
 _lib = None
 
@@ -141,6 +157,9 @@ def load_library(path: str = LIB_PATH):
     lib.kb_allocate.argtypes = [P, C.POINTER(kb_session), C.POINTER(kb_cycle_result)]
     lib.kb_restore_nodes.argtypes = [P]
     lib.kb_get_stats.argtypes = [P, C.POINTER(kb_stats), C.c_int]
+    lib.kb_set_shard.argtypes = [P, C.POINTER(kb_shard), ALLGATHER_FN, P]
+    lib.kb_comm_unique_id.argtypes = [P]
+    lib.kb_set_shard_rccl.argtypes = [P, C.POINTER(kb_shard), P]
     _lib = lib
     return lib
 
@@ -180,14 +199,39 @@ class Context:
         if rc != KB_OK:
             raise KbError(rc, self.lib.kb_last_error(self.ctx).decode())
 
+    def set_shard(self, rank: int, world: int, n_total: int, allgather=None, rccl_id: bytes = None):
+        """Node sharding (kb_set_shard / kb_set_shard_rccl): this context holds shard_range(n_total, rank, world).
+        `allgather(send: bytes) -> bytes` (all ranks' records, rank order) for the host-staged exchange, or the
+        RCCL id from comm_unique_id() (the same bytes on every rank) for the device exchange."""
+        begin, end = shard_range(n_total, rank, world)
+        sh = kb_shard(n_total, begin, rank, world)
+        self.rows = (begin, end)
+        if rccl_id is not None:
+            buf = (C.c_uint8 * 128).from_buffer_copy(rccl_id)
+            self._check(self.lib.kb_set_shard_rccl(self.ctx, C.byref(sh), C.cast(buf, P)))
+            return
+
+        def cb(user, send, recv, nbytes):
+            try:
+                out = allgather(C.string_at(send, nbytes))
+                if len(out) != world * nbytes:
+                    return -1
+                C.memmove(recv, out, len(out))
+                return 0
+            except Exception:  # an error must not unwind through the C frames
+                return -1
+        self._ag_cb = ALLGATHER_FN(cb)  # kept alive as long as the context
+        self._check(self.lib.kb_set_shard(self.ctx, C.byref(sh), self._ag_cb, None))
+
     def upload(self, snap: E.Snapshot):
-        self.n_nodes = snap.n_nodes
         cfg = kb_config(**snap.config)
         self._check(self.lib.kb_set_config(self.ctx, C.byref(cfg)))
+        lo, hi = getattr(self, "rows", (0, snap.n_nodes))  # node sharding: only this rank's rows
+        self.n_nodes = hi - lo
         c = snap.cols
-        keep = {k: np.ascontiguousarray(v) for k, v in c.items()}
+        keep = {k: np.ascontiguousarray(v[..., lo:hi]) for k, v in c.items()}
         self._keep = [keep]
-        nodes = kb_nodes(snap.n_nodes, len(snap.scalars), snap.n_label, snap.n_port,
+        nodes = kb_nodes(hi - lo, len(snap.scalars), snap.n_label, snap.n_port,
                          *[_ptr(keep[f]) for f in ("idle_cpu", "idle_mem", "rel_cpu", "rel_mem", "idle_sc", "rel_sc",
                                                    "alloc_cpu", "alloc_mem", "nz_cpu", "nz_mem", "pod_count",
                                                    "max_pods", "flags", "label_val", "label_int", "label_int_ok",
@@ -200,6 +244,8 @@ class Context:
                          tol.shape[0], tol.shape[1], _ptr(tol))
         self._check(self.lib.kb_upload_specs(self.ctx, C.byref(specs)))
         if snap.aff is not None:
+            if hasattr(self, "rows"):
+                raise KbError(KB_E_UNSUPPORTED, "inter-pod affinity tables do not run node-sharded")
             a = snap.aff
             arrs = [np.ascontiguousarray(x) for x in (a.topo_dom, a.table_arr, a.totals, a.counters, a.spec_arr,
                                                       a.check_arr, a.lister_arr, a.hist_arr, a.h, a.incr_arr)]
@@ -273,6 +319,16 @@ class Context:
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
         return out
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id for kb_set_shard_rccl (made on one rank, broadcast to the others)."""
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.kb_comm_unique_id(C.cast(buf, P))
+    if rc != KB_OK:
+        raise KbError(rc, "ncclGetUniqueId failed")
+    return bytes(buf)
 
 
 def result_dict(snap: E.Snapshot, out: dict) -> dict:

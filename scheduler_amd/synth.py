@@ -183,3 +183,70 @@ def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_r
 
 
 CONFIGS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4}
+
+
+class ArraySnapshot:
+    """The export.Snapshot arrays of a C2-shaped cluster built directly with numpy (no per-pod objects), for
+    the large configurations (C2 at full size, C5: 50k nodes x 1M pods). Same arrays as
+    export.Snapshot(c2(...)) -- tests/test_export.py checks that field by field."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def c2_snapshot(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, fill=None) -> ArraySnapshot:
+    """export.Snapshot(c2(n_nodes, n_jobs, tasks_per_job, seed, fill)) without building the cluster."""
+    from . import export as E
+    rng = np.random.default_rng(seed)  # the same draws, in the same order, as c2()
+    cpu_cap, mem_cap = 64000, 256 * GI
+    cpus = rng.integers(1, 17, n_jobs) * 250
+    mems = rng.integers(1, 17, n_jobs) * (GI // 2)
+    if fill is not None:
+        need = float((cpus * tasks_per_job).sum())
+        cpu_cap = max(4000, int(need / fill / n_nodes) // 1000 * 1000)
+    proto = E.Snapshot(c2(n_nodes=1, n_jobs=1, tasks_per_job=1, seed=seed))  # defaults: config, tiers, tables
+    n = n_nodes
+    z = lambda dt, *s: np.zeros(s, dtype=dt)
+    cols = {"idle_cpu": np.full(n, cpu_cap, np.int64), "idle_mem": np.full(n, mem_cap, np.int64),
+            "rel_cpu": z(np.int64, n), "rel_mem": z(np.int64, n),
+            "alloc_cpu": np.full(n, cpu_cap, np.int64), "alloc_mem": np.full(n, mem_cap, np.int64),
+            "nz_cpu": z(np.int64, n), "nz_mem": z(np.int64, n), "idle_sc": z(np.int64, 0, n),
+            "rel_sc": z(np.int64, 0, n), "pod_count": z(np.int32, n), "max_pods": np.full(n, 110, np.int32),
+            "flags": z(np.uint32, n), "label_val": z(np.int32, 0, n), "label_int": z(np.int64, 0, n),
+            "label_int_ok": z(np.uint8, 0, n), "taint_set": z(np.int32, n), "port_used": z(np.uint64, 0, n)}
+    # one spec per distinct (cpu, mem), numbered in first-occurrence order (export._specs dedupes by signature)
+    pair = cpus.astype(np.int64) * (1 << 40) + mems.astype(np.int64)
+    uniq, first, inv = np.unique(pair, return_index=True, return_inverse=True)
+    order = np.argsort(first)
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    job_spec = rank[inv].astype(np.int32)
+    m = len(uniq)
+    spec_arr = np.zeros(m, E.SPEC_DTYPE)
+    spec_arr[:] = proto.spec_arr[0]
+    j0 = first[order]
+    for f, v in (("init_cpu", cpus), ("req_cpu", cpus), ("nz_cpu", cpus), ("init_mem", mems), ("req_mem", mems),
+                 ("nz_mem", mems)):
+        spec_arr[f] = v[j0]
+    nt = n_jobs * tasks_per_job
+    task_job = np.repeat(np.arange(n_jobs, dtype=np.int32), tasks_per_job)
+    resreq = np.zeros((nt, 2), np.float64)
+    resreq[:, 0] = np.repeat(cpus, tasks_per_job)
+    resreq[:, 1] = np.repeat(mems, tasks_per_job)
+    total = np.array([float(cpu_cap) * n, float(mem_cap) * n])
+    return ArraySnapshot(
+        n_nodes=n, cols=cols, config=dict(proto.config), scalars=[], n_label=0, n_port=0,
+        spec_arr=spec_arr, sc_init=np.zeros(0, np.int64), sc_req=np.zeros(0, np.int64),
+        term_arr=proto.term_arr, req_arr=proto.req_arr, val_arr=proto.val_arr, port_arr=proto.port_arr,
+        tolerates=proto.tolerates, aff=None, acc_scalars=[],
+        session_tasks=range(nt), jobs=range(n_jobs), queues=proto.queues,
+        s_task_job=task_job, s_task_spec=job_spec[task_job], s_task_status=np.full(nt, E.ST["Pending"], np.int32),
+        s_task_priority=np.ones(nt, np.int32), s_task_ctime=np.zeros(nt, np.int64),
+        s_task_uid_rank=np.arange(nt, dtype=np.int32), s_task_resreq=resreq,
+        s_task_resreq_mask=np.zeros(nt, np.uint64),
+        s_job_queue=np.zeros(n_jobs, np.int32), s_job_priority=np.full(n_jobs, proto.s_job_priority[0], np.int32),
+        s_job_min=np.full(n_jobs, tasks_per_job, np.int32), s_job_ctime=np.zeros(n_jobs, np.int64),
+        s_job_uid_rank=np.arange(n_jobs, dtype=np.int32), s_job_pg_pending=np.zeros(n_jobs, np.int32),
+        s_queue_weight=proto.s_queue_weight, s_queue_ctime=proto.s_queue_ctime,
+        s_queue_uid_rank=proto.s_queue_uid_rank, s_total=total, s_total_mask=proto.s_total_mask,
+        s_tiers=proto.s_tiers)

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 5
+    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 6
 
 
 def test_struct_layouts_match_header():
@@ -58,6 +58,7 @@ def test_struct_sizes_agree_with_the_c_compiler(tmp_path):
             "kb_config": ctypes.sizeof(runtime.kb_config), "kb_opts": ctypes.sizeof(runtime.kb_opts),
             "kb_job_req": ctypes.sizeof(runtime.kb_job_req), "kb_job_result": ctypes.sizeof(runtime.kb_job_result),
             "kb_stats": ctypes.sizeof(runtime.kb_stats), "kb_affinity": ctypes.sizeof(runtime.kb_affinity),
+            "kb_shard": ctypes.sizeof(runtime.kb_shard),
             "kb_session": ctypes.sizeof(runtime.kb_session), "kb_cycle_result": ctypes.sizeof(runtime.kb_cycle_result),
             "kb_spec": export.SPEC_DTYPE.itemsize, "kb_req": export.REQ_DTYPE.itemsize,
             "kb_term": export.TERM_DTYPE.itemsize, "kb_port": export.PORT_DTYPE.itemsize,

@@ -1,5 +1,6 @@
 """Host-side snapshot export (no GPU): node accounting, spec dedupe, interning."""
 import numpy as np
+import pytest
 
 from scheduler_amd import export as E
 from scheduler_amd import model as m
@@ -55,3 +56,28 @@ def test_invalid_selector_is_everything():
                    pod_groups=[m.PodGroup("a", "g", "q")], queues=[m.Queue("q")])
     s = E.Snapshot(cl)
     assert not (s.spec_arr["flags"][0] & E.SPEC_HAS_SELECTOR)
+
+
+@pytest.mark.parametrize("kw", [dict(n_nodes=37, n_jobs=23, tasks_per_job=7, seed=3),
+                                dict(n_nodes=20, n_jobs=30, tasks_per_job=5, seed=4, fill=0.9)])
+def test_array_snapshot_equals_exporter(kw):
+    """synth.c2_snapshot (numpy, for C2 / C5 at full size) == export.Snapshot(synth.c2(...)) array by array."""
+    from scheduler_amd import export as E
+    from scheduler_amd import synth
+    ref = E.Snapshot(synth.c2(**kw))
+    got = synth.c2_snapshot(**kw)
+    assert got.n_nodes == ref.n_nodes and got.config == ref.config and got.aff is None and ref.aff is None
+    for k, v in ref.cols.items():
+        assert np.array_equal(got.cols[k], v) and got.cols[k].dtype == v.dtype, k
+    for k in ("spec_arr", "sc_init", "sc_req", "term_arr", "req_arr", "val_arr", "port_arr", "tolerates",
+              "s_task_job", "s_task_spec", "s_task_status", "s_task_priority", "s_task_ctime", "s_task_uid_rank",
+              "s_task_resreq", "s_task_resreq_mask", "s_job_queue", "s_job_priority", "s_job_min", "s_job_ctime",
+              "s_job_uid_rank", "s_job_pg_pending", "s_queue_weight", "s_queue_ctime", "s_queue_uid_rank",
+              "s_total", "s_tiers"):
+        a, b = getattr(got, k), getattr(ref, k)
+        assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b), k
+    assert got.s_total_mask == ref.s_total_mask
+    assert (len(got.session_tasks), len(got.jobs), len(got.queues)) == (len(ref.session_tasks), len(ref.jobs),
+                                                                     len(ref.queues))
+    assert len(got.scalars) == len(ref.scalars) and len(got.acc_scalars) == len(ref.acc_scalars)
+    assert (got.n_label, got.n_port) == (ref.n_label, ref.n_port)
