@@ -39,7 +39,10 @@ CONFIGS = {
                workload="C3: 20k heterogeneous nodes x 200k pods, GPU scalars, taints/tolerations, node affinity"),
     "C4": dict(nodes=10000, jobs=1000, tasks=100, row_bytes=88,
                workload="C4: 10k nodes x 100k pods, inter-pod (anti)affinity over hostname / zone / rack"),
+    "C5": dict(nodes=50000, jobs=10000, tasks=100, row_bytes=76,
+               workload="C5: 50k nodes x 1M pods (C2 shape), node table sharded across the GPUs"),
 }
+ARRAY_CONFIGS = ("C2", "C5")  # built by synth.c2_snapshot (numpy) instead of per-pod objects
 
 
 def main():
@@ -57,6 +60,11 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
     ap.add_argument("--path", default="select", choices=["select", "engine", "trajectory", "rekey"],
                     help="device path for the runs (scheduler_amd.runtime.PATHS)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "shard"],
+                    help="N>1: replicas = every rank schedules its own cluster partition (weak scaling, no "
+                         "collective); shard = ONE cluster, node table split across the ranks, one RCCL all-gather "
+                         "per run segment. auto = replicas, plus a short sharded C5 measurement in the same line")
+    ap.add_argument("--shard-jobs", type=int, default=200, help="jobs of the sharded side measurement (auto, N>1)")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP events around the launches of every Nth job call of the timed region")
     args = ap.parse_args()
@@ -68,21 +76,32 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # KB_BENCH_SAME_GPU=1: rehearse N ranks on one GPU (gloo process group, host-staged shard exchange)
+    same_gpu = os.environ.get("KB_BENCH_SAME_GPU") == "1"
+    device = 0 if same_gpu else local_rank
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist_mod
-        torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        torch.cuda.set_device(device)
+        dist_mod.init_process_group("nccl" if torch.cuda.is_available() and not same_gpu else "gloo")
         dist = dist_mod
 
     from scheduler_amd import export, runtime, synth
 
-    # each rank: an independent cluster partition of the C2 shape (different seed per rank)
-    gen = synth.CONFIGS[args.config]
-    cl = gen(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=synth.SEED + rank)
-    snap = export.Snapshot(cl)
-    ctx = runtime.Context(local_rank, timing=not args.no_timing, timing_every=args.timing_every, path=args.path)
+    shard = args.mode == "shard" and world > 1
+    # replicas: each rank an independent cluster partition (different seed per rank); shard: one cluster
+    seed = synth.SEED + (0 if shard else rank)
+    cl = None
+    if args.config in ARRAY_CONFIGS:
+        snap = synth.c2_snapshot(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=seed)
+    else:
+        cl = synth.CONFIGS[args.config](n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job,
+                                        seed=seed)
+        snap = export.Snapshot(cl)
+    ctx = runtime.Context(device, timing=not args.no_timing, timing_every=args.timing_every, path=args.path)
+    if shard:
+        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
     ctx.upload(snap)
 
     def step():
@@ -113,15 +132,20 @@ def main():
     total_placed = placed
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tensor_device(dist, device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        p = torch.tensor([placed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(p, op=dist.ReduceOp.SUM)
-        total_placed = int(p.item())
+        if not shard:  # replicas place their own pods; sharded ranks all report the same placements
+            p = torch.tensor([placed], dtype=torch.float64, device=tensor_device(dist, device))
+            dist.all_reduce(p, op=dist.ReduceOp.SUM)
+            total_placed = int(p.item())
+    side = None
+    if args.mode == "auto" and world > 1:
+        side = shard_side(args, dist, rank, world, device)
 
     # roofline: dominant kernel by summed event time
-    k = int(np.argmax(st["kernel_ms"])) if any(st["kernel_ms"]) else 0
+    kern_ms = [0.0 if runtime.KERNELS[i] == "shard_exchange" else v for i, v in enumerate(st["kernel_ms"])]
+    k = int(np.argmax(kern_ms)) if any(kern_ms) else 0  # the collective is reported on its own
     launches = max(1, st["launches"][k])
     avg_ms = st["kernel_ms"][k] / launches
     bytes_per_launch = st["pairs"][k] * cfg["row_bytes"] / launches
@@ -148,27 +172,99 @@ def main():
         ms = elapsed / args.steps * 1e3
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            if cl is None:  # the oracle runs on the cluster objects of the same workload
+                cl = synth.CONFIGS.get(args.config, synth.c2)(n_nodes=args.nodes, n_jobs=args.jobs,
+                                                            tasks_per_job=args.tasks_per_job, seed=seed)
             cpu = cpu_baseline(cl, args.cpu_sample_tasks)
         result = {
             "metric": "pods placed/sec + p50 allocate-cycle ms at 10k nodes x 100k pods",
             "value": round(total_placed / elapsed, 1), "unit": "pods/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "p50_cycle_ms": round(statistics.median(times), 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (seeded C2 generator, SURVEY.md §8 d2)",
+            "higher_is_better": True, "scaling": "strong" if shard else "weak", "vs_baseline": None,
+            "dtype": "int64", "data": f"synthetic (seeded {args.config} generator, SURVEY.md §8 d2)",
             "config": {"workload": workload,
                        "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
-                       "pods_placed_per_cycle": placed // max(1, args.steps), "parallelism": f"replicas{world}"},
+                       "pods_placed_per_cycle": placed // max(1, args.steps),
+                       "parallelism": f"node_shard{world}" if shard else f"replicas{world}"},
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
             **({"diag_place_phases": diag_summary(st["diag"], placed, runtime.KERNELS[k])}
                if any(st["diag"]) else {}),
             "job_calls_per_step": st["job_calls"] / args.steps,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            **({"shard_exchange_us_per_segment": exchange_us(st)} if shard else {}),
+            **({"sharded": side} if side is not None else {}),
         }
         print(json.dumps(result), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def tensor_device(dist, device):
+    return "cpu" if dist is not None and dist.get_backend() == "gloo" else f"cuda:{device}"
+
+
+def shard_exchange(dist, rank, device):
+    """Context.set_shard keyword: the RCCL id made on rank 0 and broadcast over the torch process group, or
+    (gloo group: ranks sharing one GPU in a rehearsal) a host-staged all-gather over that group."""
+    import torch
+    from scheduler_amd import runtime
+    if dist.get_backend() == "gloo":
+        world = dist.get_world_size()
+
+        def allgather(b):
+            t = torch.tensor(list(b), dtype=torch.uint8)
+            outs = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(outs, t)
+            return b"".join(bytes(o.tolist()) for o in outs)
+        return {"allgather": allgather}
+    t = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{device}")
+    if rank == 0:
+        t.copy_(torch.tensor(list(runtime.comm_unique_id()), dtype=torch.uint8))
+    dist.broadcast(t, 0)
+    return {"rccl_id": bytes(t.cpu().tolist())}
+
+
+def exchange_us(st):
+    from scheduler_amd import runtime
+    k = runtime.KERNELS.index("shard_exchange")
+    return round(st["kernel_ms"][k] * 1e3 / st["launches"][k], 2) if st["launches"][k] else None
+
+
+def shard_side(args, dist, rank, world, device):
+    """The node-sharded path measured next to the replicas line: ONE C5-shaped cluster (50k nodes, or 20k
+    per rank when fewer ranks would overflow the selection kernel's LDS plan), the first `shard_jobs` jobs,
+    node table split across the ranks, one RCCL all-gather per run segment. Reports pods/s (max-over-ranks
+    wall time) and the per-segment exchange latency (HIP events around ncclAllGather)."""
+    import torch
+    from scheduler_amd import runtime, synth
+    nodes = min(50000, 20000 * world)
+    try:
+        snap = synth.c2_snapshot(n_nodes=nodes, n_jobs=args.shard_jobs, tasks_per_job=100, seed=synth.SEED)
+        ctx = runtime.Context(device, timing=True, timing_every=1)
+        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+        ctx.upload(snap)
+        ctx.allocate(snap)  # warm-up cycle
+        ctx.restore()
+        ctx.stats(reset=True)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = ctx.allocate(snap)
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tensor_device(dist, device))
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        st = ctx.stats()
+        ctx.close()
+        placed = int(out["n_events"])
+        return {"workload": f"C5 shape, {nodes} nodes x {args.shard_jobs * 100} pods, node_shard{world}",
+                "value": round(placed / float(el.item()), 1), "unit": "pods/s", "pods_placed": placed,
+                "cycle_ms": round(float(el.item()) * 1e3, 3), "exchange_us_per_segment": exchange_us(st),
+                "segments": st["launches"][runtime.KERNELS.index("shard_exchange")]}
+    except Exception as e:  # the side measurement never takes the main line down
+        return {"error": repr(e)[:300]}
 
 
 def pmc_traffic(kernel):
