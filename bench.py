@@ -160,7 +160,9 @@ def main():
                 "avg_us_per_launch": {runtime.KERNELS[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
                                       for i in range(len(runtime.KERNELS)) if st["launches"][i]}}
 
-    tr = pmc_traffic(runtime.KERNELS[k])
+    # the committed PMC pass was taken on the default C2 line: its bytes apply to that workload only
+    c2_default = (args.config, args.nodes, args.jobs, args.tasks_per_job) == ("C2", 10000, 1000, 100)
+    tr = pmc_traffic(runtime.KERNELS[k]) if c2_default else None
     if tr is not None:
         roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
 

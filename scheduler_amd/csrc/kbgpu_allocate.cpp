@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -28,13 +29,14 @@ struct Res {
 
   bool has(int s) const { return (mask >> s) & 1; }
   double sc(int s) const { return has(s) ? v[2 + s] : 0.0; }
-  void add(const Res& r) {  // Add (:131-143)
-    v[0] += r.v[0];
-    v[1] += r.v[1];
+  void add(const Res& r) { add_raw(r.v, r.mask); }
+  void add_raw(const double* p, uint64_t m) {  // Add (:131-143) of a resreq row (cpu, mem, scalars) + its mask
+    v[0] += p[0];
+    v[1] += p[1];
     for (int s = 0; s < S; ++s)
-      if (r.has(s)) {
+      if ((m >> s) & 1) {
         mask |= kHasMap | (1ull << s);
-        v[2 + s] += r.v[2 + s];
+        v[2 + s] += p[2 + s];
       }
   }
   bool less_equal(const Res& rr) const {  // LessEqual (:253-276)
@@ -192,10 +194,20 @@ struct Driver {
   std::vector<int> task_status;
   std::vector<std::vector<int>> job_allocated;  // tasks with status Allocated per job (dispatch set)
   bool has[8] = {false};
+  bool task_prio = false;
   Res total;
 
   Driver(kb_ctx* c, const kb_session& ss, kb_cycle_result* o) : ctx(c), s(ss), out(o), S((int)ss.n_rscalar) {}
 
+  const double* task_req(int t) const { return s.task_resreq + (size_t)t * (2 + S); }
+  bool task_res_empty(int t) const {  // Resource.IsEmpty (resource_info.go:96-108) on the raw row
+    const double* p = task_req(t);
+    const uint64_t m = s.task_resreq_mask[t];
+    if (!(p[0] < kMinMilliCPU && p[1] < kMinMemory)) return false;
+    for (int k = 0; k < S; ++k)
+      if (((m >> k) & 1) && p[2 + k] >= kMinMilliScalar) return false;
+    return true;
+  }
   Res task_res(int t) const {
     Res r;
     r.S = S;
@@ -246,13 +258,11 @@ struct Driver {
     return s.queue_ctime[l] < s.queue_ctime[r];
   }
   // TaskOrderFn (session_plugins.go:336-369)
+  // Only the priority plugin orders tasks, so the tier walk reduces to one flag (task_prio, set in init).
   bool task_less(int l, int r) const {
-    for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
-      const kb_tier_plugin& p = s.tier_plugins[i];
-      if (!(p.enable & KB_EN_TASK_ORDER) || p.plugin != KB_PLUGIN_PRIORITY) continue;
+    if (task_prio) {
       int a = s.task_priority[l], b = s.task_priority[r];  // priority.go:40-56
-      int j = a == b ? 0 : (a > b ? -1 : 1);
-      if (j != 0) return j < 0;
+      if (a != b) return a > b;
     }
     if (s.task_ctime[l] == s.task_ctime[r]) return s.task_uid_rank[l] < s.task_uid_rank[r];
     return s.task_ctime[l] < s.task_ctime[r];
@@ -270,6 +280,7 @@ struct Driver {
     for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
       int p = s.tier_plugins[i].plugin;
       if (p >= 0 && p < 8) has[p] = true;
+      if (p == KB_PLUGIN_PRIORITY && (s.tier_plugins[i].enable & KB_EN_TASK_ORDER)) task_prio = true;
     }
     total.S = S;
     for (int i = 0; i < 2 + S; ++i) total.v[i] = s.total_alloc[i];
@@ -288,7 +299,7 @@ struct Driver {
       if (st == KB_ST_PIPELINED) jobs[j].waiting++;
       if (allocated_status(st) || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
       if (st == KB_ST_ALLOCATED) job_allocated[j].push_back((int)t);
-      if (allocated_status(st)) jobs[j].drf_alloc.add(task_res(t));
+      if (allocated_status(st)) jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
     }
     for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
     if (has[KB_PLUGIN_PROPORTION]) open_proportion();
@@ -303,10 +314,10 @@ struct Driver {
       QueueS& q = queues[s.job_queue[s.task_job[t]]];
       int st = task_status[t];
       if (allocated_status(st)) {
-        q.allocated.add(task_res(t));
-        q.request.add(task_res(t));
+        q.allocated.add_raw(task_req(t), s.task_resreq_mask[t]);
+        q.request.add_raw(task_req(t), s.task_resreq_mask[t]);
       } else if (st == KB_ST_PENDING) {
-        q.request.add(task_res(t));
+        q.request.add_raw(task_req(t), s.task_resreq_mask[t]);
       }
     }
     std::vector<int> order;
@@ -359,32 +370,188 @@ struct Driver {
     }
   }
 
-  void on_allocate_event(int t) {  // drf.go:135-144, proportion.go:236-246
+  // drf.go:135-144, proportion.go:236-246. The allocated sums take every task in event order, as the
+  // handlers do; the shares they feed are read only by the job / queue orders at the next heap push, so
+  // share_update() computes them once per job instead of once per event (same value).
+  void on_allocate_event(int t) {
     int j = s.task_job[t];
-    Res r = task_res(t);
-    if (has[KB_PLUGIN_DRF]) {
-      jobs[j].drf_alloc.add(r);
-      jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
-    }
+    const double* p = task_req(t);
+    const uint64_t m = s.task_resreq_mask[t];
+    if (has[KB_PLUGIN_DRF]) jobs[j].drf_alloc.add_raw(p, m);
+    if (has[KB_PLUGIN_PROPORTION]) queues[s.job_queue[j]].allocated.add_raw(p, m);
+  }
+  void share_update(int j) {
+    if (has[KB_PLUGIN_DRF]) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
     if (has[KB_PLUGIN_PROPORTION]) {
       QueueS& q = queues[s.job_queue[j]];
-      q.allocated.add(r);
       q.share = dominant_share(q.allocated, q.deserved);
     }
   }
 
+  // ---- the allocate loop (actions/allocate/allocate.go:40-176) ----
+  GoHeap<int> qheap;
+  std::vector<GoHeap<int>> jheaps;
+  std::vector<std::vector<int>> job_pending;
+  std::vector<int32_t> specs, pn, pk;
+  uint32_t n_events = 0;
+  bool gang_ready_on = false;
+
+  void build_pending(int j) {  // allocate.go:114-129 (BestEffort tasks skipped)
+    JobS& js = jobs[j];
+    if (js.pending_built) return;
+    js.pending.reserve(job_pending[j].size());
+    for (int t : job_pending[j])
+      if (!task_res_empty(t)) js.pending.push_back(t);
+    std::sort(js.pending.begin(), js.pending.end(), [this](int a, int b) { return task_less(a, b); });
+    js.pending_built = true;
+  }
+
+  // The loop head: pop queues / jobs until a job with pending tasks comes out (allocate.go:90-112).
+  // Queues that are overused or out of jobs are dropped; a job without pending tasks is dropped and its
+  // queue pushed back. `jh` maps a queue to the job heap to use (the real ones, or scratch copies).
+  template <class JH>
+  bool next_job(GoHeap<int>& qh, JH&& jh, int& q, int& j) {
+    while (!qh.empty()) {
+      q = qh.pop();
+      if (overused(q)) continue;
+      GoHeap<int>& h = jh(q);
+      if (h.empty()) continue;
+      j = h.pop();
+      build_pending(j);
+      if (jobs[j].cursor < jobs[j].pending.size()) return true;
+      qh.push(q);
+    }
+    return false;
+  }
+
+  kb_job_req make_req(int j) {
+    JobS& js = jobs[j];
+    const size_t nt = js.pending.size() - js.cursor;
+    specs.resize(nt);
+    for (size_t i = 0; i < nt; ++i) specs[i] = s.task_spec[js.pending[js.cursor + i]];
+    return kb_job_req{specs.data(), (uint32_t)nt, js.ready, s.job_min_available[j], gang_ready_on ? 1 : 0};
+  }
+  int check_specs(int j) const {
+    const JobS& js = jobs[j];
+    for (size_t i = js.cursor; i < js.pending.size(); ++i)
+      if (s.task_spec[js.pending[i]] < 0) return KB_E_INVALID;
+    return KB_OK;
+  }
+
+  // Session.Allocate / Session.Pipeline for the job's placements, then the heap pushes of the loop tail.
+  void apply(int q, int j, const kb_job_result& res) {
+    JobS& js = jobs[j];
+    for (uint32_t i = 0; i < res.n_placed; ++i) {
+      int t = js.pending[js.cursor + i];
+      out->task_node[t] = pn[i];
+      out->event_task[n_events++] = t;
+      if (pk[i] == KB_PLACE_ALLOCATE) {  // Session.Allocate (session.go:242-297)
+        task_status[t] = KB_ST_ALLOCATED;
+        js.ready++;
+        job_allocated[j].push_back(t);
+        on_allocate_event(t);
+        if (job_ready(j)) {  // dispatch every Allocated task (session.go:286-294)
+          for (int a : job_allocated[j]) task_status[a] = KB_ST_BINDING;
+          job_allocated[j].clear();
+        }
+      } else {  // Session.Pipeline (session.go:199-239)
+        task_status[t] = KB_ST_PIPELINED;
+        js.waiting++;
+        on_allocate_event(t);
+      }
+    }
+    if (res.n_placed) share_update(j);
+    js.cursor += res.n_placed;
+    if (res.stop == KB_STOP_NO_FIT) {
+      out->job_fail_task[j] = js.pending[js.cursor];
+      memcpy(out->job_reason_hist + (size_t)j * KB_NUM_REASONS, res.reason_hist, sizeof(res.reason_hist));
+    } else if (res.stop == KB_STOP_READY) {
+      jheaps[q].push(j);
+    }
+    qheap.push(q);
+  }
+
+  // The place call's outcome when every task it places is Allocated (the stop rules of the place
+  // kernels): a gang job stops READY at the task that brings ready to minAvailable, a job without the
+  // gang JobReady check after its first task; otherwise every task places and the call ends DONE.
+  void predict(int j, int& stop, int& placed) const {
+    const JobS& js = jobs[j];
+    const int nt = (int)(js.pending.size() - js.cursor);
+    if (!gang_ready_on) {
+      stop = KB_STOP_READY;
+      placed = 1;
+      return;
+    }
+    const int need = std::max(1, s.job_min_available[j] - js.ready);
+    stop = need <= nt ? KB_STOP_READY : KB_STOP_DONE;
+    placed = std::min(need, nt);
+  }
+
+  // Speculation: with job j (queue q) in flight in slot `busy`, find the job the loop pops next IF j ends
+  // as predicted, and issue it into the other slot guarded on that prediction. The driver state is
+  // advanced as the prediction says, the loop head is run on scratch copies of the heaps, and the state
+  // is put back. Returns false (nothing issued) when there is no next job or it cannot be guarded.
+  GoHeap<int> sq;
+  std::vector<std::pair<int, GoHeap<int>>> sjh;
+  bool speculate(int q, int j, int busy, int& q2, int& j2, kb_job_pred& pred) {
+    int stop, placed;
+    predict(j, stop, placed);
+    JobS& js = jobs[j];
+    QueueS& qs = queues[q];
+    const int ready0 = js.ready;
+    const size_t cursor0 = js.cursor;
+    const Res drf0 = js.drf_alloc, qalloc0 = qs.allocated;
+    const double drf_share0 = js.drf_share, qshare0 = qs.share;
+    for (int i = 0; i < placed; ++i) on_allocate_event(js.pending[cursor0 + i]);
+    js.ready += placed;
+    js.cursor += placed;
+    share_update(j);
+    sq.items = qheap.items;
+    sq.push(q);
+    sjh.clear();
+    auto jh = [&](int qq) -> GoHeap<int>& {
+      for (auto& e : sjh)
+        if (e.first == qq) return e.second;
+      sjh.emplace_back(qq, jheaps[qq]);
+      if (qq == q && stop == KB_STOP_READY) sjh.back().second.push(j);
+      return sjh.back().second;
+    };
+    // the pushes of job j's loop tail happen before the next head: touch queue q's job heap first
+    if (stop == KB_STOP_READY) jh(q);
+    bool ok = next_job(sq, jh, q2, j2) && check_specs(j2) == KB_OK;
+    int rc = KB_OK;
+    if (ok) {
+      const kb_job_req req = make_req(j2);
+      ok = kb_job_guardable(ctx, &req) != 0;
+      if (ok) {
+        pred = kb_job_pred{busy, stop, placed, ready0 + placed};
+        rc = kb_job_issue(ctx, &req, busy ^ 1, &pred);
+        ok = rc == KB_OK;
+      }
+    }
+    js.ready = ready0;
+    js.cursor = cursor0;
+    js.drf_alloc = drf0;
+    js.drf_share = drf_share0;
+    qs.allocated = qalloc0;
+    qs.share = qshare0;
+    return ok;
+  }
+
   int run() {
-    GoHeap<int> qheap;
     qheap.less = [this](const int& a, const int& b) { return queue_less(a, b); };
-    std::vector<GoHeap<int>> jheaps(s.n_queues);
+    sq.less = qheap.less;
+    jheaps.assign(s.n_queues, GoHeap<int>());
     for (auto& h : jheaps) h.less = [this](const int& a, const int& b) { return job_less(a, b); };
+    gang_ready_on = has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY);
     std::vector<int> jorder(s.n_jobs);
     for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
     std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
-    // pending tasks per job
-    std::vector<std::vector<int>> job_pending(s.n_jobs);
+    job_pending.assign(s.n_jobs, {});
+    uint32_t max_pending = 1;
     for (uint32_t t = 0; t < s.n_tasks; ++t)
       if (task_status[t] == KB_ST_PENDING) job_pending[s.task_job[t]].push_back((int)t);
+    for (uint32_t j = 0; j < s.n_jobs; ++j) max_pending = std::max<uint32_t>(max_pending, job_pending[j].size());
     for (int j : jorder) {
       if (s.job_pg_pending[j]) continue;                                              // allocate.go:50-52
       if (has[KB_PLUGIN_GANG] && jobs[j].valid < s.job_min_available[j]) continue;  // JobValid, gang.go:48-69
@@ -393,64 +560,61 @@ struct Driver {
       qheap.push(q);
       jheaps[q].push(j);
     }
-    std::vector<int32_t> specs, pn, pk;
-    uint32_t n_events = 0;
-    while (!qheap.empty()) {
-      int q = qheap.pop();
-      if (overused(q)) continue;
-      if (jheaps[q].empty()) continue;
-      int j = jheaps[q].pop();
-      JobS& js = jobs[j];
-      if (!js.pending_built) {  // allocate.go:114-129 (BestEffort tasks skipped)
-        for (int t : job_pending[j]) {
-          Res r = task_res(t);
-          if (!r.is_empty()) js.pending.push_back(t);
-        }
-        std::sort(js.pending.begin(), js.pending.end(), [this](int a, int b) { return task_less(a, b); });
-        js.pending_built = true;
+    pn.resize(max_pending);
+    pk.resize(max_pending);
+    // Pipelined: job k+1 is launched (guarded) before job k's result is read, so the device runs the jobs
+    // back to back while the host does the bookkeeping. Otherwise one kb_place_job per job.
+    const bool pipe = kb_job_pipeline_ok(ctx) && getenv("KB_NO_PIPELINE") == nullptr;
+    if (pipe)
+      if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
+    int q, j, slot = 0;
+    bool have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
+    if (have && check_specs(j)) return KB_E_INVALID;
+    if (have && pipe) {
+      const kb_job_req req = make_req(j);
+      if (int rc = kb_job_issue(ctx, &req, slot, nullptr)) return rc;
+    }
+    while (have) {
+      int q2 = -1, j2 = -1;
+      kb_job_pred pred{};
+      const bool spec = pipe && speculate(q, j, slot, q2, j2, pred);
+      kb_job_result res;
+      int rc;
+      if (pipe) {
+        rc = kb_job_finish(ctx, slot, pn.data(), pk.data(), &res, 0);
+      } else {
+        const kb_job_req req = make_req(j);
+        rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res);
       }
-      if (js.cursor < js.pending.size()) {
-        const size_t nt = js.pending.size() - js.cursor;
-        specs.resize(nt);
-        pn.resize(nt);
-        pk.resize(nt);
-        for (size_t i = 0; i < nt; ++i) {
-          specs[i] = s.task_spec[js.pending[js.cursor + i]];
-          if (specs[i] < 0) return KB_E_INVALID;
+      const bool match = spec && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
+                         jobs[j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
+                                                         (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
+      if (spec && !match) {  // the guard fails on the device as well: drain the skipped job
+        kb_job_result skip;
+        const int rc2 = kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &skip, 1);
+        if (rc == KB_OK) rc = rc2;
+      }
+      if (rc) return rc;
+      apply(q, j, res);
+      int nq, nj;
+      have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj);
+      if (match) {
+        if (!have || nq != q2 || nj != j2) {  // cannot happen: the speculation replays the same loop head
+          kb_job_result drain;
+          (void)kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &drain, 1);
+          ctx->err = "speculative job does not match the loop order";
+          return KB_E_STATE;
         }
-        kb_job_req req{specs.data(), (uint32_t)nt, js.ready, s.job_min_available[j],
-                       (has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY)) ? 1 : 0};
-        kb_job_result res;
-        int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res);
-        if (rc) return rc;
-        for (uint32_t i = 0; i < res.n_placed; ++i) {
-          int t = js.pending[js.cursor + i];
-          out->task_node[t] = pn[i];
-          out->event_task[n_events++] = t;
-          if (pk[i] == KB_PLACE_ALLOCATE) {  // Session.Allocate (session.go:242-297)
-            task_status[t] = KB_ST_ALLOCATED;
-            js.ready++;
-            job_allocated[j].push_back(t);
-            on_allocate_event(t);
-            if (job_ready(j)) {  // dispatch every Allocated task (session.go:286-294)
-              for (int a : job_allocated[j]) task_status[a] = KB_ST_BINDING;
-              job_allocated[j].clear();
-            }
-          } else {  // Session.Pipeline (session.go:199-239)
-            task_status[t] = KB_ST_PIPELINED;
-            js.waiting++;
-            on_allocate_event(t);
-          }
-        }
-        js.cursor += res.n_placed;
-        if (res.stop == KB_STOP_NO_FIT) {
-          out->job_fail_task[j] = js.pending[js.cursor];
-          memcpy(out->job_reason_hist + (size_t)j * KB_NUM_REASONS, res.reason_hist, sizeof(res.reason_hist));
-        } else if (res.stop == KB_STOP_READY) {
-          jheaps[q].push(j);
+        slot ^= 1;
+      } else if (have) {
+        if (check_specs(nj)) return KB_E_INVALID;
+        if (pipe) {
+          const kb_job_req req = make_req(nj);
+          if (int rc3 = kb_job_issue(ctx, &req, slot, nullptr)) return rc3;
         }
       }
-      qheap.push(q);
+      q = nq;
+      j = nj;
     }
     out->n_events = n_events;
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -62,6 +63,26 @@ struct kb_ctx {
   char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)
   char* h_job_dev = nullptr; // device address of h_job
   uint32_t job_cap = 0;
+  // Job slots of the pipelined driver (kb_allocate): slot 0 = d_job / h_job above, slot 1 below. The
+  // driver issues job k+1 into the free slot, guarded on job k's predicted outcome, before reading job k.
+  struct JobSlot {
+    char *d = nullptr, *h = nullptr, *hdev = nullptr;
+    uint32_t seq = 0;        // sequence number the slot's last launch reports
+    size_t ev_b = 0, ev_e = 0;  // its timing events in `pending`
+    bool busy = false;
+    int keys_spec_before = -1;  // restored when the slot's job turns out skipped
+    std::chrono::steady_clock::time_point t_issue;
+    double issue_ms = 0;
+  };
+  JobSlot slot[2];
+  char* d_job1 = nullptr;
+  char* h_job1 = nullptr;
+  uint32_t job1_cap = 0;
+  uint64_t issue_count = 0;
+  // spec whose level-0 keys (traj[0..n)) and static cache (stat) are current once the issued work is done;
+  // -1 when anything else may have touched them. A selection run of that spec skips its sweep.
+  int keys_spec = -1;
+  int last_spec = -1;  // spec of the last single-run selection job issued
   char* h_eval = nullptr;
 
   double device_ms = 0;  // wall time inside kb_place_job
@@ -81,7 +102,7 @@ struct kb_ctx {
   hipEvent_t ev_get();
   void ev_begin(hipEvent_t* a);
   void ev_end(hipEvent_t a, int kind, uint64_t pairs);
-  void ev_collect(bool all);
+  size_t ev_collect(bool all, size_t limit = (size_t)-1);  // returns the event pairs it folded
   size_t pending_job_begin = 0;  // first pending event pair of the current kb_place_job call
 };
 
@@ -90,3 +111,22 @@ extern "C" __attribute__((visibility("hidden"))) int kb_check_score_range(kb_ctx
 extern "C" __attribute__((visibility("hidden"))) void kb_update_traj_ok(kb_ctx* c);
 // stops the placement engine (if running) before other work touches the device state
 extern "C" __attribute__((visibility("hidden"))) int kb_engine_stop(kb_ctx* c);
+
+// Pipelined placement for kb_allocate's driver (kbgpu_host.cpp). kb_job_pipeline_ok: the context runs
+// jobs through the launch paths (not sharded, no engine). kb_job_guardable: every task of the job takes
+// the selection path, whose first launches can carry a SpecGuard. kb_job_issue launches the job into
+// `slot`; with `pred` set it runs only if the job of slot pred->prev_slot ended with exactly
+// (stop, placed, ready). kb_job_reserve sizes both slots beforehand. kb_job_finish waits for the slot and
+// reads its result (skipped: the caller knows the guard failed and only drains the slot).
+struct kb_job_pred {
+  int prev_slot;
+  int32_t stop, placed, ready;
+};
+extern "C" __attribute__((visibility("hidden"))) int kb_job_pipeline_ok(kb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) int kb_job_guardable(kb_ctx* c, const kb_job_req* job);
+extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, uint32_t max_tasks);
+extern "C" __attribute__((visibility("hidden"))) int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot,
+                                                                  const kb_job_pred* pred);
+extern "C" __attribute__((visibility("hidden"))) int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node,
+                                                                   int32_t* placed_kind, kb_job_result* result,
+                                                                   int skipped);

@@ -84,6 +84,13 @@ struct JobState {
   uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
 };
 
+// Speculative issue (kb_allocate's driver): a job launched before the previous job's result is known runs
+// only if that job ended as predicted; otherwise every kernel of the speculative job is a no-op.
+struct SpecGuard {
+  const JobState* prev;  // nullptr: no guard
+  int32_t stop, placed, ready;
+};
+
 // Node sharding (kb_set_shard): one rank's proposal for a run segment, exchanged by an all-gather.
 constexpr int kShardSegMax = 100;  // == the selection path's segment length (kSegMax)
 struct ShardRec {
@@ -135,11 +142,15 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
 // keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.
 int sel_lds_bytes(int n);
+// A guard (g.prev set) replaces the JobState gate of a job's first run. keys_out (== keys32): the place
+// kernel writes the new level-0 key of every row it commits, so the buffer stays current for the spec.
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
-                      uint64_t* stat, const JobState* js, bool aff, void* stream);
+                      uint64_t* stat, const JobState* js, bool aff, void* stream,
+                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0});
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
-                      int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+                      int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
+                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, uint32_t* keys_out = nullptr);
 
 // Placement engine (kbgpu_device.hip): the selection path as one persistent workgroup serving the
 // commands posted to `cmd` from sequence number seq0 on; exits on KB_ENG_EXIT or after idle_ticks

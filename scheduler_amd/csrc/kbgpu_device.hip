@@ -432,6 +432,12 @@ __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int s
 }
 
 // A launch that finds its batch already stopped still reports completion.
+__device__ __forceinline__ bool guard_fails(const SpecGuard& g) {
+  if (g.prev == nullptr) return false;
+  const JobState* p = g.prev;
+  return p->panic != 0 || p->stop != g.stop || p->n_placed != g.placed || p->ready_num != g.ready;
+}
+
 __device__ __forceinline__ void signal_skip(JobState* hjs, uint32_t seq) {
   if (threadIdx.x == 0) __hip_atomic_store(&hjs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1297,7 +1303,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         int idx_bits, const uint64_t* stat, int& ready, int minav, int gang,
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
-                                        ShardRec* rec SEL_DIAG_PARAMS) {
+                                        ShardRec* rec, uint32_t* keys_out SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -1655,13 +1661,17 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
       __syncthreads();
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram
+      // keys_out: the level-0 key buffer stays current for the next job of the same spec (no sweep)
       const bool rekey = kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count);
       if (tid < (int)S && sh.fin[tid] > 0) {
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
         store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
-        if (rekey)
-          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
-                                idx_bits);
+        if (rekey || keys_out != nullptr) {
+          const uint32_t k = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A),
+                                          w + N.base, idx_bits);
+          k32[w] = k;
+          if (keys_out != nullptr) keys_out[w] = k;
+        }
       }
       __syncthreads();
       KB_SEL_PH(5);
@@ -1726,10 +1736,11 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
 __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
-    uint32_t seq) {
+    uint32_t seq, SpecGuard g, uint32_t* keys_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
-  if (!first && js->stopped) {
+  if ((!first && js->stopped) || guard_fails(g)) {
+    if (threadIdx.x == 0) js->stopped = 1;  // later runs of a skipped speculative job skip too
     signal_skip(hjs, seq);
     return;
   }
@@ -1760,7 +1771,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   KB_SEL_PH(0);
 
   sel_run(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
-          panic, stopped, hout, js, hjs, rp, nullptr SEL_DIAG_ARGS);
+          panic, stopped, hout, js, hjs, rp, nullptr, keys_out SEL_DIAG_ARGS);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
@@ -1864,7 +1875,7 @@ __global__ __launch_bounds__(kSelThreads) void engine_kernel(DevNodes N, DevSpec
       KB_SEL_PH(0);
       const kb_spec sp = P.specs[spec];
       sel_run(sh, k32, cand, N, P, C, sp, spec, sh.run.t_begin, sh.run.t_count, idx_bits, stat, ready, minav, gang, placed,
-              stop, fail_task, panic, stopped, hout, js, hjs, rp, nullptr SEL_DIAG_ARGS);
+              stop, fail_task, panic, stopped, hout, js, hjs, rp, nullptr, nullptr SEL_DIAG_ARGS);
     }
 #ifdef KB_DIAG
     if (tid == 0) {
@@ -1896,8 +1907,9 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
 // ~160 workgroups, spread over the chip), no trajectory levels.
 template <bool AFF>
 __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
-                                                      uint32_t* keys32, uint64_t* stat, const JobState* js) {
-  if (js != nullptr && js->stopped) return;
+                                                      uint32_t* keys32, uint64_t* stat, const JobState* js,
+                                                      SpecGuard g) {
+  if ((js != nullptr && js->stopped) || guard_fails(g)) return;
   const int n = blockIdx.x * 64 + threadIdx.x;
   if (n >= N.n) return;
   const kb_spec sp = P.specs[spec];
@@ -1909,14 +1921,14 @@ __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, D
 }
 
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
-                      uint64_t* stat, const JobState* js, bool aff, void* stream) {
+                      uint64_t* stat, const JobState* js, bool aff, void* stream, SpecGuard g) {
   const int blocks = (N.n + 63) / 64;
   if (aff)
     hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
-                       keys32, stat, js);
+                       keys32, stat, js, g);
   else
     hipLaunchKernelGGL(sel_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec,
-                       idx_bits, keys32, stat, js);
+                       idx_bits, keys32, stat, js, g);
 }
 
 // ===========================================================================
@@ -1951,7 +1963,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
 #endif
   __syncthreads();
   sel_run<true>(sh, k32, cand, N, P, C, sp, spec, 0, t_count, idx_bits, stat, ready, 0, 0, placed, stop, fail_task,
-                panic, stopped, nullptr, nullptr, nullptr, rp, rec SEL_DIAG_ARGS);
+                panic, stopped, nullptr, nullptr, nullptr, rp, rec, nullptr SEL_DIAG_ARGS);
 }
 
 // Elements of a proposal list (descending) greater than v.
@@ -2130,10 +2142,11 @@ int sel_lds_bytes(int n) {
 
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
-                      int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+                      int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
+                      SpecGuard g, uint32_t* keys_out) {
   hipLaunchKernelGGL(sel_place_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P, C,
                      spec, t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs,
-                     seq);
+                     seq, g, keys_out);
 }
 
 // ---------------------------------------------------------------------------

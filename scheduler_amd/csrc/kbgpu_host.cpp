@@ -23,7 +23,10 @@ int fail(kb_ctx* c, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (c) c->err = buf;
+  if (c) {
+    c->err = buf;
+    c->keys_spec = -1;
+  }
   return code;
 }
 
@@ -93,14 +96,15 @@ void kb_ctx::ev_end(hipEvent_t a, int kind, uint64_t pairs) {
 }
 // Fold finished event pairs into the stats, oldest first. `all`: wait for the stream first; otherwise
 // stop at the first pair still in flight (it is collected by a later call, off the job's critical path).
-void kb_ctx::ev_collect(bool all) {
+// Pairs of kind < 0 (a skipped speculative job) are recycled without counting.
+size_t kb_ctx::ev_collect(bool all, size_t limit) {
   if (all && !pending.empty()) (void)hipStreamSynchronize(stream);
   size_t k = 0;
-  for (; k < pending.size(); ++k) {
+  for (; k < pending.size() && k < limit; ++k) {
     Pending& p = pending[k];
     if (!all && hipEventQuery(p.b) != hipSuccess) break;
     float ms = 0;
-    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+    if (p.kind >= 0 && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       stats.kernel_ms[p.kind] += ms;
       stats.launches[p.kind] += 1;
       stats.pairs[p.kind] += p.pairs;
@@ -109,6 +113,11 @@ void kb_ctx::ev_collect(bool all) {
     ev_pool.push_back(p.b);
   }
   pending.erase(pending.begin(), pending.begin() + k);
+  for (auto& sl : slot) {
+    sl.ev_b = sl.ev_b > k ? sl.ev_b - k : 0;
+    sl.ev_e = sl.ev_e > k ? sl.ev_e - k : 0;
+  }
+  return k;
 }
 
 extern "C" {
@@ -160,6 +169,7 @@ void kb_destroy(kb_ctx* c) {
   free_all(c->aff_mem);
   free_all(c->work_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
+  if (c->h_job1) (void)hipHostFree(c->h_job1);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -180,6 +190,7 @@ void kb_destroy(kb_ctx* c) {
 const char* kb_last_error(const kb_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int kb_set_config(kb_ctx* c, const kb_config* cfg) {
+  if (c) c->keys_spec = -1;
   if (!c || !cfg) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   c->cfg = DevCfg{cfg->predicates_enabled, cfg->nodeorder_enabled, cfg->mem_pressure, cfg->disk_pressure,
@@ -189,6 +200,7 @@ int kb_set_config(kb_ctx* c, const kb_config* cfg) {
 }
 
 int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
+  if (c) c->keys_spec = -1;
   if (!c || !in) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -274,6 +286,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
 }
 
 int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
+  if (c) c->keys_spec = -1;
   if (!c || !in) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -341,6 +354,7 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
 }
 
 int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
+  if (c) c->keys_spec = -1;
   if (!c || !a) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -455,9 +469,7 @@ int kb_check_score_range(kb_ctx* c) {
 // Wait for the last place launch of a job: spin on the sequence number it writes to pinned host memory
 // (cheaper than a stream synchronisation's wake-up), checking the stream now and then so a failed launch
 // is reported instead of waited on. Kernel timing events are then complete or nearly so.
-static int wait_seq(kb_ctx* c) {
-  const JobState* hs = (const JobState*)c->h_job;
-  const uint32_t want = c->seq;
+static int wait_seq(kb_ctx* c, const JobState* hs, uint32_t want) {
   auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spin = 0;; ++spin) {
     if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == want) break;
@@ -474,6 +486,7 @@ static int wait_seq(kb_ctx* c) {
   }
   return KB_OK;
 }
+static int wait_seq(kb_ctx* c) { return wait_seq(c, (const JobState*)c->h_job, c->seq); }
 
 static int ensure_job_buffers(kb_ctx* c, uint32_t n_tasks) {
   if (!c->d_job) {
@@ -773,13 +786,8 @@ static int shard_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_nod
   return KB_OK;
 }
 
-int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
-                 kb_job_result* result) {
-  if (!c || !job || !result) return KB_E_INVALID;
+static int validate_job(kb_ctx* c, const kb_job_req* job) {
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
-  memset(result, 0, sizeof(*result));
-  result->fail_task = -1;
-  if (job->n_tasks == 0) return KB_OK;
   for (uint32_t i = 0; i < job->n_tasks; ++i) {
     if (job->task_specs[i] < 0 || job->task_specs[i] >= c->P.m)
       return fail(c, KB_E_INVALID, "task %u spec %d out of range", i, job->task_specs[i]);
@@ -787,18 +795,50 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
       return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first",
                   job->task_specs[i]);
   }
-  if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
-  if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
-  if (int rc = kb_engine_stop(c)) return rc;
-  int rc = ensure_job_buffers(c, job->n_tasks);
-  if (rc) return rc;
-  auto t0 = std::chrono::steady_clock::now();
-  c->pending_job_begin = c->pending.size();
-  c->timing_now = c->timing && (c->stats.job_calls % c->timing_every == 0);
-  JobState* js = (JobState*)c->d_job;
-  JobState* hjs_dev = (JobState*)c->h_job_dev;
-  memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
-  int32_t* hout_dev = (int32_t*)(c->h_job_dev + sizeof(JobState));
+  return KB_OK;
+}
+
+// Both job slots with room for n_tasks placements (slot 0 = d_job / h_job).
+static int ensure_slots(kb_ctx* c, uint32_t n_tasks, bool both) {
+  if (int rc = ensure_job_buffers(c, n_tasks)) return rc;
+  c->slot[0].d = c->d_job;
+  c->slot[0].h = c->h_job;
+  c->slot[0].hdev = c->h_job_dev;
+  if (!both) return KB_OK;
+  if (!c->d_job1) {
+    void* p;
+    HIP_OK(c, hipMalloc(&p, sizeof(JobState)));
+    HIP_OK(c, hipMemset(p, 0, sizeof(JobState)));
+    c->work_mem.push_back(p);
+    c->d_job1 = (char*)p;
+  }
+  if (!c->h_job1 || c->job1_cap < c->job_cap) {
+    if (c->h_job1) (void)hipHostFree(c->h_job1);
+    c->h_job1 = nullptr;
+    const size_t bytes = sizeof(JobState) + (size_t)c->job_cap * 2 * sizeof(int32_t);
+    HIP_OK(c, hipHostMalloc((void**)&c->h_job1, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_OK(c, hipHostGetDevicePointer((void**)&c->slot[1].hdev, c->h_job1, 0));
+    memset(c->h_job1, 0, bytes);
+    ((JobState*)c->h_job1)->seq = c->seq;
+    c->job1_cap = c->job_cap;
+  }
+  c->slot[1].d = c->d_job1;
+  c->slot[1].h = c->h_job1;
+  return KB_OK;
+}
+
+// Launch every run of the job into slot `si`. The path per run: block-wide re-sweep (self-dependent
+// affinity), selection, trajectory, or rekey. `g` (first run only) guards a speculative job.
+static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard& g) {
+  kb_ctx::JobSlot& S = c->slot[si];
+  S.t_issue = std::chrono::steady_clock::now();
+  S.ev_b = c->pending.size();
+  c->timing_now = c->timing && (c->issue_count++ % c->timing_every == 0);
+  JobState* js = (JobState*)S.d;
+  JobState* hjs_dev = (JobState*)S.hdev;
+  memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
+  int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
+  S.keys_spec_before = c->keys_spec;
   uint32_t t = 0;
   while (t < job->n_tasks) {
     uint32_t e = t + 1;
@@ -813,6 +853,9 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     const bool key32 = c->spec_traj_ok[spec] && c->traj != nullptr;
     const bool sel = !dyn && c->use_sel && key32 && c->sel_ok;
     const bool traj = !sel && !dyn && c->use_traj && key32 && c->traj_full && traj_lds_bytes(c->N.n, run, &pbc) > 0;
+    if (first && g.prev && !sel) return fail(c, KB_E_INVALID, "guarded job does not take the selection path");
+    const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
+    if (!sel) c->keys_spec = -1;  // the other paths reuse the key / static-cache buffers
     if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
       c->ev_begin(&ea);
       launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->P.A.mm, first ? nullptr : js, c->stream);
@@ -824,14 +867,26 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
     } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
-      c->ev_begin(&ea);
-      launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, aff,
-                       c->stream);
-      c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
+      // A job that is one selection run of a spec without inter-pod terms leaves the key buffer current
+      // for that spec (the place kernel re-keys the rows it commits): the next such run skips its sweep.
+      // The run executes whenever the job does (it is the job's only run), so the host-side tag is exact.
+      // The write-back re-keys the committed rows (a little work per commit), so it is done while jobs of
+      // one spec follow each other: from the second same-spec job on.
+      const bool one_run = !aff && t == 0 && e == job->n_tasks;
+      const bool keep = one_run && c->last_spec == spec;
+      c->last_spec = one_run ? spec : -1;
+      if (!(keep && c->keys_spec == spec)) {
+        c->ev_begin(&ea);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, aff,
+                         c->stream, gr);
+        c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
+      }
       c->ev_begin(&ea);
       launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, c->traj, c->stat, js, first,
-                       job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
+                       job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream,
+                       gr, keep ? c->traj : nullptr);
       c->ev_end(ea, KB_KERNEL_SEL_PLACE, 0);
+      c->keys_spec = keep ? spec : -1;
     } else if (traj) {
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
@@ -858,20 +913,38 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
     t = e;
   }
   HIP_OK(c, hipGetLastError());
-  {
-    int rc2 = wait_seq(c);
-    if (rc2) return rc2;
+  S.seq = c->seq;
+  S.ev_e = c->pending.size();
+  S.busy = true;
+  S.issue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S.t_issue).count();
+  return KB_OK;
+}
+
+static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed_kind, kb_job_result* result,
+                        bool skipped) {
+  kb_ctx::JobSlot& S = c->slot[si];
+  if (!S.busy) return fail(c, KB_E_STATE, "job slot %d has nothing in flight", si);
+  S.busy = false;
+  const JobState* hs = (const JobState*)S.h;
+  const auto t_wait = std::chrono::steady_clock::now();
+  if (int rc = wait_seq(c, hs, S.seq)) return rc;
+  // host time spent in the device path for this job: issuing it plus waiting for it (jobs overlap when
+  // pipelined, so issue-to-finish walls would count the overlap twice)
+  const double wall =
+      S.issue_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count();
+  if (skipped) {  // a speculative job whose guard failed: nothing ran, nothing to count
+    c->keys_spec = S.keys_spec_before;
+    for (size_t k = S.ev_b; k < S.ev_e && k < c->pending.size(); ++k) c->pending[k].kind = -1;
+    return KB_OK;
   }
-  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   c->device_ms += wall;
   c->stats.device_ms += wall;
   c->stats.job_calls += 1;
-  const JobState* hs = (const JobState*)c->h_job;
   for (int k = 0; k < 8; ++k) c->stats.diag[k] += hs->diag[k];
   if (c->timing) {
-    // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the batch's launches
+    // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the job's launches
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
-    for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
+    for (size_t k = S.ev_b; k < S.ev_e && k < c->pending.size(); ++k) {
       auto& p = c->pending[k];
       if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE ||
           p.kind == KB_KERNEL_SEL_PLACE) {
@@ -879,9 +952,9 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
         tasks = 0;
       }
     }
-    c->ev_collect(false);
+    c->ev_collect(false, S.ev_e);  // never a later job's pairs, whose counts are not known yet
   }
-  const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
+  const int32_t* ho = (const int32_t*)(S.h + sizeof(JobState));
   result->n_placed = (uint32_t)hs->n_placed;
   result->stop = hs->stop;
   result->fail_task = hs->fail_task;
@@ -895,8 +968,67 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   return KB_OK;
 }
 
+int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
+                 kb_job_result* result) {
+  if (!c || !job || !result) return KB_E_INVALID;
+  memset(result, 0, sizeof(*result));
+  result->fail_task = -1;
+  if (int rc = validate_job(c, job)) return rc;
+  if (job->n_tasks == 0) return KB_OK;
+  if (c->sharded || engine_ok(c, job)) c->keys_spec = -1;  // these paths own the key buffers
+  if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
+  if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
+  if (int rc = kb_engine_stop(c)) return rc;
+  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  if (int rc = ensure_slots(c, job->n_tasks, false)) return rc;
+  if (int rc = place_issue(c, job, 0, SpecGuard{nullptr, 0, 0, 0})) return rc;
+  return place_finish(c, 0, placed_node, placed_kind, result, false);
+}
+
+int kb_job_pipeline_ok(kb_ctx* c) { return c && !c->sharded && !c->use_engine && !c->broken; }
+
+int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
+  if (!c->use_sel || !c->sel_ok || !c->traj || job->n_tasks == 0) return 0;
+  const int s0 = job->task_specs[0];
+  if (s0 < 0 || s0 >= c->P.m || !c->spec_traj_ok[s0]) return 0;
+  if (c->aff_ok && c->spec_needs_aff[s0] && c->spec_dyn[s0]) return 0;
+  return 1;
+}
+
+int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
+  if (!c) return KB_E_INVALID;
+  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  return ensure_slots(c, std::max<uint32_t>(max_tasks, 1), true);
+}
+
+int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* pred) {
+  if (!c || !job || slot < 0 || slot > 1) return KB_E_INVALID;
+  if (int rc = validate_job(c, job)) return rc;
+  if (job->n_tasks == 0) return fail(c, KB_E_INVALID, "empty job");
+  if (c->slot[slot].busy) return fail(c, KB_E_STATE, "job slot %d is busy", slot);
+  if (job->n_tasks > c->job_cap || job->n_tasks > c->job1_cap)  // growing would free a slot in flight
+    return fail(c, KB_E_STATE, "kb_job_reserve(%u) first", job->n_tasks);
+  if (int rc = kb_engine_stop(c)) return rc;
+  if (int rc = ensure_slots(c, job->n_tasks, true)) return rc;
+  SpecGuard g{nullptr, 0, 0, 0};
+  if (pred) {
+    if (!kb_job_guardable(c, job)) return fail(c, KB_E_INVALID, "job cannot be issued speculatively");
+    g = SpecGuard{(const JobState*)c->slot[pred->prev_slot].d, pred->stop, pred->placed, pred->ready};
+  }
+  return place_issue(c, job, slot, g);
+}
+
+int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kind, kb_job_result* result,
+                  int skipped) {
+  if (!c || !result || slot < 0 || slot > 1) return KB_E_INVALID;
+  memset(result, 0, sizeof(*result));
+  result->fail_task = -1;
+  return place_finish(c, slot, placed_node, placed_kind, result, skipped != 0);
+}
+
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   if (c) c->timing_now = c->timing;
+  if (c) c->keys_spec = -1;
   if (!c || (!spec_ids && t)) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
@@ -950,6 +1082,7 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
 }
 
 int kb_restore_nodes(kb_ctx* c) {
+  if (c) c->keys_spec = -1;
   if (!c) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");

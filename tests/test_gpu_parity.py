@@ -192,3 +192,30 @@ def test_engine_idle_exit_and_relaunch():
     (a, na, ka, sa, pa), (b, nb, kb, sb, pb) = outs
     assert np.array_equal(a["task_node"], b["task_node"]) and np.array_equal(a["event_task"], b["event_task"])
     assert np.array_equal(na, nb) and np.array_equal(ka, kb) and (sa, pa) == (sb, pb)
+
+
+def _partial_gang(cl, frac):
+    for pg in cl.pod_groups:
+        pg.min_member = max(1, int(pg.min_member * frac))
+    return cl
+
+
+PIPE_CLUSTERS = CLUSTERS + [
+    # minMember below the job size: jobs stop READY mid-way and are pushed back (the speculated next job
+    # is often the same job), and ready jobs compete with unready ones in the gang order
+    ("C2-halfgang", _partial_gang(synth.c2(n_nodes=120, n_jobs=30, tasks_per_job=20, seed=31), 0.5)),
+    ("C1-thirdgang", _partial_gang(synth.c1(n_nodes=100, n_jobs=20, tasks_per_job=24, seed=32), 0.34)),
+]
+
+
+@pytest.mark.parametrize("pipeline", [True, False], ids=["pipelined", "serial"])
+@pytest.mark.parametrize("name,cluster", PIPE_CLUSTERS, ids=[c[0] for c in PIPE_CLUSTERS])
+def test_driver_pipeline_parity(name, cluster, pipeline, monkeypatch):
+    """kb_allocate's driver issues job k+1 before job k's result is read, guarded on job k's predicted
+    outcome (a failed guard turns job k+1 into no-ops and the driver re-issues the real next job), and
+    skips the level-0 sweep when the key buffer is current for the spec. Both drivers match the oracle."""
+    if not pipeline:
+        monkeypatch.setenv("KB_NO_PIPELINE", "1")
+    ref = pyoracle.allocate(cluster)
+    got = runtime.allocate(cluster)
+    _compare(ref, got)
