@@ -1733,6 +1733,34 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   }
 }
 
+// The level-0 keys into LDS (zero padding past n): every load of the thread is issued before the first
+// LDS store, so the copy costs one memory latency instead of one per element.
+__device__ __forceinline__ void load_keys_lds(uint32_t* k32, const uint32_t* keys32, int n, int n_pad) {
+  const int tid = threadIdx.x;
+  const int nv = n_pad >> 2, full = n >> 2;
+  const uint4* src = (const uint4*)keys32;
+  uint4* dst = (uint4*)k32;
+  uint4 x[kSelQ4];
+#pragma unroll
+  for (int c = 0; c < kSelQ4; ++c) {
+    const int v = tid + c * kSelThreads;
+    x[c] = make_uint4(0u, 0u, 0u, 0u);
+    if (v < full) {
+      x[c] = src[v];
+    } else if (v == full) {  // the vector n falls in
+      const int b = 4 * v;
+      x[c].x = b < n ? keys32[b] : 0u;
+      x[c].y = b + 1 < n ? keys32[b + 1] : 0u;
+      x[c].z = b + 2 < n ? keys32[b + 2] : 0u;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < kSelQ4; ++c) {
+    const int v = tid + c * kSelThreads;
+    if (v < nv) dst[v] = x[c];
+  }
+}
+
 __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
@@ -1753,7 +1781,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   uint32_t* k32 = lds32;           // [n_pad] current key of every node
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap] candidate composites, a list per selected node
   const kb_spec sp = P.specs[spec];
-  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
+  load_keys_lds(k32, keys32, n, n_pad);
   int ready = first ? ready0 : js->ready_num;
   const int minav = first ? minav0 : js->min_available;
   const int gang = first ? gang0 : js->gang_ready;
@@ -1955,7 +1983,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   const kb_spec sp = P.specs[spec];
-  for (int i = tid; i < n_pad; i += kSelThreads) k32[i] = i < n ? keys32[i] : 0u;
+  load_keys_lds(k32, keys32, n, n_pad);
   int ready = 0, placed = 0, stop = 0, fail_task = -1, panic = 0, stopped = 0, rp = 0;
 #ifdef KB_DIAG
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
