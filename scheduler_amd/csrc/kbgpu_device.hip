@@ -774,7 +774,7 @@ __device__ __forceinline__ bool idle_fits_after(const DevNodes& N, const kb_spec
 }
 
 // A = number of consecutive Allocates before InitResreq stops fitting Idle (capped at 65535).
-__device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+__device__ __forceinline__ int allocs_before_full_search(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
                                                   const int64_t* scr, const Row& r, int n) {
   if (!idle_fits_after(N, sp, sci, scr, r, n, 0)) return 0;
   int lo = 0, hi = 65535;  // fits(lo) holds; find the largest such lo
@@ -785,6 +785,36 @@ __device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_sp
     else hi = mid;
   }
   return lo + 1;
+}
+
+// Allocations of the spec the node's Idle takes before it stops fitting (capped at 65535). Each resource's
+// test init - (idle - a * req) < tol (idle_fits_after) is a * req < X with X = tol - init + idle, so for
+// req >= 0 the largest fitting a is min over resources of (X - 1) / req: a closed form of the search above
+// (which stays as the fallback for negative requests), with one load per scalar instead of one per step.
+__device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+                                                  const int64_t* scr, const Row& r, int n) {
+  int64_t lo = 65535;
+  bool ok = true, neg = false;
+  const auto bound = [&](int64_t init, int64_t idle, int64_t req, int64_t tol) {
+    const int64_t X = tol - init + idle;
+    if (X <= 0) ok = false;
+    else if (req > 0) lo = (X - 1) / req < lo ? (X - 1) / req : lo;
+    else if (req < 0) neg = true;
+  };
+  bound(sp.init_cpu, r.idle_cpu, sp.req_cpu, 10);
+  bound(sp.init_mem, r.idle_mem, sp.req_mem, 10ll * 1024 * 1024);
+  if (sp.flags & KB_SPEC_INIT_HAS_MAP) {
+    if (!(r.flags & KB_NODE_IDLE_HAS_MAP)) return 0;  // rr.ScalarResources == nil
+    uint64_t m = sp.init_sc_mask;
+    while (m) {
+      const int q = __builtin_ctzll(m);
+      m &= m - 1;
+      bound(sci[q], N.idle_sc[(size_t)q * N.n + n], scr[q], 10);
+    }
+  }
+  if (neg) return allocs_before_full_search(N, sp, sci, scr, r, n);
+  if (!ok) return 0;
+  return lo >= 65535 ? 65535 : (int)lo + 1;
 }
 
 // Full 64-bit key of node n after j commits of the spec (A allocations at most, the rest pipelined).
