@@ -70,7 +70,6 @@ struct kb_ctx {
     uint32_t seq = 0;        // sequence number the slot's last launch reports
     size_t ev_b = 0, ev_e = 0;  // its timing events in `pending`
     bool busy = false;
-    int keys_spec_before = -1;  // restored when the slot's job turns out skipped
     std::chrono::steady_clock::time_point t_issue;
     double issue_ms = 0;
   };
@@ -79,10 +78,22 @@ struct kb_ctx {
   char* h_job1 = nullptr;
   uint32_t job1_cap = 0;
   uint64_t issue_count = 0;
-  // spec whose level-0 keys (traj[0..n)) and static cache (stat) are current once the issued work is done;
-  // -1 when anything else may have touched them. A selection run of that spec skips its sweep.
-  int keys_spec = -1;
-  int last_spec = -1;  // spec of the last single-run selection job issued
+  // Selection runs of the pipelined driver use per-slot level-0 keys / static cache / commit lists, so the
+  // level-0 sweep of job i can run on stream_b while job i-1's place kernel runs on `stream`; job i then
+  // re-keys the rows job i-1 committed, from that job's commit list. Every job before job i-1 has been
+  // read back by the host when job i is issued (two slots), so the sweep needs no stream dependency; the
+  // place kernel waits on sweep_ctr[slot] reaching sweep_target[slot] (device counter, no events).
+  uint32_t* sel_keys[2] = {nullptr, nullptr};
+  uint64_t* sel_stat[2] = {nullptr, nullptr};
+  int32_t* commits[2] = {nullptr, nullptr};
+  int32_t sel_n = -1;       // node count the per-slot buffers were sized for
+  uint32_t commits_cap = 0;
+  hipStream_t stream_b = nullptr;
+  uint32_t* sweep_ctr = nullptr;  // [2] device counters
+  uint32_t sweep_target[2] = {0, 0};
+  bool prev_listed = false; // the last issued job was one selection run that lists its commits
+  int prev_slot = -1;
+  uint64_t n_overlap = 0;   // sweeps that ran overlapped
   char* h_eval = nullptr;
 
   double device_ms = 0;  // wall time inside kb_place_job
@@ -100,8 +111,8 @@ struct kb_ctx {
   std::vector<Pending> pending;
   kb_stats stats{};
   hipEvent_t ev_get();
-  void ev_begin(hipEvent_t* a);
-  void ev_end(hipEvent_t a, int kind, uint64_t pairs);
+  void ev_begin(hipEvent_t* a, hipStream_t s = nullptr);  // nullptr: `stream`
+  void ev_end(hipEvent_t a, int kind, uint64_t pairs, hipStream_t s = nullptr);
   size_t ev_collect(bool all, size_t limit = (size_t)-1);  // returns the event pairs it folded
   size_t pending_job_begin = 0;  // first pending event pair of the current kb_place_job call
 };

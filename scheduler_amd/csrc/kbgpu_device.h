@@ -81,6 +81,8 @@ struct JobState {
   uint64_t diag[8];   // -DKB_DIAG builds: per-phase shader cycles of the place loop, [7] = realtime ticks
   uint64_t t_recv, t_done;  // placement engine: s_memrealtime (100 MHz) at command receipt / completion
   uint32_t exit_seq;  // placement engine: the command it was waiting for when it exited idle (0: none)
+  int32_t n_commit;   // selection place kernel: rows in its commit list (device copy only)
+  int32_t stall;      // host copy: 1 = the place kernel gave up waiting for its overlapped sweep
   uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
 };
 
@@ -142,15 +144,20 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
 // keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.
 int sel_lds_bytes(int n);
-// A guard (g.prev set) replaces the JobState gate of a job's first run. keys_out (== keys32): the place
-// kernel writes the new level-0 key of every row it commits, so the buffer stays current for the spec.
+// A guard (g.prev set) replaces the JobState gate of a job's first run. commit_out: the place kernel lists
+// every row it commits (count in js->n_commit); patch / patch_js: the previous job's list, whose rows this
+// run re-keys after loading keys32 (its sweep ran concurrently with that job). done_ctr: the sweep's
+// blocks each add 1 when their keys are written; wait_ctr / wait_target: the place kernel waits for the
+// counter to reach the target first.
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
                       uint64_t* stat, const JobState* js, bool aff, void* stream,
-                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0});
+                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, uint32_t* done_ctr = nullptr);
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
-                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, uint32_t* keys_out = nullptr);
+                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, int32_t* commit_out = nullptr,
+                      const int32_t* patch = nullptr, const JobState* patch_js = nullptr,
+                      const uint32_t* wait_ctr = nullptr, uint32_t wait_target = 0);
 
 // Placement engine (kbgpu_device.hip): the selection path as one persistent workgroup serving the
 // commands posted to `cmd` from sequence number seq0 on; exits on KB_ENG_EXIT or after idle_ticks

@@ -1182,6 +1182,7 @@ struct SelShared {
   uint32_t emin[128];      // running prefix minimum
   int32_t done[128];
   int32_t fin[128];        // commits of this node in the segment
+  int32_t n_commit;        // rows listed in commit_out so far
   int32_t act[128];        // active slots of a generation round
   uint32_t red[2][3][kSelWaves];  // reduction scratch, alternating halves: one barrier per reduction
   uint32_t hist[KB_NUM_REASONS];
@@ -1333,7 +1334,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         int idx_bits, const uint64_t* stat, int& ready, int minav, int gang,
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
-                                        ShardRec* rec, uint32_t* keys_out SEL_DIAG_PARAMS) {
+                                        ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -1691,17 +1692,16 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
       __syncthreads();
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram
-      // keys_out: the level-0 key buffer stays current for the next job of the same spec (no sweep)
+      // the touched nodes' keys matter only to a later segment or to the no-fit histogram; commit_out
+      // lists the rows for the next job, whose level-0 sweep ran before these stores (kb_job_issue)
       const bool rekey = kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count);
       if (tid < (int)S && sh.fin[tid] > 0) {
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
         store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
-        if (rekey || keys_out != nullptr) {
-          const uint32_t k = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A),
-                                          w + N.base, idx_bits);
-          k32[w] = k;
-          if (keys_out != nullptr) keys_out[w] = k;
-        }
+        if (rekey)
+          k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
+                                idx_bits);
+        if (commit_out != nullptr) commit_out[atomicAdd(&sh.n_commit, 1)] = w;
       }
       __syncthreads();
       KB_SEL_PH(5);
@@ -1794,11 +1794,15 @@ __device__ __forceinline__ void load_keys_lds(uint32_t* k32, const uint32_t* key
 __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
-    uint32_t seq, SpecGuard g, uint32_t* keys_out) {
+    uint32_t seq, SpecGuard g, int32_t* commit_out, const int32_t* patch, const JobState* patch_js,
+    const uint32_t* wait_ctr, uint32_t wait_target) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   if ((!first && js->stopped) || guard_fails(g)) {
-    if (threadIdx.x == 0) js->stopped = 1;  // later runs of a skipped speculative job skip too
+    if (threadIdx.x == 0) {
+      js->stopped = 1;  // later runs of a skipped speculative job skip too
+      js->n_commit = 0;  // nothing for the next job to patch
+    }
     signal_skip(hjs, seq);
     return;
   }
@@ -1811,7 +1815,37 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   uint32_t* k32 = lds32;           // [n_pad] current key of every node
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap] candidate composites, a list per selected node
   const kb_spec sp = P.specs[spec];
+  if (wait_ctr != nullptr) {
+    // this job's level-0 sweep runs on the other stream: wait for all its blocks (acquire), bounded so a
+    // missing signal ends the kernel instead of hanging it (reported to the host through stall)
+    if (tid == 0) {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(wait_ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - wait_target > 0x7fffffffu) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == (1u << 26)) {
+          hjs->stall = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
   load_keys_lds(k32, keys32, n, n_pad);
+  if (tid == 0) sh.n_commit = 0;
+  if (patch != nullptr) {
+    // the level-0 sweep of this job overlapped the previous job's place kernel: re-key the rows that
+    // job committed, from their stored state (the static cache is commit-independent)
+    __syncthreads();
+    const int np = patch_js->n_commit;
+    const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+    for (int i = tid; i < np; i += kSelThreads) {
+      const int w = patch[i];
+      const Row r = load_row(N, w);
+      const uint64_t st = stat[w];
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, w);
+      k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), w), w + N.base, idx_bits);
+    }
+  }
   int ready = first ? ready0 : js->ready_num;
   const int minav = first ? minav0 : js->min_available;
   const int gang = first ? gang0 : js->gang_ready;
@@ -1829,7 +1863,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   KB_SEL_PH(0);
 
   sel_run(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
-          panic, stopped, hout, js, hjs, rp, nullptr, keys_out SEL_DIAG_ARGS);
+          panic, stopped, hout, js, hjs, rp, nullptr, commit_out SEL_DIAG_ARGS);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
@@ -1839,6 +1873,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
+    if (commit_out != nullptr) js->n_commit = sh.n_commit;
     __threadfence_system();
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
@@ -1966,27 +2001,33 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
 template <bool AFF>
 __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
                                                       uint32_t* keys32, uint64_t* stat, const JobState* js,
-                                                      SpecGuard g) {
+                                                      SpecGuard g, uint32_t* done_ctr) {
   if ((js != nullptr && js->stopped) || guard_fails(g)) return;
   const int n = blockIdx.x * 64 + threadIdx.x;
-  if (n >= N.n) return;
-  const kb_spec sp = P.specs[spec];
-  const Row r = load_row(N, n);
-  const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
-  stat[n] = st;
-  const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
-  keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
+  if (n < N.n) {
+    const kb_spec sp = P.specs[spec];
+    const Row r = load_row(N, n);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    stat[n] = st;
+    const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
+    keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
+  }
+  // overlapped sweep (stream_b): one release per block (the wave's stores, written back to memory for
+  // the place kernel on another XCD), counted by the place kernel of the same job
+  if (done_ctr != nullptr && threadIdx.x == 0)
+    __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
-                      uint64_t* stat, const JobState* js, bool aff, void* stream, SpecGuard g) {
+                      uint64_t* stat, const JobState* js, bool aff, void* stream, SpecGuard g,
+                      uint32_t* done_ctr) {
   const int blocks = (N.n + 63) / 64;
   if (aff)
     hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
-                       keys32, stat, js, g);
+                       keys32, stat, js, g, done_ctr);
   else
     hipLaunchKernelGGL(sel_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec,
-                       idx_bits, keys32, stat, js, g);
+                       idx_bits, keys32, stat, js, g, done_ctr);
 }
 
 // ===========================================================================
@@ -2201,10 +2242,11 @@ int sel_lds_bytes(int n) {
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
-                      SpecGuard g, uint32_t* keys_out) {
+                      SpecGuard g, int32_t* commit_out, const int32_t* patch, const JobState* patch_js,
+                      const uint32_t* wait_ctr, uint32_t wait_target) {
   hipLaunchKernelGGL(sel_place_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P, C,
                      spec, t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs,
-                     seq, g, keys_out);
+                     seq, g, commit_out, patch, patch_js, wait_ctr, wait_target);
 }
 
 // ---------------------------------------------------------------------------

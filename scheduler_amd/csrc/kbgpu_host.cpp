@@ -25,7 +25,7 @@ int fail(kb_ctx* c, int code, const char* fmt, ...) {
   va_end(ap);
   if (c) {
     c->err = buf;
-    c->keys_spec = -1;
+    c->prev_listed = false;
   }
   return code;
 }
@@ -82,16 +82,16 @@ hipEvent_t kb_ctx::ev_get() {
   (void)hipEventCreate(&e);
   return e;
 }
-void kb_ctx::ev_begin(hipEvent_t* a) {
+void kb_ctx::ev_begin(hipEvent_t* a, hipStream_t s) {
   *a = nullptr;
   if (!timing_now) return;
   *a = ev_get();
-  (void)hipEventRecord(*a, stream);
+  (void)hipEventRecord(*a, s ? s : stream);
 }
-void kb_ctx::ev_end(hipEvent_t a, int kind, uint64_t pairs) {
+void kb_ctx::ev_end(hipEvent_t a, int kind, uint64_t pairs, hipStream_t s) {
   if (!timing || !a) return;
   hipEvent_t b = ev_get();
-  (void)hipEventRecord(b, stream);
+  (void)hipEventRecord(b, s ? s : stream);
   pending.push_back({a, b, kind, pairs});
 }
 // Fold finished event pairs into the stats, oldest first. `all`: wait for the stream first; otherwise
@@ -170,6 +170,13 @@ void kb_destroy(kb_ctx* c) {
   free_all(c->work_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
   if (c->h_job1) (void)hipHostFree(c->h_job1);
+  for (int s = 0; s < 2; ++s) {
+    if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
+    if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
+    if (c->commits[s]) (void)hipFree(c->commits[s]);
+  }
+  if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
+  if (c->sweep_ctr) (void)hipFree(c->sweep_ctr);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -190,7 +197,7 @@ void kb_destroy(kb_ctx* c) {
 const char* kb_last_error(const kb_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int kb_set_config(kb_ctx* c, const kb_config* cfg) {
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c || !cfg) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   c->cfg = DevCfg{cfg->predicates_enabled, cfg->nodeorder_enabled, cfg->mem_pressure, cfg->disk_pressure,
@@ -200,7 +207,7 @@ int kb_set_config(kb_ctx* c, const kb_config* cfg) {
 }
 
 int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c || !in) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -286,7 +293,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
 }
 
 int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c || !in) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -354,7 +361,7 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
 }
 
 int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c || !a) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
@@ -798,9 +805,47 @@ static int validate_job(kb_ctx* c, const kb_job_req* job) {
   return KB_OK;
 }
 
+// Per-slot selection buffers (level-0 keys, static cache, commit list), the sweep stream and its events.
+static int ensure_sel_bufs(kb_ctx* c) {
+  if (c->sel_n != c->N.n) {
+    for (int s = 0; s < 2; ++s) {
+      if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
+      if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
+      c->sel_keys[s] = nullptr;
+      c->sel_stat[s] = nullptr;
+    }
+    c->sel_n = -1;
+    const size_t n = (size_t)std::max(c->N.n, 1);
+    for (int s = 0; s < 2; ++s) {
+      HIP_OK(c, hipMalloc((void**)&c->sel_keys[s], n * 4));
+      HIP_OK(c, hipMalloc((void**)&c->sel_stat[s], n * 8));
+    }
+    c->sel_n = c->N.n;
+    c->prev_listed = false;
+  }
+  if (c->commits_cap < c->job_cap) {
+    for (int s = 0; s < 2; ++s) {
+      if (c->commits[s]) (void)hipFree(c->commits[s]);
+      c->commits[s] = nullptr;
+    }
+    c->commits_cap = 0;
+    for (int s = 0; s < 2; ++s) HIP_OK(c, hipMalloc((void**)&c->commits[s], (size_t)c->job_cap * 4));
+    c->commits_cap = c->job_cap;
+    c->prev_listed = false;
+  }
+  if (!c->stream_b) {
+    HIP_OK(c, hipMalloc((void**)&c->sweep_ctr, 2 * sizeof(uint32_t)));
+    HIP_OK(c, hipMemset(c->sweep_ctr, 0, 2 * sizeof(uint32_t)));
+    c->sweep_target[0] = c->sweep_target[1] = 0;
+    HIP_OK(c, hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+  }
+  return KB_OK;
+}
+
 // Both job slots with room for n_tasks placements (slot 0 = d_job / h_job).
 static int ensure_slots(kb_ctx* c, uint32_t n_tasks, bool both) {
   if (int rc = ensure_job_buffers(c, n_tasks)) return rc;
+  if (int rc = ensure_sel_bufs(c)) return rc;
   c->slot[0].d = c->d_job;
   c->slot[0].h = c->h_job;
   c->slot[0].hdev = c->h_job_dev;
@@ -838,7 +883,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
   JobState* hjs_dev = (JobState*)S.hdev;
   memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
   int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
-  S.keys_spec_before = c->keys_spec;
+  bool listed = false;
   uint32_t t = 0;
   while (t < job->n_tasks) {
     uint32_t e = t + 1;
@@ -855,7 +900,6 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     const bool traj = !sel && !dyn && c->use_traj && key32 && c->traj_full && traj_lds_bytes(c->N.n, run, &pbc) > 0;
     if (first && g.prev && !sel) return fail(c, KB_E_INVALID, "guarded job does not take the selection path");
     const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
-    if (!sel) c->keys_spec = -1;  // the other paths reuse the key / static-cache buffers
     if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
       c->ev_begin(&ea);
       launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->P.A.mm, first ? nullptr : js, c->stream);
@@ -867,26 +911,33 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
     } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
-      // A job that is one selection run of a spec without inter-pod terms leaves the key buffer current
-      // for that spec (the place kernel re-keys the rows it commits): the next such run skips its sweep.
-      // The run executes whenever the job does (it is the job's only run), so the host-side tag is exact.
-      // The write-back re-keys the committed rows (a little work per commit), so it is done while jobs of
-      // one spec follow each other: from the second same-spec job on.
+      uint32_t* kt = c->sel_keys[si];
+      uint64_t* st = c->sel_stat[si];
+      // A job that is one run without inter-pod terms lists the rows it commits. When the previous job
+      // (the other slot) did, this run's level-0 sweep goes to stream_b right after the job before that
+      // one, overlapping the previous job's place kernel, and the place kernel re-keys that job's rows.
       const bool one_run = !aff && t == 0 && e == job->n_tasks;
-      const bool keep = one_run && c->last_spec == spec;
-      c->last_spec = one_run ? spec : -1;
-      if (!(keep && c->keys_spec == spec)) {
+      const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1);
+      if (ov) {
+        c->ev_begin(&ea, c->stream_b);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, false, c->stream_b,
+                         SpecGuard{nullptr, 0, 0, 0}, c->sweep_ctr + si);
+        c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
+        c->sweep_target[si] += (uint32_t)((c->N.n + 63) / 64);
+        c->n_overlap++;
+      } else {
         c->ev_begin(&ea);
-        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, aff,
-                         c->stream, gr);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, aff, c->stream, gr);
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
       }
       c->ev_begin(&ea);
-      launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, c->traj, c->stat, js, first,
-                       job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream,
-                       gr, keep ? c->traj : nullptr);
+      launch_sel_place(c->N, c->P, c->cfg, spec, (int)t, run, c->idx_bits, kt, st, js, first, job->ready_num,
+                       job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream, gr,
+                       one_run ? c->commits[si] : nullptr, ov ? c->commits[si ^ 1] : nullptr,
+                       ov ? (const JobState*)c->slot[si ^ 1].d : nullptr, ov ? c->sweep_ctr + si : nullptr,
+                       c->sweep_target[si]);
       c->ev_end(ea, KB_KERNEL_SEL_PLACE, 0);
-      c->keys_spec = keep ? spec : -1;
+      listed = one_run;
     } else if (traj) {
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
@@ -913,6 +964,8 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     t = e;
   }
   HIP_OK(c, hipGetLastError());
+  c->prev_listed = listed;
+  c->prev_slot = si;
   S.seq = c->seq;
   S.ev_e = c->pending.size();
   S.busy = true;
@@ -932,8 +985,9 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
   // pipelined, so issue-to-finish walls would count the overlap twice)
   const double wall =
       S.issue_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count();
+  if (hs->stall)
+    return fail(c, KB_E_HIP, "place kernel gave up waiting for its overlapped level-0 sweep");
   if (skipped) {  // a speculative job whose guard failed: nothing ran, nothing to count
-    c->keys_spec = S.keys_spec_before;
     for (size_t k = S.ev_b; k < S.ev_e && k < c->pending.size(); ++k) c->pending[k].kind = -1;
     return KB_OK;
   }
@@ -975,7 +1029,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   result->fail_task = -1;
   if (int rc = validate_job(c, job)) return rc;
   if (job->n_tasks == 0) return KB_OK;
-  if (c->sharded || engine_ok(c, job)) c->keys_spec = -1;  // these paths own the key buffers
+  c->prev_listed = false;
   if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
   if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
   if (int rc = kb_engine_stop(c)) return rc;
@@ -1028,7 +1082,7 @@ int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kin
 
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   if (c) c->timing_now = c->timing;
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c || (!spec_ids && t)) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
@@ -1082,7 +1136,7 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
 }
 
 int kb_restore_nodes(kb_ctx* c) {
-  if (c) c->keys_spec = -1;
+  if (c) c->prev_listed = false;
   if (!c) return KB_E_INVALID;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok) return fail(c, KB_E_STATE, "no node table");
