@@ -200,6 +200,24 @@ class Cluster:
     def dumps(self) -> str:
         return json.dumps(self.to_json(), separators=(",", ":"))
 
+    @staticmethod
+    def from_json(d) -> "Cluster":
+        """Inverse of to_json (fixtures under tests/golden/)."""
+        def ctr(c):
+            return Container(req=dict(c["req"]), ports=list(c["ports"]))
+        nodes = [Node(name=n["name"], alloc=dict(n["alloc"]), cap=dict(n["cap"]), labels=dict(n["labels"]),
+                      taints=list(n["taints"]), unschedulable=n["unschedulable"], conditions=list(n["conditions"]))
+                 for n in d["nodes"]]
+        pods = [Pod(ns=p["ns"], name=p["name"], uid=p["uid"], node=p["node"], phase=p["phase"],
+                    deleting=p["deleting"], group=p["group"], priority=p["priority"], ctime=p["ctime"],
+                    labels=dict(p["labels"]), containers=[ctr(c) for c in p["containers"]],
+                    init=[ctr(c) for c in p["init"]], node_selector=dict(p["nodeSelector"]),
+                    tolerations=list(p["tolerations"]), affinity=p["affinity"]) for p in d["pods"]]
+        groups = [PodGroup(ns=g["ns"], name=g["name"], queue=g["queue"], min_member=g["minMember"], phase=g["phase"],
+                           ctime=g["ctime"], priority=g["priority"]) for g in d["podGroups"]]
+        queues = [Queue(name=q["name"], weight=q["weight"], ctime=q["ctime"]) for q in d["queues"]]
+        return Cluster(nodes=nodes, pods=pods, pod_groups=groups, queues=queues, tiers=d["tiers"])
+
     def copy(self) -> "Cluster":
         return copy.deepcopy(self)
 
