@@ -27,6 +27,8 @@ struct kb_ctx {
   std::vector<char> spec_dyn;   // per spec: KB_AFF_SELF_DYNAMIC -> block-wide re-sweep loop
   std::vector<char> spec_hist;  // per spec: has InterPodAffinity histograms
   std::vector<char> spec_incr;  // per spec: its commits update affinity tables
+  std::vector<char> spec_aff_reg;  // per spec: its entry count when the register-resident loop takes it, else 0
+  bool use_aff_reg = true;
   int64_t* mm_eval = nullptr;   // [2 * chunk] per-spec IPA min / max for kb_eval
   uint32_t mm_eval_cap = 0;
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec

@@ -140,6 +140,14 @@ void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec
 void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       uint64_t* base, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
                       int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+// The same loop with every thread's nodes (base keys, domain ids) held for the whole run; n <= 10240 and at
+// most 4 checks + histograms per spec (ne of them), 8 table updates per commit (aff_reg_npt(n) < 0: use
+// launch_aff_place).
+int aff_reg_npt(int n);
+bool aff_reg_fits(int n, int ne);
+void launch_aff_reg(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int ne, int t_begin,
+                    int t_count, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                    int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
 // keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.

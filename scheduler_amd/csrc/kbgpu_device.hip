@@ -2528,6 +2528,457 @@ __global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
 
 int aff_pb_cap(int t_count) { return t_count < 8192 ? (t_count < 1 ? 1 : t_count) : 8192; }
 
+// ---------------------------------------------------------------------------
+// Register-resident variant of aff_place_kernel (same semantics, same outputs). Every thread owns the
+// nodes i = k * kAffThreads + tid (k < NPT) for the whole run and keeps, in registers, their base keys and
+// the live value of every affinity entry of the spec (checks: the count-table entry of the node's domain;
+// histograms: the InterPodAffinity histogram entry). Within the run only this kernel's own commits change
+// those tables, and a commit changes a handful of (table, domain) entries, all known: thread 0 broadcasts
+// them and every thread patches the nodes of those domains (domain ids in LDS). A task therefore reads no
+// global memory for its re-sweep: counts, reasons, min / max and keys come from registers. The global
+// tables are still updated (atomics) for the kernels that follow. Specs with more than kAffRegE entries,
+// more than kAffRegU table updates per commit, or more than NPT * kAffThreads nodes take aff_place_kernel.
+// ---------------------------------------------------------------------------
+#ifdef KB_DIAG_AFF  // phase stamps of this kernel only (Makefile target diagaff)
+#define AFF_STAMP(k)                                  \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    dg[k] += t_ - dg_last;                            \
+    dg_last = t_;                                     \
+  } while (0)
+#else
+#define AFF_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+constexpr int kAffRegE = 4;  // entries (checks + histograms) per spec, at most
+constexpr int kAffRegU = 8;
+constexpr int kAffRegMaxNpt = 10;  // n <= 10240 (domain ids < n fit 16 bits)
+
+struct AffUpd {
+  int32_t kind;   // 0: count table (lister join), 1: histogram (commit increment)
+  int32_t key;    // table id / histogram h_off
+  int32_t dom;    // the committed node's domain (-1: none, nothing changes)
+  int32_t delta;
+};
+
+template <int NPT, int NE>
+__global__ __launch_bounds__(kAffThreads) void aff_reg_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, uint64_t* stat, JobState* js, int first,
+    int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, int pb_cap, uint32_t seq) {
+  // dynamic LDS: [NPT * kAffThreads] u64 base keys, [NE][NPT * kAffThreads] u16 domain ids (0xffff: no
+  // domain), then [pb_cap] placements
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ar[];
+  constexpr int kStride = NPT * kAffThreads;
+  uint64_t* bkl = (uint64_t*)lds_ar;
+  uint16_t* dm16 = (uint16_t*)(bkl + kStride);
+  uint32_t* pbs = (uint32_t*)(dm16 + NE * kStride);
+  __shared__ uint64_t red[16];
+  __shared__ int64_t rmin[16], rmax[16];
+  __shared__ uint32_t hist_s[KB_NUM_REASONS];
+  __shared__ int32_t sh_kind, sh_w;
+  __shared__ uint64_t sh_base;
+  __shared__ AffUpd sh_upd[kAffRegU];
+  __shared__ int64_t sh_bp[10];
+  __shared__ LoopOut lo;
+  if (!first && js->stopped) {
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = N.n;
+  const DevAff& A = P.A;
+  const kb_spec sp = P.specs[spec];
+  const kb_aff_spec as = A.specs[sp.aff_class];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const int nc = (int)as.check_cnt, ne = (int)(as.check_cnt + as.hist_cnt);
+  // entry e < nc: check (counters[cnt_off + dom] of table e_key); nc <= e < ne: histogram (h[e_key + dom])
+  int32_t e_slot[NE], e_off[NE], e_kind[NE], e_key[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    e_slot[e] = 0, e_off[e] = 0, e_kind[e] = 0, e_key[e] = -1;
+    if (e < nc) {
+      const kb_aff_check c = A.checks[as.check_off + e];
+      const kb_aff_table t = A.tables[c.table];
+      e_slot[e] = t.slot, e_off[e] = (int32_t)t.cnt_off, e_kind[e] = c.kind, e_key[e] = c.table;
+    } else if (e < ne) {
+      const kb_ipa_hist h = A.hists[as.hist_off + (e - nc)];
+      e_slot[e] = h.slot, e_off[e] = (int32_t)h.h_off, e_key[e] = (int32_t)h.h_off;
+    }
+  }
+#ifdef KB_DIAG_AFF
+  // phases: 0 prologue, 1 counts + min/max, 2 keys + argmax, 3 commit (thread 0), 4 table updates,
+  // 5 stop rules / flush, 6 no-fit histogram
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  int32_t v[NPT][NE];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = k * kAffThreads + tid;
+    bkl[i] = 0;  // padding: infeasible with no reason bits (never wins, adds nothing to the histogram)
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      dm16[e * kStride + i] = 0xffffu;
+      v[k][e] = 0;
+    }
+    if (i < n) {
+      const Row r = load_row(N, i);
+      const uint64_t st = static_eval<false>(N, P, C, sp, r.flags, i, nullptr);
+      stat[i] = st;
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
+      bkl[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        if (e < ne) {
+          const int32_t d = A.topo_dom[(size_t)e_slot[e] * A.n + i];
+          if (d >= 0) {
+            dm16[e * kStride + i] = (uint16_t)d;
+            v[k][e] = ld_cnt<true>((e < nc ? A.counters : A.h) + e_off[e] + d);
+          }
+        }
+    }
+  }
+  int32_t tot[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) tot[e] = e < nc ? ld_cnt<true>(&A.totals[e_key[e]]) : 0;
+  int ready = first ? ready0 : js->ready_num;
+  int minav = first ? minav0 : js->min_available;
+  int gang = first ? gang0 : js->gang_ready;
+  int placed = first ? 0 : js->n_placed;
+  int pb_n = 0, pb_base = t_begin;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  const bool ipa = C.nodeorder && as.hist_cnt;
+  __syncthreads();
+  AFF_STAMP(0);
+  // The task loop reads the launch's uniform structs from LDS copies (thread 0's commit needs the node
+  // columns, the spec and the affinity tables; kept in scalar registers across the loop they spilled).
+  __shared__ DevNodes LN;
+  __shared__ DevSpecs LP;
+  __shared__ DevCfg LC;
+  __shared__ kb_spec LS;
+  __shared__ kb_aff_spec LAS;
+  if (tid == 0) {
+    LN = N;
+    LP = P;
+    LC = C;
+    LS = sp;
+    LAS = as;
+  }
+  const DevAff& LA = LP.A;
+  const int c_pred = C.predicates;
+  const int64_t c_wpa = C.w_pa;
+  for (int t = 0; t < t_count; ++t) {
+    // counts and reasons of every owned node from the registers (aff_reasons / ipa_count); computed again
+    // in the key pass rather than held across the min / max reduction (register budget)
+    const auto count_of = [&](int k) -> int32_t {
+      int32_t c = 0;
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        if (e >= nc) c += v[k][e];
+      return c;
+    };
+    const auto reasons_of = [&](int k) -> uint32_t {
+      if (!c_pred) return 0u;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        if (e >= nc) break;
+        if (e_kind[e] == KB_AFF_EXISTING_ANTI) {
+          if (v[k][e] > 0) return kAffExistingAnti;
+        } else if (e_kind[e] == KB_AFF_ANTI) {
+          if (v[k][e] > 0) return kAffAntiRules;
+        } else if (v[k][e] == 0 && (tot[e] > 0 || !LAS.self_match)) {
+          return kAffAffinityRules;
+        }
+      }
+      return 0u;
+    };
+    int64_t mn = 0, mx = 0;
+    if (ipa) {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int32_t c = count_of(k);
+        if (k * kAffThreads + tid < n) {  // min / max over every node, from 0 (interpod_affinity.go:221-238)
+          mn = c < mn ? c : mn;
+          mx = c > mx ? c : mx;
+        }
+      }
+      mn = wave_min_i64(mn);
+      mx = wave_max_i64(mx);
+      if (lane == 0) {
+        rmin[wv] = mn;
+        rmax[wv] = mx;
+      }
+      __syncthreads();
+      mn = 0, mx = 0;
+#pragma unroll
+      for (int w = 0; w < kAffThreads / 64; ++w) {
+        mn = rmin[w] < mn ? rmin[w] : mn;
+        mx = rmax[w] > mx ? rmax[w] : mx;
+      }
+      // ipa_score is monotone in the count: its 10 breakpoints, exactly. a_s = ceil(s * b / 10) is the
+      // first offset with 10 a / b >= s; the float64 formula can only fall short of s where 10 a / b == s
+      // exactly (elsewhere the gap is >= 1 / b, far above the rounding error), and then a_s + 1 is it.
+      if (tid < 10) {
+        const int64_t bb = mx - mn;
+        int64_t as_ = INT64_MAX;
+        if (bb > 0) {
+          const int64_t sb = (int64_t)(tid + 1) * bb;
+          as_ = (sb + 9) / 10;
+          if (sb % 10 == 0 && ipa_score(mn + as_, mn, mx) < tid + 1) ++as_;
+        }
+        sh_bp[tid] = as_;
+      }
+      __syncthreads();
+    }
+    int64_t bp[10];  // uniform: scalar registers
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int64_t x = ipa ? sh_bp[q] : INT64_MAX;
+      const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)x);
+      const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+      bp[q] = (int64_t)(((uint64_t)hi32 << 32) | lo32);
+    }
+    AFF_STAMP(1);
+    // aff_key on the registers
+    const auto key_of = [&](int k) -> uint64_t {
+      const uint64_t b = bkl[k * kAffThreads + tid];
+      if (!(b & kFeasible)) return b;
+      const uint32_t ar = reasons_of(k);
+      if (ar) return ar;
+      if (!ipa) return b;
+      const int64_t off = (int64_t)count_of(k) - mn;
+      int32_t sc = 0;  // == ipa_score(count, mn, mx)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) sc += off >= bp[q];
+      const int64_t score = (int64_t)((b >> 24) & ((1ull << 39) - 1)) - kScoreBias + (int64_t)sc * c_wpa;
+      return make_key(0, score, k * kAffThreads + tid);
+    };
+    uint64_t best = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) best = umax64(best, key_of(k));
+    best = wave_max_u64(best);
+    if (lane == 0) red[wv] = best;
+    __syncthreads();
+    best = 0;
+#pragma unroll
+    for (int k = 0; k < kAffThreads / 64; ++k) best = umax64(best, red[k]);
+    AFF_STAMP(2);
+    if (!(best & kFeasible)) {
+      // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes.
+      if (tid < KB_NUM_REASONS) hist_s[tid] = 0;
+      __syncthreads();
+      uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const uint64_t kk = key_of(k);
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (uint32_t)(kk >> b) & 1u;
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) {
+        const uint32_t s = wave_sum_u32(h[b]);
+        if (lane == 0 && s) atomicAdd(&hist_s[b], s);
+      }
+      __syncthreads();
+      if (tid < KB_NUM_REASONS) {
+        js->hist[tid] = hist_s[tid];
+        hjs->hist[tid] = hist_s[tid];
+      }
+      stop = KB_STOP_NO_FIT;
+      fail_task = t_begin + t;
+      stopped = 1;
+      AFF_STAMP(6);
+      break;
+    }
+    const int64_t score = (int64_t)((best >> 24) & ((1ull << 39) - 1)) - kScoreBias;
+    if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
+      fail_task = t_begin + t;
+      panic = 1;
+      stopped = 1;
+      break;
+    }
+    const int w = (int)(kIdxMask - (uint32_t)(best & kIdxMask));
+    if (tid == 0) {  // commit: Session.Allocate / Pipeline on the winner's row (allocate.go:159-182)
+      const int64_t* lsci = LP.sc_init + (size_t)spec * LN.S;
+      const int64_t* lscr = LP.sc_req + (size_t)spec * LN.S;
+      Row r = load_row(LN, w);
+      const uint64_t st = stat[w];
+      const bool to_idle = le_tol(LS.init_cpu, r.idle_cpu, 10) && le_tol(LS.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                           scalars_fit(LN, LS, lsci, r.flags & KB_NODE_IDLE_HAS_MAP, LN.idle_sc, w);
+      int kind;
+      if (to_idle) {
+        r.idle_cpu -= LS.req_cpu;
+        r.idle_mem -= LS.req_mem;
+        if (r.flags & KB_NODE_IDLE_HAS_MAP) {
+          uint64_t m = LS.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            LN.idle_sc[(size_t)q * n + w] -= lscr[q];
+          }
+        }
+        kind = KB_PLACE_ALLOCATE;
+      } else {
+        r.rel_cpu -= LS.req_cpu;
+        r.rel_mem -= LS.req_mem;
+        if (r.flags & KB_NODE_REL_HAS_MAP) {
+          uint64_t m = LS.req_sc_mask;
+          while (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            LN.rel_sc[(size_t)q * n + w] -= lscr[q];
+          }
+        }
+        kind = KB_PLACE_PIPELINE;
+      }
+      r.pod_count += 1;
+      r.nz_cpu += LS.nz_cpu;
+      r.nz_mem += LS.nz_mem;
+      for (uint32_t i = 0; i < LS.port_cnt; ++i) {
+        const kb_port p = LP.ports[LS.port_off + i];
+        LN.port_used[(size_t)p.slot * n + w] |= 1ull << p.ip;
+      }
+      store_row(LN, w, r);
+      const uint32_t rs = row_reasons(LN, LP, LC, LS, lsci, r, st, w);
+      sh_base = make_key(rs, rs ? 0 : row_score(LC, LS, r, st), w);
+      sh_w = w;
+      pbs[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
+      sh_kind = kind;
+    } else if (tid <= (int)(LAS.lister_cnt + LAS.incr_cnt)) {
+      // the table entries this commit changes (apply_commit_tables), loaded beside thread 0's row work:
+      // lister joins (applied on an Allocate only), then the histogram increments (every commit)
+      const int u = tid - 1;
+      if (u < (int)LAS.lister_cnt) {
+        const int32_t tb = LA.lister[LAS.lister_off + u];
+        sh_upd[u] = AffUpd{0, tb, LA.topo_dom[(size_t)LA.tables[tb].slot * n + w], 1};
+      } else {
+        const kb_ipa_incr e = LA.incr[LAS.incr_off + (u - (int)LAS.lister_cnt)];
+        sh_upd[u] = AffUpd{1, (int32_t)e.h_off, LA.topo_dom[(size_t)e.slot * n + w], e.weight};
+      }
+    }
+    __syncthreads();
+    AFF_STAMP(3);
+    const int kind = sh_kind;
+    if (tid == 0) bkl[sh_w] = sh_base;  // the committed node's new base key (read after the next barrier)
+    // the global tables (read by the kernels after this one): atomics, completed before the final publish
+    const int nupd = (int)(LAS.lister_cnt + LAS.incr_cnt);
+    const bool joins = kind == KB_PLACE_ALLOCATE;  // a Pipelined task does not join the lister tables
+    if (tid < nupd && (joins || sh_upd[tid].kind == 1)) {
+      const AffUpd up = sh_upd[tid];
+      if (up.kind == 0) {
+        if (up.dom >= 0) atomicAdd(&LA.counters[LA.tables[up.key].cnt_off + up.dom], up.delta);
+        atomicAdd(&LA.totals[up.key], up.delta);
+      } else if (up.dom >= 0) {
+        atomicAdd(&LA.h[up.key + up.dom], up.delta);
+      }
+    }
+    // ... and the same updates on the registers: the nodes of the committed node's domains
+    for (int u = 0; u < nupd; ++u) {
+      const AffUpd up = sh_upd[u];
+      if (up.kind == 0 && !joins) continue;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const bool hit = up.kind == 0 ? e < nc && e_key[e] == up.key : e >= nc && e < ne && e_key[e] == up.key;
+        if (!hit) continue;
+        if (up.kind == 0) tot[e] += up.delta;
+        if (up.dom < 0) continue;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k)
+          if (dm16[e * kStride + k * kAffThreads + tid] == (uint32_t)up.dom) v[k][e] += up.delta;
+      }
+    }
+    AFF_STAMP(4);
+    ++placed;
+    ++pb_n;
+    if (kind == KB_PLACE_ALLOCATE) ++ready;
+    if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+      stop = KB_STOP_READY;
+      stopped = 1;
+      break;
+    }
+    if (pb_n == pb_cap) {
+      for (int k = tid; k < pb_n; k += kAffThreads) {
+        const uint32_t e = pbs[k];
+        hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+        hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+      }
+      __syncthreads();
+      pb_base += pb_n;
+      pb_n = 0;
+    }
+    AFF_STAMP(5);
+  }
+  for (int k = tid; k < pb_n; k += kAffThreads) {
+    const uint32_t e = pbs[k];
+    hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+    hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+  }
+#ifdef KB_DIAG_AFF
+  if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
+  if (tid == 0) lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, pb_n, pb_base, 0, 0};
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0)
+    publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic,
+                  seq);
+}
+
+int aff_reg_npt(int n) {
+  int npt = (n + kAffThreads - 1) / kAffThreads;
+  npt = npt < 2 ? 2 : (npt + 1) & ~1;  // instantiated for even counts (padding nodes never win)
+  return npt <= kAffRegMaxNpt ? npt : -1;
+}
+
+// The register-resident loop takes (n, entries) when its LDS plan (base keys + domain ids + a placement
+// buffer of at least 256) fits.
+bool aff_reg_fits(int n, int ne) {
+  const int npt = aff_reg_npt(n);
+  if (npt < 0 || ne < 1 || ne > kAffRegE) return false;
+  return (size_t)npt * kAffThreads * (8 + 2 * ne) + 4096 + 256 * 4 <= (size_t)kLdsLimit;
+}
+
+#define KB_AFF_REG_NE(K, E)                                                                                       \
+  case (K) * 8 + (E):                                                                                             \
+    hipLaunchKernelGGL((aff_reg_kernel<K, E>), dim3(1), dim3(kAffThreads), bytes, (hipStream_t)stream, N, P, C,   \
+                       spec, t_begin, t_count, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);    \
+    break;
+#define KB_AFF_REG_CASE(K) KB_AFF_REG_NE(K, 1) KB_AFF_REG_NE(K, 2) KB_AFF_REG_NE(K, 3) KB_AFF_REG_NE(K, 4)
+
+void launch_aff_reg(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int ne, int t_begin,
+                    int t_count, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
+                    int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+  const int npt = aff_reg_npt(N.n);
+  const int E = ne < 1 ? 1 : ne;
+  int pb_cap = aff_pb_cap(t_count);
+  const size_t fixed = (size_t)npt * kAffThreads * (8 + 2 * E);  // base keys + domain ids
+  const size_t cap_max = ((size_t)kLdsLimit - 4096 - fixed) / 4;  // the kernel's static LDS stays below 4 KB
+  if ((size_t)pb_cap > cap_max) pb_cap = (int)cap_max;
+  const size_t bytes = fixed + (size_t)pb_cap * 4;
+  switch (npt * 8 + E) {
+    KB_AFF_REG_CASE(2)
+    KB_AFF_REG_CASE(4)
+    KB_AFF_REG_CASE(6)
+    KB_AFF_REG_CASE(8)
+    KB_AFF_REG_CASE(10)
+    default:
+      break;
+  }
+}
+
+#define KB_AFF_REG_FN(K) (const void*)aff_reg_kernel<K, 1>, (const void*)aff_reg_kernel<K, 2>, \
+                         (const void*)aff_reg_kernel<K, 3>, (const void*)aff_reg_kernel<K, 4>
+static const void* const kAffRegFns[] = {KB_AFF_REG_FN(2), KB_AFF_REG_FN(4), KB_AFF_REG_FN(6), KB_AFF_REG_FN(8),
+                                        KB_AFF_REG_FN(10)};
+#undef KB_AFF_REG_FN
+#undef KB_AFF_REG_CASE
+#undef KB_AFF_REG_NE
+
 void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec_ids, int spec, int count,
                        int64_t* mm, const JobState* js, void* stream) {
   hipLaunchKernelGGL(ipa_minmax_kernel, dim3(count), dim3(kAffThreads), 0, (hipStream_t)stream, N, P, spec_ids, spec,
@@ -2599,6 +3050,10 @@ int configure_kernels() {
                        (const void*)traj_place_kernel};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit);
+    if (e != hipSuccess) return (int)e;
+  }
+  for (const void* f : kAffRegFns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - 4096);
     if (e != hipSuccess) return (int)e;
   }
   for (const void* f : {(const void*)sel_place_kernel, (const void*)engine_kernel, (const void*)shard_propose_kernel}) {

@@ -129,6 +129,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->device = opts ? opts->device : 0;
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
+  c->use_aff_reg = getenv("KB_NO_AFF_REG") == nullptr;  // testing: force the global-memory affinity loop
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
@@ -408,6 +409,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   c->spec_dyn.assign(a->m, 0);
   c->spec_hist.assign(a->m, 0);
   c->spec_incr.assign(a->m, 0);
+  c->spec_aff_reg.assign(a->m, 0);
   for (uint32_t s = 0; s < a->m; ++s) {
     const int32_t ac = specs[s].aff_class;
     if (ac < -1 || ac >= (int32_t)a->m) return fail(c, KB_E_INVALID, "spec %u aff_class %d", s, ac);
@@ -415,6 +417,11 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
       c->spec_dyn[s] = (a->specs[ac].flags & KB_AFF_SELF_DYNAMIC) != 0;
       c->spec_hist[s] = a->specs[ac].hist_cnt > 0;
       c->spec_incr[s] = a->specs[ac].lister_cnt > 0 || a->specs[ac].incr_cnt > 0;
+      const kb_aff_spec& e = a->specs[ac];
+      bool ok = e.check_cnt + e.hist_cnt <= 4 && e.lister_cnt + e.incr_cnt <= 8;  // kAffRegE, kAffRegU; 16-bit domains
+      for (uint32_t i = 0; ok && i < e.check_cnt; ++i) ok = D[a->tables[a->checks[e.check_off + i].table].slot] < 0xffff;
+      for (uint32_t i = 0; ok && i < e.hist_cnt; ++i) ok = D[a->hists[e.hist_off + i].slot] < 0xffff;
+      c->spec_aff_reg[s] = ok && e.check_cnt + e.hist_cnt > 0 ? (char)(e.check_cnt + e.hist_cnt) : 0;  // entries (0: not eligible)
     }
   }
   DevAff& A = c->P.A;
@@ -907,8 +914,12 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     }
     if (dyn) {
       c->ev_begin(&ea);
-      launch_aff_place(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->stat, js, first, job->ready_num,
+      if (c->use_aff_reg && c->spec_aff_reg[spec] && aff_reg_fits(c->N.n, c->spec_aff_reg[spec]))
+        launch_aff_reg(c->N, c->P, c->cfg, spec, c->spec_aff_reg[spec], (int)t, run, c->stat, js, first, job->ready_num,
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
+      else
+        launch_aff_place(c->N, c->P, c->cfg, spec, (int)t, run, c->keys, c->stat, js, first, job->ready_num,
+                         job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
     } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
       uint32_t* kt = c->sel_keys[si];

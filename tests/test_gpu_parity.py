@@ -219,3 +219,16 @@ def test_driver_pipeline_parity(name, cluster, pipeline, monkeypatch):
     ref = pyoracle.allocate(cluster)
     got = runtime.allocate(cluster)
     _compare(ref, got)
+
+
+@pytest.mark.parametrize("reg", [True, False], ids=["aff-reg", "aff-global"])
+@pytest.mark.parametrize("name,cluster", affinity_clusters(), ids=[c[0] for c in affinity_clusters()])
+def test_affinity_loop_variants(name, cluster, reg, monkeypatch):
+    """Specs whose own commits move their inter-pod affinity inputs: the register-resident loop
+    (aff_reg_kernel, the default when n <= 10240) and the global-memory loop (aff_place_kernel) both match
+    the oracle."""
+    if not reg:
+        monkeypatch.setenv("KB_NO_AFF_REG", "1")
+    ref = pyoracle.allocate(cluster)
+    got = runtime.allocate(cluster)
+    _compare(ref, got)
