@@ -1327,7 +1327,9 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 // ready / placed advance, and the stop state is set when the run stops the job.
 // PROPOSE (node sharding): one segment of t_count <= kSegMax tasks, no commit; the rank's best picks go
 // to `rec` instead (launch_shard_propose).
-template <bool PROPOSE = false>
+// QN > 0: the node count needs exactly QN key groups per thread (compile-time passes over 4 * QN keys);
+// QN = 0: the group count is taken from n at run time (passes unrolled to kSelQ4 with the spare groups 0).
+template <bool PROPOSE = false, int QN = 0>
 __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* cand, const DevNodes& N,
                                         const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
                                         int t_begin, int t_count,
@@ -1337,7 +1339,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
-  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  constexpr int QU = QN > 0 ? QN : kSelQ4;  // unroll bound of the key passes
+  const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const uint4* k32v = (const uint4*)k32;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
@@ -1349,11 +1352,11 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
     // ---- 1. S = the T best nodes by current key (keys in registers for this phase) ----
-    uint4 kv[kSelQ4];
+    uint4 kv[QU];
 #pragma unroll
-    for (int c = 0; c < kSelQ4; ++c) kv[c] = c < Q4 ? k32v[tid * Q4 + c] : make_uint4(0u, 0u, 0u, 0u);
+    for (int c = 0; c < QU; ++c) kv[c] = (QN > 0 || c < Q4) ? k32v[tid * Q4 + c] : make_uint4(0u, 0u, 0u, 0u);
 #define SEL_EACH_KEY(BODY)                                       \
-  _Pragma("unroll") for (int c_ = 0; c_ < kSelQ4; ++c_) {       \
+  _Pragma("unroll") for (int c_ = 0; c_ < QU; ++c_) {           \
     const uint32_t ks_[4] = {kv[c_].x, kv[c_].y, kv[c_].z, kv[c_].w}; \
     _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {           \
       const uint32_t k = ks_[q_];                                \
@@ -1765,14 +1768,15 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
 
 // The level-0 keys into LDS (zero padding past n): every load of the thread is issued before the first
 // LDS store, so the copy costs one memory latency instead of one per element.
+template <int QU = kSelQ4>
 __device__ __forceinline__ void load_keys_lds(uint32_t* k32, const uint32_t* keys32, int n, int n_pad) {
   const int tid = threadIdx.x;
   const int nv = n_pad >> 2, full = n >> 2;
   const uint4* src = (const uint4*)keys32;
   uint4* dst = (uint4*)k32;
-  uint4 x[kSelQ4];
+  uint4 x[QU];
 #pragma unroll
-  for (int c = 0; c < kSelQ4; ++c) {
+  for (int c = 0; c < QU; ++c) {
     const int v = tid + c * kSelThreads;
     x[c] = make_uint4(0u, 0u, 0u, 0u);
     if (v < full) {
@@ -1785,12 +1789,13 @@ __device__ __forceinline__ void load_keys_lds(uint32_t* k32, const uint32_t* key
     }
   }
 #pragma unroll
-  for (int c = 0; c < kSelQ4; ++c) {
+  for (int c = 0; c < QU; ++c) {
     const int v = tid + c * kSelThreads;
     if (v < nv) dst[v] = x[c];
   }
 }
 
+template <int QN>
 __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
@@ -1810,7 +1815,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   const int n = N.n;
   // node keys in contiguous groups of 4 per thread (index order decides the lowest-index tie-break);
   // the padding past n holds 0, an infeasible key with no reason bits
-  const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const int n_pad = 4 * kSelThreads * Q4;
   uint32_t* k32 = lds32;           // [n_pad] current key of every node
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap] candidate composites, a list per selected node
@@ -1830,7 +1835,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     }
     __syncthreads();
   }
-  load_keys_lds(k32, keys32, n, n_pad);
+  load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, keys32, n, n_pad);
   if (tid == 0) sh.n_commit = 0;
   if (patch != nullptr) {
     // the level-0 sweep of this job overlapped the previous job's place kernel: re-key the rows that
@@ -1862,7 +1867,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   __syncthreads();
   KB_SEL_PH(0);
 
-  sel_run(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
+  sel_run<false, QN>(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
           panic, stopped, hout, js, hjs, rp, nullptr, commit_out SEL_DIAG_ARGS);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
@@ -2239,14 +2244,46 @@ int sel_lds_bytes(int n) {
   return q4 <= kSelQ4 && bytes <= kSelDynLimit ? (int)bytes : -1;
 }
 
+// The sel_place_kernel instance for n: the smallest instantiated group count >= ceil(n / 2048) whose LDS
+// plan fits, else the run-time-count instance (0).
+static int sel_qn(int n) {
+  const int q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  for (int qn : {1, 2, 3, 4, 5, 6, 8, 10}) {
+    if (qn < q4) continue;
+    const long bytes = 4l * (4 * kSelThreads * qn) + 8l * kCandCap;
+    return bytes <= kSelDynLimit ? qn : 0;
+  }
+  return 0;
+}
+
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
                       SpecGuard g, int32_t* commit_out, const int32_t* patch, const JobState* patch_js,
                       const uint32_t* wait_ctr, uint32_t wait_target) {
-  hipLaunchKernelGGL(sel_place_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P, C,
-                     spec, t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs,
-                     seq, g, commit_out, patch, patch_js, wait_ctr, wait_target);
+  const int qn = sel_qn(N.n);
+  const int bytes = qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : sel_lds_bytes(N.n);
+#define KB_SEL_QN(Q)                                                                                                \
+  case Q:                                                                                                          \
+    hipLaunchKernelGGL(sel_place_kernel<Q>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C, spec,  \
+                       t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs, seq, \
+                       g, commit_out, patch, patch_js, wait_ctr, wait_target);                                     \
+    break;
+  switch (qn) {
+    KB_SEL_QN(1)
+    KB_SEL_QN(2)
+    KB_SEL_QN(3)
+    KB_SEL_QN(4)
+    KB_SEL_QN(5)
+    KB_SEL_QN(6)
+    KB_SEL_QN(8)
+    KB_SEL_QN(10)
+    default:
+      hipLaunchKernelGGL(sel_place_kernel<0>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C, spec,
+                         t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs, seq,
+                         g, commit_out, patch, patch_js, wait_ctr, wait_target);
+  }
+#undef KB_SEL_QN
 }
 
 // ---------------------------------------------------------------------------
@@ -3056,7 +3093,11 @@ int configure_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - 4096);
     if (e != hipSuccess) return (int)e;
   }
-  for (const void* f : {(const void*)sel_place_kernel, (const void*)engine_kernel, (const void*)shard_propose_kernel}) {
+  for (const void* f :
+       {(const void*)sel_place_kernel<0>, (const void*)sel_place_kernel<1>, (const void*)sel_place_kernel<2>,
+        (const void*)sel_place_kernel<3>, (const void*)sel_place_kernel<4>, (const void*)sel_place_kernel<5>,
+        (const void*)sel_place_kernel<6>, (const void*)sel_place_kernel<8>, (const void*)sel_place_kernel<10>,
+        (const void*)engine_kernel, (const void*)shard_propose_kernel}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit);
     if (e != hipSuccess) return (int)e;
   }
