@@ -1159,6 +1159,9 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
 // ===========================================================================
 constexpr int kSelThreads = 512;   // 8 waves: up to 256 VGPRs per lane, no spills
 constexpr int kSelWaves = kSelThreads / 64;
+#ifndef KB_SEL_DENSE_MAX
+#define KB_SEL_DENSE_MAX 128  // winners: rank all candidates pairwise up to this many, else threshold + takes
+#endif
 constexpr int kSegMax = 100;                           // tasks per segment (slot and level fit 7-bit fields)
 constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
 constexpr int kCandCap = 5120;                         // candidate composites: 10 per thread, five uint4 reads
@@ -1548,7 +1551,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       uint32_t K, zero = 0, ztot;
       uint32_t pos = kc;
       sel_excl_scan2(sh, rp, pos, zero, &K, &ztot);
-      if (K <= (uint32_t)kSelThreads) {
+      if (K <= (uint32_t)KB_SEL_DENSE_MAX) {
 #pragma unroll
         for (int q = 0; q < 2 * kCandV; ++q)
           if (cs[q]) sh.dense[pos++] = cs[q];
