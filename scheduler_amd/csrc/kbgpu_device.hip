@@ -1383,27 +1383,40 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
     if (!no_fit) {
       // infeasible keys (and padding) have a score field below every feasible one: never counted below
       uint32_t sstar = MN, R = 0xffffffffu;  // F <= T: every feasible node
+      uint32_t g = 0, e = 0, tg = 0, te = 0, G = 0, E = 0;
+      bool counted = false;
       if (F > T) {
-        uint32_t lo = MN, hi = MX;
-        while (lo < hi) {
-          // the first probe is the top score itself (often enough nodes share it)
-          const uint32_t mid = hi == MX && lo < hi ? hi : lo + (hi - lo + 1) / 2;
-          uint32_t c = 0;
-          SEL_EACH_KEY({ c += (k >> idx_bits) >= mid; })
-          if (sel_sum(sh, rp, c) >= T) lo = mid;
-          else hi = mid - 1;
+        // first probe: the top score itself (often enough nodes share it). Nothing lies above MX, so this
+        // pass is also the greater / equal count of the compaction when it succeeds.
+        SEL_EACH_KEY({ e += (k >> idx_bits) == MX; })
+        E = e;
+        sel_excl_scan2(sh, rp, G, E, &tg, &te);
+        if (te >= T) {
+          sstar = MX;
+          counted = true;
+        } else {
+          uint32_t lo = MN, hi = MX - 1;  // count(>= MN) = F > T; count(>= MX) < T
+          while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo + 1) / 2;
+            uint32_t c = 0;
+            SEL_EACH_KEY({ c += (k >> idx_bits) >= mid; })
+            if (sel_sum(sh, rp, c) >= T) lo = mid;
+            else hi = mid - 1;
+          }
+          sstar = lo;
         }
-        sstar = lo;
       }
       KB_SEL_FINE(2);
-      uint32_t g = 0, e = 0, tg, te;
-      SEL_EACH_KEY({
-        const uint32_t h = k >> idx_bits;
-        g += h > sstar;
-        e += h == sstar;
-      })
-      uint32_t G = g, E = e;
-      sel_excl_scan2(sh, rp, G, E, &tg, &te);
+      if (!counted) {
+        g = 0, e = 0;
+        SEL_EACH_KEY({
+          const uint32_t h = k >> idx_bits;
+          g += h > sstar;
+          e += h == sstar;
+        })
+        G = g, E = e;
+        sel_excl_scan2(sh, rp, G, E, &tg, &te);
+      }
       KB_SEL_FINE(3);
       if (F > T) R = T - tg;
       const uint32_t selE = R > E ? (R - E < e ? R - E : e) : 0u;
@@ -1823,6 +1836,14 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   uint32_t* k32 = lds32;           // [n_pad] current key of every node
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);  // [kCandCap] candidate composites, a list per selected node
   const kb_spec sp = P.specs[spec];
+#ifdef KB_DIAG
+  // phases: 0 sweep wait + key load + patch (from kernel entry), 1 node selection, 2 selected-node setup,
+  // 3 e-sequences, 4 winners + order, 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after
+  // the block barriers); diag[7]: realtime ticks from entry to the publish
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (wait_ctr != nullptr) {
     // this job's level-0 sweep runs on the other stream: wait for all its blocks (acquire), bounded so a
     // missing signal ends the kernel instead of hanging it (reported to the host through stall)
@@ -1860,13 +1881,6 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   int placed = first ? 0 : js->n_placed;
   int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
   int rp = 0;
-#ifdef KB_DIAG
-  // phases: 0 key load, 1 node selection, 2 selected-node setup, 3 e-sequences, 4 winners + order,
-  // 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after the block barriers)
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t dg_last = __builtin_amdgcn_s_memtime();
-  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   __syncthreads();
   KB_SEL_PH(0);
 
