@@ -1844,6 +1844,12 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+  // the previous job's committed rows are final when this kernel starts: their loads go out before the
+  // wait for this job's sweep (one per thread; lists longer than the block finish in the loop below)
+  const int np = patch != nullptr ? patch_js->n_commit : 0;
+  const int pw = tid < np ? patch[tid] : -1;
+  Row prow;
+  if (pw >= 0) prow = load_row(N, pw);
   if (wait_ctr != nullptr) {
     // this job's level-0 sweep runs on the other stream: wait for all its blocks (acquire), bounded so a
     // missing signal ends the kernel instead of hanging it (reported to the host through stall)
@@ -1859,15 +1865,19 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     }
     __syncthreads();
   }
+  const uint64_t pst = pw >= 0 ? stat[pw] : 0;  // issued with the key loads
   load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, keys32, n, n_pad);
   if (tid == 0) sh.n_commit = 0;
   if (patch != nullptr) {
     // the level-0 sweep of this job overlapped the previous job's place kernel: re-key the rows that
     // job committed, from their stored state (the static cache is commit-independent)
     __syncthreads();
-    const int np = patch_js->n_commit;
     const int64_t* sci = P.sc_init + (size_t)spec * N.S;
-    for (int i = tid; i < np; i += kSelThreads) {
+    if (pw >= 0) {
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, prow, pst, pw);
+      k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
+    }
+    for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
       const int w = patch[i];
       const Row r = load_row(N, w);
       const uint64_t st = stat[w];
