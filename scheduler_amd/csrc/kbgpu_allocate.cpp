@@ -567,6 +567,29 @@ struct Driver {
     const bool pipe = kb_job_pipeline_ok(ctx) && getenv("KB_NO_PIPELINE") == nullptr;
     if (pipe)
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
+    // every job one selection run of an eligible spec: the fed engine serves the whole cycle
+    bool fed = pipe;
+    for (uint32_t j = 0; fed && j < s.n_jobs; ++j) {
+      int sp0 = -1;
+      for (int t : job_pending[j]) {
+        if (task_res_empty(t)) continue;  // BestEffort: never placed by allocate
+        const int sp = s.task_spec[t];
+        if (sp0 < 0) sp0 = sp;
+        if (sp != sp0 || !kb_spec_fed_ok(ctx, sp)) {
+          fed = false;
+          break;
+        }
+      }
+    }
+    if (fed)
+      if (int rc = kb_fed_begin(ctx)) return rc;
+    struct FedEnd {  // the engine is stopped on every way out of the loop
+      kb_ctx* c;
+      bool on;
+      ~FedEnd() {
+        if (on) (void)kb_fed_end(c);
+      }
+    } fed_end{ctx, fed};
     int q, j, slot = 0;
     bool have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
     if (have && check_specs(j)) return KB_E_INVALID;
@@ -618,6 +641,10 @@ struct Driver {
     }
     out->n_events = n_events;
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
+    if (fed) {
+      fed_end.on = false;
+      if (int rc = kb_fed_end(ctx)) return rc;
+    }
     return KB_OK;
   }
 };

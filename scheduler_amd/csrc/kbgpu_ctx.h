@@ -93,6 +93,16 @@ struct kb_ctx {
   hipStream_t stream_b = nullptr;
   uint32_t* sweep_ctr = nullptr;  // [2] device counters
   uint32_t sweep_target[2] = {0, 0};
+  // fed engine (kb_fed_begin / kb_fed_end): one resident selection workgroup per allocate cycle, fed by the
+  // sweep kernels through a two-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
+  bool fed = false;
+  void* fed_ring = nullptr;
+  uint32_t* fed_ctr = nullptr;
+  int32_t* fed_exit = nullptr;
+  uint32_t fed_count[2] = {0, 0};
+  int fed_r = 0;
+  uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)
+  hipEvent_t fed_ev = nullptr;
   bool prev_listed = false; // the last issued job was one selection run that lists its commits
   int prev_slot = -1;
   uint64_t n_overlap = 0;   // sweeps that ran overlapped
@@ -138,6 +148,12 @@ struct kb_job_pred {
 extern "C" __attribute__((visibility("hidden"))) int kb_job_pipeline_ok(kb_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_guardable(kb_ctx* c, const kb_job_req* job);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, uint32_t max_tasks);
+// Fed engine for a cycle whose jobs are all one selection run of a spec without inter-pod terms
+// (kb_spec_fed_ok): kb_fed_begin after kb_job_reserve, then kb_job_issue / kb_job_finish as usual (each
+// issue launches only the job's sweep kernel), kb_fed_end before anything else runs on the context.
+extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, int spec);
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot,
                                                                   const kb_job_pred* pred);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node,

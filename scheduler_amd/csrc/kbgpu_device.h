@@ -174,6 +174,31 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
                    const EngineCmd* cmd, JobState* js, JobState* hjs, int32_t* hout, uint32_t seq0,
                    uint64_t idle_ticks, void* stream);
 
+// Fed engine (kbgpu_device.hip): one resident selection workgroup per allocate cycle; each job's sweep
+// kernel (launch_fed_cmd, on the sweep stream) also posts the job's command to a two-entry device ring and
+// counts its blocks in ctr[ring entry]; the engine serves commands in order until an EXIT command (or
+// idle_ticks without one: *exit_flag = 1).
+struct FedCmdArgs {
+  int32_t op, spec, t_begin, t_count, ready0, minav0, gang0, slot;
+  int32_t g_valid, g_stop, g_placed, g_ready;
+  uint32_t seq;
+};
+struct FedSlotPtrs {
+  uint32_t* keys[2];
+  uint64_t* stat[2];
+  int32_t* commits[2];
+  JobState* js[2];
+  JobState* hjs[2];
+  int32_t* hout[2];
+};
+size_t fed_ring_bytes();
+bool fed_fits(int n);  // the engine's LDS plan fits n nodes
+void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
+                    uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream);
+void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
+                       const void* ring, const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1, uint64_t idle_ticks,
+                       int32_t* exit_flag, void* stream);
+
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,

@@ -2313,6 +2313,229 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 #undef KB_SEL_QN
 }
 
+
+// ===========================================================================
+// Fed engine: the selection place kernel as ONE resident workgroup for a whole allocate cycle, fed through
+// device memory. Per job (one selection run) the host launches only fed_cmd_sweep_kernel on the sweep
+// stream: it computes the run's level-0 keys and static cache into the job slot's buffers, block 0
+// writes the run's command into a two-entry ring, and every block adds one to the ring entry's counter
+// with an agent-scope release. The engine waits for the counter (acquire), checks the command's guard
+// against the previous job's outcome, re-keys the rows the previous job committed (its sweep may have
+// overlapped that job), runs the selection and publishes to the slot's pinned host buffers exactly as
+// sel_place_kernel does. No per-job kernel boundary on the place stream: the launch gap, the end-of-
+// kernel release and the next kernel's acquire (5.6 us median between place kernels) go away.
+// ===========================================================================
+struct FedCmd {
+  int32_t op;  // KB_ENG_RUN / KB_ENG_EXIT
+  int32_t spec, t_begin, t_count, ready0, minav0, gang0, slot;
+  int32_t g_valid, g_stop, g_placed, g_ready;  // SpecGuard on the previous job's outcome
+  uint32_t seq;
+  int32_t pad[3];
+};
+
+struct FedSlots {
+  uint32_t* keys[2];
+  uint64_t* stat[2];
+  int32_t* commits[2];
+  JobState* js[2];   // device job state per slot
+  JobState* hjs[2];  // pinned host job state per slot (device addresses)
+  int32_t* hout[2];  // pinned host placements per slot (device addresses)
+};
+
+template <bool AFF>
+__global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
+                                                          uint32_t* keys32, uint64_t* stat, FedCmd cmd, FedCmd* ring,
+                                                          uint32_t* ctr, int sweep) {
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  if (sweep && n < N.n) {
+    const kb_spec sp = P.specs[cmd.spec];
+    const Row r = load_row(N, n);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    stat[n] = st;
+    const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)cmd.spec * N.S, r, st, n);
+    keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
+  }
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) *ring = cmd;
+    // a non-sweeping command (EXIT) adds the whole count at once
+    const uint32_t add = sweep ? 1u : (uint32_t)((N.n + 63) / 64);
+    __hip_atomic_fetch_add(ctr, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int QN>
+__global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
+                                                                 FedSlots S, const FedCmd* ring,
+                                                                 const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1,
+                                                                 uint64_t idle_ticks, int32_t* exit_flag) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  __shared__ SelShared sh;
+  __shared__ FedCmd cm;
+  __shared__ int32_t s_op;
+  const int tid = threadIdx.x;
+  const int n = N.n;
+  const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  uint32_t* k32 = lds32;
+  uint64_t* cand = (uint64_t*)(lds32 + n_pad);
+  const uint32_t blocks = (uint32_t)((n + 63) / 64);
+  uint32_t tgt[2] = {tgt0, tgt1};
+  int last_stop = -1, last_placed = -1, last_ready = -1, last_panic = 1;  // no previous job: guards fail
+  int prev_slot = -1, prev_ncommit = 0;
+  int rp = 0;
+#ifdef KB_DIAG
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+#endif
+  for (int r = 0;; r ^= 1) {
+    tgt[r] += blocks;
+    if (tid == 0) {  // wait for the ring entry's command and keys (acquire), bounded by idle_ticks
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int op = KB_ENG_EXIT_IDLE;
+      for (;;) {
+        if (__hip_atomic_load(&ctr[r], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - tgt[r] <= 0x7fffffffu) {
+          cm = ring[r];
+          op = cm.op;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_op = op;
+      if (op == KB_ENG_EXIT_IDLE) *exit_flag = 1;
+    }
+    __syncthreads();
+    if (s_op != KB_ENG_RUN) break;
+    const int slot = cm.slot, spec = cm.spec;
+    JobState* js = S.js[slot];
+    JobState* hjs = S.hjs[slot];
+    if (cm.g_valid && (last_panic || last_stop != cm.g_stop || last_placed != cm.g_placed ||
+                       last_ready != cm.g_ready)) {  // mispredicted speculative job: nothing runs
+      if (tid == 0) {
+        js->stopped = 1;
+        js->n_commit = 0;
+        __hip_atomic_store(&hjs->seq, cm.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      last_panic = 1;
+      prev_slot = slot;
+      prev_ncommit = 0;
+      __syncthreads();
+      continue;
+    }
+#ifdef KB_DIAG
+    for (int k = 0; k < 7; ++k) dg[k] = 0;
+    dg_last = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const kb_spec sp = P.specs[spec];
+    const uint64_t* stat = S.stat[slot];
+    // the previous job's commits (final rows) re-keyed for this spec: their loads first
+    const int np = prev_slot >= 0 ? prev_ncommit : 0;
+    const int32_t* patch = prev_slot >= 0 ? S.commits[prev_slot] : nullptr;
+    const int pw = tid < np ? patch[tid] : -1;
+    Row prow;
+    if (pw >= 0) prow = load_row(N, pw);
+    const uint64_t pst = pw >= 0 ? stat[pw] : 0;
+    load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+    if (tid == 0) sh.n_commit = 0;
+    __syncthreads();
+    if (np > 0) {
+      const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+      if (pw >= 0) {
+        const uint32_t rs = row_reasons(N, P, C, sp, sci, prow, pst, pw);
+        k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
+      }
+      for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
+        const int w = patch[i];
+        const Row rr = load_row(N, w);
+        const uint64_t st = stat[w];
+        const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
+        k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+      }
+      __syncthreads();
+    }
+    KB_SEL_PH(0);
+    int ready = cm.ready0, placed = 0;
+    const int minav = cm.minav0, gang = cm.gang0;
+    int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+    sel_run<false, QN>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav, gang,
+                       placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
+                       S.commits[slot] SEL_DIAG_ARGS);
+#ifdef KB_DIAG
+    if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
+    // every wave's host-buffer and row stores are complete before the barrier; one lane then releases at
+    // system scope and publishes (the host spins on the sequence number)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ncommit = sh.n_commit;
+    if (tid == 0) {
+      js->n_commit = ncommit;
+      __threadfence_system();
+      publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
+    }
+    last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
+    prev_slot = slot;
+    prev_ncommit = ncommit;
+    __syncthreads();  // cm / sh reused by the next command
+  }
+}
+
+int fed_lds_bytes(int n) {
+  const int qn = sel_qn(n);
+  return qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : sel_lds_bytes(n);
+}
+
+bool fed_fits(int n) {
+  const int b = fed_lds_bytes(n);
+  return b >= 0 && b <= kSelDynLimit - 256;
+}
+
+void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
+                    uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream) {
+  FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
+             a.g_placed, a.g_ready, a.seq, {0, 0, 0}};
+  const int blocks = sweep ? (N.n + 63) / 64 : 1;
+  hipLaunchKernelGGL(fed_cmd_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, idx_bits,
+                     keys32, stat, cmd, (FedCmd*)ring, ctr, sweep ? 1 : 0);
+}
+
+size_t fed_ring_bytes() { return 2 * sizeof(FedCmd); }
+
+void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
+                       const void* ring, const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1, uint64_t idle_ticks,
+                       int32_t* exit_flag, void* stream) {
+  FedSlots S;
+  for (int s = 0; s < 2; ++s) {
+    S.keys[s] = sp.keys[s];
+    S.stat[s] = sp.stat[s];
+    S.commits[s] = sp.commits[s];
+    S.js[s] = sp.js[s];
+    S.hjs[s] = sp.hjs[s];
+    S.hout[s] = sp.hout[s];
+  }
+  const int qn = sel_qn(N.n);
+  const int bytes = fed_lds_bytes(N.n);
+#define KB_FED_QN(Q)                                                                                              \
+  case Q:                                                                                                        \
+    hipLaunchKernelGGL(fed_engine_kernel<Q>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C,     \
+                       idx_bits, S, (const FedCmd*)ring, ctr, tgt0, tgt1, idle_ticks, exit_flag);                \
+    break;
+  switch (qn) {
+    KB_FED_QN(1)
+    KB_FED_QN(2)
+    KB_FED_QN(3)
+    KB_FED_QN(4)
+    KB_FED_QN(5)
+    KB_FED_QN(6)
+    KB_FED_QN(8)
+    KB_FED_QN(10)
+    default:
+      KB_FED_QN(0)
+  }
+#undef KB_FED_QN
+}
+
 // ---------------------------------------------------------------------------
 // ===========================================================================
 // Inter-pod affinity kernels.
@@ -3126,6 +3349,14 @@ int configure_kernels() {
         (const void*)sel_place_kernel<6>, (const void*)sel_place_kernel<8>, (const void*)sel_place_kernel<10>,
         (const void*)engine_kernel, (const void*)shard_propose_kernel}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit);
+    if (e != hipSuccess) return (int)e;
+  }
+  // the fed engine's static block also holds its command (FedCmd + op): a smaller dynamic budget
+  for (const void* f :
+       {(const void*)fed_engine_kernel<0>, (const void*)fed_engine_kernel<1>, (const void*)fed_engine_kernel<2>,
+        (const void*)fed_engine_kernel<3>, (const void*)fed_engine_kernel<4>, (const void*)fed_engine_kernel<5>,
+        (const void*)fed_engine_kernel<6>, (const void*)fed_engine_kernel<8>, (const void*)fed_engine_kernel<10>}) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit - 256);
     if (e != hipSuccess) return (int)e;
   }
   return 0;

@@ -178,6 +178,9 @@ void kb_destroy(kb_ctx* c) {
   }
   if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
   if (c->sweep_ctr) (void)hipFree(c->sweep_ctr);
+  if (c->fed_ring) (void)hipFree(c->fed_ring);
+  if (c->fed_ctr) (void)hipFree(c->fed_ctr);
+  if (c->fed_exit) (void)hipFree(c->fed_exit);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -1006,6 +1009,7 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
   c->stats.device_ms += wall;
   c->stats.job_calls += 1;
   for (int k = 0; k < 8; ++k) c->stats.diag[k] += hs->diag[k];
+  if (c->fed) c->fed_tasks += (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
   if (c->timing) {
     // a place launch covers (tasks it placed or tried) x n pairs; attribute them to the job's launches
     uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
@@ -1066,6 +1070,84 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
   return ensure_slots(c, std::max<uint32_t>(max_tasks, 1), true);
 }
 
+int kb_spec_fed_ok(kb_ctx* c, int spec) {
+  if (!c || spec < 0 || spec >= c->P.m) return 0;
+  if (c->sharded || c->use_engine || !c->use_sel || !c->sel_ok || !c->traj || !c->spec_traj_ok[spec]) return 0;
+  if (!fed_fits(c->N.n)) return 0;
+  if (c->aff_ok && c->spec_needs_aff[spec]) return 0;
+  return getenv("KB_NO_FED") == nullptr;
+}
+
+constexpr uint64_t kFedIdleTicks = 100000000ull;  // 1 s of s_memrealtime without a command: the engine exits
+
+int kb_fed_begin(kb_ctx* c) {
+  if (!c) return KB_E_INVALID;
+  if (c->fed) return fail(c, KB_E_STATE, "fed engine already running");
+  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  if (!c->slot[1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
+  if (!c->fed_ring) {
+    HIP_OK(c, hipMalloc(&c->fed_ring, fed_ring_bytes()));
+    HIP_OK(c, hipMalloc((void**)&c->fed_ctr, 2 * sizeof(uint32_t)));
+    HIP_OK(c, hipMalloc((void**)&c->fed_exit, sizeof(int32_t)));
+    HIP_OK(c, hipMemset(c->fed_ctr, 0, 2 * sizeof(uint32_t)));
+    c->fed_count[0] = c->fed_count[1] = 0;
+  }
+  HIP_OK(c, hipMemsetAsync(c->fed_exit, 0, sizeof(int32_t), c->stream));
+  FedSlotPtrs sp;
+  for (int s = 0; s < 2; ++s) {
+    sp.keys[s] = c->sel_keys[s];
+    sp.stat[s] = c->sel_stat[s];
+    sp.commits[s] = c->commits[s];
+    sp.js[s] = (JobState*)c->slot[s].d;
+    sp.hjs[s] = (JobState*)c->slot[s].hdev;
+    sp.hout[s] = (int32_t*)(c->slot[s].hdev + sizeof(JobState));
+  }
+  c->fed_r = 0;
+  c->fed_tasks = 0;
+  c->fed_ev = nullptr;
+  if (c->timing) {  // the engine is one launch per cycle: always timed
+    const bool tn = c->timing_now;
+    c->timing_now = true;
+    c->ev_begin(&c->fed_ev);
+    c->timing_now = tn;
+  }
+  launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count[0], c->fed_count[1],
+                    kFedIdleTicks, c->fed_exit, c->stream);
+  HIP_OK(c, hipGetLastError());
+  c->fed = true;
+  c->prev_listed = false;
+  return KB_OK;
+}
+
+// Post a command to the engine (sweep: the job's level-0 keys into its slot buffers first).
+static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
+  const int r = c->fed_r;
+  launch_fed_cmd(c->N, c->P, c->cfg, c->idx_bits, c->sel_keys[si], c->sel_stat[si], a,
+                 (char*)c->fed_ring + r * (fed_ring_bytes() / 2), c->fed_ctr + r, sweep, c->stream_b);
+  HIP_OK(c, hipGetLastError());
+  c->fed_count[r] += (uint32_t)((c->N.n + 63) / 64);
+  c->fed_r ^= 1;
+  return KB_OK;
+}
+
+int kb_fed_end(kb_ctx* c) {
+  if (!c || !c->fed) return KB_OK;
+  c->fed = false;
+  FedCmdArgs a{KB_ENG_EXIT, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int rc = fed_post(c, a, 0, false);
+  if (c->fed_ev) {  // queued behind the engine on the place stream
+    c->ev_end(c->fed_ev, KB_KERNEL_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
+    c->fed_ev = nullptr;
+  }
+  const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit
+  if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
+  if (c->timing) c->ev_collect(true);
+  int32_t idle = 0;
+  if (rc == KB_OK && hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
+    rc = fail(c, KB_E_HIP, "fed engine exited idle (a command never arrived)");
+  return rc;
+}
+
 int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* pred) {
   if (!c || !job || slot < 0 || slot > 1) return KB_E_INVALID;
   if (int rc = validate_job(c, job)) return rc;
@@ -1075,6 +1157,23 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     return fail(c, KB_E_STATE, "kb_job_reserve(%u) first", job->n_tasks);
   if (int rc = kb_engine_stop(c)) return rc;
   if (int rc = ensure_slots(c, job->n_tasks, true)) return rc;
+  if (c->fed) {  // one selection run: the sweep kernel carries the command to the resident engine
+    for (uint32_t i = 1; i < job->n_tasks; ++i)
+      if (job->task_specs[i] != job->task_specs[0]) return fail(c, KB_E_INVALID, "fed engine: one run per job");
+    if (!kb_spec_fed_ok(c, job->task_specs[0])) return fail(c, KB_E_INVALID, "fed engine: spec not eligible");
+    kb_ctx::JobSlot& S = c->slot[slot];
+    S.t_issue = std::chrono::steady_clock::now();
+    S.ev_b = S.ev_e = c->pending.size();
+    memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
+    FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
+                 job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
+                 pred ? pred->ready : 0, ++c->seq};
+    if (int rc = fed_post(c, a, slot, true)) return rc;
+    S.seq = c->seq;
+    S.busy = true;
+    S.issue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S.t_issue).count();
+    return KB_OK;
+  }
   SpecGuard g{nullptr, 0, 0, 0};
   if (pred) {
     if (!kb_job_guardable(c, job)) return fail(c, KB_E_INVALID, "job cannot be issued speculatively");
