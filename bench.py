@@ -163,15 +163,29 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": None, "traffic_source": None,
                 "avg_launch_us": round(avg_ms * 1e3, 3), "timed_launches": launches,
-                "timing": f"HIP events on the library stream around every launch of every {args.timing_every}th "
-                          f"job call in the timed region",
+                "timing": ("HIP events on the library stream around the resident engine's one launch per "
+                           "allocate cycle, every cycle of the timed region"
+                           if runtime.KERNELS[k] == "fed_engine_kernel" else
+                           f"HIP events on the library stream around every launch of every {args.timing_every}th "
+                           f"job call in the timed region"),
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
                 "avg_us_per_launch": {runtime.KERNELS[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
                                       for i in range(len(runtime.KERNELS)) if st["launches"][i]}}
 
     # the committed PMC pass was taken on the default C2 line: its bytes apply to that workload only
     c2_default = (args.config, args.nodes, args.jobs, args.tasks_per_job) == ("C2", 10000, 1000, 100)
-    tr = pmc_traffic(runtime.KERNELS[k]) if c2_default else None
+    tr = None
+    if c2_default and runtime.KERNELS[k] == "fed_engine_kernel":
+        # counter collection serialises dispatches, under which the resident engine cannot be fed: its HBM
+        # bytes are the launch path's per-job selection kernel bytes (same work, KB_NO_FED PMC pass) times
+        # the jobs it serves per launch
+        per_job = pmc_traffic("sel_place_kernel")
+        jobs = st["job_calls"] / max(1, st["launches"][k])
+        if per_job is not None:
+            tr = {"bytes_per_launch": round(per_job["bytes_per_launch"] * jobs, 1),
+                  "source": f"{per_job['source']}: sel_place_kernel per job (KB_NO_FED pass) x {jobs:.0f} jobs"}
+    elif c2_default:
+        tr = pmc_traffic(runtime.KERNELS[k])
     if tr is not None:
         roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
 
@@ -299,6 +313,8 @@ DIAG_PHASES = {
     "traj_place_kernel": ["argmax", "commit", "rereduce", "lmax", "prefetch_store", "loop", "fill"],
     "sel_place_kernel": ["key_load", "node_select", "node_setup", "e_sequences", "winners_order", "stop_commit",
                          "nofit_hist"],
+    "fed_engine_kernel": ["key_load", "node_select", "node_setup", "e_sequences", "winners_order", "stop_commit",
+                          "nofit_hist"],
     "aff_place_kernel": ["prologue", "live_loads_minmax", "keys_argmax", "commit", "table_incr_fence", "stop_flush",
                          "nofit_hist"],
 }

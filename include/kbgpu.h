@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 6
+#define KBGPU_ABI_VERSION 7
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -364,7 +364,8 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_SHARD_PROPOSE 10 /* node sharding: the rank's proposal for a segment */
 #define KB_KERNEL_SHARD_EXCHANGE 11 /* node sharding: the all-gather of the proposals (RCCL) */
 #define KB_KERNEL_SHARD_COMMIT 12  /* node sharding: global merge, stop rules, own commits */
-#define KB_NUM_KERNELS 13
+#define KB_KERNEL_FED_ENGINE 13    /* kb_allocate: resident selection workgroup fed by the sweeps, one launch per cycle */
+#define KB_NUM_KERNELS 14
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */

@@ -1136,7 +1136,7 @@ int kb_fed_end(kb_ctx* c) {
   FedCmdArgs a{KB_ENG_EXIT, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int rc = fed_post(c, a, 0, false);
   if (c->fed_ev) {  // queued behind the engine on the place stream
-    c->ev_end(c->fed_ev, KB_KERNEL_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
+    c->ev_end(c->fed_ev, KB_KERNEL_FED_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
     c->fed_ev = nullptr;
   }
   const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit

@@ -97,7 +97,7 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 13), ("kernel_ms", C.c_double * 13), ("pairs", C.c_uint64 * 13),
+    _fields_ = [("launches", C.c_uint64 * 14), ("kernel_ms", C.c_double * 14), ("pairs", C.c_uint64 * 14),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
 
 
@@ -107,7 +107,7 @@ KB_OPT_NO_SELECT = 4
 KB_OPT_ENGINE = 8
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
-           "shard_propose_kernel", "shard_exchange", "shard_commit_kernel")
+           "shard_propose_kernel", "shard_exchange", "shard_commit_kernel", "fed_engine_kernel")
 # device paths for a run of same-spec tasks (kb_place_job picks the first one that applies):
 #   select     - per-job launches of the level-0 sweep + the top-T selection kernel (default)
 #   engine     - the same selection served by one persistent workgroup (no launches; single-CU sweep)
@@ -116,7 +116,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 6  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 7  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",

@@ -35,12 +35,16 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
-  # HBM bytes per launch: one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass)
+  # HBM bytes per launch: one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
+  # Counter collection serialises dispatches, which the resident fed engine cannot run under (it waits for
+  # sweep kernels on another stream): these passes take the per-job launch path (KB_NO_FED=1).
+  export KB_NO_FED=1
   export TMPDIR=/tmp
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/pmc_fetch" -o run --output-format csv -- \
        python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
   step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/pmc_write" -o run --output-format csv -- \
        python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
+  unset KB_NO_FED
   python3 scripts/prof_summary.py "$OUT/prof" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/prof_summary.json" \
        > "$OUT/prof_summary.log" 2>&1; echo "=== prof_summary rc=$?"
 fi

@@ -208,13 +208,17 @@ PIPE_CLUSTERS = CLUSTERS + [
 ]
 
 
-@pytest.mark.parametrize("pipeline", [True, False], ids=["pipelined", "serial"])
+@pytest.mark.parametrize("mode", ["fed", "launch", "serial"])
 @pytest.mark.parametrize("name,cluster", PIPE_CLUSTERS, ids=[c[0] for c in PIPE_CLUSTERS])
-def test_driver_pipeline_parity(name, cluster, pipeline, monkeypatch):
+def test_driver_pipeline_parity(name, cluster, mode, monkeypatch):
     """kb_allocate's driver issues job k+1 before job k's result is read, guarded on job k's predicted
-    outcome (a failed guard turns job k+1 into no-ops and the driver re-issues the real next job), and
-    skips the level-0 sweep when the key buffer is current for the spec. Both drivers match the oracle."""
-    if not pipeline:
+    outcome (a failed guard turns job k+1 into no-ops and the driver re-issues the real next job), with
+    job k+1's level-0 sweep overlapping job k. fed: one resident selection workgroup fed by the sweeps
+    (cycles whose jobs are single selection runs); launch: a place kernel per job; serial: one
+    kb_place_job round trip per job. All match the oracle."""
+    if mode == "launch":
+        monkeypatch.setenv("KB_NO_FED", "1")
+    elif mode == "serial":
         monkeypatch.setenv("KB_NO_PIPELINE", "1")
     ref = pyoracle.allocate(cluster)
     got = runtime.allocate(cluster)
