@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
 constexpr int kSelThreads = 512;   // 8 waves: up to 256 VGPRs per lane, no spills
 constexpr int kSelWaves = kSelThreads / 64;
 #ifndef KB_SEL_DENSE_MAX
-#define KB_SEL_DENSE_MAX 128  // winners: rank all candidates pairwise up to this many, else threshold + takes
+#define KB_SEL_DENSE_MAX 32  // winners: rank all candidates pairwise up to this many, else threshold + takes
 #endif
 constexpr int kSegMax = 100;                           // tasks per segment (slot and level fit 7-bit fields)
 constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
@@ -1587,7 +1587,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
             HN = h < HN ? h : HN;
           }
         sel_reduce3(sh, rp, kk, HX, HN);
-        uint32_t lo = HN, hi = HX;  // K > T here
+        uint32_t lo = HN, hi = HX;  // K < T ends at lo = HN: every candidate
         while (lo < hi) {
           const uint32_t mid = lo + (hi - lo + 1) / 2;
           uint32_t c = 0;
@@ -1613,8 +1613,11 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           const uint32_t pb = Ta + wave_excl_scan_u32(tb, lane);
           for (uint32_t j = 0; j < ta; ++j) sh.comp[pa + j] = cand[sh.off[a] + j];
           for (uint32_t j = 0; j < tb; ++j) sh.comp[pb + j] = cand[sh.off[b] + j];
-          for (uint32_t p = T + lane; p < 128; p += 64) sh.comp[p] = 0;
-          if (lane == 0) sh.s_count = (int)T;
+          // fewer candidates than tasks (K < T: the threshold is the lowest score and every candidate is
+          // taken) fills only K entries
+          const uint32_t Kt = K < T ? K : T;
+          for (uint32_t p = Kt + lane; p < 128; p += 64) sh.comp[p] = 0;
+          if (lane == 0) sh.s_count = (int)Kt;
         }
         __syncthreads();
         {  // rank of every taken element, 4 threads per element

@@ -200,7 +200,22 @@ def _partial_gang(cl, frac):
     return cl
 
 
+def _few_candidates():
+    """40 nodes with room for exactly one task each and a 60-task gang job: the selection sees K = 40
+    candidates, more than the all-pairs rank takes and fewer than the segment's T = 60 tasks (threshold
+    path with K < T), then the no-fit stop."""
+    rl = m.build_resource_list
+    cl = m.Cluster(nodes=[m.build_node(f"n{i:02d}", dict(rl("1", "4Gi"), pods=110)) for i in range(40)],
+                   pods=[m.build_pod("c1", f"p{i:02d}", "", "Pending", rl("600m", "1Gi"), "pg1") for i in range(60)]
+                   + [m.build_pod("c2", f"q{i:02d}", "", "Pending", rl("300m", "512Mi"), "pg2") for i in range(30)],
+                   pod_groups=[m.PodGroup(ns="c1", name="pg1", queue="q", min_member=60),
+                               m.PodGroup(ns="c2", name="pg2", queue="q", min_member=30)],
+                   queues=[m.Queue(name="q")])
+    return cl
+
+
 PIPE_CLUSTERS = CLUSTERS + [
+    ("few-candidates", _few_candidates()),
     # minMember below the job size: jobs stop READY mid-way and are pushed back (the speculated next job
     # is often the same job), and ready jobs compete with unready ones in the gang order
     ("C2-halfgang", _partial_gang(synth.c2(n_nodes=120, n_jobs=30, tasks_per_job=20, seed=31), 0.5)),
