@@ -427,8 +427,9 @@ __device__ __forceinline__ void publish_state(JobState* js, JobState* hjs, int s
   hjs->min_available = minav;
   hjs->gang_ready = gang;
   hjs->panic = panic;
-  __threadfence_system();
-  __hip_atomic_store(&hjs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // the host spins on this
+  // the host spins on seq: a system-scope release orders every earlier write of the workgroup (each wave
+  // waited for its stores before the barrier that precedes this call) ahead of it
+  __hip_atomic_store(&hjs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A launch that finds its batch already stopped still reports completion.
@@ -1909,7 +1910,6 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   __syncthreads();
   if (tid == 0) {
     if (commit_out != nullptr) js->n_commit = sh.n_commit;
-    __threadfence_system();
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
   }
@@ -2387,8 +2387,11 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   int prev_slot = -1, prev_ncommit = 0;
   int rp = 0;
 #ifdef KB_DIAG
+  // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
+  // publish (fence + host writes)
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  uint64_t t_wait0 = dg_last, pub_prev = 0;
 #endif
   for (int r = 0;; r ^= 1) {
     tgt[r] += blocks;
@@ -2428,6 +2431,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #ifdef KB_DIAG
     for (int k = 0; k < 7; ++k) dg[k] = 0;
     dg_last = __builtin_amdgcn_s_memtime();
+    dg[0] = dg_last - t_wait0;  // wait for the command (+ guard)
+    dg[6] = pub_prev;
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const kb_spec sp = P.specs[spec];
@@ -2469,18 +2474,24 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
     // every wave's host-buffer and row stores are complete before the barrier; one lane then releases at
     // system scope and publishes (the host spins on the sequence number)
+#ifdef KB_DIAG
+    const uint64_t t_pub = __builtin_amdgcn_s_memtime();
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ncommit = sh.n_commit;
     if (tid == 0) {
       js->n_commit = ncommit;
-      __threadfence_system();
       publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
     }
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
     prev_slot = slot;
     prev_ncommit = ncommit;
     __syncthreads();  // cm / sh reused by the next command
+#ifdef KB_DIAG
+    t_wait0 = __builtin_amdgcn_s_memtime();
+    pub_prev = t_wait0 - t_pub;
+#endif
   }
 }
 
