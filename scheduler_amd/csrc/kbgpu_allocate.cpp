@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -389,6 +390,7 @@ struct Driver {
   }
 
   // ---- the allocate loop (actions/allocate/allocate.go:40-176) ----
+  double loop_ms = 0;  // KB_HOST_TRACE: time in the job loop of run()
   GoHeap<int> qheap;
   std::vector<GoHeap<int>> jheaps;
   std::vector<std::vector<int>> job_pending;
@@ -569,16 +571,24 @@ struct Driver {
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
     // every job one selection run of an eligible spec: the fed engine serves the whole cycle
     bool fed = pipe;
+    std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
     for (uint32_t j = 0; fed && j < s.n_jobs; ++j) {
       int sp0 = -1;
       for (int t : job_pending[j]) {
-        if (task_res_empty(t)) continue;  // BestEffort: never placed by allocate
         const int sp = s.task_spec[t];
-        if (sp0 < 0) sp0 = sp;
-        if (sp != sp0 || !kb_spec_fed_ok(ctx, sp)) {
+        if (sp == sp0) continue;
+        if (task_res_empty(t)) continue;  // BestEffort: never placed by allocate
+        if (sp < 0) {
           fed = false;
           break;
         }
+        if ((size_t)sp >= spec_fed.size()) spec_fed.resize(sp + 1, -1);
+        if (spec_fed[sp] < 0) spec_fed[sp] = (int8_t)kb_spec_fed_ok(ctx, sp);
+        if (sp0 >= 0 || !spec_fed[sp]) {  // a second spec in the job, or an ineligible one
+          fed = false;
+          break;
+        }
+        sp0 = sp;
       }
     }
     if (fed)
@@ -597,10 +607,22 @@ struct Driver {
       const kb_job_req req = make_req(j);
       if (int rc = kb_job_issue(ctx, &req, slot, nullptr)) return rc;
     }
+    // KB_HOST_TRACE=1: per-job host timings on stderr at the end of the cycle (speculative issue, wait in
+    // finish, bookkeeping after it)
+    const bool trace = getenv("KB_HOST_TRACE") != nullptr;
+    const auto loop0 = std::chrono::steady_clock::now();
+    double t_spec = 0, t_fin = 0, t_apply = 0;
+    uint64_t n_iter = 0;
+    using clk = std::chrono::steady_clock;
+    const auto us = [](clk::time_point a, clk::time_point b) {
+      return std::chrono::duration<double, std::micro>(b - a).count();
+    };
     while (have) {
       int q2 = -1, j2 = -1;
       kb_job_pred pred{};
+      const auto c0 = clk::now();
       const bool spec = pipe && speculate(q, j, slot, q2, j2, pred);
+      const auto c1 = clk::now();
       kb_job_result res;
       int rc;
       if (pipe) {
@@ -618,6 +640,7 @@ struct Driver {
         if (rc == KB_OK) rc = rc2;
       }
       if (rc) return rc;
+      const auto c2 = clk::now();
       apply(q, j, res);
       int nq, nj;
       have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj);
@@ -638,7 +661,16 @@ struct Driver {
       }
       q = nq;
       j = nj;
+      if (trace) {
+        const auto c3 = clk::now();
+        t_spec += us(c0, c1), t_fin += us(c1, c2), t_apply += us(c2, c3);
+        ++n_iter;
+      }
     }
+    loop_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - loop0).count();
+    if (trace && n_iter)
+      fprintf(stderr, "kb_host_trace jobs=%llu speculate_issue_us=%.2f finish_wait_us=%.2f apply_next_us=%.2f\n",
+              (unsigned long long)n_iter, t_spec / n_iter, t_fin / n_iter, t_apply / n_iter);
     out->n_events = n_events;
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
     if (fed) {
@@ -663,8 +695,15 @@ extern "C" int kb_allocate(kb_ctx* ctx, const kb_session* ssn, kb_cycle_result* 
   for (uint32_t j = 0; j < ssn->n_jobs; ++j) out->job_fail_task[j] = -1;
   memset(out->job_reason_hist, 0, sizeof(uint32_t) * KB_NUM_REASONS * ssn->n_jobs);
   Driver d(ctx, *ssn, out);
+  const auto ti = std::chrono::steady_clock::now();
   int rc = d.init();
+  const auto tr = std::chrono::steady_clock::now();
   if (rc == KB_OK) rc = d.run();
+  if (getenv("KB_HOST_TRACE"))
+    fprintf(stderr, "kb_host_trace fill_ms=%.3f init_ms=%.3f run_ms=%.3f loop_ms=%.3f\n",
+            std::chrono::duration<double, std::milli>(ti - t0).count(),
+            std::chrono::duration<double, std::milli>(tr - ti).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count(), d.loop_ms);
   out->elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   out->device_ms = ctx->device_ms - dev0;
   return rc;

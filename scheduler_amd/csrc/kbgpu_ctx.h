@@ -96,6 +96,7 @@ struct kb_ctx {
   // fed engine (kb_fed_begin / kb_fed_end): one resident selection workgroup per allocate cycle, fed by the
   // sweep kernels through a two-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
   bool fed = false;
+  bool use_fed = true;  // KB_NO_FED unset
   void* fed_ring = nullptr;
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;

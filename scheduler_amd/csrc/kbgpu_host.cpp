@@ -130,6 +130,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
   c->use_aff_reg = getenv("KB_NO_AFF_REG") == nullptr;  // testing: force the global-memory affinity loop
+  c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
@@ -1075,7 +1076,7 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (c->sharded || c->use_engine || !c->use_sel || !c->sel_ok || !c->traj || !c->spec_traj_ok[spec]) return 0;
   if (!fed_fits(c->N.n)) return 0;
   if (c->aff_ok && c->spec_needs_aff[spec]) return 0;
-  return getenv("KB_NO_FED") == nullptr;
+  return c->use_fed ? 1 : 0;
 }
 
 constexpr uint64_t kFedIdleTicks = 100000000ull;  // 1 s of s_memrealtime without a command: the engine exits
