@@ -2077,6 +2077,40 @@ class Session {
     }
     elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+
+  // ---- backfillAction.Execute (actions/backfill/backfill.go:40-90) ----
+  // Jobs and their Pending tasks in UID order (the maps of :45 and :54), nodes in the canonical order (:62):
+  // a task with an empty InitResreq takes the first node that passes Session.PredicateFn and is allocated
+  // there (:71); a task that passes nowhere records its FitErrors histogram (:84-86). Other tasks are left
+  // alone (:87-89).
+  std::map<std::string, std::map<std::string, FitErrs>> backfill_fit_errors;
+  void backfill() {
+    for (auto& jkv : jobs) {
+      Job& job = jkv.second;
+      if (job.pg_phase == "Pending") continue;
+      if (!job_valid(&job)) continue;
+      auto pit = job.tsi.find(Pending);
+      if (pit == job.tsi.end()) continue;
+      std::vector<Task*> ts;  // allocate_task moves tasks out of the Pending index while we walk it
+      for (auto& kv : pit->second) ts.push_back(kv.second);
+      for (Task* task : ts) {
+        if (!task->initreq.is_empty()) continue;
+        FitErrs fe;
+        bool allocated = false;
+        for (size_t ni = 0; ni < nodes.size(); ++ni) {
+          PredResult p = predicate_enabled() ? predicates_fn(task, (int)ni) : PredResult();
+          if (!p.ok) {
+            for (auto& r : p.reasons) fe.hist[r]++;
+            continue;
+          }
+          allocate_task(task, (int)ni);
+          allocated = true;
+          break;
+        }
+        if (!allocated) backfill_fit_errors[job.uid][task->uid] = fe;
+      }
+    }
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -2135,6 +2169,8 @@ static Value run_allocate(const Value& in) {
   s.opt = parse_opts(in);
   s.load(in);
   s.allocate();
+  const bool backfill = in.str_at("op") == "allocate_backfill";  // the default action list (util.go:32)
+  if (backfill) s.backfill();
   Value out = vobj();
   Value ev = varr();
   for (auto& e : s.events) {
@@ -2160,6 +2196,19 @@ static Value run_allocate(const Value& in) {
     fe.o.emplace_back(jkv.first, j);
   }
   out.o.emplace_back("fit_errors", fe);
+  if (backfill) {
+    Value bfe = vobj();
+    for (auto& jkv : s.backfill_fit_errors) {
+      Value j = vobj();
+      for (auto& tkv : jkv.second) {
+        Value h = vobj();
+        for (auto& r : tkv.second.hist) h.o.emplace_back(r.first, vint(r.second));
+        j.o.emplace_back(tkv.first, h);
+      }
+      bfe.o.emplace_back(jkv.first, j);
+    }
+    out.o.emplace_back("backfill_fit_errors", bfe);
+  }
   Value st = vobj();
   for (auto& t : s.tasks) st.o.emplace_back(t.uid, vstr(status_name(t.status)));
   out.o.emplace_back("status", st);
@@ -2309,7 +2358,7 @@ char* oracle_call(const char* json_in) {
     oj::Value in = oj::parse(json_in);
     std::string op = in.str_at("op");
     oj::Value res;
-    if (op == "allocate") res = oracle::run_allocate(in);
+    if (op == "allocate" || op == "allocate_backfill") res = oracle::run_allocate(in);
     else if (op == "eval") res = oracle::run_eval(in);
     else res = oracle::run_resource_op(in);
     oracle::write(out, res);

@@ -63,6 +63,14 @@ def allocate(cluster, workers: int = 1, literal_affinity: bool = False, max_task
     return call(req)
 
 
+def allocate_backfill(cluster, literal_affinity: bool = False) -> dict:
+    """allocate then backfill (the default action list, util.go:32; actions/backfill/backfill.go:40-90)."""
+    req = dict(cluster.to_json())
+    req["op"] = "allocate_backfill"
+    req["options"] = {"workers": 1, "literal_affinity": literal_affinity, "max_tasks": -1}
+    return call(req)
+
+
 def evaluate(cluster, task_uids, literal_affinity: bool = False) -> dict:
     """Per-(task, node) predicate reasons and total score at session-open state."""
     req = dict(cluster.to_json())

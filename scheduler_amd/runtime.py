@@ -320,6 +320,61 @@ class Context:
         out["device_ms"] = res.device_ms
         return out
 
+    def backfill(self, snap: E.Snapshot, out: dict) -> dict:
+        """backfillAction.Execute (actions/backfill/backfill.go:40-90) on the session kb_allocate left in `out`.
+
+        Jobs and their Pending tasks go in UID order (the maps of backfill.go:45, :54). A task whose InitResreq
+        is empty takes the first node, in the canonical node order, that passes Session.PredicateFn (:62-71):
+        on the device that is kb_place_job of a one-task job with the node order switched off, since every
+        score is then equal and the selection keeps the lowest feasible index. Commits are Session.Allocate
+        (the empty request always fits Idle), followed by the JobReady dispatch (session.go:286-294). A task
+        that fits nowhere records the device's FitErrors histogram (:84-86). Updates `out` in place and
+        returns it with "backfill_fit" = {job index: {task index: reason histogram}}."""
+        cfg = dict(snap.config)
+        tiers = [(int(p), int(en)) for _, p, en in snap.tier_plugins]
+        has_gang = any(p == E.PLUGIN_IDS["gang"] for p, _ in tiers)
+        gang_ready = any(p == E.PLUGIN_IDS["gang"] and en >> E.EN_BITS["enabledJobReady"] & 1 for p, en in tiers)
+        st, node = out["task_status"], out["task_node"]
+        ts = snap.session_tasks
+        by_job = {}
+        for t in np.argsort(snap.s_task_uid_rank, kind="stable"):
+            by_job.setdefault(int(snap.s_task_job[t]), []).append(int(t))
+        alloc_st = E.ST["Bound"] | E.ST["Binding"] | E.ST["Running"] | E.ST["Allocated"]
+        valid_st = alloc_st | E.ST["Succeeded"] | E.ST["Pipelined"] | E.ST["Pending"]
+        fit = {}
+        n_ev = int(out["n_events"])
+        self._check(self.lib.kb_set_config(self.ctx, C.byref(kb_config(**dict(cfg, nodeorder_enabled=0)))))
+        try:
+            for j in np.argsort(snap.s_job_uid_rank, kind="stable"):
+                j = int(j)
+                if snap.s_job_pg_pending[j]:
+                    continue
+                tasks = by_job.get(j, [])
+                if has_gang and sum(1 for t in tasks if st[t] & valid_st) < snap.s_job_min[j]:
+                    continue  # JobValid (gang.go:48-69)
+                for t in [t for t in tasks if st[t] == E.ST["Pending"]]:
+                    r = ts[t]["initreq"]
+                    if not (r.cpu < 10 and r.mem < 10 * 1024 * 1024 and all(q < 10 for q in (r.sc or {}).values())):
+                        continue  # Resource.IsEmpty (resource_info.go:96-108)
+                    spec = int(snap.s_task_spec[t])
+                    placed, kinds, res = self.place_job([spec], 0, 0, 0)
+                    if len(placed) == 0:
+                        fit.setdefault(j, {})[t] = np.array(res.reason_hist, np.uint32)
+                        continue
+                    st[t], node[t] = E.ST["Allocated"], int(placed[0])
+                    out["event_task"][n_ev] = t
+                    n_ev += 1
+                    ready = sum(1 for u in tasks if st[u] & (alloc_st | E.ST["Succeeded"]))
+                    if not gang_ready or ready >= snap.s_job_min[j]:
+                        for u in tasks:
+                            if st[u] == E.ST["Allocated"]:
+                                st[u] = E.ST["Binding"]
+        finally:
+            self._check(self.lib.kb_set_config(self.ctx, C.byref(kb_config(**cfg))))
+        out["n_events"] = n_ev
+        out["backfill_fit"] = fit
+        return out
+
 
 def comm_unique_id() -> bytes:
     """RCCL unique id for kb_set_shard_rccl (made on one rank, broadcast to the others)."""
@@ -366,5 +421,23 @@ def allocate(cluster, device: int = 0, path: str = "select") -> dict:
         ctx.upload(snap)
         out = ctx.allocate(snap)
         return result_dict(snap, out)
+    finally:
+        ctx.close()
+
+
+def allocate_backfill(cluster, device: int = 0, path: str = "select") -> dict:
+    """The default action list, allocate then backfill (util.go:32), on the GPU. Returns what allocate() does
+    plus "backfill_fit_errors" in the oracle's format."""
+    snap = E.Snapshot(cluster)
+    ctx = Context(device, path=path)
+    try:
+        ctx.upload(snap)
+        out = ctx.backfill(snap, ctx.allocate(snap))
+        d = result_dict(snap, out)
+        ts = snap.session_tasks
+        d["backfill_fit_errors"] = {
+            snap.jobs[j]["uid"]: {ts[t]["uid"]: {E.REASONS[b]: int(c) for b, c in enumerate(h) if c}
+                                  for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
+        return d
     finally:
         ctx.close()

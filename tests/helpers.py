@@ -100,6 +100,27 @@ def edge_cluster(seed=7):
     return cl
 
 
+def backfill_cluster(seed=7, n_be=160):
+    """edge_cluster plus jobs of BestEffort pods (empty InitResreq) for backfill (backfill.go:54-86): plain,
+    with a node selector, with a host port (one per node), tolerating the dedicated taint, and one gang job
+    that stays invalid. Enough of them to run nodes out of pod slots, so later tasks fit nowhere."""
+    cl = edge_cluster(seed)
+    kinds = [dict(), dict(sel={"ssd": "true"}), dict(ports=[{"hostPort": 9090}]),
+             dict(tol=[{"key": "dedicated", "operator": "Exists"}])]
+    for j, sp in enumerate(kinds):
+        cl.pod_groups.append(m.PodGroup(ns="b", name=f"be{j}", queue="q1", min_member=1))
+        for t in range(n_be // len(kinds)):
+            c = m.Container(req={}, ports=[dict(x) for x in sp.get("ports", [])])
+            cl.pods.append(m.Pod(ns="b", name=f"be{j}-{t:03d}", uid=f"b-be{j}-{t:03d}", group=f"be{j}",
+                                 containers=[c], node_selector=dict(sp.get("sel", {})),
+                                 tolerations=list(sp.get("tol", []))))
+    cl.pod_groups.append(m.PodGroup(ns="b", name="be-gang", queue="q1", min_member=5))  # JobValid fails
+    for t in range(3):
+        cl.pods.append(m.Pod(ns="b", name=f"beg-{t}", uid=f"b-beg-{t}", group="be-gang",
+                             containers=[m.Container(req={})]))
+    return cl
+
+
 def affinity_edge_cluster(seed=11, n_nodes=40):
     """Inter-pod (anti)affinity edge cases: nodes missing topology labels, two namespaces, existing pods
     with required/preferred anti terms (NotIn / Exists / DoesNotExist selectors, explicit namespaces),
