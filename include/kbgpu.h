@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 7
+#define KBGPU_ABI_VERSION 8
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -70,7 +70,12 @@ extern "C" {
 #define KB_R_EXISTING_ANTI 13      /* "node(s) didn't satisfy existing pods anti-affinity rules" */
 #define KB_R_AFFINITY_RULES 14     /* "node(s) didn't match pod affinity rules" */
 #define KB_R_ANTI_AFFINITY_RULES 15/* "node(s) didn't match pod anti-affinity rules" */
-#define KB_NUM_REASONS 16
+#define KB_R_HOST_ERROR 16         /* a host-evaluated stage failed: a kb_set_host_overlay plugin predicate, or a
+                                      predicate the reference fails with a plain error string (inter-pod affinity
+                                      with an invalid selector or an empty topologyKey: vendor/.../predicates.go:
+                                      1293-1333, 1189-1214, 1401-1413). The strings are the caller's: the per-node
+                                      reason masks of the failing task come through kb_set_nofit_hook / kb_eval. */
+#define KB_NUM_REASONS 17
 
 /* ---- node flags (kb_nodes.flags) ---- */
 #define KB_NODE_IDLE_HAS_MAP (1u << 0) /* Idle.ScalarResources != nil (allocatable lists a scalar) */
@@ -148,6 +153,10 @@ typedef struct kb_term {
 #define KB_SPEC_HAS_REQUIRED (1u << 4)  /* nodeAffinity.RequiredDuringScheduling != nil */
 #define KB_SPEC_NA_ERROR (1u << 5)      /* a preferred term is invalid: map fn errors (node_affinity.go:59-62) */
 #define KB_SPEC_POD_AFFINITY (1u << 6)  /* pod (anti)affinity terms: needs the affinity tables */
+#define KB_SPEC_IPA_ERROR (1u << 7)     /* CalculateInterPodAffinityPriority errors for this pod (an invalid label
+                                           selector among the terms it meets, interpod_affinity.go:86-93): the batch
+                                           score fails, PrioritizeNodes returns no scores and SelectBestNode panics
+                                           (scheduler_helper.go:101-105,147-158) -> KB_E_PANIC once a node fits */
 
 /*
  * Task spec: everything the device needs about a pending pod. Pods of one
@@ -240,6 +249,9 @@ int kb_upload_specs(kb_ctx* ctx, const kb_specs* specs);
 #define KB_AFF_EXISTING_ANTI 0 /* fail if count > 0: "didn't satisfy existing pods anti-affinity rules" */
 #define KB_AFF_ANTI 1          /* fail if count > 0: "didn't match pod anti-affinity rules" */
 #define KB_AFF_AFFINITY 2      /* fail if count == 0 and (total > 0 or !self_match): "...affinity rules" */
+#define KB_AFF_ERROR 3         /* fail with KB_R_HOST_ERROR if count > 0: the reference returns a plain error (lister
+                                  pods carrying an invalid required anti-affinity selector; the pod's own required
+                                  affinity with an invalid selector or an empty topologyKey met by a lister pod) */
 #define KB_AFF_SELF_DYNAMIC (1u << 0) /* the spec's own commits change its checks or histograms */
 
 typedef struct kb_aff_table {
@@ -379,6 +391,59 @@ int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 /* Read back the mutable node columns (for tests and for the Go side's NodeInfo replay). */
 int kb_read_nodes(kb_ctx* ctx, int64_t* idle_cpu, int64_t* idle_mem, int64_t* rel_cpu, int64_t* rel_mem,
                   int32_t* pod_count, int64_t* nz_cpu, int64_t* nz_mem);
+
+/*
+ * ---- per-node Go fallback ----
+ * Session.PredicateFn ANDs every enabled plugin's predicate per node and Session.NodeOrderMapFn sums
+ * every plugin's node-order score (framework/session_plugins.go:372-389, 443-469). A plugin the device
+ * does not express is evaluated by the caller with the existing Go functions, per node, and handed over
+ * here for one spec: fail[i] != 0 rejects node i with KB_R_HOST_ERROR, score_add[i] is added to the
+ * node's order score. The stage sits after the device's predicate chain (a plugin later in tier order)
+ * and its score is dropped with the rest of the order score where nodeorder's map fn errors
+ * (scheduler_helper.go:74-78). Scores must be integral (every in-tree node-order fn is) and
+ * |NodeAffinity * weight + score_add| < 2^26. Either array may be NULL; both NULL clears the overlay.
+ * The overlay stays until replaced: a plugin whose answer depends on this cycle's commits is re-set by
+ * the caller between kb_place_job calls (device layer). n = this context's node rows.
+ */
+int kb_set_host_overlay(kb_ctx* ctx, int32_t spec, const uint8_t* fail, const int64_t* score_add);
+
+/*
+ * Rows changed by commits made outside the device (Go-side backfill, preempt/reclaim evictions, a
+ * plugin's own bookkeeping): NodeInfo.AddTask / RemoveTask (api/node_info.go:165-221) plus the
+ * schedulercache AddPod / RemovePod the plugins' event handlers apply (cache/node_info.go:498-630).
+ * Quantities are deltas (Idle -= Resreq is a negative idle delta). sc (n_scalar idle deltas followed by
+ * n_scalar releasing deltas per row that uses it) and ports ((slot, ip) pairs the pod takes when
+ * pods > 0, frees when pods < 0) are indexed by sc_off / port_off. spec >= 0 also applies that spec's
+ * inter-pod affinity table updates (kind KB_PLACE_ALLOCATE joins the lister, as Session.Allocate does;
+ * KB_PLACE_PIPELINE counts for the score only; pods < 0 takes them back). Deltas for the same node are
+ * summed (order-free) except flags, where every set is applied before every clear. Node indices are
+ * canonical; on a node-sharded context rows outside the rank are skipped.
+ */
+typedef struct kb_row_delta {
+  int32_t node;
+  int32_t pods;                /* pod_count delta */
+  int64_t idle_cpu, idle_mem, rel_cpu, rel_mem;
+  int64_t nz_cpu, nz_mem;      /* schedulercache nonzeroRequest delta */
+  uint32_t flags_set, flags_clear; /* KB_NODE_* (e.g. KB_NODE_REL_HAS_MAP when Releasing gains a scalar map) */
+  int32_t spec;                /* -1: no inter-pod affinity updates */
+  int32_t kind;                /* KB_PLACE_* (with spec) */
+  uint32_t sc_off;             /* UINT32_MAX: no scalar deltas */
+  uint32_t port_off, port_cnt;
+  int32_t pad;
+} kb_row_delta;
+int kb_apply(kb_ctx* ctx, const kb_row_delta* deltas, uint32_t k, const int64_t* sc, uint32_t n_sc,
+             const kb_port* ports, uint32_t n_ports);
+
+/*
+ * Called by kb_allocate when a task of a spec with host-evaluated stages (an overlay, or KB_AFF_ERROR
+ * checks) fits no node: node_reasons[i] is node i's reason mask at the failing task's state (what
+ * kb_eval returns there), so the caller can replace the KB_R_HOST_ERROR bucket of the job's histogram
+ * with its own per-node strings (FitErrors.SetNodeError, api/unschedule_info.go:40-54). n_events = the
+ * cycle's placements made before the failure (kb_cycle_result.event_task order).
+ */
+typedef void (*kb_nofit_fn)(void* user, int32_t job, int32_t task, uint32_t n_events, const uint32_t* node_reasons,
+                            uint32_t n);
+int kb_set_nofit_hook(kb_ctx* ctx, kb_nofit_fn fn, void* user);
 
 /*
  * ---- node sharding across GPUs ----

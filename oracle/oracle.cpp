@@ -62,9 +62,9 @@ static bool match_qualified_name_fmt(const std::string& s) {
     if (!(is_alnum(c) || c == '-' || c == '_' || c == '.')) return false;
   return true;
 }
-// dns1123SubdomainFmt (validation.go:108-131)
-static bool is_dns1123_subdomain(const std::string& s) {
-  if (s.size() > 253 || s.empty()) return false;
+// dns1123SubdomainFmt (validation.go:108-131), the regex alone (the length rule is separate)
+static bool match_dns1123_subdomain(const std::string& s) {
+  if (s.empty()) return false;
   size_t start = 0;
   while (true) {
     size_t dot = s.find('.', start);
@@ -79,9 +79,19 @@ static bool is_dns1123_subdomain(const std::string& s) {
   }
   return true;
 }
-// IsQualifiedName (validation.go:42-72)
-static bool is_qualified_name(const std::string& v) {
-  std::vector<std::string> parts;
+// RegexError (validation.go:347-362), double spaces included
+static std::string regex_error(const std::string& msg, const std::string& fmt, std::vector<std::string> ex) {
+  if (ex.empty()) return msg + " (regex used for validation is '" + fmt + "')";
+  std::string m = msg + " (e.g. ";
+  for (size_t i = 0; i < ex.size(); ++i) m += (i ? " or " : "") + std::string("'") + ex[i] + "', ";
+  return m + "regex used for validation is '" + fmt + "')";
+}
+static const char* kQNameFmt = "([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]";
+static const char* kQNameMsg =
+    "must consist of alphanumeric characters, '-', '_' or '.', and must start and end with an alphanumeric character";
+// IsQualifiedName (validation.go:42-71): the error list
+static std::vector<std::string> qualified_name_errs(const std::string& v) {
+  std::vector<std::string> parts, errs;
   size_t st = 0;
   while (true) {
     size_t sl = v.find('/', st);
@@ -90,20 +100,57 @@ static bool is_qualified_name(const std::string& v) {
     st = sl + 1;
   }
   std::string name;
-  bool ok = true;
-  if (parts.size() == 1) name = parts[0];
-  else if (parts.size() == 2) {
-    if (parts[0].empty() || !is_dns1123_subdomain(parts[0])) ok = false;
+  if (parts.size() == 1) {
+    name = parts[0];
+  } else if (parts.size() == 2) {
     name = parts[1];
-  } else return false;
-  if (name.empty() || name.size() > 63) ok = false;
-  if (!match_qualified_name_fmt(name)) ok = false;
-  return ok;
+    if (parts[0].empty()) {
+      errs.push_back("prefix part must be non-empty");
+    } else {  // IsDNS1123Subdomain (:135-144), messages prefixed
+      if (parts[0].size() > 253) errs.push_back("prefix part must be no more than 253 characters");
+      if (!match_dns1123_subdomain(parts[0]))
+        errs.push_back("prefix part " + regex_error("a DNS-1123 subdomain must consist of lower case alphanumeric "
+                                                    "characters, '-' or '.', and must start and end with an "
+                                                    "alphanumeric character",
+                                                    "[a-z0-9]([-a-z0-9]*[a-z0-9])?(\\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*",
+                                                    {"example.com"}));
+    }
+  } else {
+    errs.push_back("a qualified name " + regex_error(kQNameMsg, kQNameFmt, {"MyName", "my.name", "123-abc"}) +
+                   " with an optional DNS subdomain prefix and '/' (e.g. 'example.com/MyName')");
+    return errs;
+  }
+  if (name.empty()) errs.push_back("name part must be non-empty");
+  else if (name.size() > 63) errs.push_back("name part must be no more than 63 characters");
+  if (!match_qualified_name_fmt(name))
+    errs.push_back("name part " + regex_error(kQNameMsg, kQNameFmt, {"MyName", "my.name", "123-abc"}));
+  return errs;
 }
+static bool is_qualified_name(const std::string& v) { return qualified_name_errs(v).empty(); }
 // IsValidLabelValue (validation.go:97-106)
-static bool is_valid_label_value(const std::string& v) {
-  if (v.size() > 63) return false;
-  return v.empty() || match_qualified_name_fmt(v);
+static std::vector<std::string> label_value_errs(const std::string& v) {
+  std::vector<std::string> errs;
+  if (v.size() > 63) errs.push_back("must be no more than 63 characters");
+  if (!(v.empty() || match_qualified_name_fmt(v)))
+    errs.push_back(regex_error("a valid label must be an empty string or consist of alphanumeric characters, '-', "
+                               "'_' or '.', and must start and end with an alphanumeric character",
+                               std::string("(") + kQNameFmt + ")?", {"MyValue", "my_value", "12345"}));
+  return errs;
+}
+static bool is_valid_label_value(const std::string& v) { return label_value_errs(v).empty(); }
+static std::string join(const std::vector<std::string>& v, const char* sep) {
+  std::string o;
+  for (size_t i = 0; i < v.size(); ++i) o += (i ? sep : "") + v[i];
+  return o;
+}
+// fmt %q of a printable ASCII string (strconv.Quote)
+static std::string go_quote(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    o += c;
+  }
+  return o + "\"";
 }
 
 // IsScalarResourceName and friends (vendor/k8s.io/kubernetes/pkg/apis/core/v1/helper/helpers.go:36-104)
@@ -356,28 +403,38 @@ struct Requirement {
   }
 };
 
-// NewRequirement (selector.go:133-170); returns false on validation error.
-static bool new_requirement(const std::string& key, Op op, const std::vector<std::string>& vals, Requirement* out) {
-  if (!is_qualified_name(key)) return false;
+// NewRequirement (selector.go:133-170); returns false on validation error (its text in *err).
+static bool new_requirement(const std::string& key, Op op, const std::vector<std::string>& vals, Requirement* out,
+                            std::string* err = nullptr) {
+  auto bad = [&](const std::string& m) {
+    if (err) *err = m;
+    return false;
+  };
+  {  // validateLabelKey (:833-838)
+    auto e = qualified_name_errs(key);
+    if (!e.empty()) return bad("invalid label key " + go_quote(key) + ": " + join(e, "; "));
+  }
   switch (op) {
     case OP_IN: case OP_NOTIN:
-      if (vals.empty()) return false;
+      if (vals.empty()) return bad("for 'in', 'notin' operators, values set can't be empty");
       break;
     case OP_EQ: case OP_NEQ:
-      if (vals.size() != 1) return false;
+      if (vals.size() != 1) return bad("exact-match compatibility requires one single value");
       break;
     case OP_EXISTS: case OP_DNE:
-      if (!vals.empty()) return false;
+      if (!vals.empty()) return bad("values set must be empty for exists and does not exist");
       break;
     case OP_GT: case OP_LT: {
-      if (vals.size() != 1) return false;
+      if (vals.size() != 1) return bad("for 'Gt', 'Lt' operators, exactly one value is required");
       int64_t tmp;
-      if (!Requirement::parse_int64(vals[0], &tmp)) return false;
+      if (!Requirement::parse_int64(vals[0], &tmp)) return bad("for 'Gt', 'Lt' operators, the value must be an integer");
       break;
     }
   }
-  for (auto& v : vals)
-    if (!is_valid_label_value(v)) return false;
+  for (auto& v : vals) {  // validateLabelValue (:840-845)
+    auto e = label_value_errs(v);
+    if (!e.empty()) return bad("invalid label value: " + go_quote(v) + ": " + join(e, "; "));
+  }
   out->key = key;
   out->op = op;
   out->vals = vals;
@@ -490,14 +547,15 @@ struct LabelSelector {  // *metav1.LabelSelector
   std::vector<SelReq> exprs;
 };
 
-// LabelSelectorAsSelector (vendor/k8s.io/apimachinery/pkg/apis/meta/v1/helpers.go:31-67)
-static bool label_selector_as_selector(const LabelSelector& ps, Selector* out) {
+// LabelSelectorAsSelector (vendor/k8s.io/apimachinery/pkg/apis/meta/v1/helpers.go:31-67). matchLabels go in
+// key order (a Go map: the order, and so which of several invalid pairs is reported, is random there).
+static bool label_selector_as_selector(const LabelSelector& ps, Selector* out, std::string* err = nullptr) {
   if (!ps.present) { *out = Selector::nothing(); return true; }
   if (ps.match_labels.size() + ps.exprs.size() == 0) { *out = Selector::everything(); return true; }
   Selector s;
   for (auto& kv : ps.match_labels) {
     Requirement r;
-    if (!new_requirement(kv.first, OP_EQ, {kv.second}, &r)) return false;
+    if (!new_requirement(kv.first, OP_EQ, {kv.second}, &r, err)) return false;
     s.reqs.push_back(r);
   }
   for (auto& e : ps.exprs) {
@@ -506,9 +564,12 @@ static bool label_selector_as_selector(const LabelSelector& ps, Selector* out) {
     else if (e.op == "NotIn") op = OP_NOTIN;
     else if (e.op == "Exists") op = OP_EXISTS;
     else if (e.op == "DoesNotExist") op = OP_DNE;
-    else return false;
+    else {
+      if (err) *err = go_quote(e.op) + " is not a valid pod selector operator";
+      return false;
+    }
     Requirement r;
-    if (!new_requirement(e.key, op, e.values, &r)) return false;
+    if (!new_requirement(e.key, op, e.values, &r, err)) return false;
     s.reqs.push_back(r);
   }
   *out = s;
@@ -1537,14 +1598,20 @@ class Session {
     std::vector<const Task*> filtered = lister_list(task, ni);
     // satisfiesExistingPodsAntiAffinity (:1293-1333) via getMatchingAntiAffinityTopologyPairsOfPods (:1247-1291)
     std::set<std::pair<std::string, std::string>> pairs;
+    // errors come back as FitErrors.SetNodeError(err): the error's own string, no reason constants
+    const std::string pn = pod.ns + "/" + pod.name;  // podName (vendor/.../predicates.go:721-723)
     for (const Task* et : filtered) {
       int en = node_of(et->node_name);
-      if (en < 0) return PredResult::fail({std::string("failed to find node <") + et->node_name + ">"});
+      if (en < 0)
+        return PredResult::fail({"Failed to get all terms that pod " + pn + " matches, err: failed to find node <" +
+                                 et->node_name + ">"});
       const Pod& ep = *et->pod;
       if (!ep.has_affinity || !ep.aff.has_anti) continue;
       for (auto& term : ep.aff.anti.required) {
         Selector sel;
-        if (!label_selector_as_selector(term.sel, &sel)) return PredResult::fail({"invalid label selector"});
+        std::string err;
+        if (!label_selector_as_selector(term.sel, &sel, &err))
+          return PredResult::fail({"Failed to get all terms that pod " + pn + " matches, err: " + err});
         if (pod_matches_ns_sel(pod, term_namespaces(ep, term), sel)) {
           auto it = nodes[en].node->labels.find(term.topology_key);
           if (it != nodes[en].node->labels.end()) pairs.insert({term.topology_key, it->second});
@@ -1563,7 +1630,8 @@ class Session {
         bool all, props;
         std::string err;
         if (!pod_matches_terms(pod, tt, ni, aff_terms, &all, &props, &err))
-          return PredResult::fail({"Cannot schedule pod onto node " + node->name + ", because of PodAffinity, err: " + err});
+          return PredResult::fail({"Cannot schedule pod " + pn + " onto node " + node->name +
+                                   ", because of PodAffinity, err: " + err});
         if (props) sel_found = true;
         if (all) match_found = true;
       }
@@ -1588,11 +1656,12 @@ class Session {
   bool pod_matches_terms(const Pod& pod, const Task* target, int ni, const std::vector<PodAffinityTerm>& terms,
                          bool* all, bool* props_ok, std::string* err) const {
     *all = *props_ok = false;
-    for (auto& t : terms) {
-      Selector sel;
-      if (!label_selector_as_selector(t.sel, &sel)) { *err = "invalid label selector"; return false; }
-      if (!pod_matches_ns_sel(*target->pod, term_namespaces(pod, t), sel)) return true;
-    }
+    // getAffinityTermProperties (metadata.go:317-331) builds every term's selector first
+    std::vector<Selector> sels(terms.size());
+    for (size_t i = 0; i < terms.size(); ++i)
+      if (!label_selector_as_selector(terms[i].sel, &sels[i], err)) return false;
+    for (size_t i = 0; i < terms.size(); ++i)  // podMatchesAllAffinityTermProperties (:334-345)
+      if (!pod_matches_ns_sel(*target->pod, term_namespaces(pod, terms[i]), sels[i])) return true;
     int tn = node_of(target->node_name);
     if (tn < 0) { *err = "failed to find node <" + target->node_name + ">"; return false; }
     for (auto& t : terms) {
@@ -2334,6 +2403,37 @@ static Value run_resource_op(const Value& in) {
     Value keys = varr();
     for (auto& k : ni.task_keys) keys.a.push_back(vstr(k));
     out.o.emplace_back("tasks", keys);
+  } else if (op == "JobTasks") {
+    // NewJobInfo + AddTaskInfo / DeleteTaskInfo (api/job_info.go:160-179, 239-283): Allocated,
+    // TotalRequest and the TaskStatusIndex
+    Job job;
+    std::deque<Pod> ps;
+    std::deque<Task> tk;
+    auto mk = [&](const Value& pv) {
+      ps.push_back(parse_pod(pv));
+      tk.emplace_back();
+      Task& t = tk.back();
+      t.pod = &ps.back();
+      t.uid = ps.back().uid;
+      t.status = get_task_status(ps.back());
+      t.resreq = pod_resreq(ps.back());
+      t.initreq = pod_initreq(ps.back());
+      return &t;
+    };
+    for (auto& pv : in.arr_at("pods")) job.add_task_info(mk(pv));
+    for (auto& pv : in.arr_at("remove")) job.delete_task_info(mk(pv));
+    out.o.emplace_back("allocated", job.allocated.to_json());
+    out.o.emplace_back("total_request", job.total_request.to_json());
+    Value idx = vobj();
+    for (auto& kv : job.tsi) {
+      Value u = varr();
+      for (auto& tkv : kv.second) u.a.push_back(vstr(tkv.first));
+      idx.o.emplace_back(status_name(kv.first), u);
+    }
+    out.o.emplace_back("status_index", idx);
+    Value all = varr();
+    for (auto& kv : job.tasks) all.a.push_back(vstr(kv.first));
+    out.o.emplace_back("tasks", all);
   } else if (op == "IsScalarResourceName") {
     out.o.emplace_back("result", vbool(is_scalar_resource_name(in.str_at("name"))));
   } else if (op == "SelectorMatches") {

@@ -27,9 +27,20 @@ Commits update the tables: an Allocate adds the task to the lister (PodLister.Up
 util.go:108-130; Pipelined tasks are not listed), every commit adds the pod to its node for the score
 (nodeorder.go:161-172). Those updates are precomputed per spec as increment lists.
 
-Inputs the device path does not express raise `export.Unsupported` (invalid selectors, required terms
-with an empty topologyKey, lister pods on nodes outside the session): the reference returns an error for
-those per node; here the snapshot is refused, there is no fallback.
+Where the reference's predicate returns a plain error instead of a failure reason, the node fails with
+that error's string (FitErrors.SetNodeError, api/unschedule_info.go:40-54). Those cases are tables too,
+checked with KB_AFF_ERROR (the device reports KB_R_HOST_ERROR; `host_error_string` below gives the string):
+    XB            - lister pods carrying a required anti-affinity term with an invalid selector
+                    (satisfiesExistingPodsAntiAffinity errors for every node, predicates.go:1302-1313);
+    ALL           - every lister pod: a pod whose own required affinity has an invalid selector errors as
+                    soon as the lister has a pod (podMatchesPodAffinityTerms, :1189-1214, 1401-1413), and
+                    its invalid required anti-affinity fails every node (:1431-1440);
+    C / B prefix  - a required term with an empty topologyKey errors (affinity) or fails (anti-affinity)
+                    where every earlier term's topology is shared (:1205-1212): the table's slot is the key
+                    tuple before the first empty key.
+An invalid selector among the terms CalculateInterPodAffinityPriority meets makes the batch score error,
+and SelectBestNode then panics (KB_SPEC_IPA_ERROR). Still refused (export.Unsupported): lister pods on
+nodes outside the session, and a pending pod with invalid score terms whose own evaluation may not error.
 """
 from __future__ import annotations
 
@@ -38,7 +49,7 @@ from collections import defaultdict
 import numpy as np
 
 # kbgpu.h
-AFF_EXISTING_ANTI, AFF_ANTI, AFF_AFFINITY = 0, 1, 2
+AFF_EXISTING_ANTI, AFF_ANTI, AFF_AFFINITY, AFF_ERROR = 0, 1, 2, 3
 AFF_SELF_DYNAMIC = 1 << 0
 
 AFF_TABLE_DTYPE = np.dtype([("slot", "<i4"), ("cnt_off", "<u4")], align=True)
@@ -57,10 +68,18 @@ NOTHING = None          # nil selector: matches nothing
 EVERYTHING = ()         # empty selector: matches everything
 
 
-def label_selector(sel, unsupported):
-    """Canonical requirement tuple; `unsupported` is raised for selectors the reference rejects
-    (LabelSelectorAsSelector returns an error: the predicate fails with an error string per node)."""
-    from .export import is_qualified_name, is_valid_label_value
+class Invalid(str):
+    """LabelSelectorAsSelector's error (the text the reference puts into its error strings)."""
+
+
+EMPTY_TOPOLOGY_KEY = "empty topologyKey is not allowed except for PreferredDuringScheduling pod anti-affinity"
+_SEL_OPS = {"In": "in", "NotIn": "notin", "Exists": "exists", "DoesNotExist": "!"}
+
+
+def label_selector(sel, unsupported=None):
+    """Canonical requirement tuple, or Invalid(error text) for a selector the reference rejects.
+    matchLabels go in key order (a Go map: random there when several pairs are invalid)."""
+    from .export import go_quote, new_requirement_error
     if sel is None:
         return NOTHING
     ml = sel.get("matchLabels") or {}
@@ -68,24 +87,24 @@ def label_selector(sel, unsupported):
     if not ml and not ex:
         return EVERYTHING
     reqs = []
-    for k, v in ml.items():
-        if not is_qualified_name(k) or not is_valid_label_value(v):
-            raise unsupported(f"invalid label selector {k}={v}")
-        reqs.append((k, "In", (v,)))
+    for k in sorted(ml):
+        err = new_requirement_error(k, "=", [ml[k]])
+        if err:
+            return Invalid(err)
+        reqs.append((k, "In", (ml[k],)))
     for e in ex:
         op, k, vs = e.get("operator"), e.get("key", ""), tuple(e.get("values") or [])
-        if op not in ("In", "NotIn", "Exists", "DoesNotExist") or not is_qualified_name(k):
-            raise unsupported(f"invalid label selector expression {e}")
-        if op in ("In", "NotIn") and not vs or op in ("Exists", "DoesNotExist") and vs:
-            raise unsupported(f"invalid label selector expression {e}")
-        if not all(is_valid_label_value(v) for v in vs):
-            raise unsupported(f"invalid label selector value in {e}")
+        if op not in _SEL_OPS:
+            return Invalid(f"{go_quote(str(op))} is not a valid pod selector operator")
+        err = new_requirement_error(k, _SEL_OPS[op], vs)
+        if err:
+            return Invalid(err)
         reqs.append((k, op, tuple(sorted(set(vs)))))
     return tuple(sorted(reqs))
 
 
 def selector_matches(reqs, labels) -> bool:  # labels.internalSelector.Matches (selector.go:185-236)
-    if reqs is NOTHING:
+    if reqs is NOTHING or isinstance(reqs, Invalid):
         return False
     for k, op, vs in reqs:
         has = k in labels
@@ -108,10 +127,14 @@ class Term:
     priorities/util/topologies.go:28-38)."""
     __slots__ = ("ns", "sel", "key")
 
-    def __init__(self, owner_ns, d, unsupported):
+    def __init__(self, owner_ns, d, unsupported=None):
         self.ns = frozenset(d.get("namespaces") or [owner_ns])
-        self.sel = label_selector(d.get("labelSelector"), unsupported)
+        self.sel = label_selector(d.get("labelSelector"))
         self.key = d.get("topologyKey", "")
+
+    @property
+    def invalid(self):
+        return isinstance(self.sel, Invalid)
 
     def ident(self):
         return (self.ns, self.sel)
@@ -210,7 +233,7 @@ class Tables:
         snap, U = self.snap, self.U
         node_index = snap.node_index
         # lister pods: allocated-status session tasks (NewPodLister, util.go:57-82)
-        from .export import allocated_status
+        from .export import allocated_status, has_pod_affinity
         lister = [t for t in snap.session_tasks if allocated_status(t["status"])]
         for t in lister:
             if t["pod"].node not in node_index:
@@ -232,23 +255,37 @@ class Tables:
                 a = aff_cache[k] = PodAff(pod, U)
             return a
 
-        for a in (paff(p) for p in spec_pod):
-            for t in a.req_aff + a.req_anti:
-                if not t.key:
-                    raise U("required pod (anti)affinity term with an empty topologyKey")
+        def first_invalid(terms):
+            return next((t.sel for t in terms if t.invalid), None)
+
+        def prefix(terms):  # the key tuple before the first empty topologyKey (all keys when none is empty)
+            keys = tuple(t.key for t in terms)
+            return keys[:keys.index("")] if "" in keys else keys
 
         # ---- predicate tables ----
         checks = [[] for _ in range(m)]
         lister_incr = [[] for _ in range(m)]
         self_match = [0] * m
+        # XB: lister pods with an invalid required anti-affinity selector; every spec checks it first
+        # (satisfiesExistingPodsAntiAffinity errors before it looks at any term, predicates.go:1302-1313)
+        self.xb_pods = sorted((t["uid"], first_invalid(paff(t["pod"]).req_anti)) for t in lister
+                              if first_invalid(paff(t["pod"]).req_anti))
+        self.xb_spec = {s: first_invalid(paff(spec_pod[s]).req_anti) for s in range(m)
+                        if first_invalid(paff(spec_pod[s]).req_anti)}
+        if self.xb_pods or self.xb_spec:
+            xb = self.table(("XB",), (), AFF_ERROR)
+            for s in range(m):
+                checks[s].append((xb, AFF_ERROR))
+            for s in self.xb_spec:
+                lister_incr[s].append(xb)
         e_classes = {}  # (ns, sel, key) -> table id
         for t in lister:
             for term in paff(t["pod"]).req_anti:
-                if term.key:
+                if term.key and not term.invalid:
                     e_classes.setdefault((term.ns, term.sel, term.key), None)
         for s in range(m):
             for term in paff(spec_pod[s]).req_anti:
-                if term.key:
+                if term.key and not term.invalid:
                     e_classes.setdefault((term.ns, term.sel, term.key), None)
         for ck in list(e_classes):
             e_classes[ck] = self.table(("E",) + ck, (ck[2],), AFF_EXISTING_ANTI)
@@ -260,27 +297,45 @@ class Tables:
             for s in range(m):
                 if term.matches(spec_pod[s].ns, spec_pod[s].labels):
                     checks[s].append((tid, AFF_EXISTING_ANTI))
+        # the pod's own terms (satisfiesPodsAffinityAntiAffinity, :1401-1457): an affinity error comes from
+        # the first target pod, before any anti-affinity failure; anti failures come before the affinity
+        # rule that is decided after the loop
+        self.own_err = {}
+        bc = {}  # table id -> terms whose properties a lister pod must match
+        all_t = None
+
+        def table_all():
+            nonlocal all_t
+            if all_t is None:
+                all_t = self.table(("ALL",), (), AFF_ANTI)
+            return all_t
         for s in range(m):
             a = paff(spec_pod[s])
-            if a.req_anti:
-                tid = self.table(("B", tuple(t.ident() for t in a.req_anti), tuple(t.key for t in a.req_anti)),
-                                 tuple(t.key for t in a.req_anti), AFF_ANTI)
-                checks[s].append((tid, AFF_ANTI))
+            aff_chk = []
             if a.has_pod and a.req_aff:
-                tid = self.table(("C", tuple(t.ident() for t in a.req_aff), tuple(t.key for t in a.req_aff)),
-                                 tuple(t.key for t in a.req_aff), AFF_AFFINITY)
-                checks[s].append((tid, AFF_AFFINITY))
+                inv = first_invalid(a.req_aff)
+                if inv is not None:  # getAffinityTermProperties errors once the lister has a pod
+                    self.own_err[s] = str(inv)
+                    checks[s].append((table_all(), AFF_ERROR))
+                    aff_chk = [(table_all(), AFF_AFFINITY)]
+                else:
+                    keys = prefix(a.req_aff)
+                    tid = self.table(("C", tuple(t.ident() for t in a.req_aff), keys), keys, AFF_AFFINITY)
+                    bc[tid] = a.req_aff
+                    if len(keys) < len(a.req_aff):  # an empty topologyKey reached: error
+                        self.own_err[s] = EMPTY_TOPOLOGY_KEY
+                        checks[s].append((tid, AFF_ERROR))
+                    aff_chk = [(tid, AFF_AFFINITY)]
                 self_match[s] = int(_all_match(a.req_aff, spec_pod[s].ns, spec_pod[s].labels))
-        # B/C tables: which identities (lister or pending) match all their terms
-        bc = {}  # table id -> list of terms
-        for s in range(m):
-            a = paff(spec_pod[s])
             if a.req_anti:
-                bc[self.tables[("B", tuple(t.ident() for t in a.req_anti), tuple(t.key for t in a.req_anti))]] = \
-                    a.req_anti
-            if a.has_pod and a.req_aff:
-                bc[self.tables[("C", tuple(t.ident() for t in a.req_aff), tuple(t.key for t in a.req_aff))]] = \
-                    a.req_aff
+                if first_invalid(a.req_anti) is not None:  # any lister pod fails every node
+                    checks[s].append((table_all(), AFF_ANTI))
+                else:
+                    keys = prefix(a.req_anti)
+                    tid = self.table(("B", tuple(t.ident() for t in a.req_anti), keys), keys, AFF_ANTI)
+                    bc[tid] = a.req_anti
+                    checks[s].append((tid, AFF_ANTI))
+            checks[s] += aff_chk
         # identities of lister pods (with their nodes) and of pending specs
         lid = defaultdict(list)
         for t in lister:
@@ -306,8 +361,15 @@ class Tables:
 
         for t in lister:  # existing-anti classes carried by lister pods
             for term in paff(t["pod"]).req_anti:
-                if term.key:
+                if term.key and not term.invalid:
                     add_nodes(e_classes[(term.ns, term.sel, term.key)], [node_index[t["pod"].node]])
+        if self.xb_pods:
+            add_nodes(self.tables[("XB",)], [node_index[t["pod"].node] for t in lister
+                                            if first_invalid(paff(t["pod"]).req_anti)])
+        if all_t is not None:
+            add_nodes(all_t, [node_index[t["pod"].node] for t in lister])
+            for s in range(m):
+                lister_incr[s].append(all_t)
         spec_by_ident = defaultdict(list)
         for s, ident in enumerate(spec_ids):
             spec_by_ident[ident].append(s)
@@ -322,7 +384,7 @@ class Tables:
                     lister_incr[s].append(tid)
         for s in range(m):
             for term in paff(spec_pod[s]).req_anti:
-                if term.key:
+                if term.key and not term.invalid:
                     lister_incr[s].append(e_classes[(term.ns, term.sel, term.key)])
             lister_incr[s] = sorted(set(lister_incr[s]))
 
@@ -349,13 +411,40 @@ class Tables:
         for s, p in enumerate(spec_pod):
             for lk, lv in p.labels.items():
                 s_index[(lk, lv)].add(s)
+        # CalculateInterPodAffinityPriority errors when processTerm meets an invalid selector
+        # (interpod_affinity.go:86-93): the incoming pod's preferred terms against every pod it considers,
+        # and the considered pods' own score terms (:150-187)
+        def own_score_terms(a):  # the terms a pod contributes as an existing pod
+            return (a.req_aff + [t for _, t in a.pref_aff] if a.has_pod else []) + \
+                   ([t for _, t in a.pref_anti] if a.has_anti else [])
+
+        def incoming_terms(a):
+            return ([t for _, t in a.pref_aff] if a.has_pod else []) + ([t for _, t in a.pref_anti] if a.has_anti else [])
+        bad_e = [first_invalid(own_score_terms(paff(e_pod[k]))) is not None for k in all_e]
+        any_e = bool(all_e and any(k in e_nodes for k in all_e))
+        any_e_aff = any(k in e_nodes and has_pod_affinity(e_pod[k]) for k in all_e)
+        bad_e_present = any(b and k in e_nodes for b, k in zip(bad_e, all_e))
+        self.ipa_error = [False] * m
+        for s in range(m):
+            a = paff(spec_pod[s])
+            considered = any_e if (a.has_pod or a.has_anti) else any_e_aff
+            own = first_invalid(incoming_terms(a)) is not None
+            self.ipa_error[s] = bool(snap.config["nodeorder_enabled"]) and (bad_e_present or (considered and own))
+        if snap.config["nodeorder_enabled"]:
+            for s in range(m):  # a pod with invalid score terms that can commit would make later scores error
+                a = paff(spec_pod[s])
+                if first_invalid(own_score_terms(a)) is None or self.ipa_error[s]:
+                    continue
+                if snap.config["predicates_enabled"] and a.has_pod and first_invalid(a.req_aff) is not None:
+                    continue  # fails every node's predicate: never commits
+                raise U("a pending pod with invalid inter-pod affinity score terms may commit")
         W = defaultdict(lambda: defaultdict(int))  # (s, e) -> {key: weight}
         for s in range(m):
             a = paff(spec_pod[s])
             terms = ([(w, t) for w, t in a.pref_aff] if a.has_pod else []) + \
                     ([(-w, t) for w, t in a.pref_anti] if a.has_anti else [])
             for w, term in terms:
-                if not term.key or w == 0:
+                if not term.key or w == 0 or term.invalid:
                     continue
                 for k in _candidates([term], e_index, all_e):
                     if term.matches(k[0], dict(k[1])):
@@ -368,7 +457,7 @@ class Tables:
             if a.has_anti:
                 terms += [(-w, t) for w, t in a.pref_anti]
             for w, term in terms:
-                if not term.key or w == 0:
+                if not term.key or w == 0 or term.invalid:
                     continue
                 for s in _candidates([term], s_index, range(m)):
                     if term.matches(spec_pod[s].ns, spec_pod[s].labels):
@@ -435,4 +524,20 @@ class Tables:
         self.h = H.astype(np.int32)
         self.incr_arr = np.array(inc, IPA_INCR_DTYPE) if inc else np.zeros(0, IPA_INCR_DTYPE)
         self.n_self_dynamic = sum(1 for f in flags if f & AFF_SELF_DYNAMIC)
+        from .export import SPEC_IPA_ERROR
+        for s in range(m):
+            if self.ipa_error[s]:
+                snap.spec_arr["flags"][s] |= SPEC_IPA_ERROR
         return self
+
+    def host_error_string(self, pod, spec, node_name, allocated_before):
+        """The FitErrors string of a node the device failed with KB_R_HOST_ERROR at the affinity stage: the
+        error the reference's predicate returns there (FitErrors.SetNodeError, unschedule_info.go:40-54).
+        `allocated_before`: (uid, spec) of the cycle's Allocate commits before the failing task (the lister's
+        additions). XB errors first (predicates.go:1302-1313; the first such lister pod in UID order -- a Go
+        map walk, so random there when several differ), else the pod's own required affinity (:1401-1413)."""
+        pn = f"{pod.ns}/{pod.name}"  # podName (predicates.go:721-723)
+        xb = list(self.xb_pods) + [(u, self.xb_spec[sp]) for u, sp in allocated_before if sp in self.xb_spec]
+        if xb:
+            return f"Failed to get all terms that pod {pn} matches, err: {min(xb)[1]}"
+        return f"Cannot schedule pod {pn} onto node {node_name}, because of PodAffinity, err: {self.own_err[spec]}"

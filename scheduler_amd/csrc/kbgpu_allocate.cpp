@@ -395,6 +395,8 @@ struct Driver {
   std::vector<GoHeap<int>> jheaps;
   std::vector<std::vector<int>> job_pending;
   std::vector<int32_t> specs, pn, pk;
+  std::vector<uint32_t> node_reasons;  // NO_FIT hook
+  int hook_rc = KB_OK;
   uint32_t n_events = 0;
   bool gang_ready_on = false;
 
@@ -465,8 +467,17 @@ struct Driver {
     if (res.n_placed) share_update(j);
     js.cursor += res.n_placed;
     if (res.stop == KB_STOP_NO_FIT) {
-      out->job_fail_task[j] = js.pending[js.cursor];
+      const int ft = js.pending[js.cursor];
+      out->job_fail_task[j] = ft;
       memcpy(out->job_reason_hist + (size_t)j * KB_NUM_REASONS, res.reason_hist, sizeof(res.reason_hist));
+      // host-evaluated stages: the caller turns the KB_R_HOST_ERROR bucket into its per-node strings from
+      // the reason masks at this state (nothing has run since the failing task)
+      const int sp = s.task_spec[ft];
+      if (ctx->nofit_fn && ctx->host_reasons(sp)) {
+        node_reasons.resize((size_t)ctx->N.n);
+        if (int rc = kb_node_reasons(ctx, sp, node_reasons.data())) hook_rc = rc;
+        else ctx->nofit_fn(ctx->nofit_user, j, ft, n_events, node_reasons.data(), (uint32_t)ctx->N.n);
+      }
     } else if (res.stop == KB_STOP_READY) {
       jheaps[q].push(j);
     }
@@ -642,6 +653,7 @@ struct Driver {
       if (rc) return rc;
       const auto c2 = clk::now();
       apply(q, j, res);
+      if (hook_rc) return hook_rc;
       int nq, nj;
       have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj);
       if (match) {

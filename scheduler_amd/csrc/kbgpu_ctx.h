@@ -41,6 +41,22 @@ struct kb_ctx {
   int idx_bits = 0;
   std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
   std::vector<int64_t> spec_pref_weight;
+  std::vector<char> spec_ipa_err;   // per spec: KB_SPEC_IPA_ERROR (the batch score errors: 64-bit keys)
+  std::vector<char> spec_aff_err;   // per spec: its affinity checks include KB_AFF_ERROR
+  // host overlay (kb_set_host_overlay): per spec the slot of its rows (-1 none), per slot the rows
+  std::vector<int32_t> ov_slot;
+  std::vector<std::vector<uint8_t>> ov_fail;
+  std::vector<std::vector<int32_t>> ov_score;
+  std::vector<int64_t> ov_absmax;   // per spec: max |score_add| (score-range bound)
+  std::vector<char> ov_any_fail;    // per spec: some node is rejected by the overlay
+  std::vector<void*> ov_mem;        // device copies (P.ov_slot / ov_fail / ov_score)
+  // NO_FIT hook (kb_set_nofit_hook)
+  kb_nofit_fn nofit_fn = nullptr;
+  void* nofit_user = nullptr;
+  bool host_reasons(int spec) const {  // the NO_FIT histogram of this spec has host-evaluated buckets
+    return (spec < (int)ov_any_fail.size() && ov_any_fail[spec]) ||
+           (spec < (int)spec_aff_err.size() && spec_aff_err[spec]);
+  }
   bool use_traj = true, use_sel = true, use_engine = false;
   // persistent placement engine (the selection path as one resident workgroup)
   bool eng_running = false;
@@ -135,6 +151,9 @@ extern "C" __attribute__((visibility("hidden"))) int kb_check_score_range(kb_ctx
 extern "C" __attribute__((visibility("hidden"))) void kb_update_traj_ok(kb_ctx* c);
 // stops the placement engine (if running) before other work touches the device state
 extern "C" __attribute__((visibility("hidden"))) int kb_engine_stop(kb_ctx* c);
+// per-node reason masks of one spec at the current node-table state (kb_eval without scores), for the
+// NO_FIT hook of kb_allocate's driver
+extern "C" __attribute__((visibility("hidden"))) int kb_node_reasons(kb_ctx* c, int spec, uint32_t* reasons);
 
 // Pipelined placement for kb_allocate's driver (kbgpu_host.cpp). kb_job_pipeline_ok: the context runs
 // jobs through the launch paths (not sharded, no engine). kb_job_guardable: every task of the job takes

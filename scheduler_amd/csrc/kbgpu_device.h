@@ -51,6 +51,10 @@ struct DevAff {
 
 struct DevSpecs {
   DevAff A;
+  // host overlay (kb_set_host_overlay): ov_slot[spec] = row of ov_fail / ov_score, -1 none (ov_slot null: none)
+  int32_t* ov_slot;
+  uint8_t* ov_fail;   // [slots][n]
+  int32_t* ov_score;  // [slots][n]
   kb_spec* specs;
   int64_t *sc_init, *sc_req;
   kb_term* terms;
@@ -99,9 +103,10 @@ struct ShardRec {
   int32_t kp;                      // proposals (feasible picks, best first)
   int32_t pad;
   uint32_t hist[KB_NUM_REASONS];   // reason histogram of this rank's rows after all kp picks (kp < T only)
+  int32_t pad1;
   uint64_t comp[kShardSegMax];     // pick-order composites (global node index inside)
   int32_t node_kind[kShardSegMax]; // global node | kind << 30
-  int32_t pad2[2];
+  int32_t pad2[4];
 };
 static_assert(sizeof(ShardRec) % 16 == 0, "ShardRec is exchanged as raw bytes");
 
@@ -207,6 +212,10 @@ void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
                          int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+
+// kb_apply: row deltas of commits made outside the device (one thread per delta, atomics).
+void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
+                  const kb_port* ports, void* stream);
 
 // Opt the place kernels into the dynamic LDS they need; returns 0 or the hipError_t.
 int configure_kernels();

@@ -179,6 +179,9 @@ __device__ __forceinline__ void store_row(const DevNodes& N, int n, const Row& r
 constexpr uint32_t kAffExistingAnti = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_EXISTING_ANTI);
 constexpr uint32_t kAffAntiRules = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_ANTI_AFFINITY_RULES);
 constexpr uint32_t kAffAffinityRules = (1u << KB_R_POD_AFFINITY) | (1u << KB_R_AFFINITY_RULES);
+// a plain error from the reference's predicate (FitErrors.SetNodeError with the error's own string, no
+// PredicateFailureReason): the caller supplies the string (kb_set_nofit_hook)
+constexpr uint32_t kHostError = 1u << KB_R_HOST_ERROR;
 
 // InterPodAffinityMatches (vendor/.../predicates.go:1155-1185) through the count tables, in the
 // reference's order: existing pods' anti-affinity (:1293-1333), then the pod's own anti-affinity and
@@ -202,6 +205,8 @@ __device__ uint32_t aff_reasons(const DevAff& A, const kb_aff_spec& as, int n) {
       if (cnt > 0) return kAffExistingAnti;
     } else if (c.kind == KB_AFF_ANTI) {
       if (cnt > 0) return kAffAntiRules;
+    } else if (c.kind == KB_AFF_ERROR) {
+      if (cnt > 0) return kHostError;
     } else if (cnt == 0 && (ld_cnt<COH>(&A.totals[c.table]) > 0 || !as.self_match)) {
       return kAffAffinityRules;
     }
@@ -254,17 +259,28 @@ __device__ void apply_commit_tables(const DevAff& A, const kb_spec& sp, int w, i
 
 // Static part of the predicate chain and score for (spec, node): everything that no commit changes.
 //   bits  0..15: first failing static stage BEFORE the host-port check (conditions, node selector)
-//   bits 16..31: first failing static stage AFTER it (taints, pressure, then inter-pod affinity)
-//   bits 32..59: NodeAffinity priority count (node_affinity.go:34-74), signed 28-bit
-//   bits 60..63: InterPodAffinity priority (0..10)
+//   bits 16..32: first failing static stage AFTER it (taints, pressure, inter-pod affinity, then the host
+//                overlay of kb_set_host_overlay: a plugin later in tier order)
+//   bits 33..59: NodeAffinity priority count x its weight + the overlay's score (node_affinity.go:34-74),
+//                signed 27-bit (the host bounds it)
+//   bits 60..63: InterPodAffinity priority (0..10); kIpaErrorField: the batch score errors
 // `mm` (this spec's InterPodAffinity min / max) non-null: the spec's affinity inputs do not change
-// during its run, so the affinity predicate and priority are folded in here too.
+// during its run, so the affinity predicate and priority are folded in here too. A spec with inter-pod
+// affinity evaluated without them (the block-wide loops) defers the overlay's predicate to aff_key.
 // AFF = false compiles the affinity lookups out (specs without inter-pod affinity: fewer live registers).
+constexpr uint32_t kIpaErrorField = 15;
+constexpr int64_t kIpaErrorScore = -(1ll << 36);  // every feasible node <= -1: SelectBestNode panics
+
+__device__ __forceinline__ int32_t ov_row(const DevSpecs& P, int spec) {
+  return P.ov_slot != nullptr ? P.ov_slot[spec] : -1;
+}
+
 template <bool AFF>
 __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
-                                uint32_t f, int n, const int64_t* mm) {
+                                int spec, uint32_t f, int n, const int64_t* mm) {
   uint32_t pre = 0, post = 0;
   const bool aff = AFF && mm != nullptr && sp.aff_class >= 0;
+  const int32_t ov = ov_row(P, spec);
   if (C.predicates) {
     // CheckNodeConditionPredicate (vendor/.../predicates.go:1568-1596): one reason per bad condition
     pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
@@ -286,6 +302,8 @@ __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevC
     // InterPodAffinityMatches, the last predicate (plugins/predicates/predicates.go:278-296)
     if (aff && !pre && !post) post = aff_reasons(P.A, P.A.specs[sp.aff_class], n);
   }
+  // the host overlay's predicate (deferred behind the live affinity check when that is not folded in)
+  if (ov >= 0 && !pre && !post && (aff || sp.aff_class < 0) && P.ov_fail[(size_t)ov * N.n + n]) post = kHostError;
   int32_t na = 0;
   uint32_t ipa = 0;
   if (C.nodeorder) {
@@ -295,16 +313,23 @@ __device__ uint64_t static_eval(const DevNodes& N, const DevSpecs& P, const DevC
         if (t.weight == 0) continue;
         if (term_match(N, P, t, n)) na += t.weight;
       }
-    if (aff) {
+    na *= C.w_na;
+    if (sp.flags & KB_SPEC_IPA_ERROR) {
+      ipa = kIpaErrorField;
+    } else if (aff) {
       const kb_aff_spec as = P.A.specs[sp.aff_class];
       if (as.hist_cnt) ipa = (uint32_t)ipa_score(ipa_count(P.A, as, n), mm[0], mm[1]);
     }
   }
-  return (uint64_t)pre | ((uint64_t)post << 16) | ((uint64_t)((uint32_t)na & 0x0fffffffu) << 32) |
+  if (ov >= 0) na += P.ov_score[(size_t)ov * N.n + n];
+  return (uint64_t)pre | ((uint64_t)post << 16) | ((uint64_t)((uint32_t)na & 0x07ffffffu) << 33) |
          ((uint64_t)ipa << 60);
 }
 
-__device__ __forceinline__ int32_t stat_na(uint64_t st) { return (int32_t)((uint32_t)(st >> 32) << 4) >> 4; }
+__device__ __forceinline__ uint32_t stat_pre(uint64_t st) { return (uint32_t)(st & 0xffffu); }
+__device__ __forceinline__ uint32_t stat_post(uint64_t st) { return (uint32_t)((st >> 16) & 0x1ffffu); }
+// weighted NodeAffinity + overlay score
+__device__ __forceinline__ int32_t stat_na(uint64_t st) { return (int32_t)((uint32_t)(st >> 33) << 5) >> 5; }
 __device__ __forceinline__ int32_t stat_ipa(uint64_t st) { return (int32_t)(st >> 60); }
 
 __device__ __forceinline__ bool sc_fit(const DevNodes& N, const kb_spec& sp, const int64_t* sci, bool has_map,
@@ -324,9 +349,9 @@ __device__ __forceinline__ uint32_t row_reasons(const DevNodes& N, const DevSpec
                     sc_fit(N, sp, sci, r.flags & KB_NODE_REL_HAS_MAP, N.rel_sc, n);
     if (!fr) return 1u << KB_R_RESOURCE_FIT;
   }
-  if (!C.predicates) return 0;
+  if (!C.predicates) return stat_post(st);  // the host overlay only
   if (r.max_pods <= r.pod_count) return 1u << KB_R_POD_NUMBER;  // predicates.go:162-166
-  const uint32_t pre = (uint32_t)(st & 0xffff);
+  const uint32_t pre = stat_pre(st);
   if (pre) return pre;
   // PodFitsHostPorts (vendor/.../predicates.go:1031-1052; cache/host_ports.go:96-125)
   for (uint32_t i = 0; i < sp.port_cnt; ++i) {
@@ -335,20 +360,21 @@ __device__ __forceinline__ uint32_t row_reasons(const DevNodes& N, const DevSpec
     const uint64_t hit = p.ip == 0 ? used : (used & (1ull | (1ull << p.ip)));
     if (hit) return 1u << KB_R_HOST_PORTS;
   }
-  return (uint32_t)((st >> 16) & 0xffff);
+  return stat_post(st);
 }
 
 // nodeOrderFn (nodeorder.go:188-226) + the InterPodAffinity batch score (:229-246) from the static cache.
 // All terms are integers, so the reference's float64 sum equals this int64 sum.
 __device__ __forceinline__ int64_t row_score(const DevCfg& C, const kb_spec& sp, const Row& r, uint64_t st) {
-  if (!C.nodeorder) return 0;
+  if (!C.nodeorder) return stat_na(st);  // the host overlay's score only
+  if (stat_ipa(st) == (int32_t)kIpaErrorField) return kIpaErrorScore;  // batch error: no scores at all
   const int64_t batch = (int64_t)stat_ipa(st) * C.w_pa;
   if (sp.flags & KB_SPEC_NA_ERROR) return batch;  // map fn error: the node keeps only the batch score
   const int64_t rc = sp.nz_cpu + r.nz_cpu, rm = sp.nz_mem + r.nz_mem;
   const int64_t lr = (lr_score(rc, r.alloc_cpu) + lr_score(rm, r.alloc_mem)) / 2;
   const double cf = frac_cap(rc, r.alloc_cpu), mf = frac_cap(rm, r.alloc_mem);
   const int64_t bra = (cf >= 1.0 || mf >= 1.0) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 10.0);
-  return lr * C.w_lr + bra * C.w_bra + (int64_t)stat_na(st) * C.w_na + batch;
+  return lr * C.w_lr + bra * C.w_bra + (int64_t)stat_na(st) + batch;
 }
 
 __device__ __forceinline__ uint64_t make_key(uint32_t reasons, int64_t score, int n) {
@@ -387,7 +413,7 @@ __global__ __launch_bounds__(256) void sweep_keys_kernel(DevNodes N, DevSpecs P,
   uint64_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, spec, r.flags, n, P.A.mm);
     stat[n] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, n);
     k = make_key(rs, rs ? 0 : row_score(C, sp, r, st), n);
@@ -718,7 +744,7 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   const int s = spec_ids[j];
   const kb_spec sp = P.specs[s];
   const Row r = load_row(N, n);
-  const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, AFF ? mm + 2 * j : nullptr);
+  const uint64_t st = static_eval<AFF>(N, P, C, sp, s, r.flags, n, AFF ? mm + 2 * j : nullptr);
   reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
   scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
 }
@@ -840,11 +866,12 @@ __device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCf
                     scalars_fit_after(N, sp, sci, scr, r.flags & KB_NODE_REL_HAS_MAP, N.rel_sc, n, p);
     if (!fr) reasons = 1u << KB_R_RESOURCE_FIT;
   }
+  if (!reasons && !C.predicates) reasons = stat_post(st);  // the host overlay only
   if (!reasons && C.predicates) {
     if (r.max_pods <= r.pod_count) {
       reasons = 1u << KB_R_POD_NUMBER;
-    } else if (st & 0xffff) {
-      reasons = (uint32_t)(st & 0xffff);
+    } else if (stat_pre(st)) {
+      reasons = stat_pre(st);
     } else {
       for (uint32_t i = 0; i < sp.port_cnt && !reasons; ++i) {
         const kb_port q = P.ports[sp.port_off + i];
@@ -856,7 +883,7 @@ __device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCf
           }
         if (q.ip == 0 ? used : (used & (1ull | (1ull << q.ip)))) reasons = 1u << KB_R_HOST_PORTS;
       }
-      if (!reasons) reasons = (uint32_t)((st >> 16) & 0xffff);
+      if (!reasons) reasons = stat_post(st);
     }
   }
   if (reasons) return reasons;
@@ -886,7 +913,7 @@ __global__ __launch_bounds__(256) void traj_sweep_kernel(DevNodes N, DevSpecs P,
   uint32_t k = 0;
   if (n < N.n) {
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, spec, r.flags, n, P.A.mm);
     const int A = allocs_before_full(N, sp, sci, scr, r, n);
     k = compress_key(traj_key64(N, P, C, sp, sci, scr, r, st, n, j, A), n, idx_bits);
     traj[(size_t)j * N.n + n] = k;
@@ -1993,7 +2020,7 @@ __global__ __launch_bounds__(kSelThreads) void engine_kernel(DevNodes N, DevSpec
         const int64_t* sci = P.sc_init + (size_t)spec * N.S;
         for (int i = tid; i < n; i += kSelThreads) {
           const Row row = load_row(N, i);
-          const uint64_t st = static_eval<false>(N, P, C, sp, row.flags, i, nullptr);
+          const uint64_t st = static_eval<false>(N, P, C, sp, spec, row.flags, i, nullptr);
           stat[i] = st;
           const uint32_t rs = row_reasons(N, P, C, sp, sci, row, st, i);
           k32[i] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, row, st), i), i + N.base, idx_bits);
@@ -2042,7 +2069,7 @@ __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, D
   if (n < N.n) {
     const kb_spec sp = P.specs[spec];
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, spec, r.flags, n, P.A.mm);
     stat[n] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
     keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
@@ -2353,7 +2380,7 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
   if (sweep && n < N.n) {
     const kb_spec sp = P.specs[cmd.spec];
     const Row r = load_row(N, n);
-    const uint64_t st = static_eval<AFF>(N, P, C, sp, r.flags, n, P.A.mm);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, cmd.spec, r.flags, n, P.A.mm);
     stat[n] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)cmd.spec * N.S, r, st, n);
     keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
@@ -2634,13 +2661,15 @@ __global__ __launch_bounds__(256) void aff_commit_kernel(DevSpecs P, int spec, i
 // Key of node i for a spec whose affinity inputs move with its own commits: the cached base key (row
 // + static predicates + LR/BRA/NodeAffinity), then the inter-pod affinity predicate (the last one) and
 // the InterPodAffinity batch score from the live tables.
+// ovf: the spec's host-overlay predicate row (kb_set_host_overlay), checked after the affinity predicate.
 __device__ __forceinline__ uint64_t aff_key(const DevAff& A, const kb_aff_spec& as, const DevCfg& C, uint64_t b,
-                                            int i, int64_t mn, int64_t mx) {
+                                            int i, int64_t mn, int64_t mx, const uint8_t* ovf) {
   if (!(b & kFeasible)) return b;
   if (C.predicates) {
     const uint32_t ar = aff_reasons<true>(A, as, i);
     if (ar) return ar;
   }
+  if (ovf != nullptr && ovf[i]) return kHostError;
   if (!C.nodeorder || !as.hist_cnt) return b;
   const int64_t score = (int64_t)((b >> 24) & ((1ull << 39) - 1)) - kScoreBias +
                         (int64_t)ipa_score(ipa_count<true>(A, as, i), mn, mx) * C.w_pa;
@@ -2672,9 +2701,11 @@ __global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
   const kb_aff_spec as = P.A.specs[sp.aff_class];
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const int32_t ov = ov_row(P, spec);
+  const uint8_t* ovf = ov >= 0 ? P.ov_fail + (size_t)ov * n : nullptr;
   for (int i = tid; i < n; i += kAffThreads) {  // base keys (no inter-pod affinity)
     const Row r = load_row(N, i);
-    const uint64_t st = static_eval<false>(N, P, C, sp, r.flags, i, nullptr);
+    const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
     stat[i] = st;
     const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
     base[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
@@ -2691,7 +2722,7 @@ __global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
     int64_t mn = 0, mx = 0;
     if (ipa) block_ipa_minmax<true>(P.A, as, n, rmin, rmax, &mn, &mx);
     uint64_t best = 0;
-    for (int i = tid; i < n; i += kAffThreads) best = umax64(best, aff_key(P.A, as, C, base[i], i, mn, mx));
+    for (int i = tid; i < n; i += kAffThreads) best = umax64(best, aff_key(P.A, as, C, base[i], i, mn, mx, ovf));
     best = wave_max_u64(best);
     if (lane == 0) red[wv] = best;
     __syncthreads();
@@ -2705,7 +2736,7 @@ __global__ __launch_bounds__(kAffThreads) void aff_place_kernel(
 #pragma unroll
       for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
       for (int i = tid; i < n; i += kAffThreads) {
-        const uint64_t k = aff_key(P.A, as, C, base[i], i, mn, mx);
+        const uint64_t k = aff_key(P.A, as, C, base[i], i, mn, mx, ovf);
 #pragma unroll
         for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (uint32_t)(k >> b) & 1u;
       }
@@ -2927,7 +2958,7 @@ __global__ __launch_bounds__(kAffThreads) void aff_reg_kernel(
     }
     if (i < n) {
       const Row r = load_row(N, i);
-      const uint64_t st = static_eval<false>(N, P, C, sp, r.flags, i, nullptr);
+      const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
       stat[i] = st;
       const uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
       bkl[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
@@ -2990,6 +3021,8 @@ __global__ __launch_bounds__(kAffThreads) void aff_reg_kernel(
           if (v[k][e] > 0) return kAffExistingAnti;
         } else if (e_kind[e] == KB_AFF_ANTI) {
           if (v[k][e] > 0) return kAffAntiRules;
+        } else if (e_kind[e] == KB_AFF_ERROR) {
+          if (v[k][e] > 0) return kHostError;
         } else if (v[k][e] == 0 && (tot[e] > 0 || !LAS.self_match)) {
           return kAffAffinityRules;
         }
@@ -3427,6 +3460,54 @@ void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const in
   else
     hipLaunchKernelGGL(eval_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons,
                        scores, mm);
+}
+
+// kb_apply: one thread per row delta of a commit made outside the device -- NodeInfo.AddTask / RemoveTask
+// (api/node_info.go:165-221) and the plugins' schedulercache AddPod / RemovePod (cache/node_info.go:498-630,
+// host_ports.go), plus the inter-pod affinity table updates of the pod's spec. Sums are atomics (order-free);
+// flags: every set in pass 0, every clear in pass 1.
+__global__ __launch_bounds__(256) void apply_kernel(DevNodes N, DevSpecs P, const kb_row_delta* d, int k,
+                                                    const int64_t* sc, const kb_port* ports, int pass) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  const kb_row_delta e = d[i];
+  const int w = e.node - N.base;
+  if (w < 0 || w >= N.n) return;  // another rank's row
+  if (pass == 1) {
+    if (e.flags_clear) atomicAnd(&N.flags[w], ~e.flags_clear);
+    return;
+  }
+  using u64 = unsigned long long;
+  atomicAdd((u64*)&N.idle_cpu[w], (u64)e.idle_cpu);
+  atomicAdd((u64*)&N.idle_mem[w], (u64)e.idle_mem);
+  atomicAdd((u64*)&N.rel_cpu[w], (u64)e.rel_cpu);
+  atomicAdd((u64*)&N.rel_mem[w], (u64)e.rel_mem);
+  atomicAdd((u64*)&N.nz_cpu[w], (u64)e.nz_cpu);
+  atomicAdd((u64*)&N.nz_mem[w], (u64)e.nz_mem);
+  atomicAdd(&N.pod_count[w], e.pods);
+  if (e.flags_set) atomicOr(&N.flags[w], e.flags_set);
+  if (e.sc_off != 0xffffffffu)
+    for (int q = 0; q < N.S; ++q) {
+      atomicAdd((u64*)&N.idle_sc[(size_t)q * N.n + w], (u64)sc[e.sc_off + q]);
+      atomicAdd((u64*)&N.rel_sc[(size_t)q * N.n + w], (u64)sc[e.sc_off + N.S + q]);
+    }
+  for (uint32_t j = 0; j < e.port_cnt; ++j) {
+    const kb_port p = ports[e.port_off + j];
+    u64* used = (u64*)&N.port_used[(size_t)p.slot * N.n + w];
+    if (e.pods >= 0) atomicOr(used, 1ull << p.ip);
+    else atomicAnd(used, ~(1ull << p.ip));
+  }
+  if (e.spec >= 0) {
+    const int sign = e.pods < 0 ? -1 : 1;
+    apply_commit_tables(P.A, P.specs[e.spec], w, e.kind == KB_PLACE_ALLOCATE ? sign : 0, sign);
+  }
+}
+
+void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
+                  const kb_port* ports, void* stream) {
+  const int blocks = (k + 255) / 256;
+  for (int pass = 0; pass < 2; ++pass)
+    hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, d, k, sc, ports, pass);
 }
 
 }  // namespace kbgpu

@@ -58,6 +58,18 @@ void free_all(std::vector<void*>& v) {
   v.clear();
 }
 
+void drop_overlay(kb_ctx* c) {
+  free_all(c->ov_mem);
+  c->ov_slot.clear();
+  c->ov_fail.clear();
+  c->ov_score.clear();
+  c->ov_absmax.clear();
+  c->ov_any_fail.clear();
+  c->P.ov_slot = nullptr;
+  c->P.ov_fail = nullptr;
+  c->P.ov_score = nullptr;
+}
+
 void drop_affinity(kb_ctx* c) {
   free_all(c->aff_mem);
   c->aff_pristine.clear();
@@ -66,6 +78,7 @@ void drop_affinity(kb_ctx* c) {
   c->spec_dyn.clear();
   c->spec_hist.clear();
   c->spec_incr.clear();
+  c->spec_aff_err.clear();
   c->mm_eval = nullptr;
   c->mm_eval_cap = 0;
 }
@@ -170,6 +183,7 @@ void kb_destroy(kb_ctx* c) {
   free_all(c->spec_mem);
   free_all(c->aff_mem);
   free_all(c->work_mem);
+  free_all(c->ov_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
   if (c->h_job1) (void)hipHostFree(c->h_job1);
   for (int s = 0; s < 2; ++s) {
@@ -222,6 +236,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   free_all(c->node_mem);
   free_all(c->work_mem);
   drop_affinity(c);
+  drop_overlay(c);
   c->nodes_ok = false;
   DevNodes& N = c->N;
   const size_t n = in->n;
@@ -307,6 +322,7 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   free_all(c->spec_mem);
   c->specs_ok = false;
   drop_affinity(c);
+  drop_overlay(c);
   if (in->n_tol_sets == 0 || in->n_taint_sets == 0) return fail(c, KB_E_INVALID, "empty toleration/taint tables");
   // host-side validation of every index the kernels will follow (no out-of-bounds device access)
   const uint32_t S = (uint32_t)c->N.S;
@@ -351,6 +367,9 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   c->max_pref_weight = 0;
   c->spec_pref_weight.assign(in->m, 0);
   c->spec_needs_aff.assign(in->m, 0);
+  c->spec_ipa_err.assign(in->m, 0);
+  c->ov_absmax.assign(in->m, 0);
+  for (uint32_t i = 0; i < in->m; ++i) c->spec_ipa_err[i] = (in->specs[i].flags & KB_SPEC_IPA_ERROR) != 0;
   for (uint32_t i = 0; i < in->m; ++i)
     c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
   for (uint32_t i = 0; i < in->m; ++i) {
@@ -392,7 +411,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   }
   for (uint32_t i = 0; i < a->n_checks; ++i)
     if (a->checks[i].table < 0 || (uint32_t)a->checks[i].table >= a->n_tables || a->checks[i].kind < 0 ||
-        a->checks[i].kind > KB_AFF_AFFINITY)
+        a->checks[i].kind > KB_AFF_ERROR)
       return fail(c, KB_E_INVALID, "affinity check %u", i);
   for (uint32_t i = 0; i < a->n_lister; ++i)
     if (a->lister[i] < 0 || (uint32_t)a->lister[i] >= a->n_tables) return fail(c, KB_E_INVALID, "lister %u", i);
@@ -414,10 +433,13 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   c->spec_hist.assign(a->m, 0);
   c->spec_incr.assign(a->m, 0);
   c->spec_aff_reg.assign(a->m, 0);
+  c->spec_aff_err.assign(a->m, 0);
   for (uint32_t s = 0; s < a->m; ++s) {
     const int32_t ac = specs[s].aff_class;
     if (ac < -1 || ac >= (int32_t)a->m) return fail(c, KB_E_INVALID, "spec %u aff_class %d", s, ac);
     if (ac >= 0) {
+      for (uint32_t i = 0; i < a->specs[ac].check_cnt; ++i)
+        if (a->checks[a->specs[ac].check_off + i].kind == KB_AFF_ERROR) c->spec_aff_err[s] = 1;
       c->spec_dyn[s] = (a->specs[ac].flags & KB_AFF_SELF_DYNAMIC) != 0;
       c->spec_hist[s] = a->specs[ac].hist_cnt > 0;
       c->spec_incr[s] = a->specs[ac].lister_cnt > 0 || a->specs[ac].incr_cnt > 0;
@@ -467,20 +489,28 @@ void kb_update_traj_ok(kb_ctx* c) {
   const long double bias32 = (long double)(1ll << (30 - c->idx_bits));
   c->spec_traj_ok.assign(c->spec_pref_weight.size(), 0);
   for (size_t i = 0; i < c->spec_pref_weight.size(); ++i) {
+    const int64_t ov = i < c->ov_absmax.size() ? c->ov_absmax[i] : 0;
     long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
-                        (long double)c->spec_pref_weight[i] * std::llabs((long long)C.w_na) +
+                        (long double)c->spec_pref_weight[i] * std::llabs((long long)C.w_na) + (long double)ov +
                         10.0L * std::llabs((long long)C.w_pa);
-    c->spec_traj_ok[i] = bound < bias32 - 1;
+    // a batch-score error (KB_SPEC_IPA_ERROR) scores far below any 32-bit key
+    c->spec_traj_ok[i] = bound < bias32 - 1 && !(i < c->spec_ipa_err.size() && c->spec_ipa_err[i]);
   }
 }
 
 int kb_check_score_range(kb_ctx* c) {
-  // |score| must stay inside the key's 39-bit biased field.
+  // |score| must stay inside the key's 39-bit biased field, and |NodeAffinity x weight + overlay score|
+  // inside the static cache's signed 27-bit field.
   const DevCfg& C = c->cfg;
-  long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
-                      (long double)c->max_pref_weight * std::llabs((long long)C.w_na) +
-                      10.0L * std::llabs((long long)C.w_pa);
-  if (bound >= (long double)(kScoreBias / 2)) return fail(c, KB_E_UNSUPPORTED, "score range exceeds 2^37");
+  for (size_t i = 0; i < c->spec_pref_weight.size(); ++i) {
+    const int64_t ov = i < c->ov_absmax.size() ? c->ov_absmax[i] : 0;
+    const long double na = (long double)c->spec_pref_weight[i] * std::llabs((long long)C.w_na) + (long double)ov;
+    const long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) + na +
+                              10.0L * std::llabs((long long)C.w_pa);
+    if (bound >= (long double)(kScoreBias / 2)) return fail(c, KB_E_UNSUPPORTED, "score range exceeds 2^37");
+    if (na >= (long double)(1 << 26))
+      return fail(c, KB_E_UNSUPPORTED, "spec %zu: NodeAffinity x weight + overlay score exceeds 2^26", i);
+  }
   return KB_OK;
 }
 
@@ -918,7 +948,8 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     }
     if (dyn) {
       c->ev_begin(&ea);
-      if (c->use_aff_reg && c->spec_aff_reg[spec] && aff_reg_fits(c->N.n, c->spec_aff_reg[spec]))
+      if (c->use_aff_reg && c->spec_aff_reg[spec] && aff_reg_fits(c->N.n, c->spec_aff_reg[spec]) &&
+          !((size_t)spec < c->ov_slot.size() && c->ov_slot[spec] >= 0))
         launch_aff_reg(c->N, c->P, c->cfg, spec, c->spec_aff_reg[spec], (int)t, run, c->stat, js, first, job->ready_num,
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       else
@@ -1076,6 +1107,7 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (c->sharded || c->use_engine || !c->use_sel || !c->sel_ok || !c->traj || !c->spec_traj_ok[spec]) return 0;
   if (!fed_fits(c->N.n)) return 0;
   if (c->aff_ok && c->spec_needs_aff[spec]) return 0;
+  if (c->host_reasons(spec)) return 0;  // its NO_FIT needs a mid-cycle kb_node_reasons (not beside the engine)
   return c->use_fed ? 1 : 0;
 }
 
@@ -1191,6 +1223,8 @@ int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kin
   return place_finish(c, slot, placed_node, placed_kind, result, skipped != 0);
 }
 
+static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores);
+
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   if (c) c->timing_now = c->timing;
   if (c) c->prev_listed = false;
@@ -1204,6 +1238,18 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
                   spec_ids[i]);
   }
   HIP_OK(c, hipSetDevice(c->device));
+  return eval_impl(c, spec_ids, t, reasons, scores);
+}
+
+int kb_node_reasons(kb_ctx* c, int spec, uint32_t* reasons) {
+  const bool tn = c->timing_now;
+  c->timing_now = false;
+  const int rc = eval_impl(c, &spec, 1, reasons, nullptr);
+  c->timing_now = tn;
+  return rc;
+}
+
+static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   const size_t n = (size_t)c->N.n;
   const uint32_t chunk = 8192;
   int32_t* d_ids;
@@ -1243,6 +1289,149 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
   (void)hipFree(d_r);
   (void)hipFree(d_s);
   if (rc) return fail(c, rc, "kb_eval: HIP failure");
+  return KB_OK;
+}
+
+// Device copies of the host overlays (after every change; overlays change rarely, between jobs).
+static int overlay_upload(kb_ctx* c) {
+  // kernels of earlier jobs may still hold the old arrays
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (c->stream_b) HIP_OK(c, hipStreamSynchronize(c->stream_b));
+  free_all(c->ov_mem);
+  c->P.ov_slot = nullptr;
+  c->P.ov_fail = nullptr;
+  c->P.ov_score = nullptr;
+  bool any = false;
+  for (int32_t sl : c->ov_slot) any = any || sl >= 0;
+  if (!any) return KB_OK;
+  const size_t n = (size_t)c->N.n, slots = c->ov_fail.size();
+  std::vector<uint8_t> f(slots * n);
+  std::vector<int32_t> sc(slots * n);
+  for (size_t k = 0; k < slots; ++k) {
+    memcpy(f.data() + k * n, c->ov_fail[k].data(), n);
+    memcpy(sc.data() + k * n, c->ov_score[k].data(), n * 4);
+  }
+  int rc;
+  if ((rc = upload(c, c->ov_mem, &c->P.ov_slot, c->ov_slot.data(), c->ov_slot.size()))) return rc;
+  if ((rc = upload(c, c->ov_mem, &c->P.ov_fail, f.data(), f.size()))) return rc;
+  if ((rc = upload(c, c->ov_mem, &c->P.ov_score, sc.data(), sc.size()))) return rc;
+  return KB_OK;
+}
+
+int kb_set_host_overlay(kb_ctx* c, int32_t spec, const uint8_t* fail_in, const int64_t* score_add) {
+  if (c) c->prev_listed = false;
+  if (!c) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (spec < 0 || spec >= c->P.m) return fail(c, KB_E_INVALID, "spec %d out of range", spec);
+  HIP_OK(c, hipSetDevice(c->device));
+  const size_t n = (size_t)c->N.n, m = (size_t)c->P.m;
+  if (c->ov_slot.size() != m) {
+    c->ov_slot.assign(m, -1);
+    c->ov_any_fail.assign(m, 0);
+  }
+  if (c->ov_absmax.size() != m) c->ov_absmax.assign(m, 0);
+  int32_t sl = c->ov_slot[spec];
+  if (!fail_in && !score_add) {  // clear
+    c->ov_slot[spec] = -1;
+    c->ov_any_fail[spec] = 0;
+    c->ov_absmax[spec] = 0;
+  } else {
+    int64_t mx = 0;
+    if (score_add)
+      for (size_t i = 0; i < n; ++i) {
+        const int64_t v = score_add[i] < 0 ? -score_add[i] : score_add[i];
+        if (v >= (1ll << 26)) return fail(c, KB_E_UNSUPPORTED, "overlay score %lld at node %zu exceeds 2^26",
+                                          (long long)score_add[i], i);
+        mx = std::max(mx, v);
+      }
+    if (sl < 0) {  // a free row (one no spec points at), else a new one
+      std::vector<char> used(c->ov_fail.size(), 0);
+      for (int32_t x : c->ov_slot)
+        if (x >= 0) used[x] = 1;
+      sl = (int32_t)(std::find(used.begin(), used.end(), 0) - used.begin());
+      if ((size_t)sl == c->ov_fail.size()) {
+        c->ov_fail.emplace_back(n, 0);
+        c->ov_score.emplace_back(n, 0);
+      }
+    }
+    auto& f = c->ov_fail[sl];
+    auto& sc = c->ov_score[sl];
+    f.assign(n, 0);
+    sc.assign(n, 0);
+    char any = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (fail_in && fail_in[i]) f[i] = 1, any = 1;
+      if (score_add) sc[i] = (int32_t)score_add[i];
+    }
+    c->ov_slot[spec] = sl;
+    c->ov_any_fail[spec] = any;
+    c->ov_absmax[spec] = mx;
+  }
+  kb_update_traj_ok(c);
+  if (int rc = kb_check_score_range(c)) {  // refused: take the overlay back
+    c->ov_slot[spec] = -1;
+    c->ov_any_fail[spec] = 0;
+    c->ov_absmax[spec] = 0;
+    kb_update_traj_ok(c);
+    (void)overlay_upload(c);
+    return rc;
+  }
+  return overlay_upload(c);
+}
+
+int kb_apply(kb_ctx* c, const kb_row_delta* d, uint32_t k, const int64_t* sc, uint32_t n_sc, const kb_port* ports,
+             uint32_t n_ports) {
+  if (c) c->prev_listed = false;  // rows changed outside any job's commit list
+  if (!c || (!d && k)) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (k == 0) return KB_OK;
+  // every index the kernel follows is checked here
+  const uint32_t S = (uint32_t)c->N.S;
+  for (uint32_t i = 0; i < k; ++i) {
+    const kb_row_delta& e = d[i];
+    const int64_t lo = c->N.base, hi = (int64_t)c->N.base + c->N.n;
+    const int64_t total = c->sharded ? (int64_t)c->shard.n_total : hi;
+    if (e.node < 0 || e.node >= total) return fail(c, KB_E_INVALID, "delta %u: node %d", i, e.node);
+    (void)lo;
+    if (e.sc_off != 0xffffffffu && (uint64_t)e.sc_off + 2ull * S > n_sc)
+      return fail(c, KB_E_INVALID, "delta %u: scalar deltas out of range", i);
+    if ((uint64_t)e.port_off + e.port_cnt > n_ports) return fail(c, KB_E_INVALID, "delta %u: ports", i);
+    for (uint32_t j = 0; j < e.port_cnt; ++j) {
+      const kb_port& p = ports[e.port_off + j];
+      if (p.slot < 0 || p.slot >= c->N.P || p.ip < 0 || p.ip > 63) return fail(c, KB_E_INVALID, "delta %u port", i);
+    }
+    if (e.spec >= c->P.m || (e.spec >= 0 && c->spec_needs_aff[e.spec] && !c->aff_ok))
+      return fail(c, KB_E_INVALID, "delta %u: spec %d", i, e.spec);
+  }
+  HIP_OK(c, hipSetDevice(c->device));
+  std::vector<void*> tmp;
+  kb_row_delta* dd;
+  int64_t* dsc;
+  kb_port* dp;
+  int rc;
+  if ((rc = upload(c, tmp, &dd, d, k)) || (rc = upload(c, tmp, &dsc, sc, n_sc, false)) ||
+      (rc = upload(c, tmp, &dp, ports, n_ports, false))) {
+    free_all(tmp);
+    return rc;
+  }
+  launch_apply(c->N, c->P, dd, (int)k, dsc, dp, c->stream);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  free_all(tmp);
+  if (e != hipSuccess) return fail(c, KB_E_HIP, "kb_apply: %s", hipGetErrorString(e));
+  return KB_OK;
+}
+
+int kb_set_nofit_hook(kb_ctx* c, kb_nofit_fn fn, void* user) {
+  if (!c) return KB_E_INVALID;
+  c->nofit_fn = fn;
+  c->nofit_user = user;
   return KB_OK;
 }
 

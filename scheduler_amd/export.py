@@ -12,6 +12,8 @@ The device never sees a string; node index = position in name order.
 """
 from __future__ import annotations
 
+import re
+
 import numpy as np
 
 from . import model as M
@@ -35,6 +37,7 @@ NODE_NOT_READY, NODE_OUT_OF_DISK, NODE_NET_UNAVAIL, NODE_UNSCHEDULABLE = 1 << 2,
 NODE_MEM_PRESSURE, NODE_DISK_PRESSURE, NODE_PID_PRESSURE = 1 << 9, 1 << 10, 1 << 11
 SPEC_INIT_HAS_MAP, SPEC_REQ_HAS_MAP, SPEC_BEST_EFFORT = 1 << 0, 1 << 1, 1 << 2
 SPEC_HAS_SELECTOR, SPEC_HAS_REQUIRED, SPEC_NA_ERROR, SPEC_POD_AFFINITY = 1 << 3, 1 << 4, 1 << 5, 1 << 6
+SPEC_IPA_ERROR = 1 << 7
 OP_IN, OP_NOTIN, OP_EXISTS, OP_DNE, OP_GT, OP_LT, OP_TRUE, OP_FALSE = range(8)
 
 ST = {"Pending": 1 << 0, "Allocated": 1 << 1, "Pipelined": 1 << 2, "Binding": 1 << 3, "Bound": 1 << 4,
@@ -53,7 +56,8 @@ REASONS = [  # bit i of a reason mask (kbgpu.h KB_R_*)
     "node(s) had taints that the pod didn't tolerate", "node(s) had memory pressure", "node(s) had disk pressure",
     "node(s) had pid pressure", "node(s) didn't match pod affinity/anti-affinity",
     "node(s) didn't satisfy existing pods anti-affinity rules", "node(s) didn't match pod affinity rules",
-    "node(s) didn't match pod anti-affinity rules"]
+    "node(s) didn't match pod anti-affinity rules",
+    None]  # KB_R_HOST_ERROR: the string is the host's (a plain error of the reference's predicate, or an overlay's)
 
 
 class Unsupported(RuntimeError):
@@ -73,32 +77,95 @@ def _qname_fmt(s):
     return bool(s) and _alnum(s[0]) and _alnum(s[-1]) and all(_alnum(c) or c in "-_." for c in s)
 
 
-def _dns1123_subdomain(s):
-    if not s or len(s) > 253:
-        return False
-    for lab in s.split("."):
-        if not lab or not all((c.isascii() and (c.islower() or c.isdigit())) or c == "-" for c in lab):
-            return False
-        if lab[0] == "-" or lab[-1] == "-":
-            return False
-    return True
-
-
 def is_qualified_name(v: str) -> bool:
+    return not qualified_name_errors(v)
+
+
+def is_valid_label_value(v: str) -> bool:
+    return not label_value_errors(v)
+
+
+# the error texts (validation.go:38-106, 342-372): the reference puts them into FitErrors strings
+_QNAME_FMT = "([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]"
+_QNAME_MSG = ("must consist of alphanumeric characters, '-', '_' or '.', and must start and end with an "
+              "alphanumeric character")
+_DNS1123_FMT = "[a-z0-9]([-a-z0-9]*[a-z0-9])?(\\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*"
+_DNS1123_MSG = ("a DNS-1123 subdomain must consist of lower case alphanumeric characters, '-' or '.', and must "
+                "start and end with an alphanumeric character")
+_LABEL_FMT = "(" + _QNAME_FMT + ")?"
+_LABEL_MSG = ("a valid label must be an empty string or consist of alphanumeric characters, '-', '_' or '.', and "
+              "must start and end with an alphanumeric character")
+
+
+def _regex_error(msg, fmt, *examples):  # RegexError (validation.go:347-362), double spaces included
+    if not examples:
+        return msg + " (regex used for validation is '" + fmt + "')"
+    msg += " (e.g. "
+    for i, e in enumerate(examples):
+        msg += (" or " if i else "") + "'" + e + "', "
+    return msg + "regex used for validation is '" + fmt + "')"
+
+
+_DNS1123_RE = re.compile(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*")
+
+
+def qualified_name_errors(v: str):  # IsQualifiedName (validation.go:42-71)
+    errs = []
     parts = v.split("/")
     if len(parts) == 1:
         name = parts[0]
     elif len(parts) == 2:
-        if not parts[0] or not _dns1123_subdomain(parts[0]):
-            return False
-        name = parts[1]
+        prefix, name = parts
+        if not prefix:
+            errs.append("prefix part must be non-empty")
+        else:  # IsDNS1123Subdomain (validation.go:135-144), each message prefixed
+            if len(prefix) > 253:
+                errs.append("prefix part must be no more than 253 characters")
+            if not _DNS1123_RE.fullmatch(prefix):
+                errs.append("prefix part " + _regex_error(_DNS1123_MSG, _DNS1123_FMT, "example.com"))
     else:
-        return False
-    return 0 < len(name) <= 63 and _qname_fmt(name)
+        return ["a qualified name " + _regex_error(_QNAME_MSG, _QNAME_FMT, "MyName", "my.name", "123-abc") +
+                " with an optional DNS subdomain prefix and '/' (e.g. 'example.com/MyName')"]
+    if not name:
+        errs.append("name part must be non-empty")
+    elif len(name) > 63:
+        errs.append("name part must be no more than 63 characters")
+    if not _qname_fmt(name):
+        errs.append("name part " + _regex_error(_QNAME_MSG, _QNAME_FMT, "MyName", "my.name", "123-abc"))
+    return errs
 
 
-def is_valid_label_value(v: str) -> bool:
-    return len(v) <= 63 and (v == "" or _qname_fmt(v))
+def label_value_errors(v: str):  # IsValidLabelValue (validation.go:97-106)
+    errs = []
+    if len(v) > 63:
+        errs.append("must be no more than 63 characters")
+    if not (v == "" or _qname_fmt(v)):
+        errs.append(_regex_error(_LABEL_MSG, _LABEL_FMT, "MyValue", "my_value", "12345"))
+    return errs
+
+
+def go_quote(s: str) -> str:
+    """fmt %q of a printable ASCII string (strconv.Quote)."""
+    return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
+
+
+def new_requirement_error(key: str, op: str, vals) -> str | None:
+    """labels.NewRequirement's error text (apimachinery/pkg/labels/selector.go:133-170), or None; op is the
+    selection operator ("=" for matchLabels pairs, "in", "notin", "exists", "!")."""
+    e = qualified_name_errors(key)
+    if e:
+        return f"invalid label key {go_quote(key)}: " + "; ".join(e)
+    if op in ("in", "notin") and not vals:
+        return "for 'in', 'notin' operators, values set can't be empty"
+    if op == "=" and len(vals) != 1:
+        return "exact-match compatibility requires one single value"
+    if op in ("exists", "!") and vals:
+        return "values set must be empty for exists and does not exist"
+    for v in vals:
+        e = label_value_errors(v)
+        if e:
+            return f"invalid label value: {go_quote(v)}: " + "; ".join(e)
+    return None
 
 
 def is_scalar_resource_name(n: str) -> bool:  # core/v1/helper/helpers.go:36-104
@@ -728,3 +795,72 @@ class Snapshot:
             if t["uid"] == uid:
                 return t["spec"]
         raise KeyError(uid)
+
+
+# ---- kb_apply rows: commits made outside the device ----------------------------------------------------
+def pod_delta(snap: Snapshot, pod: M.Pod, node: int, remove: bool = False, spec: int = -1, kind: int = 1):
+    """The kb_row_delta of NodeInfo.AddTask (or RemoveTask) of `pod` on session node `node` (api/node_info.go:
+    165-221) plus the plugins' schedulercache AddPod / RemovePod (cache/node_info.go:498-630): Idle /
+    Releasing by the pod's status, pod count, non-zero requests, host ports. The node's resource maps are the
+    session-open ones (a caller that commits in between keeps its own). Returns (row dict, scalar deltas,
+    ports): the scalar deltas are [idle per slot..., releasing per slot...] or None."""
+    st = task_status(pod)
+    rr = Res()
+    for c in pod.containers:
+        rr.add(Res.from_list(c.req))
+    idle, rel = snap.nodes[node]["idle"].copy(), snap.nodes[node]["rel"].copy()
+    i0, r0 = idle.copy(), rel.copy()
+    if not remove:
+        if st == ST["Releasing"]:
+            rel.add(rr)
+            idle.sub(rr)
+        elif st == ST["Pipelined"]:
+            rel.sub(rr)
+        else:
+            idle.sub(rr)
+    else:
+        if st == ST["Releasing"]:
+            rel.sub(rr)
+            idle.add(rr)
+        elif st == ST["Pipelined"]:
+            rel.add(rr)
+        else:
+            idle.add(rr)
+    sign = -1 if remove else 1
+    nzc = nzm = 0
+    for c in pod.containers:
+        a, b = nonzero(c.req)
+        nzc += a
+        nzm += b
+    flags_set = (NODE_IDLE_HAS_MAP if i0.sc is None and idle.sc is not None else 0) | \
+        (NODE_REL_HAS_MAP if r0.sc is None and rel.sc is not None else 0)
+    sc = None
+    if snap.scalars and (idle.sc is not None or rel.sc is not None):
+        sc = [(idle.sc or {}).get(k, 0) - (i0.sc or {}).get(k, 0) for k in snap.scalars] + \
+             [(rel.sc or {}).get(k, 0) - (r0.sc or {}).get(k, 0) for k in snap.scalars]
+    ports = []
+    for c in pod.containers:  # HostPortInfo.Add / Remove, only the (protocol, port) slots a spec asks for
+        for pt in c.ports:
+            hp = int(pt.get("hostPort", 0) or 0)
+            s_id = snap.port_slots.ids.get((pt.get("protocol") or "TCP", hp)) if hp > 0 else None
+            if s_id is not None:
+                ports.append((s_id, snap.port_ips[s_id].ids.get(pt.get("hostIP") or "0.0.0.0", 63)))
+    row = {"node": node, "pods": sign, "idle_cpu": idle.cpu - i0.cpu, "idle_mem": idle.mem - i0.mem,
+           "rel_cpu": rel.cpu - r0.cpu, "rel_mem": rel.mem - r0.mem, "nz_cpu": sign * nzc, "nz_mem": sign * nzm,
+           "flags_set": flags_set, "flags_clear": 0, "spec": spec, "kind": kind}
+    return row, sc, ports
+
+
+def row_deltas(rows):
+    """Pack pod_delta results into kb_apply's arrays (deltas, scalar deltas, ports)."""
+    from .runtime import ROW_DELTA_DTYPE
+    d = np.zeros(len(rows), ROW_DELTA_DTYPE)
+    sc, ports = [], []
+    for i, (row, s, p) in enumerate(rows):
+        for k, v in row.items():
+            d[i][k] = v
+        d[i]["sc_off"] = 0xffffffff if s is None else len(sc)
+        sc += s or []
+        d[i]["port_off"], d[i]["port_cnt"] = len(ports), len(p)
+        ports += p
+    return d, np.array(sc, np.int64), np.array(ports, PORT_DTYPE) if ports else np.zeros(0, PORT_DTYPE)

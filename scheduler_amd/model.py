@@ -183,6 +183,47 @@ def default_tiers(nodeorder_args=None, predicate_args=None):
     ]
 
 
+# pkg/scheduler/util.go:30-40 (defaultSchedulerConf)
+DEFAULT_SCHEDULER_CONF = """
+actions: "allocate, backfill"
+tiers:
+- plugins:
+  - name: priority
+  - name: gang
+- plugins:
+  - name: drf
+  - name: predicates
+  - name: proportion
+  - name: nodeorder
+"""
+ACTIONS = ("reclaim", "allocate", "backfill", "preempt", "enqueue")  # actions/factory.go:29-35
+# conf.PluginOption yaml tags (conf/scheduler_conf.go:33-56) -> the flag names used in tier dicts
+_YAML_FLAGS = {"enable" + f[len("enabled"):]: f for f in PLUGIN_FLAGS}
+
+
+def load_scheduler_conf(text: str):
+    """loadSchedulerConf (pkg/scheduler/util.go:44-73): parse the YAML conf, apply the plugin defaults to
+    every unset enable flag (plugins/defaults.go:22-52) and resolve the comma-separated action list.
+    Returns (action names, tiers); an unknown action raises ValueError as the reference returns an error."""
+    import yaml
+    doc = yaml.safe_load(text) or {}
+    tiers = []
+    for t in doc.get("tiers") or []:
+        plugins = []
+        for p in t.get("plugins") or []:
+            flags = {_YAML_FLAGS[k]: bool(v) for k, v in p.items() if k in _YAML_FLAGS and v is not None}
+            args = {str(k): str(v) for k, v in (p.get("arguments") or {}).items()}
+            plugins.append(plugin(p.get("name", ""), args, defaults=True, **flags))
+        tiers.append({"plugins": plugins})
+    actions = []
+    for name in str(doc.get("actions", "")).split(","):
+        name = name.strip()
+        if name not in ACTIONS:
+            raise ValueError(f"failed to found Action {name}, ignore it")
+        actions.append(name)
+    return actions, tiers
+
+
 @dataclass
 class Cluster:
     """The scheduler cache contents one allocate cycle snapshots."""

@@ -16,7 +16,8 @@ from . import export as E
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KBGPU_LIB", os.path.join(_HERE, "libkbgpu.so"))
 
-KB_NUM_REASONS = 16
+KB_NUM_REASONS = 17
+KB_R_HOST_ERROR = 16
 KB_OK, KB_E_INVALID, KB_E_HIP, KB_E_UNSUPPORTED, KB_E_NOMEM, KB_E_PANIC, KB_E_STATE = 0, -1, -2, -3, -4, -5, -6
 KB_STOP_DONE, KB_STOP_NO_FIT, KB_STOP_READY = 0, 1, 2
 KB_PLACE_ALLOCATE, KB_PLACE_PIPELINE = 1, 2
@@ -57,6 +58,15 @@ class kb_shard(C.Structure):
 
 # kb_allgather_fn: int (*)(void* user, const void* send, void* recv, size_t bytes)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+# kb_nofit_fn: void (*)(void* user, int32_t job, int32_t task, uint32_t n_events, const uint32_t* reasons, uint32_t n)
+NOFIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32)
+
+# kb_row_delta (kb_apply)
+ROW_DELTA_DTYPE = np.dtype([("node", "<i4"), ("pods", "<i4"), ("idle_cpu", "<i8"), ("idle_mem", "<i8"),
+                            ("rel_cpu", "<i8"), ("rel_mem", "<i8"), ("nz_cpu", "<i8"), ("nz_mem", "<i8"),
+                            ("flags_set", "<u4"), ("flags_clear", "<u4"), ("spec", "<i4"), ("kind", "<i4"),
+                            ("sc_off", "<u4"), ("port_off", "<u4"), ("port_cnt", "<u4"), ("pad", "<i4")], align=True)
+assert ROW_DELTA_DTYPE.itemsize == 88
 
 
 def shard_range(n_total: int, rank: int, world: int):
@@ -116,11 +126,12 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 7  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 8  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
-           "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl"]
+           "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl",
+           "kb_set_host_overlay", "kb_apply", "kb_set_nofit_hook"]
 
 _lib = None
 
@@ -160,6 +171,9 @@ def load_library(path: str = LIB_PATH):
     lib.kb_set_shard.argtypes = [P, C.POINTER(kb_shard), ALLGATHER_FN, P]
     lib.kb_comm_unique_id.argtypes = [P]
     lib.kb_set_shard_rccl.argtypes = [P, C.POINTER(kb_shard), P]
+    lib.kb_set_host_overlay.argtypes = [P, C.c_int32, P, P]
+    lib.kb_apply.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32]
+    lib.kb_set_nofit_hook.argtypes = [P, NOFIT_FN, P]
     _lib = lib
     return lib
 
@@ -174,6 +188,7 @@ class Context:
     def __init__(self, device: int = 0, timing: bool = False, path: str = "select", timing_every: int = 1):
         self.lib = load_library()
         self._keep = []
+        self.overlay_reason = {}
         opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | PATHS[path], timing_every)
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
@@ -259,6 +274,43 @@ class Context:
     def restore(self):
         self._check(self.lib.kb_restore_nodes(self.ctx))
 
+    # ---- per-node Go fallback (kb_set_host_overlay / kb_apply / kb_set_nofit_hook) ----
+    def set_host_overlay(self, spec: int, fail=None, score=None, reason=None):
+        """A plugin predicate / node-order fn the device does not express, evaluated per node on the host:
+        fail[i] rejects node i (KB_R_HOST_ERROR), score[i] is added to its order score. `reason` is the
+        plugin's FitErrors string for a rejected node: a str or a callable(node name) -> str (result_dict puts
+        it into the job's histogram). No arrays: clear the overlay."""
+        n = self.n_nodes
+        f = None if fail is None else np.ascontiguousarray(np.asarray(fail, dtype=np.uint8).reshape(n))
+        sc = None if score is None else np.ascontiguousarray(np.asarray(score, dtype=np.int64).reshape(n))
+        self._check(self.lib.kb_set_host_overlay(self.ctx, int(spec), _ptr(f), _ptr(sc)))
+        if f is None and sc is None:
+            self.overlay_reason.pop(int(spec), None)
+        else:
+            self.overlay_reason[int(spec)] = reason
+
+    def apply(self, deltas, sc=None, ports=None):
+        """kb_apply: rows changed by commits made outside the device (ROW_DELTA_DTYPE records; see
+        export.pod_delta for one pod's AddTask + AddPod)."""
+        d = np.ascontiguousarray(np.asarray(deltas, dtype=ROW_DELTA_DTYPE))
+        sc = np.ascontiguousarray(np.asarray(sc if sc is not None else [], dtype=np.int64))
+        pt = np.ascontiguousarray(np.asarray(ports if ports is not None else [], dtype=E.PORT_DTYPE))
+        self._check(self.lib.kb_apply(self.ctx, _ptr(d), len(d), _ptr(sc), len(sc), _ptr(pt), len(pt)))
+
+    def _hook(self):
+        """Collect the per-node reason masks kb_allocate hands over at a NO_FIT with host-evaluated stages."""
+        if getattr(self, "_nofit_cb", None) is not None:
+            return
+
+        def cb(user, job, task, n_events, reasons, n):
+            try:
+                self._nofit[int(job)] = (int(task), int(n_events), np.ctypeslib.as_array(reasons, shape=(n,)).copy())
+            except Exception:  # an error must not unwind through the C frames
+                self._nofit_err = True
+        self._nofit = {}
+        self._nofit_cb = NOFIT_FN(cb)  # kept alive as long as the context
+        self._check(self.lib.kb_set_nofit_hook(self.ctx, self._nofit_cb, None))
+
     def stats(self, reset=False):
         st = kb_stats()
         self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
@@ -314,7 +366,14 @@ class Context:
                "event_task": np.zeros(max(nt, 1), np.int32)}
         res = kb_cycle_result(*[_ptr(out[k]) for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist",
                                                        "event_task")], 0, 0, 0.0, 0.0)
+        self._hook()
+        self._nofit = {}
+        self._nofit_err = False
         self._check(self.lib.kb_allocate(self.ctx, C.byref(ssn), C.byref(res)))
+        if self._nofit_err:
+            raise KbError(KB_E_INVALID, "NO_FIT hook failed")
+        out["nofit"] = dict(self._nofit)
+        out["overlay_reason"] = dict(self.overlay_reason)
         out["n_events"] = res.n_events
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
@@ -407,10 +466,40 @@ def result_dict(snap: E.Snapshot, out: dict) -> dict:
     for j, job in enumerate(snap.jobs):
         ft = int(out["job_fail_task"][j])
         if ft >= 0:
-            hist = {E.REASONS[b]: int(c) for b, c in enumerate(out["job_reason_hist"][j]) if c}
+            hist = {E.REASONS[b]: int(c) for b, c in enumerate(out["job_reason_hist"][j]) if c and b != KB_R_HOST_ERROR}
+            if out["job_reason_hist"][j][KB_R_HOST_ERROR]:
+                for k, c in host_reason_strings(snap, out, j, ft).items():
+                    hist[k] = hist.get(k, 0) + c
             fit[job["uid"]] = {ts[ft]["uid"]: hist}
     return {"events": events, "binds": binds, "fit_errors": fit, "status": status, "nodes": names,
             "elapsed_ms": out["elapsed_ms"], "device_ms": out["device_ms"]}
+
+
+def host_reason_strings(snap: E.Snapshot, out: dict, job: int, task: int) -> dict:
+    """The strings of the KB_R_HOST_ERROR bucket of a failed job: per node that failed there, the error the
+    reference's affinity predicate returns (affinity.Tables.host_error_string) or the overlay plugin's reason
+    (FitErrors.SetNodeError, api/unschedule_info.go:40-54)."""
+    names = snap.node_names()
+    t = snap.session_tasks[task]
+    spec = int(t["spec"])
+    if job not in out.get("nofit", {}):
+        raise KbError(KB_E_STATE, f"job {job}: host-evaluated reasons without the NO_FIT hook's node masks")
+    _, n_events, reasons = out["nofit"][job]
+    before = []
+    for i in range(n_events):
+        u = int(out["event_task"][i])
+        if out["task_status"][u] != E.ST["Pipelined"]:
+            before.append((snap.session_tasks[u]["uid"], int(snap.session_tasks[u]["spec"])))
+    aff_err = snap.aff is not None and (spec in snap.aff.own_err or snap.aff.xb_pods or snap.aff.xb_spec)
+    ov = out.get("overlay_reason", {}).get(spec)
+    hist = {}
+    for i in np.nonzero((reasons >> KB_R_HOST_ERROR) & 1)[0]:
+        if aff_err:
+            s = snap.aff.host_error_string(t["pod"], spec, names[i], before)
+        else:
+            s = ov(names[i]) if callable(ov) else str(ov)
+        hist[s] = hist.get(s, 0) + 1
+    return hist
 
 
 def allocate(cluster, device: int = 0, path: str = "select") -> dict:

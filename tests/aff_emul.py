@@ -10,7 +10,7 @@ import numpy as np
 
 from scheduler_amd import affinity as A
 
-R_POD_AFFINITY, R_EXISTING_ANTI, R_AFFINITY_RULES, R_ANTI_RULES = 12, 13, 14, 15
+R_POD_AFFINITY, R_EXISTING_ANTI, R_AFFINITY_RULES, R_ANTI_RULES, R_HOST_ERROR = 12, 13, 14, 15, 16
 
 
 class Tables:
@@ -38,6 +38,9 @@ class Tables:
             elif c["kind"] == A.AFF_ANTI:
                 fail = cnt > 0
                 bits = (1 << R_POD_AFFINITY) | (1 << R_ANTI_RULES)
+            elif c["kind"] == A.AFF_ERROR:  # the reference's predicate returns a plain error
+                fail = cnt > 0
+                bits = 1 << R_HOST_ERROR
             else:
                 match = cnt > 0
                 fail = ~match & ((self.totals[c["table"]] > 0) | (row["self_match"] == 0))

@@ -205,3 +205,76 @@ def affinity_clusters():
         ("aff-edge", affinity_edge_cluster()),
         ("aff-edge-b", affinity_edge_cluster(seed=12, n_nodes=25)),
     ]
+
+
+def affinity_error_clusters():
+    """Inputs where the reference's inter-pod affinity code returns a plain error (FitErrors gets the error's
+    string) or its score errors (SelectBestNode panics). Each is affinity_edge_cluster plus one change."""
+    import copy
+    base = affinity_edge_cluster(seed=13, n_nodes=30)
+    bad_in = {"labelSelector": {"matchExpressions": [{"key": "app", "operator": "In", "values": []}]}}
+    bad_key = {"labelSelector": {"matchLabels": {"bad key!": "x"}}}
+    bad_op = {"labelSelector": {"matchExpressions": [{"key": "app", "operator": "Gt", "values": ["1"]}]}}
+
+    def pending(cl, name, aff, labels=None, n=4):
+        cl.pod_groups.append(m.PodGroup(ns="ns", name=name, queue="q", min_member=1))
+        for t in range(n):
+            cl.pods.append(m.Pod(ns="ns", name=f"{name}-{t}", uid=f"ns-{name}-{t}", group=name,
+                                 labels=dict(labels or {"job": name}), affinity=aff,
+                                 containers=[m.Container(req={m.CPU: 1000, m.MEMORY: 2 * GI})]))
+        return cl
+    out = []
+    # (b) a running lister pod with an invalid required anti-affinity selector: every pending pod errors
+    cl = copy.deepcopy(base)
+    run = next(p for p in cl.pods if p.name == "db-0")
+    run.affinity = {"podAntiAffinity": {"required": [dict(bad_in, topologyKey="zone")]}}
+    out.append(("err-existing-anti", cl))
+    # (a) a pending pod's required affinity with an invalid selector / operator
+    out.append(("err-own-affinity", pending(copy.deepcopy(base), "bad-aff",
+                                            {"podAffinity": {"required": [dict(bad_key, topologyKey="zone")]}})))
+    out.append(("err-own-affinity-op", pending(copy.deepcopy(base), "bad-op", {"podAffinity": {"required": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "zone"}, dict(bad_op, topologyKey="rack")]}})))
+    # (a') its required anti-affinity invalid: every node fails the anti rule while the lister has a pod
+    out.append(("err-own-anti", pending(copy.deepcopy(base), "bad-anti",
+                                        {"podAntiAffinity": {"required": [dict(bad_in, topologyKey="zone")]}})))
+    # (c) an empty topologyKey in required affinity: errors where the earlier terms' topology is shared
+    out.append(("err-empty-key", pending(copy.deepcopy(base), "nokey", {"podAffinity": {"required": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "zone"},
+        {"labelSelector": {"matchLabels": {"tier": "data"}}, "topologyKey": ""}]}})))
+    out.append(("err-empty-key-first", pending(copy.deepcopy(base), "nokey0", {"podAffinity": {"required": [
+        {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": ""}]}})))
+    # (c') an empty topologyKey in required anti-affinity (a failure reason, not an error)
+    out.append(("err-empty-key-anti", pending(copy.deepcopy(base), "nokeyanti", {"podAntiAffinity": {"required": [
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "rack"},
+        {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": ""}]}})))
+    # (b) arising mid-cycle: no lister pods at session open; the first job's commits carry an invalid required
+    # anti-affinity term, so every later task errors
+    cl = m.Cluster(tiers=m.default_tiers())
+    for i in range(12):
+        cl.nodes.append(m.Node(name=f"n{i:02d}", alloc={m.CPU: 16000, m.MEMORY: 64 * GI, m.PODS: 20},
+                               labels={"kubernetes.io/hostname": f"n{i:02d}", "zone": f"z{i % 3}"}))
+    cl.queues.append(m.Queue(name="q", weight=1))
+    pending(cl, "a-first", {"podAntiAffinity": {"required": [dict(bad_key, topologyKey="zone")]}}, n=2)
+    pending(cl, "b-later", None, n=3)
+    pending(cl, "c-later", {"podAffinity": {"preferred": [{"weight": 5, "podAffinityTerm": {
+        "labelSelector": {"matchLabels": {"job": "b-later"}}, "topologyKey": "zone"}}]}}, n=2)
+    out.append(("err-existing-anti-dynamic", cl))
+    return out
+
+
+def ipa_error_clusters():
+    """The InterPodAffinity score errors (an invalid selector among the terms it meets): SelectBestNode panics
+    once a task has a feasible node (scheduler_helper.go:101-105,147-158)."""
+    import copy
+    base = affinity_edge_cluster(seed=14, n_nodes=20)
+    bad = {"labelSelector": {"matchExpressions": [{"key": "app", "operator": "NotIn", "values": []}]}}
+    cl = copy.deepcopy(base)  # an existing pod's preferred affinity term is invalid
+    next(p for p in cl.pods if p.name == "web-0").affinity = {"podAffinity": {"preferred": [
+        {"weight": 3, "podAffinityTerm": dict(bad, topologyKey="rack")}]}}
+    out = [("ipa-err-existing", cl)]
+    cl = copy.deepcopy(base)  # a pending pod's own preferred anti-affinity term is invalid
+    for p in cl.pods:
+        if p.group == "plain":
+            p.affinity = {"podAntiAffinity": {"preferred": [{"weight": 2, "podAffinityTerm": dict(bad, topologyKey="zone")}]}}
+    out.append(("ipa-err-own", cl))
+    return out

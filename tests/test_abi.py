@@ -24,13 +24,13 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 7
+    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 8
 
 
 def test_struct_layouts_match_header():
     # sizes follow the C layout of include/kbgpu.h (x86-64 SysV, natural alignment)
     assert ctypes.sizeof(runtime.kb_nodes) == 16 + 18 * 8
-    assert ctypes.sizeof(runtime.kb_job_result) == 16 + 16 * 4
+    assert ctypes.sizeof(runtime.kb_job_result) == 16 + 17 * 4
     assert ctypes.sizeof(runtime.kb_config) == 9 * 4
     from scheduler_amd import export
     assert export.SPEC_DTYPE.itemsize == 112
@@ -64,7 +64,7 @@ def test_struct_sizes_agree_with_the_c_compiler(tmp_path):
             "kb_term": export.TERM_DTYPE.itemsize, "kb_port": export.PORT_DTYPE.itemsize,
             "kb_aff_table": A.AFF_TABLE_DTYPE.itemsize, "kb_aff_check": A.AFF_CHECK_DTYPE.itemsize,
             "kb_ipa_hist": A.IPA_HIST_DTYPE.itemsize, "kb_ipa_incr": A.IPA_INCR_DTYPE.itemsize,
-            "kb_aff_spec": A.AFF_SPEC_DTYPE.itemsize}
+            "kb_aff_spec": A.AFF_SPEC_DTYPE.itemsize, "kb_row_delta": runtime.ROW_DELTA_DTYPE.itemsize}
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "kbgpu.h"\nint main(void) {\n' +
                    "".join(f'  printf("{k} %zu\\n", sizeof({k}));\n' for k in ours) + "  return 0;\n}\n")

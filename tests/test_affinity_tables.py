@@ -97,15 +97,23 @@ def test_tables_after_commits(name, cluster):
 
 
 def test_unsupported_inputs_fail_loudly():
+    """What the device path still refuses (export.Unsupported, never a CPU fallback): a lister pod on a node
+    outside the session (the predicate's node lookup errors), and a pending pod with invalid score terms that
+    could commit (later scores would error mid-cycle)."""
     base = affinity_clusters()[2][1]
     bad = copy.deepcopy(base)
-    bad.pods[-1].affinity = {"podAffinity": {"required": [{"labelSelector": {"matchLabels": {"a": "b"}},
-                                                             "topologyKey": ""}]}}
+    p = next(p for p in bad.pods if p.name == "db-1")
+    p.node = "elsewhere"  # a node the cache does not know
     with pytest.raises(E.Unsupported):
         E.Snapshot(bad)
-    bad = copy.deepcopy(base)
-    bad.pods[-1].affinity = {"podAntiAffinity": {"required": [{"labelSelector": {"matchExpressions": [
-        {"key": "a", "operator": "In", "values": []}]}, "topologyKey": "zone"}]}}
+    # no pod runs anywhere, so the pod's own score cannot error (nothing to process its terms against)
+    bad = m.Cluster(nodes=[m.Node(name=f"n{i}", alloc={m.CPU: 8000, m.MEMORY: 16 * 2 ** 30, m.PODS: 10},
+                                  labels={"zone": "z"}) for i in range(3)], queues=[m.Queue(name="q")])
+    bad.pod_groups.append(m.PodGroup(ns="ns", name="g", queue="q", min_member=1))
+    bad.pods.append(m.Pod(ns="ns", name="g-0", uid="ns-g-0", group="g", containers=[m.Container(req={m.CPU: 100})],
+                          affinity={"podAntiAffinity": {"preferred": [{"weight": 1, "podAffinityTerm": {
+                              "labelSelector": {"matchExpressions": [{"key": "a", "operator": "In", "values": []}]},
+                              "topologyKey": "zone"}}]}}))
     with pytest.raises(E.Unsupported):
         E.Snapshot(bad)
 

@@ -265,3 +265,100 @@ def test_scalar_resource_names():  # core/v1/helper/helpers.go:36-104
 def test_selector_semantics(exprs, labels, valid, exp):
     r = pyoracle.resource_op("SelectorMatches", exprs=exprs, labels=labels)
     assert r["valid"] is valid and r["result"] is exp
+
+
+# --- pkg/scheduler/api/job_info_test.go ------------------------------------
+def _api_pod(ns, name, node, phase, cpu, mem):  # api/test_utils.go:71-94 (UID "<ns>-<name>")
+    return m.Pod(ns=ns, name=name, uid=f"{ns}-{name}", node=node, phase=phase,
+                 containers=[m.Container(req=m.canon_resource_list({"cpu": cpu, "memory": mem}))]).to_json()
+
+
+def _cm(r):
+    return (r["cpu"], r["memory"])
+
+
+def test_job_add_task_info():  # TestAddTaskInfo :35-102
+    pods = [_api_pod("c1", "p1", "", "Pending", "1000m", "1G"), _api_pod("c1", "p2", "n1", "Running", "2000m", "2G"),
+            _api_pod("c1", "p3", "n1", "Pending", "1000m", "1G"), _api_pod("c1", "p4", "n1", "Pending", "1000m", "1G")]
+    r = pyoracle.resource_op("JobTasks", pods=pods)
+    assert _cm(r["allocated"]) == (4000, 4e9)
+    assert _cm(r["total_request"]) == (5000, 5e9)
+    assert r["status_index"] == {"Pending": ["c1-p1"], "Bound": ["c1-p3", "c1-p4"], "Running": ["c1-p2"]}
+    assert r["tasks"] == ["c1-p1", "c1-p2", "c1-p3", "c1-p4"]
+
+
+@pytest.mark.parametrize("ns,pods,rm", [  # TestDeleteTaskInfo :104-200
+    ("c1", [("p1", "", "Pending", "1000m", "1G"), ("p2", "n1", "Running", "2000m", "2G"),
+            ("p3", "n1", "Running", "3000m", "3G")], "p2"),
+    ("c2", [("p1", "", "Pending", "1000m", "1G"), ("p2", "n1", "Pending", "2000m", "2G"),
+            ("p3", "n1", "Running", "3000m", "3G")], "p2"),
+])
+def test_job_delete_task_info(ns, pods, rm):
+    ps = {p[0]: _api_pod(ns, *p) for p in pods}
+    r = pyoracle.resource_op("JobTasks", pods=list(ps.values()), remove=[ps[rm]])
+    assert _cm(r["allocated"]) == (3000, 3e9)
+    assert _cm(r["total_request"]) == (4000, 4e9)
+    assert r["status_index"] == {"Pending": [f"{ns}-p1"], "Running": [f"{ns}-p3"]}
+    assert r["tasks"] == [f"{ns}-p1", f"{ns}-p3"]
+
+
+# --- pkg/scheduler/cache/cache_test.go -------------------------------------
+@pytest.mark.parametrize("pods_first", [False, True])  # TestAddPod :128-188 (node first), TestAddNode :190-259
+def test_cache_node_and_job_state(pods_first):
+    """The cache's NodeInfo for n1 holds the running pod p2 (Idle 1000m / 9G, Used 1000m / 1G) whichever of
+    node and pods arrives first, and the job holds both tasks. The session snapshot is built from the final
+    state only (cache/cache.go:584-654), so the arrival order cannot change it."""
+    node = m.build_node("n1", m.canon_resource_list({"cpu": "2000m", "memory": "10G"})).to_json()
+    p1 = _api_pod("c1", "p1", "", "Pending", "1000m", "1G")
+    p2 = _api_pod("c1", "p2", "n1", "Running", "1000m", "1G")
+    r = pyoracle.resource_op("NodeTasks", node=node, pods=[p2])
+    assert _cm(r["idle"]) == (1000, 9e9) and _cm(r["used"]) == (1000, 1e9) and r["tasks"] == ["c1/p2"]
+    j = pyoracle.resource_op("JobTasks", pods=[p2, p1] if pods_first else [p1, p2])
+    assert j["tasks"] == ["c1-p1", "c1-p2"]
+    assert _cm(j["allocated"]) == (1000, 1e9) and _cm(j["total_request"]) == (2000, 2e9)
+
+
+def test_cache_pods_without_job_are_not_scheduled():  # TestGetOrCreateJob :261-306 (group-annotated part)
+    """A pod that belongs to a job (pi1) becomes a task of a session job; a pod with no job of its own (pi3,
+    other scheduler) does not, so allocate never places it. The shadow-PodGroup case (pi2) is out of scope
+    (DESIGN.md §8)."""
+    rl = m.build_resource_list
+    c = m.Cluster(nodes=[m.build_node("n1", dict(rl("2", "4Gi"), pods=10))],
+                  pods=[m.build_pod("c1", "p1", "", "Pending", rl("1", "1G"), "j1"),
+                        m.build_pod("c3", "p3", "", "Pending", rl("1", "1G"), "")],
+                  pod_groups=[m.PodGroup(ns="c1", name="j1", queue="q")], queues=[m.Queue(name="q")])
+    out = pyoracle.allocate(c)
+    assert out["binds"] == {"c1/p1": "n1"}
+    assert out["status"]["c3-p3"] == "Pending"
+
+
+# --- pkg/scheduler/util_test.go ---------------------------------------------
+def test_load_scheduler_conf():  # TestLoadSchedulerConf :27-120
+    conf = """
+actions: "allocate, backfill"
+tiers:
+- plugins:
+  - name: priority
+  - name: gang
+  - name: conformance
+- plugins:
+  - name: drf
+  - name: predicates
+  - name: proportion
+  - name: nodeorder
+"""
+    actions, tiers = m.load_scheduler_conf(conf)
+    assert actions == ["allocate", "backfill"]
+    expected = [[m.plugin(n) for n in ("priority", "gang", "conformance")],
+                [m.plugin(n) for n in ("drf", "predicates", "proportion", "nodeorder")]]
+    assert [t["plugins"] for t in tiers] == expected
+    for t in tiers:
+        for p in t["plugins"]:
+            assert all(p[f] is True for f in m.PLUGIN_FLAGS)
+    # the default conf (util.go:30-40) is the tier set the benchmarks and parity clusters use
+    assert m.load_scheduler_conf(m.DEFAULT_SCHEDULER_CONF) == (["allocate", "backfill"], m.default_tiers())
+    # an explicit false survives the defaults; an unknown action is an error (util.go:62-69)
+    _, t2 = m.load_scheduler_conf("actions: allocate\ntiers:\n- plugins:\n  - name: gang\n    enableJobReady: false\n")
+    assert t2[0]["plugins"][0]["enabledJobReady"] is False and t2[0]["plugins"][0]["enabledJobOrder"] is True
+    with pytest.raises(ValueError):
+        m.load_scheduler_conf("actions: allocate, shuffle\n")
