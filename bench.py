@@ -6,11 +6,17 @@ step   : one allocateAction.Execute (actions/allocate/allocate.go:42-193) over t
          then kb_allocate (host ordering plugins + per-job device sweep/argmax/commit). The snapshot is
          uploaded once before the timed region; value = pods placed / second over the timed steps.
 
-Multi-GPU (torchrun): every rank schedules its own independent C2 cluster partition (weak scaling, no
-data-path collective); torch.distributed is used only for the barrier and the max-over-ranks time.
+Multi-GPU (N > 1, one process per GPU): BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped
+nodes x 1M pods whose node table is sharded across the N ranks (each rank holds a contiguous block; per run
+segment the ranks exchange their proposals with one RCCL all-gather over xGMI; every rank commits its own
+rows). `value` = the cycle's pods / the max-over-ranks time. A rank holds at most SEL_NODES_PER_GPU rows
+on the selection path, so at N = 2 the cluster is 2 x that (stated in config.nodes). The replicas line
+(every rank an independent C2 cluster, no collective) is reported beside it under "replicas".
+`python bench.py --gpus N` without torchrun's environment starts the N ranks itself (before any GPU call).
 
-Extra JSON fields: roofline (dominant kernel, HIP events on the library's stream during the timed region)
-and cpu_baseline (the oracle's C++ restatement of the reference algorithm on a bounded sample).
+Extra JSON fields: roofline (dominant kernel, HIP events on the library's stream during the timed region),
+eval_roofline (the fit/score sweep kb_eval at 256 specs x 50k nodes: the HBM-bound kernel), and cpu_baseline
+(the oracle's C++ restatement of the reference algorithm on a bounded sample).
 """
 from __future__ import annotations
 
@@ -43,6 +49,7 @@ CONFIGS = {
                workload="C5: 50k nodes x 1M pods (C2 shape), node table sharded across the GPUs"),
 }
 ARRAY_CONFIGS = ("C2", "C5")  # built by synth.c2_snapshot (numpy) instead of per-pod objects
+SEL_NODES_PER_GPU = 24576  # the selection kernel's LDS plan (kbgpu_device.hip kSelQ4: 512 threads x 48 keys)
 
 
 def main():
@@ -50,8 +57,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
-                    help="BASELINE.json configuration (C2 = the headline metric's)")
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE.json configuration (default: C2, the headline metric's; C5 node-sharded at N>1)")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--tasks-per-job", type=int, default=None)
@@ -61,19 +68,30 @@ def main():
     ap.add_argument("--path", default="select", choices=["select", "engine", "trajectory", "rekey"],
                     help="device path for the runs (scheduler_amd.runtime.PATHS)")
     ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "shard"],
-                    help="N>1: replicas = every rank schedules its own cluster partition (weak scaling, no "
-                         "collective); shard = ONE cluster, node table split across the ranks, one RCCL all-gather "
-                         "per run segment. auto = replicas, plus a short sharded C5 measurement in the same line")
-    ap.add_argument("--shard-jobs", type=int, default=200, help="jobs of the sharded side measurement (auto, N>1)")
+                    help="N>1: shard = ONE cluster, node table split across the ranks, one RCCL all-gather per run "
+                         "segment; replicas = every rank schedules its own cluster (no collective). auto = shard "
+                         "(C5) as the line, plus a short replicas measurement beside it")
+    ap.add_argument("--side-steps", type=int, default=5, help="cycles of the side measurement (auto, N>1)")
+    ap.add_argument("--no-eval", action="store_true", help="skip the kb_eval roofline measurement (N=1)")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP events around the launches of every Nth job call of the timed region")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)  # torchrun's environment is missing: start the ranks (no GPU touched yet)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    mode = args.mode if args.mode != "auto" else ("shard" if world > 1 else "replicas")
+    args.mode = mode
+    args.config = args.config or ("C5" if mode == "shard" and world > 1 else "C2")
     cfg = CONFIGS[args.config]
     args.nodes = args.nodes or cfg["nodes"]
+    if mode == "shard" and world > 1:
+        args.nodes = min(args.nodes, SEL_NODES_PER_GPU * world)  # every rank's block on the selection path
     args.jobs = args.jobs or cfg["jobs"]
     args.tasks_per_job = args.tasks_per_job or cfg["tasks"]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # KB_BENCH_SAME_GPU=1: rehearse N ranks on one GPU (gloo process group, host-staged shard exchange)
@@ -149,8 +167,11 @@ def main():
             dist.all_reduce(p, op=dist.ReduceOp.SUM)
             total_placed = int(p.item())
     side = None
-    if args.mode == "auto" and world > 1:
-        side = shard_side(args, dist, rank, world, device)
+    if world > 1 and mode == "shard":
+        side = replicas_side(args, dist, rank, world, device)
+    ev = None
+    if world == 1 and rank == 0 and not args.no_eval:
+        ev = eval_side(device)
 
     # roofline: dominant kernel by summed event time
     kern_ms = [0.0 if runtime.KERNELS[i] == "shard_exchange" else v for i, v in enumerate(st["kernel_ms"])]
@@ -192,6 +213,8 @@ def main():
     workload = cfg["workload"]
     if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
         workload = f"{args.config} shape at {args.nodes} nodes x {args.jobs * args.tasks_per_job} pods"
+        if shard and args.nodes < cfg["nodes"]:
+            workload += f" (node table sharded {world} ways, at most {SEL_NODES_PER_GPU} rows per GPU)"
     result = None
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -219,8 +242,11 @@ def main():
             "job_calls_per_step": st["job_calls"] / args.steps,
             "roofline": roofline,
             "cpu_baseline": cpu,
-            **({"shard_exchange_us_per_segment": exchange_us(st)} if shard else {}),
-            **({"sharded": side} if side is not None else {}),
+            **({"shard_exchange_us_per_segment": exchange_us(st),
+                "shard_segments_per_step": st["launches"][runtime.KERNELS.index("shard_exchange")] / args.steps}
+               if shard else {}),
+            **({"replicas": side} if side is not None else {}),
+            **({"eval_roofline": ev} if ev is not None else {}),
         }
         print(json.dumps(result), flush=True)
     ctx.close()
@@ -259,39 +285,86 @@ def exchange_us(st):
     return round(st["kernel_ms"][k] * 1e3 / st["launches"][k], 2) if st["launches"][k] else None
 
 
-def shard_side(args, dist, rank, world, device):
-    """The node-sharded path measured next to the replicas line: ONE C5-shaped cluster (50k nodes, or 20k
-    per rank when fewer ranks would overflow the selection kernel's LDS plan), the first `shard_jobs` jobs,
-    node table split across the ranks, one RCCL all-gather per run segment. Reports pods/s (max-over-ranks
-    wall time) and the per-segment exchange latency (HIP events around ncclAllGather)."""
+def replicas_side(args, dist, rank, world, device):
+    """Beside the sharded line: every rank schedules its own independent C2 cluster (different seed per rank,
+    no collective), `side_steps` cycles; pods/s over all ranks at the max-over-ranks time."""
     import torch
     from scheduler_amd import runtime, synth
-    nodes = min(50000, 20000 * world)
     try:
-        snap = synth.c2_snapshot(n_nodes=nodes, n_jobs=args.shard_jobs, tasks_per_job=100, seed=synth.SEED)
-        ctx = runtime.Context(device, timing=True, timing_every=1)
-        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+        c = CONFIGS["C2"]
+        snap = synth.c2_snapshot(n_nodes=c["nodes"], n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED + rank)
+        ctx = runtime.Context(device)
         ctx.upload(snap)
         ctx.allocate(snap)  # warm-up cycle
-        ctx.restore()
-        ctx.stats(reset=True)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        out = ctx.allocate(snap)
+        placed = 0
+        for _ in range(args.side_steps):
+            ctx.restore()
+            placed += int(ctx.allocate(snap)["n_events"])
         dist.barrier()
         torch.cuda.synchronize()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tensor_device(dist, device))
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        st = ctx.stats()
+        p = torch.tensor([placed], dtype=torch.float64, device=tensor_device(dist, device))
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
         ctx.close()
-        placed = int(out["n_events"])
-        return {"workload": f"C5 shape, {nodes} nodes x {args.shard_jobs * 100} pods, node_shard{world}",
-                "value": round(placed / float(el.item()), 1), "unit": "pods/s", "pods_placed": placed,
-                "cycle_ms": round(float(el.item()) * 1e3, 3), "exchange_us_per_segment": exchange_us(st),
-                "segments": st["launches"][runtime.KERNELS.index("shard_exchange")]}
+        return {"workload": f"C2 replicas: {world} independent 10k x 100k clusters, one per rank (no collective)",
+                "value": round(float(p.item()) / float(el.item()), 1), "unit": "pods/s", "steps": args.side_steps,
+                "scaling": "weak", "ms_per_step": round(float(el.item()) / args.side_steps * 1e3, 3)}
     except Exception as e:  # the side measurement never takes the main line down
         return {"error": repr(e)[:300]}
+
+
+EVAL_SPECS, EVAL_NODES = 256, 50000
+
+
+def eval_side(device):
+    """The fit/score sweep on its own (kb_eval): reasons + scores of EVAL_SPECS specs x
+    EVAL_NODES nodes (a C2-shaped table, one spec per job). HIP events around the kernel; algorithmic bytes
+    = the output (4 B reason mask + 8 B score per pair) + one read of every node row (76 B), the least HBM
+    traffic the sweep needs. Measured HBM bytes come from the committed rocprofv3 PMC pass (pmc_traffic)."""
+    from scheduler_amd import runtime, synth
+    try:
+        snap = synth.c2_snapshot(n_nodes=EVAL_NODES, n_jobs=EVAL_SPECS, tasks_per_job=1, seed=synth.SEED)
+        ctx = runtime.Context(device, timing=True)
+        ctx.upload(snap)
+        ids = (np.arange(EVAL_SPECS) % len(snap.spec_arr)).astype(np.int32)  # (equal requests share a spec)
+        ctx.eval(ids)  # warm-up
+        ctx.stats(reset=True)
+        for _ in range(5):
+            ctx.eval(ids)
+        st = ctx.stats()
+        ctx.close()
+        k = runtime.KERNELS.index("eval_kernel")
+        us = st["kernel_ms"][k] * 1e3 / max(1, st["launches"][k])
+        pairs = len(ids) * EVAL_NODES
+        alg = pairs * 12 + EVAL_NODES * 76
+        out = {"kernel": "eval_kernel", "bound": "hbm", "specs": len(ids), "nodes": EVAL_NODES,
+               "avg_launch_us": round(us, 3), "algorithmic_bytes_per_launch": alg,
+               "achieved": round(alg / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None, "measured_frac": None}
+        tr = pmc_traffic("eval_kernel")
+        if tr is not None:
+            out["traffic"], out["traffic_source"] = tr["bytes_per_launch"], tr["source"]
+            out["measured_frac"] = round(tr["bytes_per_launch"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        return out
+    except Exception as e:
+        return {"error": repr(e)[:300]}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: run N ranks as `torch.distributed.run` children (one process per
+    GPU, rendezvous on 127.0.0.1) and exit with their code. Nothing here has touched the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def pmc_traffic(kernel):
@@ -349,4 +422,4 @@ def cpu_baseline(cluster, sample_tasks):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -385,6 +385,8 @@ typedef struct kb_stats {
   uint64_t job_calls;
   double device_ms;                   /* wall time inside kb_place_job */
   uint64_t diag[8];                   /* diagnostic builds only: place-loop phase cycles, [7] realtime */
+  uint64_t fed_abandon;               /* kb_allocate cycles the resident engine idled out of (host stall > its
+                                         idle bound): finished on the launch path */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

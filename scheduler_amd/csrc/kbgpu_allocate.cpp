@@ -12,6 +12,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kbgpu_ctx.h"
@@ -621,6 +622,11 @@ struct Driver {
     // KB_HOST_TRACE=1: per-job host timings on stderr at the end of the cycle (speculative issue, wait in
     // finish, bookkeeping after it)
     const bool trace = getenv("KB_HOST_TRACE") != nullptr;
+    const char* stall_env = getenv("KB_TEST_STALL_JOB");  // tests: sleep KB_TEST_STALL_MS before finishing job k
+    const int64_t stall_job = stall_env ? atoll(stall_env) : -1;
+    const char* stall_ms_env = getenv("KB_TEST_STALL_MS");
+    const int stall_ms = stall_ms_env ? atoi(stall_ms_env) : 1500;
+    uint64_t n_iter_all = 0;
     const auto loop0 = std::chrono::steady_clock::now();
     double t_spec = 0, t_fin = 0, t_apply = 0;
     uint64_t n_iter = 0;
@@ -632,12 +638,24 @@ struct Driver {
       int q2 = -1, j2 = -1;
       kb_job_pred pred{};
       const auto c0 = clk::now();
-      const bool spec = pipe && speculate(q, j, slot, q2, j2, pred);
+      bool spec = pipe && speculate(q, j, slot, q2, j2, pred);
       const auto c1 = clk::now();
+      if (stall_job >= 0 && (int64_t)n_iter_all == stall_job)  // KB_TEST_STALL_JOB: a host stall (GC pause, ...)
+        std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
+      ++n_iter_all;
       kb_job_result res;
       int rc;
       if (pipe) {
         rc = kb_job_finish(ctx, slot, pn.data(), pk.data(), &res, 0);
+        if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this job and the rest of the
+          rc = kb_fed_abandon(ctx);  // cycle run on the launch path (the speculative job never ran)
+          spec = false;
+          if (rc == KB_OK) {
+            const kb_job_req req = make_req(j);
+            rc = kb_job_issue(ctx, &req, slot, nullptr);
+          }
+          if (rc == KB_OK) rc = kb_job_finish(ctx, slot, pn.data(), pk.data(), &res, 0);
+        }
       } else {
         const kb_job_req req = make_req(j);
         rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res);
@@ -647,7 +665,8 @@ struct Driver {
                                                          (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
       if (spec && !match) {  // the guard fails on the device as well: drain the skipped job
         kb_job_result skip;
-        const int rc2 = kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &skip, 1);
+        int rc2 = kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &skip, 1);
+        if (rc2 == kFedIdleExit) rc2 = kb_fed_abandon(ctx);  // it never ran: nothing to drain
         if (rc == KB_OK) rc = rc2;
       }
       if (rc) return rc;

@@ -123,6 +123,7 @@ struct kb_ctx {
   bool prev_listed = false; // the last issued job was one selection run that lists its commits
   int prev_slot = -1;
   uint64_t n_overlap = 0;   // sweeps that ran overlapped
+  uint64_t n_fed_abandon = 0;  // cycles finished on the launch path after the engine idled out
   char* h_eval = nullptr;
 
   double device_ms = 0;  // wall time inside kb_place_job
@@ -174,6 +175,9 @@ extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, u
 extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, int spec);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);
+// kb_job_finish's code when the resident engine idled out before serving the job (see kb_fed_abandon)
+constexpr int kFedIdleExit = -100;
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_abandon(kb_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot,
                                                                   const kb_job_pred* pred);
 extern "C" __attribute__((visibility("hidden"))) int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node,

@@ -735,18 +735,26 @@ done:
                   seq);
 }
 
+// Parity / snapshot sweep (kb_eval): reasons + scores for T specs x N nodes. Node-stationary: a thread
+// loads its node's row once and evaluates kEvalSpecs specs against it (the spec fields are wave-uniform:
+// scalar loads), writing one coalesced 4 B + 8 B pair per spec. HBM traffic is the 12 B/pair of output; the
+// 76 B row is read once per kEvalSpecs specs.
+constexpr int kEvalSpecs = 16;
 template <bool AFF>
-__global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
+__global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids, int t,
                                                    uint32_t* reasons, int64_t* scores, const int64_t* mm) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = blockIdx.y;
   if (n >= N.n) return;
-  const int s = spec_ids[j];
-  const kb_spec sp = P.specs[s];
+  const int j0 = blockIdx.y * kEvalSpecs;
+  const int j1 = j0 + kEvalSpecs < t ? j0 + kEvalSpecs : t;
   const Row r = load_row(N, n);
-  const uint64_t st = static_eval<AFF>(N, P, C, sp, s, r.flags, n, AFF ? mm + 2 * j : nullptr);
-  reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
-  scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
+  for (int j = j0; j < j1; ++j) {
+    const int s = spec_ids[j];
+    const kb_spec sp = P.specs[s];
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, s, r.flags, n, AFF ? mm + 2 * j : nullptr);
+    reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
+    scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
+  }
 }
 
 // ===========================================================================
@@ -3453,12 +3461,12 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
-  dim3 grid((N.n + 255) / 256, t);
+  dim3 grid((N.n + 255) / 256, (t + kEvalSpecs - 1) / kEvalSpecs);
   if (mm)
-    hipLaunchKernelGGL(eval_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons, scores,
-                       mm);
+    hipLaunchKernelGGL(eval_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, reasons,
+                       scores, mm);
   else
-    hipLaunchKernelGGL(eval_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, reasons,
+    hipLaunchKernelGGL(eval_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, reasons,
                        scores, mm);
 }
 

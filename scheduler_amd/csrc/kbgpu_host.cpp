@@ -525,6 +525,11 @@ static int wait_seq(kb_ctx* c, const JobState* hs, uint32_t want) {
       hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) {
         if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == want) break;
+        if (c->fed) {  // the resident engine left: idle exit (a host stall longer than the idle bound)?
+          int32_t idle = 0;
+          if (hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
+            return fail(c, kFedIdleExit, "fed engine exited idle before command %u", want);
+        }
         return fail(c, KB_E_HIP, "place kernel finished without reporting (seq %u, want %u)", hs->seq, want);
       }
       if (q != hipErrorNotReady) return fail(c, KB_E_HIP, "place kernel failed: %s", hipGetErrorString(q));
@@ -1111,7 +1116,12 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
   return c->use_fed ? 1 : 0;
 }
 
-constexpr uint64_t kFedIdleTicks = 100000000ull;  // 1 s of s_memrealtime without a command: the engine exits
+// 1 s of s_memrealtime (100 MHz) without a command: the engine exits (KB_FED_IDLE_MS: tests shorten it)
+static uint64_t fed_idle_ticks() {
+  const char* e = getenv("KB_FED_IDLE_MS");
+  const long ms = e ? atol(e) : 0;
+  return ms > 0 ? (uint64_t)ms * 100000ull : 100000000ull;
+}
 
 int kb_fed_begin(kb_ctx* c) {
   if (!c) return KB_E_INVALID;
@@ -1145,7 +1155,7 @@ int kb_fed_begin(kb_ctx* c) {
     c->timing_now = tn;
   }
   launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count[0], c->fed_count[1],
-                    kFedIdleTicks, c->fed_exit, c->stream);
+                    fed_idle_ticks(), c->fed_exit, c->stream);
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1175,10 +1185,32 @@ int kb_fed_end(kb_ctx* c) {
   const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit
   if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
   if (c->timing) c->ev_collect(true);
+  // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;
-  if (rc == KB_OK && hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
-    rc = fail(c, KB_E_HIP, "fed engine exited idle (a command never arrived)");
+  if (rc == KB_OK && (c->slot[0].busy || c->slot[1].busy) &&
+      hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
+    rc = fail(c, KB_E_HIP, "fed engine exited idle with a job in flight");
   return rc;
+}
+
+// The engine idled out while the host stalled (kFedIdleExit from kb_job_finish): it served every command
+// before the one the host waits for and none after. Leave fed mode; the caller re-issues the unserved job on
+// the launch path (the speculative one, never run, is dropped) and the cycle goes on there.
+int kb_fed_abandon(kb_ctx* c) {
+  if (!c || !c->fed) return KB_OK;
+  c->fed = false;
+  if (c->fed_ev) {
+    c->ev_end(c->fed_ev, KB_KERNEL_FED_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
+    c->fed_ev = nullptr;
+  }
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream_b));  // the unserved jobs' sweeps (they only read rows)
+  HIP_OK(c, hipMemset(c->fed_exit, 0, sizeof(int32_t)));
+  c->slot[0].busy = c->slot[1].busy = false;
+  c->prev_listed = false;
+  c->n_fed_abandon++;
+  c->stats.fed_abandon++;
+  return KB_OK;
 }
 
 int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* pred) {

@@ -108,7 +108,8 @@ class kb_cycle_result(C.Structure):
 
 class kb_stats(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 14), ("kernel_ms", C.c_double * 14), ("pairs", C.c_uint64 * 14),
-                ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8)]
+                ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8),
+                ("fed_abandon", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -315,7 +316,8 @@ class Context:
         st = kb_stats()
         self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
         return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
-                "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag)}
+                "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag),
+                "fed_abandon": st.fed_abandon}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
@@ -383,12 +385,19 @@ class Context:
         """backfillAction.Execute (actions/backfill/backfill.go:40-90) on the session kb_allocate left in `out`.
 
         Jobs and their Pending tasks go in UID order (the maps of backfill.go:45, :54). A task whose InitResreq
-        is empty takes the first node, in the canonical node order, that passes Session.PredicateFn (:62-71):
-        on the device that is kb_place_job of a one-task job with the node order switched off, since every
-        score is then equal and the selection keeps the lowest feasible index. Commits are Session.Allocate
-        (the empty request always fits Idle), followed by the JobReady dispatch (session.go:286-294). A task
-        that fits nowhere records the device's FitErrors histogram (:84-86). Updates `out` in place and
-        returns it with "backfill_fit" = {job index: {task index: reason histogram}}."""
+        is empty takes the first node, in the canonical node order, that passes Session.PredicateFn (:62-71).
+        On the device that is kb_place_job with the node order switched off -- every score is then equal and
+        the selection keeps the lowest feasible index -- and the job's JobReady stop out of reach, so one call
+        places a whole run of same-spec tasks (each pick is still the lowest feasible index after the previous
+        commit). A task that fits nowhere records the device's FitErrors histogram (:84-86); the rest of its
+        run sees the same table and fails the same way. Commits are Session.Allocate, each followed by the
+        JobReady dispatch (session.go:286-294). Updates `out` in place and returns it with
+        "backfill_fit" = {job index: {task index: reason histogram}}.
+
+        The device's predicate also applies allocate's resource check (InitResreq <= Idle or Releasing), which
+        backfill.go does not: an empty request passes it unless a node's Idle is below the tolerance or the
+        scalar-map rule bites (a zero scalar request against a node without scalars, resource_info.go:264-267),
+        where the reference's own Resource.Sub would then assert. Such a divergence raises KbError."""
         cfg = dict(snap.config)
         tiers = [(int(p), int(en)) for _, p, en in snap.tier_plugins]
         has_gang = any(p == E.PLUGIN_IDS["gang"] for p, _ in tiers)
@@ -402,6 +411,7 @@ class Context:
         valid_st = alloc_st | E.ST["Succeeded"] | E.ST["Pipelined"] | E.ST["Pending"]
         fit = {}
         n_ev = int(out["n_events"])
+        never = 1 << 30  # JobReady never stops a backfill run on the device; the host replays it per task
         self._check(self.lib.kb_set_config(self.ctx, C.byref(kb_config(**dict(cfg, nodeorder_enabled=0)))))
         try:
             for j in np.argsort(snap.s_job_uid_rank, kind="stable"):
@@ -411,23 +421,39 @@ class Context:
                 tasks = by_job.get(j, [])
                 if has_gang and sum(1 for t in tasks if st[t] & valid_st) < snap.s_job_min[j]:
                     continue  # JobValid (gang.go:48-69)
-                for t in [t for t in tasks if st[t] == E.ST["Pending"]]:
-                    r = ts[t]["initreq"]
-                    if not (r.cpu < 10 and r.mem < 10 * 1024 * 1024 and all(q < 10 for q in (r.sc or {}).values())):
-                        continue  # Resource.IsEmpty (resource_info.go:96-108)
-                    spec = int(snap.s_task_spec[t])
-                    placed, kinds, res = self.place_job([spec], 0, 0, 0)
-                    if len(placed) == 0:
-                        fit.setdefault(j, {})[t] = np.array(res.reason_hist, np.uint32)
+                be = []
+                for t in tasks:
+                    if st[t] != E.ST["Pending"]:
                         continue
-                    st[t], node[t] = E.ST["Allocated"], int(placed[0])
-                    out["event_task"][n_ev] = t
-                    n_ev += 1
-                    ready = sum(1 for u in tasks if st[u] & (alloc_st | E.ST["Succeeded"]))
-                    if not gang_ready or ready >= snap.s_job_min[j]:
-                        for u in tasks:
-                            if st[u] == E.ST["Allocated"]:
+                    r = ts[t]["initreq"]
+                    if r.cpu < 10 and r.mem < 10 * 1024 * 1024 and all(q < 10 for q in (r.sc or {}).values()):
+                        be.append(t)  # Resource.IsEmpty (resource_info.go:96-108); others are left alone
+                ready = sum(1 for u in tasks if st[u] & (alloc_st | E.ST["Succeeded"]))
+                allocated = [u for u in tasks if st[u] == E.ST["Allocated"]]
+                k = 0
+                while k < len(be):
+                    spec = int(snap.s_task_spec[be[k]])
+                    e = k
+                    while e < len(be) and int(snap.s_task_spec[be[e]]) == spec:
+                        e += 1
+                    placed, kinds, res = self.place_job([spec] * (e - k), 0, never, 1)
+                    if (kinds != KB_PLACE_ALLOCATE).any() or (len(placed) < e - k and res.reason_hist[0]):
+                        raise KbError(KB_E_UNSUPPORTED, "backfill: the device's resource check diverges from "
+                                                        "backfill.go's PredicateFn-only test (DESIGN.md §7b)")
+                    for i, w in enumerate(placed):
+                        t = be[k + i]
+                        st[t], node[t] = E.ST["Allocated"], int(w)
+                        out["event_task"][n_ev] = t
+                        n_ev += 1
+                        ready += 1
+                        allocated.append(t)
+                        if not gang_ready or ready >= snap.s_job_min[j]:  # dispatch (session.go:286-294)
+                            for u in allocated:
                                 st[u] = E.ST["Binding"]
+                            allocated = []
+                    for t in be[k + len(placed):e]:  # the run's failed task and the rest of the run
+                        fit.setdefault(j, {})[t] = np.array(res.reason_hist, np.uint32)
+                    k = e
         finally:
             self._check(self.lib.kb_set_config(self.ctx, C.byref(kb_config(**cfg))))
         out["n_events"] = n_ev

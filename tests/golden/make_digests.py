@@ -1,0 +1,80 @@
+"""Full-size placement digests: the oracle's allocate outcome on BASELINE.json's
+configurations at full size, frozen as data so the GPU test can compare the HIP path against the oracle at
+the sizes the bench runs, without re-running the oracle on the GPU box.
+
+For each config: digest-<cfg>.npz holds the placement sequence (session-task index, node index, kind per
+event, in the cycle's order) plus every job's failing task, and digest-<cfg>.json the sha256 of those
+arrays, the counts and the FitErrors of the failed jobs. Indices follow export.Snapshot of the same
+seeded cluster (synth.CONFIGS[cfg]() with the generator defaults).
+
+Run from the repo root:  python tests/golden/make_digests.py C1 C2 [C3 C4]   (oracle on 8 threads;
+C2 takes about 1.5 minutes here, C3 several)
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from helpers import digest_arrays  # noqa: E402
+from oracle import pyoracle  # noqa: E402
+from scheduler_amd import export as E  # noqa: E402
+from scheduler_amd import synth  # noqa: E402
+
+KIND = {"allocate": 1, "pipeline": 2}
+
+
+# BASELINE.json configs[4] (C5: 50k nodes) has no single-GPU selection path; its sharded test compares the
+# first placements of a 300-job C5-shaped cluster with this prefix of the oracle's cycle
+HEADS = {"C5-head": (dict(n_nodes=50000, n_jobs=300, tasks_per_job=100), 3000)}
+
+
+def cluster_of(cfg):
+    if cfg in HEADS:
+        return synth.c2(**HEADS[cfg][0])
+    return synth.CONFIGS[cfg]()
+
+
+def make(cfg, workers=8):
+    cl = cluster_of(cfg)
+    snap = E.Snapshot(cl)
+    max_tasks = HEADS[cfg][1] if cfg in HEADS else -1
+    t0 = time.time()
+    out = pyoracle.allocate(cl, workers=workers, max_tasks=max_tasks)
+    secs = time.time() - t0
+    uid = {t["uid"]: i for i, t in enumerate(snap.session_tasks)}
+    nidx = snap.node_index
+    ev = out["events"]
+    event_task = np.array([uid[e["task"]] for e in ev], np.int32)
+    event_node = np.array([nidx[e["node"]] for e in ev], np.int32)
+    event_kind = np.array([KIND[e["kind"]] for e in ev], np.int8)
+    job_fail = np.full(len(snap.jobs), -1, np.int32)
+    jidx = {j["uid"]: i for i, j in enumerate(snap.jobs)}
+    for ju, tf in out["fit_errors"].items():
+        for tu in tf:
+            job_fail[jidx[ju]] = uid[tu]
+    np.savez_compressed(os.path.join(HERE, f"digest-{cfg}.npz"), event_task=event_task, event_node=event_node,
+                        event_kind=event_kind, job_fail=job_fail)
+    meta = {"config": cfg, "generator": ("synth.c2(**%r)" % (HEADS[cfg][0],) if cfg in HEADS else
+                                         "synth.CONFIGS[%r]() defaults" % cfg) + " (seed %d)" % synth.SEED,
+            "max_tasks": max_tasks,
+            "nodes": snap.n_nodes, "pods": len(snap.session_tasks), "events": len(ev),
+            "failed_jobs": int((job_fail >= 0).sum()), "sha256": digest_arrays(event_task, event_node, event_kind,
+                                                                              job_fail),
+            "fit_errors": out["fit_errors"], "oracle_seconds": round(secs, 1), "oracle_workers": workers,
+            "source": "oracle/oracle.cpp (CPU restatement) via tests/golden/make_digests.py"}
+    with open(os.path.join(HERE, f"digest-{cfg}.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(cfg, "events", len(ev), "oracle", round(secs, 1), "s", meta["sha256"][:16], flush=True)
+
+
+if __name__ == "__main__":
+    for c in sys.argv[1:] or ["C1", "C2"]:
+        make(c)

@@ -1,4 +1,8 @@
 """Shared fixtures: seeded parity-size clusters of every configuration shape + edge cases."""
+import hashlib
+
+import numpy as np
+
 from scheduler_amd import model as m
 from scheduler_amd import synth
 
@@ -278,3 +282,11 @@ def ipa_error_clusters():
             p.affinity = {"podAntiAffinity": {"preferred": [{"weight": 2, "podAffinityTerm": dict(bad, topologyKey="zone")}]}}
     out.append(("ipa-err-own", cl))
     return out
+
+
+def digest_arrays(event_task, event_node, event_kind, job_fail):
+    """sha256 of a cycle's placement arrays (tests/golden/digest-*.npz)."""
+    h = hashlib.sha256()
+    for a in (event_task, event_node, event_kind, job_fail):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()

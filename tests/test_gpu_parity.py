@@ -251,3 +251,24 @@ def test_affinity_loop_variants(name, cluster, reg, monkeypatch):
     ref = pyoracle.allocate(cluster)
     got = runtime.allocate(cluster)
     _compare(ref, got)
+
+
+def test_fed_engine_survives_a_host_stall(monkeypatch):
+    """The resident engine exits after its idle bound without a command. A host stall longer than that in
+    the middle of a cycle (a GC pause, descheduling) must not fail the cycle: the job the host waits for, and
+    the rest of the cycle, finish on the launch path with the oracle's placements."""
+    monkeypatch.setenv("KB_FED_IDLE_MS", "40")
+    monkeypatch.setenv("KB_TEST_STALL_JOB", "3")
+    monkeypatch.setenv("KB_TEST_STALL_MS", "400")
+    cl = synth.c2(n_nodes=300, n_jobs=20, tasks_per_job=20, seed=9)
+    ref = pyoracle.allocate(cl)
+    snap = E.Snapshot(cl)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    assert st["fed_abandon"] == 1
+    _compare(ref, runtime.result_dict(snap, out))

@@ -14,7 +14,7 @@ import pytest
 from scheduler_amd import export as E
 from scheduler_amd import runtime, synth
 
-from helpers import parity_clusters
+from helpers import backfill_cluster, parity_clusters
 
 pytestmark = pytest.mark.gpu
 
@@ -27,9 +27,24 @@ def _clusters():
 
 def _summary(out):
     n = int(out["n_events"])
-    return {"task_node": out["task_node"].tolist(), "event_task": out["event_task"][:n].tolist(),
-            "task_status": out["task_status"].tolist(), "job_fail_task": out["job_fail_task"].tolist(),
-            "job_reason_hist": out["job_reason_hist"].tolist()}
+    s = {"task_node": out["task_node"].tolist(), "event_task": out["event_task"][:n].tolist(),
+         "task_status": out["task_status"].tolist(), "job_fail_task": out["job_fail_task"].tolist(),
+         "job_reason_hist": out["job_reason_hist"].tolist()}
+    if "backfill_fit" in out:  # backfill: first fit with every score equal; FitErrors merged over the ranks
+        s["backfill_fit"] = {j: {t: h.tolist() for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
+    return s
+
+
+def _run(name, snap, ctx):
+    ctx.upload(snap)
+    out = ctx.allocate(snap)
+    if name == "backfill":
+        out = ctx.backfill(snap, out)
+    return _summary(out)
+
+
+def _cases():
+    return dict(_clusters(), backfill=backfill_cluster())
 
 
 def _rank_main(rank, world, port, q):
@@ -46,13 +61,12 @@ def _rank_main(rank, world, port, q):
 
     res = {}
     try:
-        for name, cl in _clusters().items():
+        for name, cl in _cases().items():
             snap = E.Snapshot(cl)
             ctx = runtime.Context(0)
             try:
                 ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
-                ctx.upload(snap)
-                res[name] = _summary(ctx.allocate(snap))
+                res[name] = _run(name, snap, ctx)
             finally:
                 ctx.close()
         q.put((rank, res, None))
@@ -72,12 +86,10 @@ def _free_port():
 def test_sharded_equals_one_gpu(world):
     import torch.multiprocessing as mp
     ref = {}
-    for name, cl in _clusters().items():
-        snap = E.Snapshot(cl)
+    for name, cl in _cases().items():
         ctx = runtime.Context(0)
         try:
-            ctx.upload(snap)
-            ref[name] = _summary(ctx.allocate(snap))
+            ref[name] = _run(name, E.Snapshot(cl), ctx)
         finally:
             ctx.close()
     ctxm = mp.get_context("spawn")
@@ -115,3 +127,77 @@ def test_rccl_exchange_one_rank():
     finally:
         ctx.close()
     assert got == ref
+
+
+def _c5_rank(rank, world, port, q):
+    import torch.distributed as dist
+    import torch
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+    try:
+        snap = synth.c2_snapshot(n_nodes=50000, n_jobs=300, tasks_per_job=100, seed=synth.SEED)
+        ctx = runtime.Context(0, timing=True)
+        try:
+            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+            ctx.upload(snap)
+            out = _summary(ctx.allocate(snap))
+            st = ctx.stats()
+        finally:
+            ctx.close()
+        k = runtime.KERNELS.index("shard_exchange")
+        q.put((rank, (out, st["launches"][k]), None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_sharded_matches_one_gpu_and_oracle_prefix():
+    """BASELINE.json configs[4] shape (C5: C2 nodes at 50k) with 300 jobs: 3 ranks sharing the GPU (each
+    ~16.7k rows, the selection path per shard, one exchange per run segment over gloo) give the placements
+    of one GPU holding all 50k rows (the per-commit re-key path, the only one that fits 50k nodes), and
+    that cycle's first 3000 placements are the oracle's (tests/golden/digest-C5-head)."""
+    import json
+    import torch.multiprocessing as mp
+    from helpers import digest_arrays
+    snap = synth.c2_snapshot(n_nodes=50000, n_jobs=300, tasks_per_job=100, seed=synth.SEED)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+    finally:
+        ctx.close()
+    ref = _summary(out)
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(golden, "digest-C5-head.json")) as f:
+        meta = json.load(f)
+    want = np.load(os.path.join(golden, "digest-C5-head.npz"), allow_pickle=False)
+    k = meta["events"]
+    et = np.asarray(ref["event_task"][:k], np.int32)
+    assert np.array_equal(et, want["event_task"])
+    assert np.array_equal(np.asarray(ref["task_node"])[et].astype(np.int32), want["event_node"])
+    assert digest_arrays(et, want["event_node"], want["event_kind"], want["job_fail"]) == meta["sha256"]
+    world = 3
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_c5_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=300)
+        assert err is None, f"rank {rank}: {err}"
+        got[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        summary, exchanges = got[r]
+        assert summary == ref, r
+        assert exchanges >= 300  # at least one all-gather per job
