@@ -337,13 +337,15 @@ __device__ __forceinline__ bool sc_fit(const DevNodes& N, const kb_spec& sp, con
   return scalars_fit(N, sp, sci, has_map, node_sc, n);
 }
 
-// Reason mask of the full chain from a loaded row + the static cache (0 = fits).
+// Reason mask of the full chain from a loaded row + the static cache (0 = fits). RES = false: Session.PredicateFn
+// alone, without allocate's resource check (preempt's sweep, preempt.go:189).
+template <bool RES = true>
 __device__ __forceinline__ uint32_t row_reasons(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                                                 const kb_spec& sp, const int64_t* sci, const Row& r, uint64_t st,
                                                 int n) {
   // allocate.go:88: InitResreq <= Idle || InitResreq <= Releasing
-  const bool fi = le_tol(sp.init_cpu, r.idle_cpu, 10) && le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
-                  sc_fit(N, sp, sci, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, n);
+  const bool fi = !RES || (le_tol(sp.init_cpu, r.idle_cpu, 10) && le_tol(sp.init_mem, r.idle_mem, 10ll * 1024 * 1024) &&
+                           sc_fit(N, sp, sci, r.flags & KB_NODE_IDLE_HAS_MAP, N.idle_sc, n));
   if (!fi) {
     const bool fr = le_tol(sp.init_cpu, r.rel_cpu, 10) && le_tol(sp.init_mem, r.rel_mem, 10ll * 1024 * 1024) &&
                     sc_fit(N, sp, sci, r.flags & KB_NODE_REL_HAS_MAP, N.rel_sc, n);
@@ -3516,6 +3518,81 @@ void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, i
   const int blocks = (k + 255) / 256;
   for (int pass = 0; pass < 2; ++pass)
     hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, d, k, sc, ports, pass);
+}
+
+// ---- preempt's sweep (actions/preempt/preempt.go:189-195): PredicateNodes with Session.PredicateFn (no
+// resource check), PrioritizeNodes, SortNodes (util/scheduler_helper.go:132-144): every feasible node by score,
+// descending, lowest index first among equal scores. The 64-bit keys (score << 24 | ~index) sort in exactly
+// that order; infeasible keys (reason masks) sink to the end. Bitonic sort over a power-of-two buffer.
+template <bool AFF>
+__global__ __launch_bounds__(256) void sort_keys_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, const int64_t* mm,
+                                                        uint64_t* keys, int n_pad) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= n_pad) return;
+  uint64_t k = 0;  // padding: below every key
+  if (n < N.n) {
+    const kb_spec sp = P.specs[spec];
+    const Row r = load_row(N, n);
+    const uint64_t st = static_eval<AFF>(N, P, C, sp, spec, r.flags, n, mm);
+    const uint32_t rs = row_reasons<false>(N, P, C, sp, P.sc_init + (size_t)spec * N.S, r, st, n);
+    k = make_key(rs, rs ? 0 : row_score(C, sp, r, st), n);
+  }
+  keys[n] = k;
+}
+
+// one compare-exchange stage (stride j of merge size k) across the whole buffer; descending overall
+__global__ __launch_bounds__(256) void bitonic_global_kernel(uint64_t* a, int j, int k) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int p = i ^ j;
+  if (p <= i) return;
+  const uint64_t x = a[i], y = a[p];
+  const bool desc = (i & k) == 0;
+  if (desc ? x < y : x > y) {
+    a[i] = y;
+    a[p] = x;
+  }
+}
+
+// every stage of merge size k with stride <= j0 (< 2048) inside one 2048-key tile in LDS
+constexpr int kBitonicTile = 2048;
+__global__ __launch_bounds__(1024) void bitonic_tile_kernel(uint64_t* a, int j0, int k) {
+  __shared__ uint64_t t[kBitonicTile];
+  const int base = blockIdx.x * kBitonicTile, tid = threadIdx.x;
+  t[tid] = a[base + tid];
+  t[tid + 1024] = a[base + tid + 1024];
+  __syncthreads();
+  for (int j = j0; j > 0; j >>= 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + h * 1024, p = e ^ j;
+      if (p > e) {
+        const uint64_t x = t[e], y = t[p];
+        const bool desc = ((base + e) & k) == 0;
+        if (desc ? x < y : x > y) {
+          t[e] = y;
+          t[p] = x;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  a[base + tid] = t[tid];
+  a[base + tid + 1024] = t[tid + 1024];
+}
+
+void launch_sort_nodes(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, const int64_t* mm,
+                       uint64_t* keys, int n_pad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (mm)
+    hipLaunchKernelGGL(sort_keys_kernel<true>, dim3(n_pad / 256), dim3(256), 0, s, N, P, C, spec, mm, keys, n_pad);
+  else
+    hipLaunchKernelGGL(sort_keys_kernel<false>, dim3(n_pad / 256), dim3(256), 0, s, N, P, C, spec, mm, keys, n_pad);
+  for (int k = 2; k <= n_pad; k <<= 1) {
+    int j = k >> 1;
+    for (; j >= kBitonicTile; j >>= 1)
+      hipLaunchKernelGGL(bitonic_global_kernel, dim3(n_pad / 256), dim3(256), 0, s, keys, j, k);
+    hipLaunchKernelGGL(bitonic_tile_kernel, dim3(n_pad / kBitonicTile), dim3(1024), 0, s, keys, j, k);
+  }
 }
 
 }  // namespace kbgpu
