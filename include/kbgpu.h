@@ -352,6 +352,24 @@ int kb_place_job(kb_ctx* ctx, const kb_job_req* job, int32_t* placed_node, int32
 int kb_eval(kb_ctx* ctx, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores);
 
 /*
+ * preempt's use of the sweep (actions/preempt/preempt.go:189-195): PredicateNodes with Session.PredicateFn
+ * alone (no allocate resource check), PrioritizeNodes, then SortNodes (util/scheduler_helper.go:132-144) for
+ * one spec at the current node-table state. order[0..*n_out) = the feasible nodes by score, descending, and
+ * the lowest index first among equal scores (the reference appends a score bucket's nodes in goroutine
+ * completion order); scores[i] = order[i]'s score (either array may be NULL; capacity n). A batch-score error
+ * (KB_SPEC_IPA_ERROR) gives an empty list: PrioritizeNodes returns no scores there. Not node-sharded.
+ */
+int kb_sort_nodes(kb_ctx* ctx, int32_t spec, int32_t* order, int64_t* scores, uint32_t* n_out);
+
+/*
+ * util.PredicateNodes(task, nodes, ssn.PredicateFn) alone (util/scheduler_helper.go:34-64): the nodes passing
+ * Session.PredicateFn for one spec at the current state, in canonical order, and the FitErrors histogram of the
+ * rest. reclaim walks this set for victims (actions/reclaim/reclaim.go:122-126), preempt sorts it (above).
+ * nodes: capacity n (may be NULL); reason_hist: KB_NUM_REASONS counters (may be NULL).
+ */
+int kb_predicate_nodes(kb_ctx* ctx, int32_t spec, int32_t* nodes, uint32_t* n_out, uint32_t* reason_hist);
+
+/*
  * Restore the node table to its state at the last kb_upload_nodes (device-to-device copy of the
  * mutable columns). A fresh allocate cycle over the same cache snapshot re-opens its session this way
  * without another host upload.

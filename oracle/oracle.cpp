@@ -1973,6 +1973,31 @@ class Session {
       s->score[i] = score;
     }
   }
+  // preempt's sweep (actions/preempt/preempt.go:187-195): PredicateNodes with ssn.PredicateFn alone (the
+  // allocate closure's resource check is not part of it), PrioritizeNodes, SortNodes (util/scheduler_helper.go:
+  // 132-144): scores descending, a bucket's nodes in canonical order (the reference appends them in goroutine
+  // completion order). A batch-score error leaves no scores, so no nodes.
+  std::vector<std::pair<int, double>> sort_nodes(const Task* task, Sweep* sw = nullptr) const {
+    Sweep local;
+    Sweep& s = sw ? *sw : local;
+    s.pred.assign(nodes.size(), PredResult());
+    sweep_aff = &aff_pre(task);
+    const bool pe = predicate_enabled();
+    pool->run((int)nodes.size(), [&](int i) { s.pred[i] = pe ? predicates_fn(task, i) : PredResult(); });
+    sweep_aff = nullptr;
+    for (size_t i = 0; i < nodes.size(); ++i)
+      if (s.pred[i].ok) s.feasible.push_back((int)i);
+    std::vector<std::pair<int, double>> out;
+    if (s.feasible.empty()) return out;
+    prioritize_nodes(task, &s);
+    if (s.batch_error) return out;
+    for (size_t i = 0; i < s.feasible.size(); ++i) out.emplace_back(s.feasible[i], s.score[i]);
+    std::stable_sort(out.begin(), out.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) {
+      return a.second > b.second;  // sort.Reverse(sort.Float64Slice(keys)); feasible is in index order
+    });
+    return out;
+  }
+
   // SelectBestNode with the lowest-index tie-break; -1 where the reference panics.
   static int select_best(const Sweep& s) {
     double max_score = -1.0;
@@ -2337,6 +2362,40 @@ static Value run_eval(const Value& in) {
   return out;
 }
 
+// SortNodes order of preempt's sweep for each task of eval_tasks at session-open state.
+static Value run_sort_nodes(const Value& in) {
+  Session s;
+  s.opt = parse_opts(in);
+  s.load(in);
+  std::map<std::string, const Task*> by_uid;
+  for (auto& t : s.tasks) by_uid[t.uid] = &t;
+  Value out = vobj(), res = varr();
+  for (auto& u : in.arr_at("eval_tasks")) {
+    Value tr = vobj(), order = varr(), scores = varr(), feas = varr(), hist = vobj();
+    Session::Sweep sw;
+    for (auto& p : s.sort_nodes(by_uid.at(u.as_str()), &sw)) {
+      order.a.push_back(vstr(s.nodes[p.first].name));
+      scores.a.push_back(vint((int64_t)p.second));
+    }
+    // util.PredicateNodes(task, nodes, ssn.PredicateFn): the feasible set in node order + the FitErrors
+    std::map<std::string, int> h;
+    for (size_t i = 0; i < sw.pred.size(); ++i) {
+      if (sw.pred[i].ok) feas.a.push_back(vstr(s.nodes[i].name));
+      else
+        for (auto& r : sw.pred[i].reasons) h[r]++;
+    }
+    for (auto& kv : h) hist.o.emplace_back(kv.first, vint(kv.second));
+    tr.o.emplace_back("feasible", feas);
+    tr.o.emplace_back("fit_errors", hist);
+    tr.o.emplace_back("task", vstr(u.as_str()));
+    tr.o.emplace_back("order", order);
+    tr.o.emplace_back("score", scores);
+    res.a.push_back(tr);
+  }
+  out.o.emplace_back("tasks", res);
+  return out;
+}
+
 // Resource / NodeInfo / pod-request primitives for the restated api unit tests.
 static Value run_resource_op(const Value& in) {
   std::string op = in.str_at("op");
@@ -2460,6 +2519,7 @@ char* oracle_call(const char* json_in) {
     oj::Value res;
     if (op == "allocate" || op == "allocate_backfill") res = oracle::run_allocate(in);
     else if (op == "eval") res = oracle::run_eval(in);
+    else if (op == "sort_nodes") res = oracle::run_sort_nodes(in);
     else res = oracle::run_resource_op(in);
     oracle::write(out, res);
   } catch (const oracle::Panic& e) {

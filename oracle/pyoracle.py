@@ -80,6 +80,16 @@ def evaluate(cluster, task_uids, literal_affinity: bool = False) -> dict:
     return call(req)
 
 
+def sort_nodes(cluster, task_uids, literal_affinity: bool = False) -> dict:
+    """preempt's sweep per task: PredicateNodes(PredicateFn) -> PrioritizeNodes -> SortNodes order
+    (actions/preempt/preempt.go:187-195) at session-open state."""
+    req = dict(cluster.to_json())
+    req["op"] = "sort_nodes"
+    req["eval_tasks"] = list(task_uids)
+    req["options"] = {"workers": 1, "literal_affinity": literal_affinity}
+    return call(req)
+
+
 def resource_op(op: str, **kw) -> dict:
     req = {"op": op}
     req.update(kw)

@@ -213,10 +213,11 @@ void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, 
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
                          int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 
+constexpr int kBitonicMin = 2048;  // == the sort's LDS tile
 // kb_sort_nodes: the spec's keys (PredicateFn + PrioritizeNodes) sorted descending into keys[0..n_pad), n_pad a
 // power of two >= max(n, 2048); mm: the spec's InterPodAffinity min / max (affinity tables) or null.
 void launch_sort_nodes(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, const int64_t* mm,
-                       uint64_t* keys, int n_pad, void* stream);
+                       uint64_t* keys, int n_pad, void* stream, bool sort = true);
 // kb_apply: row deltas of commits made outside the device (one thread per delta, atomics).
 void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
                   const kb_port* ports, void* stream);

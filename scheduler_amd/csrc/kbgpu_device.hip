@@ -3581,13 +3581,13 @@ __global__ __launch_bounds__(1024) void bitonic_tile_kernel(uint64_t* a, int j0,
 }
 
 void launch_sort_nodes(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, const int64_t* mm,
-                       uint64_t* keys, int n_pad, void* stream) {
+                       uint64_t* keys, int n_pad, void* stream, bool sort) {
   hipStream_t s = (hipStream_t)stream;
   if (mm)
     hipLaunchKernelGGL(sort_keys_kernel<true>, dim3(n_pad / 256), dim3(256), 0, s, N, P, C, spec, mm, keys, n_pad);
   else
     hipLaunchKernelGGL(sort_keys_kernel<false>, dim3(n_pad / 256), dim3(256), 0, s, N, P, C, spec, mm, keys, n_pad);
-  for (int k = 2; k <= n_pad; k <<= 1) {
+  for (int k = 2; sort && k <= n_pad; k <<= 1) {
     int j = k >> 1;
     for (; j >= kBitonicTile; j >>= 1)
       hipLaunchKernelGGL(bitonic_global_kernel, dim3(n_pad / 256), dim3(256), 0, s, keys, j, k);

@@ -1324,6 +1324,84 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
   return KB_OK;
 }
 
+// The keys of kb_sort_nodes / kb_predicate_nodes (PredicateFn without allocate's resource check +
+// PrioritizeNodes) into h, sorted descending or in node order.
+static int pred_keys(kb_ctx* c, int32_t spec, bool sort, std::vector<uint64_t>& h);
+
+int kb_sort_nodes(kb_ctx* c, int32_t spec, int32_t* order, int64_t* scores, uint32_t* n_out) {
+  if (!c || !n_out) return KB_E_INVALID;
+  *n_out = 0;
+  std::vector<uint64_t> h;
+  if (int rc = pred_keys(c, spec, true, h)) return rc;
+  if (c->cfg.nodeorder && c->spec_ipa_err[spec]) return KB_OK;  // PrioritizeNodes' batch error: no scores
+  uint32_t k = 0;
+  for (; k < (uint32_t)h.size() && (h[k] & kFeasible); ++k) {
+    if (order) order[k] = (int32_t)(kIdxMask - (uint32_t)(h[k] & kIdxMask));
+    if (scores) scores[k] = (int64_t)((h[k] >> 24) & ((1ull << 39) - 1)) - kScoreBias;
+  }
+  *n_out = k;
+  return KB_OK;
+}
+
+int kb_predicate_nodes(kb_ctx* c, int32_t spec, int32_t* nodes, uint32_t* n_out, uint32_t* reason_hist) {
+  if (!c || !n_out) return KB_E_INVALID;
+  *n_out = 0;
+  std::vector<uint64_t> h;
+  if (int rc = pred_keys(c, spec, false, h)) return rc;
+  uint32_t k = 0, hist[KB_NUM_REASONS] = {0};
+  for (size_t i = 0; i < h.size(); ++i) {
+    if (h[i] & kFeasible) {
+      if (nodes) nodes[k] = (int32_t)i;
+      ++k;
+    } else {
+      for (int b = 0; b < KB_NUM_REASONS; ++b) hist[b] += (uint32_t)(h[i] >> b) & 1u;
+    }
+  }
+  *n_out = k;
+  if (reason_hist) memcpy(reason_hist, hist, sizeof(hist));
+  return KB_OK;
+}
+
+static int pred_keys(kb_ctx* c, int32_t spec, bool sort, std::vector<uint64_t>& h) {
+  c->prev_listed = false;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (c->sharded) return fail(c, KB_E_UNSUPPORTED, "kb_sort_nodes does not run node-sharded");
+  if (spec < 0 || spec >= c->P.m) return fail(c, KB_E_INVALID, "spec %d out of range", spec);
+  if (c->spec_needs_aff[spec] && !c->aff_ok)
+    return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first", spec);
+  HIP_OK(c, hipSetDevice(c->device));
+  const int n = c->N.n;
+  int n_pad = kBitonicMin;
+  while (n_pad < n) n_pad <<= 1;
+  uint64_t* keys = nullptr;
+  HIP_OK(c, hipMalloc(&keys, (size_t)n_pad * 8));
+  const int64_t* mm = nullptr;
+  if (c->aff_ok && c->spec_needs_aff[spec]) {  // this spec's InterPodAffinity min / max first
+    if (c->mm_eval_cap < 1) {
+      void* q;
+      if (hipMalloc(&q, 2 * sizeof(int64_t)) != hipSuccess) {
+        (void)hipFree(keys);
+        return fail(c, KB_E_HIP, "hipMalloc");
+      }
+      c->aff_mem.push_back(q);
+      c->mm_eval = (int64_t*)q;
+      c->mm_eval_cap = 1;
+    }
+    launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->mm_eval, nullptr, c->stream);
+    mm = c->mm_eval;
+  }
+  launch_sort_nodes(c->N, c->P, c->cfg, spec, mm, keys, n_pad, c->stream, sort);
+  h.assign(n, 0);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), keys, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(keys);
+  if (e != hipSuccess) return fail(c, KB_E_HIP, "PredicateNodes sweep: %s", hipGetErrorString(e));
+  return KB_OK;
+}
+
 // Device copies of the host overlays (after every change; overlays change rarely, between jobs).
 static int overlay_upload(kb_ctx* c) {
   // kernels of earlier jobs may still hold the old arrays

@@ -132,7 +132,7 @@ ABI_VERSION = 8  # include/kbgpu.h KBGPU_ABI_VERSION
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
            "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl",
-           "kb_set_host_overlay", "kb_apply", "kb_set_nofit_hook"]
+           "kb_set_host_overlay", "kb_apply", "kb_set_nofit_hook", "kb_sort_nodes", "kb_predicate_nodes"]
 
 _lib = None
 
@@ -175,6 +175,8 @@ def load_library(path: str = LIB_PATH):
     lib.kb_set_host_overlay.argtypes = [P, C.c_int32, P, P]
     lib.kb_apply.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32]
     lib.kb_set_nofit_hook.argtypes = [P, NOFIT_FN, P]
+    lib.kb_sort_nodes.argtypes = [P, C.c_int32, P, P, C.POINTER(C.c_uint32)]
+    lib.kb_predicate_nodes.argtypes = [P, C.c_int32, P, C.POINTER(C.c_uint32), P]
     _lib = lib
     return lib
 
@@ -326,6 +328,24 @@ class Context:
         scores = np.zeros((len(ids), n), np.int64)
         self._check(self.lib.kb_eval(self.ctx, _ptr(ids), len(ids), _ptr(reasons), _ptr(scores)))
         return reasons, scores
+
+    def sort_nodes(self, spec: int):
+        """kb_sort_nodes: preempt's PredicateNodes -> PrioritizeNodes -> SortNodes for one spec (preempt.go:
+        187-195). Returns (node indices best first, their scores)."""
+        order = np.zeros(max(self.n_nodes, 1), np.int32)
+        scores = np.zeros(max(self.n_nodes, 1), np.int64)
+        k = C.c_uint32(0)
+        self._check(self.lib.kb_sort_nodes(self.ctx, int(spec), _ptr(order), _ptr(scores), C.byref(k)))
+        return order[:k.value].copy(), scores[:k.value].copy()
+
+    def predicate_nodes(self, spec: int):
+        """kb_predicate_nodes: util.PredicateNodes with Session.PredicateFn (the set reclaim walks,
+        reclaim.go:122-126). Returns (feasible node indices in node order, FitErrors reason histogram)."""
+        nodes = np.zeros(max(self.n_nodes, 1), np.int32)
+        hist = np.zeros(KB_NUM_REASONS, np.uint32)
+        k = C.c_uint32(0)
+        self._check(self.lib.kb_predicate_nodes(self.ctx, int(spec), _ptr(nodes), C.byref(k), _ptr(hist)))
+        return nodes[:k.value].copy(), hist
 
     def read_nodes(self, n):
         cols = [np.zeros(n, np.int64) for _ in range(4)] + [np.zeros(n, np.int32)] + [np.zeros(n, np.int64)

@@ -17,7 +17,7 @@ step() {  # step <name> <timeout-seconds> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests ${TEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -v -p no:cacheprovider --maxfail=${MAXFAIL:-25} --timeout 300 --timeout-method thread ${TESTS:-}
+  step gpu_tests ${TEST_TIMEOUT:-1000} python -u -m pytest -m gpu -v -p no:cacheprovider --maxfail=${MAXFAIL:-25} --timeout 300 --timeout-method thread ${TESTS:-tests}
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
