@@ -379,6 +379,49 @@ __device__ __forceinline__ int64_t row_score(const DevCfg& C, const kb_spec& sp,
   return lr * C.w_lr + bra * C.w_bra + (int64_t)stat_na(st) + batch;
 }
 
+// ---- the same scores with the node's reciprocals precomputed (kb_eval: many specs against one node) ----
+// leastRequestedScore with the quotient estimated as num * (1 / cap): the estimate is within one of the exact
+// quotient (num / cap <= 10, relative error < 2^-51), which the int64 corrections then fix.
+__device__ __forceinline__ int64_t lr_score_inv(int64_t req, int64_t cap, double inv) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t num = (cap - req) * 10;
+  if (cap > 0 && cap < (1ll << 52) && num >= 0 && num < (1ll << 62)) {
+    int64_t q = (int64_t)((double)num * inv);
+    q = q < 0 ? 0 : (q > 11 ? 11 : q);
+    if (q * cap > num) --q;
+    if ((q + 1) * cap <= num) ++q;
+    return q;
+  }
+  return num / cap;
+}
+// BalancedResourceAllocation (balanced_resource_allocation.go:41-77): fractionOfCapacity >= 1 is the integer
+// test req >= cap (cap < 2^53); otherwise int((1 - |cf - mf|) * 10) from the reciprocal estimates, which lie
+// within 1e-14 of the IEEE quotients -- unless that value is within 1e-9 of an integer, where the IEEE
+// divisions decide (the result must be the reference's bit for bit).
+__device__ __forceinline__ int64_t bra_score_inv(int64_t rc, int64_t ac, int64_t rm, int64_t am, double ic,
+                                                 double im) {
+  const bool exactable = ac > 0 && am > 0 && ac < (1ll << 53) && am < (1ll << 53) && rc >= 0 && rm >= 0;
+  if (exactable) {
+    if (rc >= ac || rm >= am) return 0;
+    const double f = (1.0 - fabs((double)rc * ic - (double)rm * im)) * 10.0;
+    const double fl = floor(f);
+    if (f - fl > 1e-9 && fl + 1.0 - f > 1e-9) return (int64_t)f;
+  }
+  const double cf = frac_cap(rc, ac), mf = frac_cap(rm, am);
+  return (cf >= 1.0 || mf >= 1.0) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 10.0);
+}
+__device__ __forceinline__ int64_t row_score_inv(const DevCfg& C, const kb_spec& sp, const Row& r, uint64_t st,
+                                                 double ic, double im) {
+  if (!C.nodeorder) return stat_na(st);
+  if (stat_ipa(st) == (int32_t)kIpaErrorField) return kIpaErrorScore;
+  const int64_t batch = (int64_t)stat_ipa(st) * C.w_pa;
+  if (sp.flags & KB_SPEC_NA_ERROR) return batch;
+  const int64_t rc = sp.nz_cpu + r.nz_cpu, rm = sp.nz_mem + r.nz_mem;
+  const int64_t lr = (lr_score_inv(rc, r.alloc_cpu, ic) + lr_score_inv(rm, r.alloc_mem, im)) / 2;
+  const int64_t bra = bra_score_inv(rc, r.alloc_cpu, rm, r.alloc_mem, ic, im);
+  return lr * C.w_lr + bra * C.w_bra + (int64_t)stat_na(st) + batch;
+}
+
 __device__ __forceinline__ uint64_t make_key(uint32_t reasons, int64_t score, int n) {
   if (reasons) return reasons;
   return kFeasible | ((uint64_t)(score + kScoreBias) << 24) | (uint64_t)(kIdxMask - (uint32_t)n);
@@ -750,12 +793,13 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   const int j0 = blockIdx.y * kEvalSpecs;
   const int j1 = j0 + kEvalSpecs < t ? j0 + kEvalSpecs : t;
   const Row r = load_row(N, n);
+  const double ic = 1.0 / (double)r.alloc_cpu, im = 1.0 / (double)r.alloc_mem;  // once per node
   for (int j = j0; j < j1; ++j) {
     const int s = spec_ids[j];
     const kb_spec sp = P.specs[s];
     const uint64_t st = static_eval<AFF>(N, P, C, sp, s, r.flags, n, AFF ? mm + 2 * j : nullptr);
     reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
-    scores[(size_t)j * N.n + n] = row_score(C, sp, r, st);
+    scores[(size_t)j * N.n + n] = row_score_inv(C, sp, r, st, ic, im);
   }
 }
 

@@ -272,3 +272,47 @@ def test_fed_engine_survives_a_host_stall(monkeypatch):
         ctx.close()
     assert st["fed_abandon"] == 1
     _compare(ref, runtime.result_dict(snap, out))
+
+
+def _ratio_cluster(seed=77, n_nodes=3000, n_specs=48):
+    """Random capacities and loads, so LeastRequested / BalancedResource see many distinct quotients (and
+    some exactly on an integer boundary, like 2000/4000 vs 3000/10000)."""
+    rng = np.random.default_rng(seed)
+    GI = 1024 ** 3
+    cl = m.Cluster()
+    for i in range(n_nodes):
+        cpu = int(rng.choice([4000, 10000, 8000, int(rng.integers(1000, 200000))]))
+        mem = int(rng.choice([10000, 16 * GI, int(rng.integers(1, 1 << 40))]))
+        cl.nodes.append(m.Node(name=f"n{i:05d}", alloc={m.CPU: cpu, m.MEMORY: mem, m.PODS: 110}))
+        for k in range(int(rng.integers(0, 3))):
+            cl.pods.append(m.Pod(ns="x", name=f"r{i}-{k}", uid=f"x-r{i}-{k}", node=f"n{i:05d}", phase="Running",
+                                 containers=[m.Container(req={m.CPU: int(rng.integers(0, cpu // 3 + 1)),
+                                                              m.MEMORY: int(rng.integers(0, mem // 3 + 1))})]))
+    cl.queues.append(m.Queue(name="q"))
+    for j in range(n_specs):
+        cl.pod_groups.append(m.PodGroup(ns="t", name=f"g{j}", queue="q", min_member=1))
+        req = {m.CPU: int(rng.choice([1000, 3000, int(rng.integers(1, 20000))])),
+               m.MEMORY: int(rng.choice([1000, 2000, int(rng.integers(1, 1 << 34))]))}
+        cl.pods.append(m.Pod(ns="t", name=f"p{j}", uid=f"t-p{j}", group=f"g{j}", containers=[m.Container(req=req)]))
+    return cl
+
+
+def test_eval_scores_random_ratios():
+    """kb_eval's reciprocal fast paths for LeastRequested / BalancedResource (exact by construction, with
+    the IEEE divisions near integer boundaries) against the oracle on ~70k (spec, node) pairs."""
+    cl = _ratio_cluster()
+    snap = E.Snapshot(cl)
+    reps = {}
+    for t in snap.session_tasks:
+        if t["status"] == E.ST["Pending"] and t["spec"] not in reps:
+            reps[t["spec"]] = t["uid"]
+    spec_ids = sorted(reps)
+    ref = pyoracle.evaluate(cl, [reps[s] for s in spec_ids])
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        reasons, scores = ctx.eval(spec_ids)
+    finally:
+        ctx.close()
+    for i, s in enumerate(spec_ids):
+        assert list(scores[i]) == ref["tasks"][i]["score"], s
