@@ -386,8 +386,8 @@ DIAG_PHASES = {
     "traj_place_kernel": ["argmax", "commit", "rereduce", "lmax", "prefetch_store", "loop", "fill"],
     "sel_place_kernel": ["key_load", "node_select", "node_setup", "e_sequences", "winners_order", "stop_commit",
                          "nofit_hist"],
-    "fed_engine_kernel": ["key_load", "node_select", "node_setup", "e_sequences", "winners_order", "stop_commit",
-                          "nofit_hist"],
+    "fed_engine_kernel": ["key_load_patch", "node_select", "node_setup", "e_sequences", "winners_order",
+                          "commit_publish_nofit", "wait_for_command"],
     "aff_place_kernel": ["prologue", "live_loads_minmax", "keys_argmax", "commit", "table_incr_fence", "stop_flush",
                          "nofit_hist"],
 }

@@ -501,54 +501,93 @@ struct Driver {
     placed = std::min(need, nt);
   }
 
-  // Speculation: with job j (queue q) in flight in slot `busy`, find the job the loop pops next IF j ends
-  // as predicted, and issue it into the other slot guarded on that prediction. The driver state is
-  // advanced as the prediction says, the loop head is run on scratch copies of the heaps, and the state
-  // is put back. Returns false (nothing issued) when there is no next job or it cannot be guarded.
+  // Jobs in flight on the device (pipelined driver), oldest first. Entry i > 0 was issued speculatively,
+  // guarded on entry i-1 ending as predicted; `pred` is the entry's own predicted outcome (set by the
+  // replay that issued the entry after it).
+  struct Flight {
+    int q, j, slot;
+    kb_job_pred pred;
+  };
+  std::vector<Flight> fl;
+
+  // Speculation: find the job the loop pops next IF every job in flight ends as predicted, and issue it into
+  // `free_slot` guarded on the last one's prediction. The predictions are applied to the driver state in
+  // order and the loop tail / head replayed on scratch copies of the heaps; then the state is put back.
+  // Returns false (nothing issued) when there is no next job or it cannot be guarded.
   GoHeap<int> sq;
   std::vector<std::pair<int, GoHeap<int>>> sjh;
-  bool speculate(int q, int j, int busy, int& q2, int& j2, kb_job_pred& pred) {
-    int stop, placed;
-    predict(j, stop, placed);
-    JobS& js = jobs[j];
-    QueueS& qs = queues[q];
-    const int ready0 = js.ready;
-    const size_t cursor0 = js.cursor;
-    const Res drf0 = js.drf_alloc, qalloc0 = qs.allocated;
-    const double drf_share0 = js.drf_share, qshare0 = qs.share;
-    for (int i = 0; i < placed; ++i) on_allocate_event(js.pending[cursor0 + i]);
-    js.ready += placed;
-    js.cursor += placed;
-    share_update(j);
+  struct SavedJob {
+    int j, ready;
+    size_t cursor;
+    Res drf;
+    double share;
+  };
+  struct SavedQueue {
+    int q;
+    Res allocated;
+    double share;
+  };
+  std::vector<SavedJob> saved_jobs;
+  std::vector<SavedQueue> saved_queues;
+  bool speculate(int free_slot) {
+    saved_jobs.clear();
+    saved_queues.clear();
     sq.items = qheap.items;
-    sq.push(q);
     sjh.clear();
     auto jh = [&](int qq) -> GoHeap<int>& {
       for (auto& e : sjh)
         if (e.first == qq) return e.second;
       sjh.emplace_back(qq, jheaps[qq]);
-      if (qq == q && stop == KB_STOP_READY) sjh.back().second.push(j);
       return sjh.back().second;
     };
-    // the pushes of job j's loop tail happen before the next head: touch queue q's job heap first
-    if (stop == KB_STOP_READY) jh(q);
-    bool ok = next_job(sq, jh, q2, j2) && check_specs(j2) == KB_OK;
-    int rc = KB_OK;
+    bool ok = true;
+    int q2 = -1, j2 = -1;
+    for (size_t i = 0; i < fl.size() && ok; ++i) {
+      Flight& f = fl[i];
+      int stop, placed;
+      predict(f.j, stop, placed);
+      JobS& js = jobs[f.j];
+      bool seen = false;
+      for (const auto& e : saved_jobs) seen = seen || e.j == f.j;
+      if (!seen) saved_jobs.push_back(SavedJob{f.j, js.ready, js.cursor, js.drf_alloc, js.drf_share});
+      seen = false;
+      for (const auto& e : saved_queues) seen = seen || e.q == f.q;
+      if (!seen) saved_queues.push_back(SavedQueue{f.q, queues[f.q].allocated, queues[f.q].share});
+      const int ready0 = js.ready;
+      for (int k = 0; k < placed; ++k) on_allocate_event(js.pending[js.cursor + k]);
+      js.ready += placed;
+      js.cursor += placed;
+      share_update(f.j);
+      f.pred = kb_job_pred{f.slot, stop, placed, ready0 + placed};
+      // the loop tail of the predicted outcome, then the next loop head
+      if (stop == KB_STOP_READY) jh(f.q).push(f.j);
+      sq.push(f.q);
+      int nq, nj;
+      ok = next_job(sq, jh, nq, nj);
+      if (ok && i + 1 < fl.size()) ok = nq == fl[i + 1].q && nj == fl[i + 1].j;  // issued by the same replay
+      q2 = nq, j2 = nj;
+    }
+    ok = ok && check_specs(j2) == KB_OK;
     if (ok) {
       const kb_job_req req = make_req(j2);
       ok = kb_job_guardable(ctx, &req) != 0;
       if (ok) {
-        pred = kb_job_pred{busy, stop, placed, ready0 + placed};
-        rc = kb_job_issue(ctx, &req, busy ^ 1, &pred);
-        ok = rc == KB_OK;
+        const kb_job_pred pred = fl.back().pred;
+        ok = kb_job_issue(ctx, &req, free_slot, &pred) == KB_OK;
       }
     }
-    js.ready = ready0;
-    js.cursor = cursor0;
-    js.drf_alloc = drf0;
-    js.drf_share = drf_share0;
-    qs.allocated = qalloc0;
-    qs.share = qshare0;
+    for (const auto& e : saved_jobs) {
+      JobS& js = jobs[e.j];
+      js.ready = e.ready;
+      js.cursor = e.cursor;
+      js.drf_alloc = e.drf;
+      js.drf_share = e.share;
+    }
+    for (const auto& e : saved_queues) {
+      queues[e.q].allocated = e.allocated;
+      queues[e.q].share = e.share;
+    }
+    if (ok) fl.push_back(Flight{q2, j2, free_slot, kb_job_pred{}});
     return ok;
   }
 
@@ -612,13 +651,9 @@ struct Driver {
         if (on) (void)kb_fed_end(c);
       }
     } fed_end{ctx, fed};
-    int q, j, slot = 0;
+    int q, j;
     bool have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
     if (have && check_specs(j)) return KB_E_INVALID;
-    if (have && pipe) {
-      const kb_job_req req = make_req(j);
-      if (int rc = kb_job_issue(ctx, &req, slot, nullptr)) return rc;
-    }
     // KB_HOST_TRACE=1: per-job host timings on stderr at the end of the cycle (speculative issue, wait in
     // finish, bookkeeping after it)
     const bool trace = getenv("KB_HOST_TRACE") != nullptr;
@@ -634,64 +669,101 @@ struct Driver {
     const auto us = [](clk::time_point a, clk::time_point b) {
       return std::chrono::duration<double, std::micro>(b - a).count();
     };
-    while (have) {
-      int q2 = -1, j2 = -1;
-      kb_job_pred pred{};
+    if (!pipe) {  // one kb_place_job per job
+      while (have) {
+        const kb_job_req req = make_req(j);
+        kb_job_result res;
+        if (int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res)) return rc;
+        apply(q, j, res);
+        if (hook_rc) return hook_rc;
+        have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
+        if (have && check_specs(j)) return KB_E_INVALID;
+      }
+    }
+    // Pipelined: jobs are issued before the result of the jobs ahead of them is read (the fed engine: two
+    // ahead, kJobSlots slots; the per-job launch path: one ahead, two slots), so the device runs them back to
+    // back while the host does the bookkeeping.
+    int n_slots = fed ? kbgpu::kJobSlots : 2;
+    const auto free_slot = [&]() {
+      for (int sl = 0; sl < n_slots; ++sl) {
+        bool used = false;
+        for (const Flight& f : fl) used = used || f.slot == sl;
+        if (!used) return sl;
+      }
+      return -1;
+    };
+    fl.clear();
+    if (have && pipe) {
+      const kb_job_req req = make_req(j);
+      if (int rc = kb_job_issue(ctx, &req, 0, nullptr)) return rc;
+      fl.push_back(Flight{q, j, 0, kb_job_pred{}});
+    }
+    while (!fl.empty()) {
       const auto c0 = clk::now();
-      bool spec = pipe && speculate(q, j, slot, q2, j2, pred);
+      for (;;) {  // top up the speculative chain
+        const int fs = (int)fl.size() < n_slots ? free_slot() : -1;
+        if (fs < 0 || !speculate(fs)) break;
+      }
       const auto c1 = clk::now();
       if (stall_job >= 0 && (int64_t)n_iter_all == stall_job)  // KB_TEST_STALL_JOB: a host stall (GC pause, ...)
         std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
       ++n_iter_all;
+      Flight f0 = fl.front();
       kb_job_result res;
-      int rc;
-      if (pipe) {
-        rc = kb_job_finish(ctx, slot, pn.data(), pk.data(), &res, 0);
-        if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this job and the rest of the
-          rc = kb_fed_abandon(ctx);  // cycle run on the launch path (the speculative job never ran)
-          spec = false;
-          if (rc == KB_OK) {
-            const kb_job_req req = make_req(j);
-            rc = kb_job_issue(ctx, &req, slot, nullptr);
-          }
-          if (rc == KB_OK) rc = kb_job_finish(ctx, slot, pn.data(), pk.data(), &res, 0);
+      int rc = kb_job_finish(ctx, f0.slot, pn.data(), pk.data(), &res, 0);
+      if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this job and the rest of the
+        rc = kb_fed_abandon(ctx);  // cycle run on the launch path (the speculative jobs never ran)
+        fl.assign(1, f0);
+        fl[0].slot = 0;
+        n_slots = 2;
+        if (rc == KB_OK) {
+          const kb_job_req req = make_req(f0.j);
+          rc = kb_job_issue(ctx, &req, 0, nullptr);
         }
-      } else {
-        const kb_job_req req = make_req(j);
-        rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res);
+        if (rc == KB_OK) rc = kb_job_finish(ctx, 0, pn.data(), pk.data(), &res, 0);
       }
-      const bool match = spec && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
-                         jobs[j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
-                                                         (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
-      if (spec && !match) {  // the guard fails on the device as well: drain the skipped job
-        kb_job_result skip;
-        int rc2 = kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &skip, 1);
-        if (rc2 == kFedIdleExit) rc2 = kb_fed_abandon(ctx);  // it never ran: nothing to drain
-        if (rc == KB_OK) rc = rc2;
+      const kb_job_pred& pred = fl.front().pred;
+      const bool chained = fl.size() > 1;
+      const bool match = chained && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
+                         jobs[f0.j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
+                                                            (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
+      if (chained && !match) {  // every later guard fails on the device as well: drain the skipped jobs
+        for (size_t i = 1; i < fl.size(); ++i) {
+          kb_job_result skip;
+          int rc2 = kb_job_finish(ctx, fl[i].slot, nullptr, nullptr, &skip, 1);
+          if (rc2 == kFedIdleExit) {  // it never ran, nor did the ones after it: nothing to drain
+            rc2 = kb_fed_abandon(ctx);
+            n_slots = 2;
+            if (rc == KB_OK) rc = rc2;
+            break;
+          }
+          if (rc == KB_OK) rc = rc2;
+        }
+        fl.resize(1);
       }
       if (rc) return rc;
       const auto c2 = clk::now();
-      apply(q, j, res);
+      apply(f0.q, f0.j, res);
       if (hook_rc) return hook_rc;
       int nq, nj;
       have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj);
-      if (match) {
-        if (!have || nq != q2 || nj != j2) {  // cannot happen: the speculation replays the same loop head
-          kb_job_result drain;
-          (void)kb_job_finish(ctx, slot ^ 1, nullptr, nullptr, &drain, 1);
+      fl.erase(fl.begin());
+      if (!fl.empty()) {
+        if (!have || nq != fl[0].q || nj != fl[0].j) {  // cannot happen: the speculation replays the loop head
+          for (const Flight& f : fl) {
+            kb_job_result drain;
+            (void)kb_job_finish(ctx, f.slot, nullptr, nullptr, &drain, 1);
+          }
           ctx->err = "speculative job does not match the loop order";
           return KB_E_STATE;
         }
-        slot ^= 1;
       } else if (have) {
         if (check_specs(nj)) return KB_E_INVALID;
-        if (pipe) {
-          const kb_job_req req = make_req(nj);
-          if (int rc3 = kb_job_issue(ctx, &req, slot, nullptr)) return rc3;
-        }
+        const kb_job_req req = make_req(nj);
+        const int fs = free_slot();
+        if (int rc3 = kb_job_issue(ctx, &req, fs, nullptr)) return rc3;
+        fl.push_back(Flight{nq, nj, fs, kb_job_pred{}});
       }
-      q = nq;
-      j = nj;
       if (trace) {
         const auto c3 = clk::now();
         t_spec += us(c0, c1), t_fin += us(c1, c2), t_apply += us(c2, c3);

@@ -81,8 +81,9 @@ struct kb_ctx {
   char* h_job = nullptr;     // pinned host JobState + placement pairs (written by the place kernel)
   char* h_job_dev = nullptr; // device address of h_job
   uint32_t job_cap = 0;
-  // Job slots of the pipelined driver (kb_allocate): slot 0 = d_job / h_job above, slot 1 below. The
-  // driver issues job k+1 into the free slot, guarded on job k's predicted outcome, before reading job k.
+  // Job slots of the pipelined driver (kb_allocate): slot 0 = d_job / h_job above, slots 1.. below. The
+  // driver issues job k+1 into a free slot, guarded on job k's predicted outcome, before reading job k (the
+  // per-job launch path: two slots; the fed engine: kJobSlots, two speculative jobs ahead).
   struct JobSlot {
     char *d = nullptr, *h = nullptr, *hdev = nullptr;
     uint32_t seq = 0;        // sequence number the slot's last launch reports
@@ -91,32 +92,37 @@ struct kb_ctx {
     std::chrono::steady_clock::time_point t_issue;
     double issue_ms = 0;
   };
-  JobSlot slot[2];
-  char* d_job1 = nullptr;
-  char* h_job1 = nullptr;
-  uint32_t job1_cap = 0;
+  JobSlot slot[kbgpu::kJobSlots];
+  char* d_jobx[kbgpu::kJobSlots] = {};  // slots 1..: device / pinned host job state (+ placements)
+  char* h_jobx[kbgpu::kJobSlots] = {};
+  uint32_t jobx_cap[kbgpu::kJobSlots] = {};
+  bool any_busy() const {
+    for (const JobSlot& s : slot)
+      if (s.busy) return true;
+    return false;
+  }
   uint64_t issue_count = 0;
   // Selection runs of the pipelined driver use per-slot level-0 keys / static cache / commit lists, so the
   // level-0 sweep of job i can run on stream_b while job i-1's place kernel runs on `stream`; job i then
   // re-keys the rows job i-1 committed, from that job's commit list. Every job before job i-1 has been
   // read back by the host when job i is issued (two slots), so the sweep needs no stream dependency; the
   // place kernel waits on sweep_ctr[slot] reaching sweep_target[slot] (device counter, no events).
-  uint32_t* sel_keys[2] = {nullptr, nullptr};
-  uint64_t* sel_stat[2] = {nullptr, nullptr};
-  int32_t* commits[2] = {nullptr, nullptr};
+  uint32_t* sel_keys[kbgpu::kJobSlots] = {};
+  uint64_t* sel_stat[kbgpu::kJobSlots] = {};
+  int32_t* commits[kbgpu::kJobSlots] = {};
   int32_t sel_n = -1;       // node count the per-slot buffers were sized for
   uint32_t commits_cap = 0;
   hipStream_t stream_b = nullptr;
   uint32_t* sweep_ctr = nullptr;  // [2] device counters
   uint32_t sweep_target[2] = {0, 0};
   // fed engine (kb_fed_begin / kb_fed_end): one resident selection workgroup per allocate cycle, fed by the
-  // sweep kernels through a two-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
+  // sweep kernels through a kJobSlots-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
   bool fed = false;
   bool use_fed = true;  // KB_NO_FED unset
   void* fed_ring = nullptr;
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;
-  uint32_t fed_count[2] = {0, 0};
+  uint32_t fed_count[kbgpu::kJobSlots] = {};
   int fed_r = 0;
   uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)
   hipEvent_t fed_ev = nullptr;

@@ -180,7 +180,7 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
                    uint64_t idle_ticks, void* stream);
 
 // Fed engine (kbgpu_device.hip): one resident selection workgroup per allocate cycle; each job's sweep
-// kernel (launch_fed_cmd, on the sweep stream) also posts the job's command to a two-entry device ring and
+// kernel (launch_fed_cmd, on the sweep stream) also posts the job's command to a kJobSlots-entry device ring and
 // counts its blocks in ctr[ring entry]; the engine serves commands in order until an EXIT command (or
 // idle_ticks without one: *exit_flag = 1).
 struct FedCmdArgs {
@@ -188,20 +188,23 @@ struct FedCmdArgs {
   int32_t g_valid, g_stop, g_placed, g_ready;
   uint32_t seq;
 };
+// Job slots: the fed engine keeps up to kJobSlots jobs in flight (the running one and two speculative ones);
+// the per-job launch path uses two of them.
+constexpr int kJobSlots = 3;
 struct FedSlotPtrs {
-  uint32_t* keys[2];
-  uint64_t* stat[2];
-  int32_t* commits[2];
-  JobState* js[2];
-  JobState* hjs[2];
-  int32_t* hout[2];
+  uint32_t* keys[kJobSlots];
+  uint64_t* stat[kJobSlots];
+  int32_t* commits[kJobSlots];
+  JobState* js[kJobSlots];
+  JobState* hjs[kJobSlots];
+  int32_t* hout[kJobSlots];
 };
 size_t fed_ring_bytes();
 bool fed_fits(int n);  // the engine's LDS plan fits n nodes
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
                     uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream);
 void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
-                       const void* ring, const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1, uint64_t idle_ticks,
+                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
                        int32_t* exit_flag, void* stream);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the

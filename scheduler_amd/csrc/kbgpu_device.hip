@@ -899,9 +899,11 @@ __device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_sp
 }
 
 // Full 64-bit key of node n after j commits of the spec (A allocations at most, the rest pipelined).
+// INV: the score from the node's reciprocal capacities ic / im (row_score_inv: the same value).
+template <bool INV = false>
 __device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
                                const int64_t* sci, const int64_t* scr, const Row& r0, uint64_t st, int n, int j,
-                               int A) {
+                               int A, double ic = 0.0, double im = 0.0) {
   const int64_t a = j < A ? j : A;
   const int64_t p = j - a;
   Row r = r0;
@@ -941,7 +943,7 @@ __device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCf
     }
   }
   if (reasons) return reasons;
-  const int64_t score = row_score(C, sp, r, st);
+  const int64_t score = INV ? row_score_inv(C, sp, r, st, ic, im) : row_score(C, sp, r, st);
   return kFeasible | ((uint64_t)(score + kScoreBias) << 24);
 }
 
@@ -1256,7 +1258,10 @@ struct SelShared {
   uint64_t stat[128];
   uint64_t comp[128];      // composites (e << 14 | (127 - slot) << 7 | (127 - level)) of the taken elements
   uint64_t ord[128];       // the same, in pick order
-  uint64_t dense[kSelThreads];  // the candidates, compacted (when there are at most one per thread)
+  union {
+    uint64_t dense[kSelThreads];  // winners: the candidates, compacted (when there are at most one per thread)
+    double recip[2][128];         // e-sequences: 1 / allocatable cpu, memory of the selected nodes
+  };
   int32_t node[128];
   uint32_t key0[128];      // current key of the selected node
   int32_t A[128];          // Allocates before InitResreq stops fitting Idle
@@ -1269,7 +1274,7 @@ struct SelShared {
   int32_t fin[128];        // commits of this node in the segment
   int32_t n_commit;        // rows listed in commit_out so far
   int32_t act[128];        // active slots of a generation round
-  uint32_t red[2][3][kSelWaves];  // reduction scratch, alternating halves: one barrier per reduction
+  uint32_t red[2][4][kSelWaves];  // reduction scratch, alternating halves: one barrier per reduction
   uint32_t hist[KB_NUM_REASONS];
   uint32_t theta0;
   int32_t n_act, s_count, cut, stop_kind, n_alloc;
@@ -1279,6 +1284,8 @@ struct SelShared {
   uint64_t t_recv;
 };
 constexpr int kSelDynLimit = 160 * 1024 - (int)sizeof(SelShared) - 64;
+static_assert(4 * (4 * kSelThreads * kSelQ4) + 8 * kCandCap <= kSelDynLimit,
+              "the selection plan's largest node count (512 x 48 keys) must fit LDS");
 
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
   (void)lane;
@@ -1313,6 +1320,43 @@ __device__ __forceinline__ void sel_reduce3(SelShared& sh, int& rp, uint32_t& s,
     mx = umax32(mx, r[1][w]);
     mn = r[2][w] < mn ? r[2][w] : mn;
   }
+}
+// Node selection's first reduction: feasible count F, max / min score field MX / MN, and the keys at MX: E in
+// total and *pre = those of the threads before this one (thread order = node order). lc: the thread's keys at
+// its own maximum mx (its count at MX when mx == MX). One barrier.
+__device__ __forceinline__ void sel_reduce_top(SelShared& sh, int& rp, uint32_t& F, uint32_t& MX, uint32_t& MN,
+                                               uint32_t& E, uint32_t& pre, uint32_t& e, uint32_t lc) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t mx = MX;
+  const uint32_t fw = wave_sum_u32(F), mxw = wave_max_u32(mx), mnw = wave_min_u32(MN);
+  const uint32_t ew = mx == mxw ? lc : 0u;
+  const uint32_t xw = wave_excl_scan_u32(ew, lane), sw = wave_sum_u32(ew);
+  uint32_t(*r)[kSelWaves] = sh.red[rp];
+  rp ^= 1;
+  if (lane == 0) {
+    r[0][wv] = fw;
+    r[1][wv] = mxw;
+    r[2][wv] = mnw;
+    r[3][wv] = sw;
+  }
+  __syncthreads();
+  F = 0, MX = 0, MN = 0xffffffffu;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) {
+    F += r[0][w];
+    MX = umax32(MX, r[1][w]);
+    MN = r[2][w] < MN ? r[2][w] : MN;
+  }
+  E = 0, pre = 0;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) {
+    const uint32_t c = r[1][w] == MX ? r[3][w] : 0u;
+    E += c;
+    pre += w < wv ? c : 0u;
+  }
+  const bool top = mxw == MX;
+  pre += top ? xw : 0u;
+  e = top ? ew : 0u;
 }
 __device__ __forceinline__ uint32_t sel_sum(SelShared& sh, int& rp, uint32_t v) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1450,16 +1494,20 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       BODY                                                       \
     }                                                            \
   }
-    uint32_t F = 0, MX = 0, MN = 0xffffffffu;
+    uint32_t F = 0, MX = 0, MN = 0xffffffffu, LC = 0;
     SEL_EACH_KEY({
       if (k >> 31) {
         ++F;
         const uint32_t h = k >> idx_bits;
+        LC = h > MX ? 1u : LC + (h == MX);
         MX = umax32(MX, h);
         MN = h < MN ? h : MN;
       }
     })
-    sel_reduce3(sh, rp, F, MX, MN);
+    // with the count at the top score: nothing lies above MX, so when at least T nodes share it this is also
+    // the greater / equal count of the compaction
+    uint32_t Etop, pre_top, e_top;
+    sel_reduce_top(sh, rp, F, MX, MN, Etop, pre_top, e_top, LC);
     KB_SEL_FINE(1);
     bool no_fit = F == 0;
     if (!no_fit) {
@@ -1468,14 +1516,12 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       uint32_t g = 0, e = 0, tg = 0, te = 0, G = 0, E = 0;
       bool counted = false;
       if (F > T) {
-        // first probe: the top score itself (often enough nodes share it). Nothing lies above MX, so this
-        // pass is also the greater / equal count of the compaction when it succeeds.
-        SEL_EACH_KEY({ e += (k >> idx_bits) == MX; })
-        E = e;
-        sel_excl_scan2(sh, rp, G, E, &tg, &te);
-        if (te >= T) {
+        if (Etop >= T) {
           sstar = MX;
           counted = true;
+          e = e_top;
+          E = pre_top;
+          te = Etop;
         } else {
           uint32_t lo = MN, hi = MX - 1;  // count(>= MN) = F > T; count(>= MX) < T
           while (lo < hi) {
@@ -1534,6 +1580,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         sh.row[tid] = r;
         sh.stat[tid] = stat[w];
         sh.A[tid] = allocs_before_full(N, sp, sci, scr, r, w);
+        sh.recip[0][tid] = 1.0 / (double)r.alloc_cpu;
+        sh.recip[1][tid] = 1.0 / (double)r.alloc_mem;
         sh.cnt[tid] = 0;
         sh.gen[tid] = 0;
         sh.emin[tid] = 0xffffffffu;
@@ -1600,8 +1648,9 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           x = sh.key0[s];
           if (j > 0) {
             const int w = sh.node[s];
-            x = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s]), w + N.base,
-                             idx_bits);
+            x = compress_key(traj_key64<true>(N, P, C, sp, sci, scr, sh.row[s], sh.stat[s], w, j, sh.A[s],
+                                              sh.recip[0][s], sh.recip[1][s]),
+                             w + N.base, idx_bits);
           }
         }
         // segmented inclusive prefix minimum over the group's lanes (levels in order)
@@ -2402,10 +2451,10 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // Fed engine: the selection place kernel as ONE resident workgroup for a whole allocate cycle, fed through
 // device memory. Per job (one selection run) the host launches only fed_cmd_sweep_kernel on the sweep
 // stream: it computes the run's level-0 keys and static cache into the job slot's buffers, block 0
-// writes the run's command into a two-entry ring, and every block adds one to the ring entry's counter
-// with an agent-scope release. The engine waits for the counter (acquire), checks the command's guard
-// against the previous job's outcome, re-keys the rows the previous job committed (its sweep may have
-// overlapped that job), runs the selection and publishes to the slot's pinned host buffers exactly as
+// writes the run's command into a kJobSlots-entry ring, and every block adds one to the ring entry's
+// counter with an agent-scope release. The engine waits for the counter (acquire), checks the command's
+// guard against the previous job's outcome, re-keys the rows the previous two jobs committed (its sweep may
+// have overlapped both), runs the selection and publishes to the slot's pinned host buffers exactly as
 // sel_place_kernel does. No per-job kernel boundary on the place stream: the launch gap, the end-of-
 // kernel release and the next kernel's acquire (5.6 us median between place kernels) go away.
 // ===========================================================================
@@ -2418,12 +2467,13 @@ struct FedCmd {
 };
 
 struct FedSlots {
-  uint32_t* keys[2];
-  uint64_t* stat[2];
-  int32_t* commits[2];
-  JobState* js[2];   // device job state per slot
-  JobState* hjs[2];  // pinned host job state per slot (device addresses)
-  int32_t* hout[2];  // pinned host placements per slot (device addresses)
+  uint32_t* keys[kJobSlots];
+  uint64_t* stat[kJobSlots];
+  int32_t* commits[kJobSlots];
+  JobState* js[kJobSlots];   // device job state per slot
+  JobState* hjs[kJobSlots];  // pinned host job state per slot (device addresses)
+  int32_t* hout[kJobSlots];  // pinned host placements per slot (device addresses)
+  uint32_t tgt[kJobSlots];   // ring counters' targets at launch
 };
 
 template <bool AFF>
@@ -2450,8 +2500,8 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
 template <int QN>
 __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                                  FedSlots S, const FedCmd* ring,
-                                                                 const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1,
-                                                                 uint64_t idle_ticks, int32_t* exit_flag) {
+                                                                 const uint32_t* ctr, uint64_t idle_ticks,
+                                                                 int32_t* exit_flag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
@@ -2463,18 +2513,22 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   const uint32_t blocks = (uint32_t)((n + 63) / 64);
-  uint32_t tgt[2] = {tgt0, tgt1};
+  uint32_t tgt[kJobSlots];
+#pragma unroll
+  for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
   int last_stop = -1, last_placed = -1, last_ready = -1, last_panic = 1;  // no previous job: guards fail
-  int prev_slot = -1, prev_ncommit = 0;
+  // the commit lists of the previous two jobs ([0] the last one): a job's sweep may have run before either
+  // committed (the host issues a job once the job three back is read)
+  int prev_slot[2] = {-1, -1}, prev_ncommit[2] = {0, 0};
   int rp = 0;
 #ifdef KB_DIAG
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
   // publish (fence + host writes)
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
-  uint64_t t_wait0 = dg_last, pub_prev = 0;
+  uint64_t t_wait0 = dg_last, pub_prev = 0, rt_wait0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  for (int r = 0;; r ^= 1) {
+  for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1) {
     tgt[r] += blocks;
     if (tid == 0) {  // wait for the ring entry's command and keys (acquire), bounded by idle_ticks
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2504,24 +2558,26 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         __hip_atomic_store(&hjs->seq, cm.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       last_panic = 1;
-      prev_slot = slot;
-      prev_ncommit = 0;
+      prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
+      prev_slot[0] = slot, prev_ncommit[0] = 0;
       __syncthreads();
       continue;
     }
 #ifdef KB_DIAG
     for (int k = 0; k < 7; ++k) dg[k] = 0;
     dg_last = __builtin_amdgcn_s_memtime();
-    dg[0] = dg_last - t_wait0;  // wait for the command (+ guard)
-    dg[6] = pub_prev;
-    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t wait_cycles = dg_last - t_wait0;  // wait for the command (+ guard)
+    dg[5] = pub_prev;
+    const uint64_t rt0 = rt_wait0;
 #endif
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
-    // the previous job's commits (final rows) re-keyed for this spec: their loads first
-    const int np = prev_slot >= 0 ? prev_ncommit : 0;
-    const int32_t* patch = prev_slot >= 0 ? S.commits[prev_slot] : nullptr;
-    const int pw = tid < np ? patch[tid] : -1;
+    // the previous two jobs' commits (final rows) re-keyed for this spec: their loads first
+    const int np0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0;
+    const int np = np0 + (prev_slot[1] >= 0 ? prev_ncommit[1] : 0);
+    const int32_t* patch0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
+    const int32_t* patch1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
+    const int pw = tid < np ? (tid < np0 ? patch0[tid] : patch1[tid - np0]) : -1;
     Row prow;
     if (pw >= 0) prow = load_row(N, pw);
     const uint64_t pst = pw >= 0 ? stat[pw] : 0;
@@ -2535,7 +2591,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
       }
       for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
-        const int w = patch[i];
+        const int w = i < np0 ? patch0[i] : patch1[i - np0];
         const Row rr = load_row(N, w);
         const uint64_t st = stat[w];
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
@@ -2551,6 +2607,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                        placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
                        S.commits[slot] SEL_DIAG_ARGS);
 #ifdef KB_DIAG
+    // fed engine layout: [0] key load + patch, [1..4] as sel_run, [5] commit + the previous job's publish +
+    // the no-fit histogram, [6] waiting for this job's command; [7] realtime ticks including the wait
+    dg[5] += dg[6];
+    dg[6] = wait_cycles;
     if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
     // every wave's host-buffer and row stores are complete before the barrier; one lane then releases at
@@ -2566,11 +2626,12 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
     }
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
-    prev_slot = slot;
-    prev_ncommit = ncommit;
+    prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
+    prev_slot[0] = slot, prev_ncommit[0] = ncommit;
     __syncthreads();  // cm / sh reused by the next command
 #ifdef KB_DIAG
     t_wait0 = __builtin_amdgcn_s_memtime();
+    rt_wait0 = __builtin_amdgcn_s_memrealtime();
     pub_prev = t_wait0 - t_pub;
 #endif
   }
@@ -2595,13 +2656,14 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
                      keys32, stat, cmd, (FedCmd*)ring, ctr, sweep ? 1 : 0);
 }
 
-size_t fed_ring_bytes() { return 2 * sizeof(FedCmd); }
+size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
 
 void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
-                       const void* ring, const uint32_t* ctr, uint32_t tgt0, uint32_t tgt1, uint64_t idle_ticks,
+                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
                        int32_t* exit_flag, void* stream) {
   FedSlots S;
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < kJobSlots; ++s) {
+    S.tgt[s] = tgt[s];
     S.keys[s] = sp.keys[s];
     S.stat[s] = sp.stat[s];
     S.commits[s] = sp.commits[s];
@@ -2614,7 +2676,7 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 #define KB_FED_QN(Q)                                                                                              \
   case Q:                                                                                                        \
     hipLaunchKernelGGL(fed_engine_kernel<Q>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C,     \
-                       idx_bits, S, (const FedCmd*)ring, ctr, tgt0, tgt1, idle_ticks, exit_flag);                \
+                       idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag);                            \
     break;
   switch (qn) {
     KB_FED_QN(1)

@@ -185,8 +185,9 @@ void kb_destroy(kb_ctx* c) {
   free_all(c->work_mem);
   free_all(c->ov_mem);
   if (c->h_job) (void)hipHostFree(c->h_job);
-  if (c->h_job1) (void)hipHostFree(c->h_job1);
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < kJobSlots; ++s)
+    if (c->h_jobx[s]) (void)hipHostFree(c->h_jobx[s]);
+  for (int s = 0; s < kJobSlots; ++s) {
     if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
     if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
     if (c->commits[s]) (void)hipFree(c->commits[s]);
@@ -854,7 +855,7 @@ static int validate_job(kb_ctx* c, const kb_job_req* job) {
 // Per-slot selection buffers (level-0 keys, static cache, commit list), the sweep stream and its events.
 static int ensure_sel_bufs(kb_ctx* c) {
   if (c->sel_n != c->N.n) {
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kJobSlots; ++s) {
       if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
       if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
       c->sel_keys[s] = nullptr;
@@ -862,7 +863,7 @@ static int ensure_sel_bufs(kb_ctx* c) {
     }
     c->sel_n = -1;
     const size_t n = (size_t)std::max(c->N.n, 1);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kJobSlots; ++s) {
       HIP_OK(c, hipMalloc((void**)&c->sel_keys[s], n * 4));
       HIP_OK(c, hipMalloc((void**)&c->sel_stat[s], n * 8));
     }
@@ -870,12 +871,12 @@ static int ensure_sel_bufs(kb_ctx* c) {
     c->prev_listed = false;
   }
   if (c->commits_cap < c->job_cap) {
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kJobSlots; ++s) {
       if (c->commits[s]) (void)hipFree(c->commits[s]);
       c->commits[s] = nullptr;
     }
     c->commits_cap = 0;
-    for (int s = 0; s < 2; ++s) HIP_OK(c, hipMalloc((void**)&c->commits[s], (size_t)c->job_cap * 4));
+    for (int s = 0; s < kJobSlots; ++s) HIP_OK(c, hipMalloc((void**)&c->commits[s], (size_t)c->job_cap * 4));
     c->commits_cap = c->job_cap;
     c->prev_listed = false;
   }
@@ -888,34 +889,43 @@ static int ensure_sel_bufs(kb_ctx* c) {
   return KB_OK;
 }
 
-// Both job slots with room for n_tasks placements (slot 0 = d_job / h_job).
-static int ensure_slots(kb_ctx* c, uint32_t n_tasks, bool both) {
+// Every job slot with room for n_tasks placements (slot 0 = d_job / h_job; all: slots 1.. as well).
+static int ensure_slots(kb_ctx* c, uint32_t n_tasks, bool all) {
   if (int rc = ensure_job_buffers(c, n_tasks)) return rc;
   if (int rc = ensure_sel_bufs(c)) return rc;
   c->slot[0].d = c->d_job;
   c->slot[0].h = c->h_job;
   c->slot[0].hdev = c->h_job_dev;
-  if (!both) return KB_OK;
-  if (!c->d_job1) {
-    void* p;
-    HIP_OK(c, hipMalloc(&p, sizeof(JobState)));
-    HIP_OK(c, hipMemset(p, 0, sizeof(JobState)));
-    c->work_mem.push_back(p);
-    c->d_job1 = (char*)p;
+  if (!all) return KB_OK;
+  for (int s = 1; s < kJobSlots; ++s) {
+    if (!c->d_jobx[s]) {
+      void* p;
+      HIP_OK(c, hipMalloc(&p, sizeof(JobState)));
+      HIP_OK(c, hipMemset(p, 0, sizeof(JobState)));
+      c->work_mem.push_back(p);
+      c->d_jobx[s] = (char*)p;
+    }
+    if (!c->h_jobx[s] || c->jobx_cap[s] < c->job_cap) {
+      if (c->h_jobx[s]) (void)hipHostFree(c->h_jobx[s]);
+      c->h_jobx[s] = nullptr;
+      const size_t bytes = sizeof(JobState) + (size_t)c->job_cap * 2 * sizeof(int32_t);
+      HIP_OK(c, hipHostMalloc((void**)&c->h_jobx[s], bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_OK(c, hipHostGetDevicePointer((void**)&c->slot[s].hdev, c->h_jobx[s], 0));
+      memset(c->h_jobx[s], 0, bytes);
+      ((JobState*)c->h_jobx[s])->seq = c->seq;
+      c->jobx_cap[s] = c->job_cap;
+    }
+    c->slot[s].d = c->d_jobx[s];
+    c->slot[s].h = c->h_jobx[s];
   }
-  if (!c->h_job1 || c->job1_cap < c->job_cap) {
-    if (c->h_job1) (void)hipHostFree(c->h_job1);
-    c->h_job1 = nullptr;
-    const size_t bytes = sizeof(JobState) + (size_t)c->job_cap * 2 * sizeof(int32_t);
-    HIP_OK(c, hipHostMalloc((void**)&c->h_job1, bytes, hipHostMallocMapped | hipHostMallocCoherent));
-    HIP_OK(c, hipHostGetDevicePointer((void**)&c->slot[1].hdev, c->h_job1, 0));
-    memset(c->h_job1, 0, bytes);
-    ((JobState*)c->h_job1)->seq = c->seq;
-    c->job1_cap = c->job_cap;
-  }
-  c->slot[1].d = c->d_job1;
-  c->slot[1].h = c->h_job1;
   return KB_OK;
+}
+
+// the smallest capacity over the pipelined driver's slots
+static uint32_t slots_cap(const kb_ctx* c) {
+  uint32_t cap = c->job_cap;
+  for (int s = 1; s < kJobSlots; ++s) cap = std::min(cap, c->jobx_cap[s]);
+  return cap;
 }
 
 // Launch every run of the job into slot `si`. The path per run: block-wide re-sweep (self-dependent
@@ -1085,7 +1095,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
   if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
   if (int rc = kb_engine_stop(c)) return rc;
-  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
   if (int rc = ensure_slots(c, job->n_tasks, false)) return rc;
   if (int rc = place_issue(c, job, 0, SpecGuard{nullptr, 0, 0, 0})) return rc;
   return place_finish(c, 0, placed_node, placed_kind, result, false);
@@ -1103,7 +1113,7 @@ int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
 
 int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
   if (!c) return KB_E_INVALID;
-  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
   return ensure_slots(c, std::max<uint32_t>(max_tasks, 1), true);
 }
 
@@ -1126,18 +1136,18 @@ static uint64_t fed_idle_ticks() {
 int kb_fed_begin(kb_ctx* c) {
   if (!c) return KB_E_INVALID;
   if (c->fed) return fail(c, KB_E_STATE, "fed engine already running");
-  if (c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
-  if (!c->slot[1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
+  if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+  if (!c->slot[kJobSlots - 1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
   if (!c->fed_ring) {
     HIP_OK(c, hipMalloc(&c->fed_ring, fed_ring_bytes()));
-    HIP_OK(c, hipMalloc((void**)&c->fed_ctr, 2 * sizeof(uint32_t)));
+    HIP_OK(c, hipMalloc((void**)&c->fed_ctr, kJobSlots * sizeof(uint32_t)));
     HIP_OK(c, hipMalloc((void**)&c->fed_exit, sizeof(int32_t)));
-    HIP_OK(c, hipMemset(c->fed_ctr, 0, 2 * sizeof(uint32_t)));
-    c->fed_count[0] = c->fed_count[1] = 0;
+    HIP_OK(c, hipMemset(c->fed_ctr, 0, kJobSlots * sizeof(uint32_t)));
+    for (int s = 0; s < kJobSlots; ++s) c->fed_count[s] = 0;
   }
   HIP_OK(c, hipMemsetAsync(c->fed_exit, 0, sizeof(int32_t), c->stream));
   FedSlotPtrs sp;
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < kJobSlots; ++s) {
     sp.keys[s] = c->sel_keys[s];
     sp.stat[s] = c->sel_stat[s];
     sp.commits[s] = c->commits[s];
@@ -1154,8 +1164,8 @@ int kb_fed_begin(kb_ctx* c) {
     c->ev_begin(&c->fed_ev);
     c->timing_now = tn;
   }
-  launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count[0], c->fed_count[1],
-                    fed_idle_ticks(), c->fed_exit, c->stream);
+  launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count, fed_idle_ticks(),
+                    c->fed_exit, c->stream);
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1166,10 +1176,10 @@ int kb_fed_begin(kb_ctx* c) {
 static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
   const int r = c->fed_r;
   launch_fed_cmd(c->N, c->P, c->cfg, c->idx_bits, c->sel_keys[si], c->sel_stat[si], a,
-                 (char*)c->fed_ring + r * (fed_ring_bytes() / 2), c->fed_ctr + r, sweep, c->stream_b);
+                 (char*)c->fed_ring + r * (fed_ring_bytes() / kJobSlots), c->fed_ctr + r, sweep, c->stream_b);
   HIP_OK(c, hipGetLastError());
   c->fed_count[r] += (uint32_t)((c->N.n + 63) / 64);
-  c->fed_r ^= 1;
+  c->fed_r = r + 1 == kJobSlots ? 0 : r + 1;
   return KB_OK;
 }
 
@@ -1187,7 +1197,7 @@ int kb_fed_end(kb_ctx* c) {
   if (c->timing) c->ev_collect(true);
   // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;
-  if (rc == KB_OK && (c->slot[0].busy || c->slot[1].busy) &&
+  if (rc == KB_OK && c->any_busy() &&
       hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
     rc = fail(c, KB_E_HIP, "fed engine exited idle with a job in flight");
   return rc;
@@ -1206,7 +1216,7 @@ int kb_fed_abandon(kb_ctx* c) {
   HIP_OK(c, hipStreamSynchronize(c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream_b));  // the unserved jobs' sweeps (they only read rows)
   HIP_OK(c, hipMemset(c->fed_exit, 0, sizeof(int32_t)));
-  c->slot[0].busy = c->slot[1].busy = false;
+  for (auto& sl : c->slot) sl.busy = false;
   c->prev_listed = false;
   c->n_fed_abandon++;
   c->stats.fed_abandon++;
@@ -1214,11 +1224,12 @@ int kb_fed_abandon(kb_ctx* c) {
 }
 
 int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* pred) {
-  if (!c || !job || slot < 0 || slot > 1) return KB_E_INVALID;
+  if (!c || !job || slot < 0 || slot >= kJobSlots) return KB_E_INVALID;
+  if (!c->fed && slot > 1) return fail(c, KB_E_INVALID, "the per-job launch path pipelines two slots");
   if (int rc = validate_job(c, job)) return rc;
   if (job->n_tasks == 0) return fail(c, KB_E_INVALID, "empty job");
   if (c->slot[slot].busy) return fail(c, KB_E_STATE, "job slot %d is busy", slot);
-  if (job->n_tasks > c->job_cap || job->n_tasks > c->job1_cap)  // growing would free a slot in flight
+  if (job->n_tasks > slots_cap(c))  // growing would free a slot in flight
     return fail(c, KB_E_STATE, "kb_job_reserve(%u) first", job->n_tasks);
   if (int rc = kb_engine_stop(c)) return rc;
   if (int rc = ensure_slots(c, job->n_tasks, true)) return rc;
@@ -1249,7 +1260,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
 
 int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kind, kb_job_result* result,
                   int skipped) {
-  if (!c || !result || slot < 0 || slot > 1) return KB_E_INVALID;
+  if (!c || !result || slot < 0 || slot >= kJobSlots) return KB_E_INVALID;
   memset(result, 0, sizeof(*result));
   result->fail_task = -1;
   return place_finish(c, slot, placed_node, placed_kind, result, skipped != 0);
@@ -1366,7 +1377,7 @@ static int pred_keys(kb_ctx* c, int32_t spec, bool sort, std::vector<uint64_t>& 
   c->prev_listed = false;
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
-  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (c->fed || c->any_busy()) return fail(c, KB_E_STATE, "a job is in flight");
   if (c->sharded) return fail(c, KB_E_UNSUPPORTED, "kb_sort_nodes does not run node-sharded");
   if (spec < 0 || spec >= c->P.m) return fail(c, KB_E_INVALID, "spec %d out of range", spec);
   if (c->spec_needs_aff[spec] && !c->aff_ok)
@@ -1434,7 +1445,7 @@ int kb_set_host_overlay(kb_ctx* c, int32_t spec, const uint8_t* fail_in, const i
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
-  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (c->fed || c->any_busy()) return fail(c, KB_E_STATE, "a job is in flight");
   if (spec < 0 || spec >= c->P.m) return fail(c, KB_E_INVALID, "spec %d out of range", spec);
   HIP_OK(c, hipSetDevice(c->device));
   const size_t n = (size_t)c->N.n, m = (size_t)c->P.m;
@@ -1499,7 +1510,7 @@ int kb_apply(kb_ctx* c, const kb_row_delta* d, uint32_t k, const int64_t* sc, ui
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
-  if (c->fed || c->slot[0].busy || c->slot[1].busy) return fail(c, KB_E_STATE, "a job is in flight");
+  if (c->fed || c->any_busy()) return fail(c, KB_E_STATE, "a job is in flight");
   if (k == 0) return KB_OK;
   // every index the kernel follows is checked here
   const uint32_t S = (uint32_t)c->N.S;

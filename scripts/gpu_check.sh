@@ -48,4 +48,7 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
   python3 scripts/prof_summary.py "$OUT/prof" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/prof_summary.json" \
        > "$OUT/prof_summary.log" 2>&1; echo "=== prof_summary rc=$?"
 fi
+if [ "$MODE" = cpubase ]; then  # the oracle's CPU baselines for every config on the box's host cores
+  step cpubase 1100 python3 scripts/cpu_baselines.py "$OUT/cpu_baselines.json"
+fi
 echo "=== done"
