@@ -405,6 +405,8 @@ typedef struct kb_stats {
   uint64_t diag[8];                   /* diagnostic builds only: place-loop phase cycles, [7] realtime */
   uint64_t fed_abandon;               /* kb_allocate cycles the resident engine idled out of (host stall > its
                                          idle bound): finished on the launch path */
+  uint64_t fed_cycles, fed_split;     /* kb_allocate cycles served by the resident engine; of those, by the
+                                         split engine (node selection one job ahead on a second workgroup) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

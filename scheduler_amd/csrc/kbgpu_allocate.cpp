@@ -643,7 +643,7 @@ struct Driver {
       }
     }
     if (fed)
-      if (int rc = kb_fed_begin(ctx)) return rc;
+      if (int rc = kb_fed_begin(ctx, max_pending)) return rc;
     struct FedEnd {  // the engine is stopped on every way out of the loop
       kb_ctx* c;
       bool on;

@@ -122,6 +122,8 @@ struct kb_ctx {
   void* fed_ring = nullptr;
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;
+  void* fed_xchg = nullptr;   // split engine exchange (fed_xchg_bytes)
+  bool use_fed_split = true;  // KB_NO_FED_SPLIT unset
   uint32_t fed_count[kbgpu::kJobSlots] = {};
   int fed_r = 0;
   uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)
@@ -179,7 +181,8 @@ extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, u
 // (kb_spec_fed_ok): kb_fed_begin after kb_job_reserve, then kb_job_issue / kb_job_finish as usual (each
 // issue launches only the job's sweep kernel), kb_fed_end before anything else runs on the context.
 extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, int spec);
-extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c);
+// max_job_tasks: the most tasks any job of the cycle can place (the split engine takes one-segment jobs only)
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);
 // kb_job_finish's code when the resident engine idled out before serving the job (see kb_fed_abandon)
 constexpr int kFedIdleExit = -100;

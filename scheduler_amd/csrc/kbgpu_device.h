@@ -203,9 +203,14 @@ size_t fed_ring_bytes();
 bool fed_fits(int n);  // the engine's LDS plan fits n nodes
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
                     uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream);
+// xchg (fed_xchg_bytes(), zeroed): the split engine, a second workgroup choosing each job's candidate nodes
+// one job ahead (fed_split_ok(n)); nullptr: one workgroup.
+constexpr int kFedSplitMaxTasks = 100;  // one selection segment (kbgpu_device.hip kSegMax)
+size_t fed_xchg_bytes();
+bool fed_split_ok(int n);
 void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                        const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                       int32_t* exit_flag, void* stream);
+                       int32_t* exit_flag, void* xchg, void* stream);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.

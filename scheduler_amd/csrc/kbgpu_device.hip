@@ -817,6 +817,7 @@ constexpr uint32_t kKey32Feasible = 1u << 31;
 constexpr uint32_t kKey32Exhausted = 0x7fffffffu;  // nxt32 sentinel: trajectory ran out, compute on demand
 
 __device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
@@ -1247,6 +1248,7 @@ constexpr int kSelWaves = kSelThreads / 64;
 #define KB_SEL_DENSE_MAX 32  // winners: rank all candidates pairwise up to this many, else threshold + takes
 #endif
 constexpr int kSegMax = 100;                           // tasks per segment (slot and level fit 7-bit fields)
+static_assert(kSegMax == kFedSplitMaxTasks, "the split fed engine's job bound is one segment");
 constexpr int kCandMax = kSegMax * (kSegMax + 1) / 2;  // sum over S of (T - rank): levels that can rank < T
 constexpr int kCandCap = 5120;                         // candidate composites: 10 per thread, five uint4 reads
 constexpr int kCandV = kCandCap / 2 / kSelThreads;     // uint4 (two composites) groups per thread
@@ -1278,6 +1280,8 @@ struct SelShared {
   uint32_t hist[KB_NUM_REASONS];
   uint32_t theta0;
   int32_t n_act, s_count, cut, stop_kind, n_alloc;
+  int32_t n_sel;      // CAND runs: the selected set published to the fed selector
+  int32_t need_hist;  // CAND runs: a no-fit whose histogram the caller computes
   LoopOut lo;
   EngineCmd cmd;  // placement engine: the command being served and its current run
   EngineRun run;
@@ -1286,6 +1290,7 @@ struct SelShared {
 constexpr int kSelDynLimit = 160 * 1024 - (int)sizeof(SelShared) - 64;
 static_assert(4 * (4 * kSelThreads * kSelQ4) + 8 * kCandCap <= kSelDynLimit,
               "the selection plan's largest node count (512 x 48 keys) must fit LDS");
+constexpr int kFedDynLimit = kSelDynLimit - 2048;  // the fed engine's own static LDS beside SelShared
 
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
   (void)lane;
@@ -1450,6 +1455,105 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 #define SEL_DIAG_ARGS
 #endif
 
+// Node selection, phase 1 of sel_run: the T best keys of k32 (LDS, 4 * kSelThreads * Q4 positions, zero padding)
+// by score field, ties to the lower position. sh.node / sh.key0 [0, S) get node_of(position) and the key, in
+// position order (cnode: the node at each position; nullptr: the position itself). Returns the feasible count
+// (0: nothing fits, S = 0). No barrier after the LDS writes.
+template <int QN>
+__device__ __forceinline__ uint32_t sel_pick(SelShared& sh, const uint32_t* k32, int n, int idx_bits, uint32_t T,
+                                             int& rp, uint32_t& S_out, const int32_t* cnode SEL_DIAG_PARAMS) {
+  const int tid = threadIdx.x;
+  constexpr int QU = QN > 0 ? QN : kSelQ4;  // unroll bound of the key passes
+  const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const uint4* k32v = (const uint4*)k32;
+  uint4 kv[QU];
+#pragma unroll
+  for (int c = 0; c < QU; ++c) kv[c] = (QN > 0 || c < Q4) ? k32v[tid * Q4 + c] : make_uint4(0u, 0u, 0u, 0u);
+#define SEL_EACH_KEY(BODY)                                       \
+  _Pragma("unroll") for (int c_ = 0; c_ < QU; ++c_) {           \
+    const uint32_t ks_[4] = {kv[c_].x, kv[c_].y, kv[c_].z, kv[c_].w}; \
+    _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {           \
+      const uint32_t k = ks_[q_];                                \
+      const int ki = (tid * Q4 + c_) * 4 + q_;                   \
+      (void)ki;                                                  \
+      BODY                                                       \
+    }                                                            \
+  }
+  // branch-free over the keys (a branch per key costs more than the arithmetic): an infeasible key counts
+  // as score field 0 for the maximum (below every feasible field) and as ~0 for the minimum
+  uint32_t F = 0, MX = 0, MN = 0xffffffffu, LC = 0;
+  SEL_EACH_KEY({
+    const bool f = (int32_t)k < 0;
+    const uint32_t h = f ? k >> idx_bits : 0u;
+    F += f;
+    LC = h > MX ? 1u : LC + (h == MX);
+    MX = umax32(MX, h);
+    MN = umin32(MN, f ? h : 0xffffffffu);
+  })
+  // with the count at the top score: nothing lies above MX, so when at least T nodes share it this is also
+  // the greater / equal count of the compaction
+  uint32_t Etop, pre_top, e_top;
+  sel_reduce_top(sh, rp, F, MX, MN, Etop, pre_top, e_top, LC);
+  KB_SEL_FINE(1);
+  S_out = 0;
+  if (F == 0) return 0;
+  // infeasible keys (and padding) have a score field below every feasible one: never counted below
+  uint32_t sstar = MN, R = 0xffffffffu;  // F <= T: every feasible node
+  uint32_t g = 0, e = 0, tg = 0, te = 0, G = 0, E = 0;
+  bool counted = false;
+  if (F > T) {
+    if (Etop >= T) {
+      sstar = MX;
+      counted = true;
+      e = e_top;
+      E = pre_top;
+      te = Etop;
+    } else {
+      uint32_t lo = MN, hi = MX - 1;  // count(>= MN) = F > T; count(>= MX) < T
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        uint32_t c = 0;
+        SEL_EACH_KEY({ c += (k >> idx_bits) >= mid; })
+        if (sel_sum(sh, rp, c) >= T) lo = mid;
+        else hi = mid - 1;
+      }
+      sstar = lo;
+    }
+  }
+  KB_SEL_FINE(2);
+  if (!counted) {
+    g = 0, e = 0;
+    SEL_EACH_KEY({
+      const uint32_t h = k >> idx_bits;
+      g += h > sstar;
+      e += h == sstar;
+    })
+    G = g, E = e;
+    sel_excl_scan2(sh, rp, G, E, &tg, &te);
+  }
+  KB_SEL_FINE(3);
+  if (F > T) R = T - tg;
+  const uint32_t selE = R > E ? (R - E < e ? R - E : e) : 0u;
+  // slot of this thread's first selected node: selected nodes before it in position order
+  uint32_t slot = G + (R > E ? E : R);
+  S_out = tg + (R < te ? R : te);
+  if (g + selE) {  // most threads hold no selected node
+    uint32_t le = 0;
+    SEL_EACH_KEY({
+      const uint32_t h = k >> idx_bits;
+      bool take = h > sstar;
+      if (h == sstar) take = le++ < selE;
+      if (take) {
+        sh.node[slot] = cnode != nullptr ? cnode[ki] : ki;
+        sh.key0[slot] = k;
+        ++slot;
+      }
+    })
+  }
+#undef SEL_EACH_KEY
+  return F;
+}
+
 // One run of same-spec tasks inside a 1024-thread workgroup (the selection algorithm above).
 // k32 (LDS, n_pad entries, zero past n) holds every node's current key at entry and is kept current;
 // cand (LDS, kCandCap) is scratch; stat is the run's static cache. Placements go to hout[2 * task];
@@ -1458,17 +1562,63 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 // to `rec` instead (launch_shard_propose).
 // QN > 0: the node count needs exactly QN key groups per thread (compile-time passes over 4 * QN keys);
 // QN = 0: the group count is taken from n at run time (passes unrolled to kSelQ4 with the spare groups 0).
-template <bool PROPOSE = false, int QN = 0>
+// The reason histogram of the infeasible keys among 4 * kSelThreads * Q4 (padding 0) into sh.hist; ends after a
+// barrier.
+__device__ void sel_hist(SelShared& sh, const uint4* k32v, int Q4) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
+  __syncthreads();
+  uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+  for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+  for (int c = 0; c < Q4; ++c) {
+    const uint4 v = k32v[tid * Q4 + c];
+    const uint32_t ks[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (ks[q] >> 31) continue;
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (ks[q] >> b) & 1u;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < KB_NUM_REASONS; ++b) {
+    const uint32_t v = wave_sum_u32(h[b]);
+    if (lane == 0 && v) atomicAdd(&sh.hist[b], v);
+  }
+  __syncthreads();
+}
+
+// The fed placer's publication to the selector (fed_engine_kernel): the nodes a job can commit to.
+struct FedPub {
+  int32_t* node = nullptr;  // [kSegMax + 28]
+  int32_t* n = nullptr;
+  int32_t* mode = nullptr;
+  uint32_t* start = nullptr;  // nullptr: nothing to publish
+  uint32_t val = 0;
+  // after a barrier that drained every wave's payload stores (write-through atomics, no L2 writeback needed)
+  __device__ void publish(int cnt) const {
+    __hip_atomic_store(n, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mode, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(start, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
+// cnode != nullptr (the fed engine's placer, one segment): k32 holds candidate keys by position (QN = 1 layout)
+// and cnode[position] their nodes; the selected set is published to the selector through `pub` once known, and a
+// no-fit sets sh.need_hist instead of the histogram (the caller rebuilds every node's key first).
+template <bool PROPOSE = false, int QN = 0, bool CAND = false>
 __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* cand, const DevNodes& N,
                                         const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
                                         int t_begin, int t_count,
                                         int idx_bits, const uint64_t* stat, int& ready, int minav, int gang,
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
-                                        ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS) {
+                                        ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS,
+                                        const int32_t* cnode = nullptr, FedPub pub = FedPub{}) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
-  constexpr int QU = QN > 0 ? QN : kSelQ4;  // unroll bound of the key passes
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const uint4* k32v = (const uint4*)k32;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
@@ -1480,91 +1630,18 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
-    // ---- 1. S = the T best nodes by current key (keys in registers for this phase) ----
-    uint4 kv[QU];
-#pragma unroll
-    for (int c = 0; c < QU; ++c) kv[c] = (QN > 0 || c < Q4) ? k32v[tid * Q4 + c] : make_uint4(0u, 0u, 0u, 0u);
-#define SEL_EACH_KEY(BODY)                                       \
-  _Pragma("unroll") for (int c_ = 0; c_ < QU; ++c_) {           \
-    const uint32_t ks_[4] = {kv[c_].x, kv[c_].y, kv[c_].z, kv[c_].w}; \
-    _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {           \
-      const uint32_t k = ks_[q_];                                \
-      const int ki = (tid * Q4 + c_) * 4 + q_;                   \
-      (void)ki;                                                  \
-      BODY                                                       \
-    }                                                            \
-  }
-    uint32_t F = 0, MX = 0, MN = 0xffffffffu, LC = 0;
-    SEL_EACH_KEY({
-      if (k >> 31) {
-        ++F;
-        const uint32_t h = k >> idx_bits;
-        LC = h > MX ? 1u : LC + (h == MX);
-        MX = umax32(MX, h);
-        MN = h < MN ? h : MN;
-      }
-    })
-    // with the count at the top score: nothing lies above MX, so when at least T nodes share it this is also
-    // the greater / equal count of the compaction
-    uint32_t Etop, pre_top, e_top;
-    sel_reduce_top(sh, rp, F, MX, MN, Etop, pre_top, e_top, LC);
-    KB_SEL_FINE(1);
-    bool no_fit = F == 0;
+    // ---- 1. S = the T best nodes by current key ----
+    uint32_t S;
+    bool no_fit;
+    if constexpr (CAND)
+      no_fit = sel_pick<1>(sh, k32, 4 * kSelThreads, idx_bits, T, rp, S, cnode SEL_DIAG_ARGS) == 0;
+    else
+      no_fit = sel_pick<QN>(sh, k32, n, idx_bits, T, rp, S, nullptr SEL_DIAG_ARGS) == 0;
+    if (CAND && no_fit && tid == 0) {  // nothing this job can commit to
+      sh.n_sel = 0;
+      if (pub.start != nullptr) pub.publish(0);
+    }
     if (!no_fit) {
-      // infeasible keys (and padding) have a score field below every feasible one: never counted below
-      uint32_t sstar = MN, R = 0xffffffffu;  // F <= T: every feasible node
-      uint32_t g = 0, e = 0, tg = 0, te = 0, G = 0, E = 0;
-      bool counted = false;
-      if (F > T) {
-        if (Etop >= T) {
-          sstar = MX;
-          counted = true;
-          e = e_top;
-          E = pre_top;
-          te = Etop;
-        } else {
-          uint32_t lo = MN, hi = MX - 1;  // count(>= MN) = F > T; count(>= MX) < T
-          while (lo < hi) {
-            const uint32_t mid = lo + (hi - lo + 1) / 2;
-            uint32_t c = 0;
-            SEL_EACH_KEY({ c += (k >> idx_bits) >= mid; })
-            if (sel_sum(sh, rp, c) >= T) lo = mid;
-            else hi = mid - 1;
-          }
-          sstar = lo;
-        }
-      }
-      KB_SEL_FINE(2);
-      if (!counted) {
-        g = 0, e = 0;
-        SEL_EACH_KEY({
-          const uint32_t h = k >> idx_bits;
-          g += h > sstar;
-          e += h == sstar;
-        })
-        G = g, E = e;
-        sel_excl_scan2(sh, rp, G, E, &tg, &te);
-      }
-      KB_SEL_FINE(3);
-      if (F > T) R = T - tg;
-      const uint32_t selE = R > E ? (R - E < e ? R - E : e) : 0u;
-      // slot of this thread's first selected node: selected nodes before it in index order
-      uint32_t slot = G + (R > E ? E : R);
-      const uint32_t S = tg + (R < te ? R : te);
-      if (g + selE) {  // most threads hold no selected node
-        uint32_t le = 0;
-        SEL_EACH_KEY({
-          const uint32_t h = k >> idx_bits;
-          bool take = h > sstar;
-          if (h == sstar) take = le++ < selE;
-          if (take) {
-            sh.node[slot] = ki;
-            sh.key0[slot] = k;
-            ++slot;
-          }
-        })
-      }
-#undef SEL_EACH_KEY
       // zero the candidate lists (an unused entry reads as 0: never counted)
       {
         uint4* cv = (uint4*)cand;
@@ -1606,7 +1683,14 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           if (rk == S - 1) sh.theta0 = k;
         }
       }
+      if (CAND && pub.start != nullptr && tid < (int)S)
+        __hip_atomic_store(&pub.node[tid], sh.node[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
+      // the nodes this job can commit to, for the selector's next job (the barrier drained every wave's stores)
+      if (CAND && tid == 0) {
+        sh.n_sel = (int)S;
+        if (pub.start != nullptr) pub.publish((int)S);
+      }
       if (wv == 0) {
         const uint32_t a = lane < (int)S ? (uint32_t)sh.lmax[lane] : 0u;
         const uint32_t b = lane + 64 < (int)S ? (uint32_t)sh.lmax[lane + 64] : 0u;
@@ -1711,12 +1795,11 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         const int fs = 14 + idx_bits;  // score field of a composite
         uint32_t HX = 0, HN = 0xffffffffu, kk = kc;
 #pragma unroll
-        for (int q = 0; q < 2 * kCandV; ++q)
-          if (cs[q]) {
-            const uint32_t h = (uint32_t)(cs[q] >> fs);
-            HX = umax32(HX, h);
-            HN = h < HN ? h : HN;
-          }
+        for (int q = 0; q < 2 * kCandV; ++q) {
+          const uint32_t h = (uint32_t)(cs[q] >> fs);  // 0 for an unused entry
+          HX = umax32(HX, h);
+          HN = umin32(HN, cs[q] ? h : 0xffffffffu);
+        }
         sel_reduce3(sh, rp, kk, HX, HN);
         uint32_t lo = HN, hi = HX;  // K < T ends at lo = HN: every candidate
         while (lo < hi) {
@@ -1847,7 +1930,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram; commit_out
       // lists the rows for the next job, whose level-0 sweep ran before these stores (kb_job_issue)
-      const bool rekey = kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count);
+      const bool rekey = !CAND && (kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count));
       if (tid < (int)S && sh.fin[tid] > 0) {
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
         store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
@@ -1876,29 +1959,16 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
     }
     if (no_fit) {
+      if constexpr (CAND) {  // the caller rebuilds every node's key for the histogram (sh.need_hist)
+        if (tid == 0) sh.need_hist = 1;
+        stop = KB_STOP_NO_FIT;
+        fail_task = t_begin + done_tasks;
+        stopped = 1;
+        break;
+      }
       // PredicateNodes found nothing (allocate.go:150-153): FitErrors histogram over all nodes at their
       // current keys (an infeasible key is its reason mask; padding keys are 0).
-      if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
-      __syncthreads();
-      uint32_t h[KB_NUM_REASONS];
-#pragma unroll
-      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
-      for (int c = 0; c < Q4; ++c) {
-        const uint4 v = k32v[tid * Q4 + c];
-        const uint32_t ks[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (ks[q] >> 31) continue;
-#pragma unroll
-          for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (ks[q] >> b) & 1u;
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < KB_NUM_REASONS; ++b) {
-        const uint32_t v = wave_sum_u32(h[b]);
-        if (lane == 0 && v) atomicAdd(&sh.hist[b], v);
-      }
-      __syncthreads();
+      sel_hist(sh, k32v, Q4);
       if (PROPOSE) {
         if (tid < KB_NUM_REASONS) rec->hist[tid] = sh.hist[tid];
         break;
@@ -2497,21 +2567,216 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
   }
 }
 
+// Split engine (grid 2): block 0, the placer, runs the jobs; block 1, the selector, runs each job's node
+// selection one job ahead. For job m the selector takes the sweep's keys, re-keys the rows job m-2 committed
+// (final by then) and drops the nodes job m-1 can commit to (its selected set S, published by the placer at
+// job m-1's node setup), then publishes the T best of the rest. The placer merges those with S of job m-1
+// re-keyed from that job's final rows: the T best of the union are the T best overall, since job m-1 touches
+// only S. Jobs of more than one segment, and the no-fit histogram, take the full path (every key in LDS).
+struct FedXchg {
+  uint32_t p_start[kJobSlots];  // placer -> selector: job number + 1 once the job's set is published
+  uint32_t p_done[kJobSlots];   //   job number + 1 once the job has committed (its commit list is final)
+  int32_t p_mode[kJobSlots];    //   0: the set p_node[0, p_n); 1: full path (patch its commit list); 2: skipped
+  int32_t p_n[kJobSlots];
+  uint32_t s_seq[kJobSlots];    // selector -> placer: job number + 1 once the job's candidates are published
+  int32_t s_n[kJobSlots];       //   candidates (-1: none, the full path)
+  int32_t p_node[kJobSlots][128];
+  int32_t s_node[kJobSlots][128];
+  uint32_t s_key[kJobSlots][128];
+  uint64_t sdiag[8];  // KB_DIAG builds: the selector's phase cycles (KB_FED_DIAG prints them at kb_fed_end)
+};
+
+// Thread 0: spin (sleeping) until *w reaches want, at most idle_ticks of s_memrealtime. ACQ: with an
+// agent-scope acquire (plain loads after it see other agents' released stores); otherwise relaxed (the
+// exchange's own words are written and read as agent-scope atomics, which bypass the non-coherent caches).
+template <bool ACQ = true>
+__device__ __forceinline__ bool fed_wait_word(const uint32_t* w, uint32_t want, uint64_t idle_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = ACQ ? __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                           : __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v - want <= 0x7fffffffu) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Re-key the rows on two commit lists (n0 entries of l0, then n1 of l1) for `spec` into k32 (node positions).
+// Ends after a barrier.
+__device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
+                          int spec, const uint64_t* stat, int idx_bits, const int32_t* l0, int n0, const int32_t* l1,
+                          int n1) {
+  const int np = n0 + n1;
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  for (int i = threadIdx.x; i < np; i += kSelThreads) {
+    const int w = i < n0 ? l0[i] : l1[i - n0];
+    const Row rr = load_row(N, w);
+    const uint64_t st = stat[w];
+    const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
+    k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+  }
+  __syncthreads();
+}
+
+// Thread 0: wait for ring entry r's command and keys (acquire), bounded by idle_ticks; s_op = its op.
+__device__ __forceinline__ void fed_wait_cmd(const uint32_t* ctr, uint32_t tgt, const FedCmd* ring, FedCmd& cm,
+                                             int32_t& s_op, uint64_t idle_ticks, int32_t* exit_flag) {
+  if (threadIdx.x == 0) {
+    int op = KB_ENG_EXIT_IDLE;
+    if (fed_wait_word(ctr, tgt, idle_ticks)) {
+      cm = *ring;
+      op = cm.op;
+    }
+    s_op = op;
+    if (op == KB_ENG_EXIT_IDLE) *exit_flag = 1;
+  }
+  __syncthreads();
+}
+
+// The split engine's selector: the second workgroup of the engine's launch (one dispatch, so both are resident
+// together; separate kernels on separate streams are not guaranteed separate hardware queues).
 template <int QN>
+__device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits,
+                                             const FedSlots& S, const FedCmd* ring, const uint32_t* ctr,
+                                             uint64_t idle_ticks, int32_t* exit_flag, FedXchg* X, uint32_t* k32,
+                                             SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_mode,
+                                             int32_t& s_n1) {
+  const int tid = threadIdx.x;
+  const int n = N.n;
+  const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
+  const int n_pad = 4 * kSelThreads * Q4;
+  const uint32_t blocks = (uint32_t)((n + 63) / 64);
+  uint32_t tgt[kJobSlots];
+#pragma unroll
+  for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
+  int slot1 = -1, slot2 = -1;  // slots of jobs m-1, m-2
+  int rp = 0;
+#ifdef KB_DIAG
+  // [0] wait for the command, [1] key load, [2] wait for the placer, [3] patch + exclusion, [4] selection,
+  // [5] publish, [6] jobs
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+#define KB_SSTAMP(k) KB_STAMP(k)
+#else
+#define KB_SSTAMP(k) \
+  do {               \
+  } while (0)
+#endif
+  uint32_t m = 0;
+  for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
+    tgt[r] += blocks;
+    fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
+    KB_SSTAMP(0);
+    if (s_op != KB_ENG_RUN) break;
+    const int slot = cm.slot, spec = cm.spec;
+    if (cm.t_count > kSegMax) {  // more than one segment: the placer takes the full path
+      if (tid == 0) {
+        __hip_atomic_store(&X->s_n[r], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&X->s_seq[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+      __syncthreads();
+      KB_SSTAMP(1);
+      const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
+      if (tid == 0) {
+        int mode = 2, n1 = 0;
+        bool ok = true;
+        if (m >= 1) {
+          ok = fed_wait_word<false>(&X->p_start[r1], m, idle_ticks);
+          if (ok) {
+            mode = __hip_atomic_load(&X->p_mode[r1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            n1 = __hip_atomic_load(&X->p_n[r1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (mode == 1) ok = fed_wait_word<false>(&X->p_done[r1], m, idle_ticks);
+          }
+          // the rows it re-keys were written back by the placer's publish of their job (a system-scope
+          // release before these words): drop any stale cached copies
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if (!ok) *exit_flag = 1;
+        s_mode = ok ? mode : -1;
+        s_n1 = n1;
+      }
+      __syncthreads();
+      KB_SSTAMP(2);
+      if (s_mode < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
+      const kb_spec sp = P.specs[spec];
+      const uint64_t* stat = S.stat[slot];
+      // rows job m-2 committed (final), and job m-1's when it took the full path (final after p_done)
+      const int n2 = slot2 >= 0 ? S.js[slot2]->n_commit : 0;
+      const int n1c = s_mode == 1 && slot1 >= 0 ? S.js[slot1]->n_commit : 0;
+      fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, n2,
+                slot1 >= 0 ? S.commits[slot1] : nullptr, n1c);
+      if (s_mode == 0) {  // the nodes job m-1 can commit to are the placer's to re-key
+        if (tid < s_n1) k32[__hip_atomic_load(&X->p_node[r1][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = 0u;
+        __syncthreads();
+      }
+      KB_SSTAMP(3);
+      uint32_t cnt;
+#ifdef KB_DIAG
+      uint64_t dgp[7] = {0, 0, 0, 0, 0, 0, 0};  // sel_pick's own fine stamps (KB_DIAG_SEL) kept apart
+      sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, nullptr, dgp, dg_last);
+#else
+      sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, nullptr);
+#endif
+      __syncthreads();
+      KB_SSTAMP(4);
+      if (tid < (int)cnt) {
+        __hip_atomic_store(&X->s_node[r][tid], sh.node[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&X->s_key[r][tid], sh.key0[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();  // every wave's stores drained
+      if (tid == 0) {
+        __hip_atomic_store(&X->s_n[r], (int32_t)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&X->s_seq[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      KB_SSTAMP(5);
+#ifdef KB_DIAG
+      dg[6]++;
+#endif
+    }
+    slot2 = slot1;
+    slot1 = slot;
+    __syncthreads();  // cm reused by the next command
+  }
+#ifdef KB_DIAG
+  if (tid == 0)
+    for (int k = 0; k < 7; ++k) X->sdiag[k] = dg[k];
+#endif
+#undef KB_SSTAMP
+}
+
+// SPLIT: grid 2, workgroup 0 the placer and 1 the selector (fed_selector); every job of the cycle one
+// segment (the host checks). Otherwise one workgroup with every node's key in LDS.
+template <int QN, bool SPLIT>
 __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
-                                                                 int32_t* exit_flag) {
+                                                                 int32_t* exit_flag, FedXchg* X) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
-  __shared__ int32_t s_op;
+  __shared__ int32_t s_op, s_cand;
+  __shared__ int32_t bprev[128];  // the previous job's selected set (split engine)
+  __shared__ uint32_t bkey[128];
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const int n_pad = 4 * kSelThreads * Q4;
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
+  if constexpr (SPLIT) {
+    if (blockIdx.x == 1) {
+      __shared__ int32_t s_mode, s_n1;
+      fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_mode, s_n1);
+      return;
+    }
+  }
+  constexpr bool split = SPLIT;  // n_pad >= 4096: the candidates and their nodes fit k32
+  uint32_t* kc = k32;                        // split: candidate keys by position (QN = 1 layout)
+  int32_t* cn = (int32_t*)(k32 + 4 * kSelThreads);  // and their nodes
   const uint32_t blocks = (uint32_t)((n + 63) / 64);
   uint32_t tgt[kJobSlots];
 #pragma unroll
@@ -2520,6 +2785,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   // the commit lists of the previous two jobs ([0] the last one): a job's sweep may have run before either
   // committed (the host issues a job once the job three back is read)
   int prev_slot[2] = {-1, -1}, prev_ncommit[2] = {0, 0};
+  int nbprev = 0;
   int rp = 0;
 #ifdef KB_DIAG
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -2528,24 +2794,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   uint64_t t_wait0 = dg_last, pub_prev = 0, rt_wait0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1) {
+  uint32_t m = 0;
+  for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     tgt[r] += blocks;
-    if (tid == 0) {  // wait for the ring entry's command and keys (acquire), bounded by idle_ticks
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int op = KB_ENG_EXIT_IDLE;
-      for (;;) {
-        if (__hip_atomic_load(&ctr[r], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - tgt[r] <= 0x7fffffffu) {
-          cm = ring[r];
-          op = cm.op;
-          break;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      s_op = op;
-      if (op == KB_ENG_EXIT_IDLE) *exit_flag = 1;
-    }
-    __syncthreads();
+    fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
     if (s_op != KB_ENG_RUN) break;
     const int slot = cm.slot, spec = cm.spec;
     JobState* js = S.js[slot];
@@ -2556,10 +2808,18 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         js->stopped = 1;
         js->n_commit = 0;
         __hip_atomic_store(&hjs->seq, cm.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (split) {  // after the release above: n_commit = 0 is visible with them
+          __hip_atomic_store(&X->p_n[r], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&X->p_mode[r], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(&X->p_start[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&X->p_done[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       last_panic = 1;
       prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
       prev_slot[0] = slot, prev_ncommit[0] = 0;
+      nbprev = 0;
       __syncthreads();
       continue;
     }
@@ -2572,40 +2832,140 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
-    // the previous two jobs' commits (final rows) re-keyed for this spec: their loads first
-    const int np0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0;
-    const int np = np0 + (prev_slot[1] >= 0 ? prev_ncommit[1] : 0);
-    const int32_t* patch0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
-    const int32_t* patch1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
-    const int pw = tid < np ? (tid < np0 ? patch0[tid] : patch1[tid - np0]) : -1;
-    Row prow;
-    if (pw >= 0) prow = load_row(N, pw);
-    const uint64_t pst = pw >= 0 ? stat[pw] : 0;
-    load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
-    if (tid == 0) sh.n_commit = 0;
-    __syncthreads();
-    if (np > 0) {
-      const int64_t* sci = P.sc_init + (size_t)spec * N.S;
-      if (pw >= 0) {
-        const uint32_t rs = row_reasons(N, P, C, sp, sci, prow, pst, pw);
-        k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
-      }
-      for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
-        const int w = i < np0 ? patch0[i] : patch1[i - np0];
-        const Row rr = load_row(N, w);
-        const uint64_t st = stat[w];
-        const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
-        k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
-      }
-      __syncthreads();
-    }
-    KB_SEL_PH(0);
+    const int64_t* sci = P.sc_init + (size_t)spec * N.S;
     int ready = cm.ready0, placed = 0;
     const int minav = cm.minav0, gang = cm.gang0;
     int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
-    sel_run<false, QN>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav, gang,
-                       placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
-                       S.commits[slot] SEL_DIAG_ARGS);
+    if (tid == 0) {
+      sh.n_commit = 0;
+      int c = -1;
+      if (split) {  // -1 from the selector: more than one segment, which the host never sends here
+        c = fed_wait_word<false>(&X->s_seq[r], m + 1, idle_ticks)
+                ? __hip_atomic_load(&X->s_n[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                : -2;
+        if (c < 0) *exit_flag = 1;
+      }
+      s_cand = c;
+    }
+    __syncthreads();
+    const int na = s_cand;
+    if (split && na < 0) break;  // the selector stopped answering: leave (the host sees the exit flag)
+    if (tid == 0) sh.need_hist = 0;
+    if constexpr (SPLIT) {
+      // candidates: the selector's T best outside the previous job's set, and that set re-keyed from its final
+      // rows; merged in node order (both lists are) so positions order ties as node indices do
+      int an = 0, bw = -1;
+      uint32_t ak = 0;
+      if (tid < na) {
+        an = __hip_atomic_load(&X->s_node[r][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ak = __hip_atomic_load(&X->s_key[r][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (tid >= 128 && tid - 128 < nbprev) {
+        bw = bprev[tid - 128];
+        const Row rr = load_row(N, bw);
+        const uint64_t st = stat[bw];
+        const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, bw);
+        bkey[tid - 128] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), bw), bw + N.base, idx_bits);
+      }
+      if (tid < na) sh.node[tid] = an;  // scratch until sel_pick: A's nodes for the B side's search
+      for (int i = tid; i < 4 * kSelThreads; i += kSelThreads)
+        if (i >= na + nbprev) kc[i] = 0u;
+      __syncthreads();
+      if (tid < na) {  // position = own index + B nodes below it
+        int lo = 0, hi = nbprev;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (bprev[mid] < an) lo = mid + 1;
+          else hi = mid;
+        }
+        kc[tid + lo] = ak;
+        cn[tid + lo] = an;
+      }
+      if (bw >= 0) {
+        int lo = 0, hi = na;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sh.node[mid] < bw) lo = mid + 1;
+          else hi = mid;
+        }
+        kc[tid - 128 + lo] = bkey[tid - 128];
+        cn[tid - 128 + lo] = bw;
+      }
+      __syncthreads();
+    } else {
+      // the previous two jobs' commits (final rows) re-keyed for this spec: their loads first
+      const int np0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0;
+      const int np = np0 + (prev_slot[1] >= 0 ? prev_ncommit[1] : 0);
+      const int32_t* patch0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
+      const int32_t* patch1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
+      const int pw = tid < np ? (tid < np0 ? patch0[tid] : patch1[tid - np0]) : -1;
+      Row prow;
+      if (pw >= 0) prow = load_row(N, pw);
+      const uint64_t pst = pw >= 0 ? stat[pw] : 0;
+      load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+      __syncthreads();
+      if (np > 0) {
+        if (pw >= 0) {
+          const uint32_t rs = row_reasons(N, P, C, sp, sci, prow, pst, pw);
+          k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
+        }
+        for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
+          const int w = i < np0 ? patch0[i] : patch1[i - np0];
+          const Row rr = load_row(N, w);
+          const uint64_t st = stat[w];
+          const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
+          k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+        }
+        __syncthreads();
+      }
+    }
+    KB_SEL_PH(0);
+    FedPub pub;
+    if constexpr (SPLIT) {
+      pub.node = X->p_node[r];
+      pub.n = &X->p_n[r];
+      pub.mode = &X->p_mode[r];
+      pub.start = &X->p_start[r];
+      pub.val = m + 1;
+    }
+    sel_run<false, QN, SPLIT>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
+                              gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
+                              S.commits[slot] SEL_DIAG_ARGS, SPLIT ? cn : nullptr, pub);
+    if constexpr (SPLIT) {
+      // the set published for the selector becomes the next job's B
+      __syncthreads();
+      const int ns = sh.n_sel;
+      if (tid < ns) bprev[tid] = sh.node[tid];
+      nbprev = ns;
+      if (sh.need_hist) {  // no fit: every node's key at this point (the sweep's, then every row changed since)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
+        __syncthreads();
+        load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+        __syncthreads();
+        const int n0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0, n1 = prev_slot[1] >= 0 ? prev_ncommit[1] : 0;
+        {  // the previous two jobs' commits and this job's own (one loop: two fed_patch calls here trip the
+           // ROCm 7.2 inliner)
+          const int32_t* l0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
+          const int32_t* l1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
+          const int n2 = sh.n_commit;
+          for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
+            const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : S.commits[slot][i - n0 - n1]);
+            const Row rr = load_row(N, w);
+            const uint64_t st = stat[w];
+            const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
+            k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+          }
+          __syncthreads();
+        }
+        sel_hist(sh, (const uint4*)k32, Q4);
+        if (tid < KB_NUM_REASONS) {
+          js->hist[tid] = sh.hist[tid];
+          hjs->hist[tid] = sh.hist[tid];
+        }
+      }
+    } else {
+      nbprev = 0;
+    }
 #ifdef KB_DIAG
     // fed engine layout: [0] key load + patch, [1..4] as sel_run, [5] commit + the previous job's publish +
     // the no-fit histogram, [6] waiting for this job's command; [7] realtime ticks including the wait
@@ -2624,6 +2984,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     if (tid == 0) {
       js->n_commit = ncommit;
       publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
+      // after that release (which wrote the job's rows and n_commit back): the selector may re-key them
+      if (split) __hip_atomic_store(&X->p_done[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
     prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
@@ -2644,7 +3006,7 @@ int fed_lds_bytes(int n) {
 
 bool fed_fits(int n) {
   const int b = fed_lds_bytes(n);
-  return b >= 0 && b <= kSelDynLimit - 256;
+  return b >= 0 && b <= kFedDynLimit;
 }
 
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
@@ -2657,10 +3019,13 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 }
 
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
+size_t fed_xchg_bytes() { return sizeof(FedXchg); }
+// the placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096
+bool fed_split_ok(int n) { return fed_fits(n) && n > 4 * kSelThreads; }
 
 void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                        const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                       int32_t* exit_flag, void* stream) {
+                       int32_t* exit_flag, void* xchg, void* stream) {
   FedSlots S;
   for (int s = 0; s < kJobSlots; ++s) {
     S.tgt[s] = tgt[s];
@@ -2673,10 +3038,15 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
   }
   const int qn = sel_qn(N.n);
   const int bytes = fed_lds_bytes(N.n);
+  // (no split instance for one key group: fed_split_ok needs n > 4 * kSelThreads)
 #define KB_FED_QN(Q)                                                                                              \
   case Q:                                                                                                        \
-    hipLaunchKernelGGL(fed_engine_kernel<Q>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C,     \
-                       idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag);                            \
+    if (xchg && Q != 1)                                                                                          \
+      hipLaunchKernelGGL((fed_engine_kernel<Q, Q != 1>), dim3(2), dim3(kSelThreads), bytes, (hipStream_t)stream, \
+                         N, P, C, idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag, (FedXchg*)xchg);   \
+    else                                                                                                         \
+      hipLaunchKernelGGL((fed_engine_kernel<Q, false>), dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream,   \
+                         N, P, C, idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag, (FedXchg*)xchg);   \
     break;
   switch (qn) {
     KB_FED_QN(1)
@@ -3514,14 +3884,14 @@ int configure_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit);
     if (e != hipSuccess) return (int)e;
   }
-  // the fed engine's static block also holds its command (FedCmd + op): a smaller dynamic budget
-  for (const void* f :
-       {(const void*)fed_engine_kernel<0>, (const void*)fed_engine_kernel<1>, (const void*)fed_engine_kernel<2>,
-        (const void*)fed_engine_kernel<3>, (const void*)fed_engine_kernel<4>, (const void*)fed_engine_kernel<5>,
-        (const void*)fed_engine_kernel<6>, (const void*)fed_engine_kernel<8>, (const void*)fed_engine_kernel<10>}) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSelDynLimit - 256);
+  // the fed engine's static block also holds its command and the split engine's merge lists: a smaller budget
+#define KB_FED_F(Q) (const void*)fed_engine_kernel<Q, false>, (const void*)fed_engine_kernel<Q, true>
+  for (const void* f : {KB_FED_F(0), (const void*)fed_engine_kernel<1, false>, KB_FED_F(2), KB_FED_F(3), KB_FED_F(4), KB_FED_F(5), KB_FED_F(6),
+                        KB_FED_F(8), KB_FED_F(10)}) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFedDynLimit);
     if (e != hipSuccess) return (int)e;
   }
+#undef KB_FED_F
   return 0;
 }
 

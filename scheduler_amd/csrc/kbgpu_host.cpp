@@ -144,6 +144,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
   c->use_aff_reg = getenv("KB_NO_AFF_REG") == nullptr;  // testing: force the global-memory affinity loop
   c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
+  c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
@@ -197,6 +198,7 @@ void kb_destroy(kb_ctx* c) {
   if (c->fed_ring) (void)hipFree(c->fed_ring);
   if (c->fed_ctr) (void)hipFree(c->fed_ctr);
   if (c->fed_exit) (void)hipFree(c->fed_exit);
+  if (c->fed_xchg) (void)hipFree(c->fed_xchg);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -1133,7 +1135,7 @@ static uint64_t fed_idle_ticks() {
   return ms > 0 ? (uint64_t)ms * 100000ull : 100000000ull;
 }
 
-int kb_fed_begin(kb_ctx* c) {
+int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return KB_E_INVALID;
   if (c->fed) return fail(c, KB_E_STATE, "fed engine already running");
   if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
@@ -1164,8 +1166,16 @@ int kb_fed_begin(kb_ctx* c) {
     c->ev_begin(&c->fed_ev);
     c->timing_now = tn;
   }
+  void* xchg = nullptr;
+  if (c->use_fed_split && fed_split_ok(c->N.n) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
+    if (!c->fed_xchg) HIP_OK(c, hipMalloc(&c->fed_xchg, fed_xchg_bytes()));
+    HIP_OK(c, hipMemsetAsync(c->fed_xchg, 0, fed_xchg_bytes(), c->stream));  // job numbers restart per cycle
+    xchg = c->fed_xchg;
+    c->stats.fed_split++;
+  }
+  c->stats.fed_cycles++;
   launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count, fed_idle_ticks(),
-                    c->fed_exit, c->stream);
+                    c->fed_exit, xchg, c->stream);
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1195,6 +1205,14 @@ int kb_fed_end(kb_ctx* c) {
   const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit
   if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
   if (c->timing) c->ev_collect(true);
+  if (getenv("KB_FED_DIAG") && c->fed_xchg && c->stats.fed_split) {  // KB_DIAG builds: the selector's phases
+    uint64_t d[8] = {};
+    if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - sizeof(d), sizeof(d), hipMemcpyDeviceToHost) ==
+        hipSuccess && d[6])
+      fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_placer=%.0f "
+              "patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
+              (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6], (double)d[5] / d[6]);
+  }
   // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;
   if (rc == KB_OK && c->any_busy() &&

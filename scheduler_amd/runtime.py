@@ -109,7 +109,7 @@ class kb_cycle_result(C.Structure):
 class kb_stats(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 14), ("kernel_ms", C.c_double * 14), ("pairs", C.c_uint64 * 14),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8),
-                ("fed_abandon", C.c_uint64)]
+                ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -319,7 +319,7 @@ class Context:
         self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
         return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
                 "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag),
-                "fed_abandon": st.fed_abandon}
+                "fed_abandon": st.fed_abandon, "fed_cycles": st.fed_cycles, "fed_split": st.fed_split}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

@@ -274,6 +274,57 @@ def test_fed_engine_survives_a_host_stall(monkeypatch):
     _compare(ref, runtime.result_dict(snap, out))
 
 
+SPLIT_CLUSTERS = [
+    ("C2-3000", synth.c2(n_nodes=3000, n_jobs=60, tasks_per_job=40, seed=41)),
+    # jobs stop READY and come back (the speculated next job is often the same job)
+    ("C2-halfgang-2500", _partial_gang(synth.c2(n_nodes=2500, n_jobs=50, tasks_per_job=30, seed=42), 0.5)),
+    # capacity for ~75% of the work: no-fit jobs (the histogram over every node's rebuilt key)
+    ("C2-nofit-2100", synth.c2(n_nodes=2100, n_jobs=70, tasks_per_job=60, seed=43, fill=1.3)),
+    # node classes, taints, GPUs, node affinity; jobs of up to 100 tasks (one segment)
+    ("C3-2500", synth.c3(n_nodes=2500, n_jobs=40, tasks_per_job=100, seed=44)),
+]
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["split", "one-workgroup"])
+@pytest.mark.parametrize("name,cluster", SPLIT_CLUSTERS, ids=[c[0] for c in SPLIT_CLUSTERS])
+def test_fed_split_engine_parity(name, cluster, split, monkeypatch):
+    """The split fed engine (n > 2048, every job one segment): a second workgroup selects each job's
+    candidate nodes one job ahead, leaving out the nodes the job before may commit to, which the placer
+    re-keys and merges in. Same placements, statuses and FitErrors as the oracle, and as the one-workgroup
+    engine (KB_NO_FED_SPLIT)."""
+    if not split:
+        monkeypatch.setenv("KB_NO_FED_SPLIT", "1")
+    ref = pyoracle.allocate(cluster)
+    snap = E.Snapshot(cluster)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    assert st["fed_cycles"] == 1 and st["fed_split"] == (1 if split else 0)
+    got = runtime.result_dict(snap, out)
+    _compare(ref, got)
+    assert len(got["events"]) > 0
+
+
+def test_fed_split_engine_steps_aside_for_long_jobs():
+    """A job of more than one segment (150 tasks) keeps the cycle on the one-workgroup engine."""
+    cl = synth.c2(n_nodes=2200, n_jobs=8, tasks_per_job=150, seed=45)
+    ref = pyoracle.allocate(cl)
+    snap = E.Snapshot(cl)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    assert st["fed_cycles"] == 1 and st["fed_split"] == 0
+    _compare(ref, runtime.result_dict(snap, out))
+
+
 def _ratio_cluster(seed=77, n_nodes=3000, n_specs=48):
     """Random capacities and loads, so LeastRequested / BalancedResource see many distinct quotients (and
     some exactly on an integer boundary, like 2000/4000 vs 3000/10000)."""
