@@ -1457,11 +1457,11 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 
 // Node selection, phase 1 of sel_run: the T best keys of k32 (LDS, 4 * kSelThreads * Q4 positions, zero padding)
 // by score field, ties to the lower position. sh.node / sh.key0 [0, S) get node_of(position) and the key, in
-// position order (cnode: the node at each position; nullptr: the position itself). Returns the feasible count
-// (0: nothing fits, S = 0). No barrier after the LDS writes.
+// position order (the position is the node). Returns the feasible count (0: nothing fits, S = 0). No barrier
+// after the LDS writes.
 template <int QN>
 __device__ __forceinline__ uint32_t sel_pick(SelShared& sh, const uint32_t* k32, int n, int idx_bits, uint32_t T,
-                                             int& rp, uint32_t& S_out, const int32_t* cnode SEL_DIAG_PARAMS) {
+                                             int& rp, uint32_t& S_out SEL_DIAG_PARAMS) {
   const int tid = threadIdx.x;
   constexpr int QU = QN > 0 ? QN : kSelQ4;  // unroll bound of the key passes
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -1544,12 +1544,13 @@ __device__ __forceinline__ uint32_t sel_pick(SelShared& sh, const uint32_t* k32,
       bool take = h > sstar;
       if (h == sstar) take = le++ < selE;
       if (take) {
-        sh.node[slot] = cnode != nullptr ? cnode[ki] : ki;
+        sh.node[slot] = ki;
         sh.key0[slot] = k;
         ++slot;
       }
     })
   }
+  if (tid >= (int)S_out && tid < 128) sh.key0[tid] = 0u;  // the rank loops read all 128 entries
 #undef SEL_EACH_KEY
   return F;
 }
@@ -1590,24 +1591,33 @@ __device__ void sel_hist(SelShared& sh, const uint4* k32v, int Q4) {
 }
 
 // The fed placer's publication to the selector (fed_engine_kernel): the nodes a job can commit to.
+// Tagged words: (tag << 32 | payload), written and read as write-through agent-scope atomics. A reader
+// takes a word once its tag is the one it waits for, so a publication needs no store ordering (no waits on
+// the writer's side) and a stale word from an earlier job reads as not there yet.
+__device__ __forceinline__ void tag_store(uint64_t* w, uint32_t tag, uint32_t v) {
+  __hip_atomic_store(w, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t x_load64(const uint64_t* w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void x_store64(uint64_t* w, uint64_t v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The fed placer's publication to the selector: the nodes a job can commit to (its selected set, in slot order).
+constexpr uint32_t kPubModeSet = 0, kPubModeSkipped = 2;
 struct FedPub {
-  int32_t* node = nullptr;  // [kSegMax + 28]
-  int32_t* n = nullptr;
-  int32_t* mode = nullptr;
-  uint32_t* start = nullptr;  // nullptr: nothing to publish
-  uint32_t val = 0;
-  // after a barrier that drained every wave's payload stores (write-through atomics, no L2 writeback needed)
-  __device__ void publish(int cnt) const {
-    __hip_atomic_store(n, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(mode, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(start, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  uint64_t* head = nullptr;  // tag << 32 | mode << 16 | count; nullptr: nothing to publish
+  uint64_t* node = nullptr;  // [128] tag << 32 | node
+  uint32_t tag = 0;
+  __device__ void set_node(int i, int w) const { tag_store(&node[i], tag, (uint32_t)w); }
+  __device__ void set_head(uint32_t mode, int cnt) const { tag_store(head, tag, (mode << 16) | (uint32_t)cnt); }
 };
 
-// cnode != nullptr (the fed engine's placer, one segment): k32 holds candidate keys by position (QN = 1 layout)
-// and cnode[position] their nodes; the selected set is published to the selector through `pub` once known, and a
-// no-fit sets sh.need_hist instead of the histogram (the caller rebuilds every node's key first).
+// CAND (the split fed engine's placer, one segment): the caller has chosen the run's nodes (sh.n_sel of them in
+// sh.node / key0 / row / stat, slots in node order, with sh.lmax = T - key rank and sh.theta0); they are
+// published to the selector through `pub`, and a no-fit sets sh.need_hist instead of the histogram (the caller
+// rebuilds every node's key first).
 template <bool PROPOSE = false, int QN = 0, bool CAND = false>
 __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* cand, const DevNodes& N,
                                         const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
@@ -1616,7 +1626,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
                                         ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS,
-                                        const int32_t* cnode = nullptr, FedPub pub = FedPub{}) {
+                                        FedPub pub = FedPub{}) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -1630,16 +1640,19 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
-    // ---- 1. S = the T best nodes by current key ----
+    // ---- 1. S = the T best nodes by current key (CAND: chosen by the caller, slots in key order with their
+    //         rows and static cache) ----
     uint32_t S;
     bool no_fit;
-    if constexpr (CAND)
-      no_fit = sel_pick<1>(sh, k32, 4 * kSelThreads, idx_bits, T, rp, S, cnode SEL_DIAG_ARGS) == 0;
-    else
-      no_fit = sel_pick<QN>(sh, k32, n, idx_bits, T, rp, S, nullptr SEL_DIAG_ARGS) == 0;
-    if (CAND && no_fit && tid == 0) {  // nothing this job can commit to
-      sh.n_sel = 0;
-      if (pub.start != nullptr) pub.publish(0);
+    if constexpr (CAND) {
+      S = (uint32_t)sh.n_sel;
+      no_fit = S == 0;
+      if (pub.head != nullptr) {  // the nodes this job can commit to, for the selector's next job
+        if (tid < (int)S) pub.set_node(tid, sh.node[tid]);
+        if (tid == 0) pub.set_head(kPubModeSet, (int)S);
+      }
+    } else {
+      no_fit = sel_pick<QN>(sh, k32, n, idx_bits, T, rp, S SEL_DIAG_ARGS) == 0;
     }
     if (!no_fit) {
       // zero the candidate lists (an unused entry reads as 0: never counted)
@@ -1653,9 +1666,14 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       // ---- 2. selected nodes: rows, A; rank by key (8 threads per node) ----
       if (tid < (int)S) {
         const int w = sh.node[tid];
-        const Row r = load_row(N, w);
-        sh.row[tid] = r;
-        sh.stat[tid] = stat[w];
+        Row r;
+        if constexpr (CAND) {
+          r = sh.row[tid];
+        } else {
+          r = load_row(N, w);
+          sh.row[tid] = r;
+          sh.stat[tid] = stat[w];
+        }
         sh.A[tid] = allocs_before_full(N, sp, sci, scr, r, w);
         sh.recip[0][tid] = 1.0 / (double)r.alloc_cpu;
         sh.recip[1][tid] = 1.0 / (double)r.alloc_mem;
@@ -1665,7 +1683,9 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         sh.fin[tid] = 0;
         sh.done[tid] = 0;
       }
-      {
+      if constexpr (CAND) {
+        // lmax and theta0 set by the caller (it ranked the candidates by key)
+      } else {
         constexpr int kPer = 32;  // keys compared per thread: 4 threads per node, 128 nodes
         static_assert(kSelThreads == 4 * 128, "rank layout");
         const int s = tid >> 2, part = tid & 3;
@@ -1674,7 +1694,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
           const int o = part * kPer + q;
-          rk += o < (int)S && sh.key0[o] > k;
+          rk += sh.key0[o] > k;  // entries past S are 0 (sel_pick): no bound test, no branch
         }
         rk += dpp_src<0xb1>(0u, rk);  // quad_perm [1,0,3,2]
         rk += dpp_src<0x4e>(0u, rk);  // quad_perm [2,3,0,1]
@@ -1683,14 +1703,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           if (rk == S - 1) sh.theta0 = k;
         }
       }
-      if (CAND && pub.start != nullptr && tid < (int)S)
-        __hip_atomic_store(&pub.node[tid], sh.node[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      // the nodes this job can commit to, for the selector's next job (the barrier drained every wave's stores)
-      if (CAND && tid == 0) {
-        sh.n_sel = (int)S;
-        if (pub.start != nullptr) pub.publish((int)S);
-      }
       if (wv == 0) {
         const uint32_t a = lane < (int)S ? (uint32_t)sh.lmax[lane] : 0u;
         const uint32_t b = lane + 64 < (int)S ? (uint32_t)sh.lmax[lane + 64] : 0u;
@@ -1787,7 +1800,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         if (tid < (int)K) {  // composites are distinct: rank = number of larger ones
           const uint64_t v = sh.dense[tid];
           uint32_t r = 0;
-          for (uint32_t q = 0; q < K; ++q) r += sh.dense[q] > v;
+#pragma unroll
+          for (uint32_t q = 0; q < (uint32_t)KB_SEL_DENSE_MAX; ++q) r += (q < K) & (sh.dense[q] > v);
           if (r < T) sh.ord[r] = v;
         }
         if (tid == 0) sh.s_count = (int)(K < T ? K : T);
@@ -2535,6 +2549,7 @@ struct FedCmd {
   uint32_t seq;
   int32_t pad[3];
 };
+static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
 
 struct FedSlots {
   uint32_t* keys[kJobSlots];
@@ -2567,23 +2582,24 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
   }
 }
 
-// Split engine (grid 2): block 0, the placer, runs the jobs; block 1, the selector, runs each job's node
-// selection one job ahead. For job m the selector takes the sweep's keys, re-keys the rows job m-2 committed
-// (final by then) and drops the nodes job m-1 can commit to (its selected set S, published by the placer at
-// job m-1's node setup), then publishes the T best of the rest. The placer merges those with S of job m-1
-// re-keyed from that job's final rows: the T best of the union are the T best overall, since job m-1 touches
-// only S. Jobs of more than one segment, and the no-fit histogram, take the full path (every key in LDS).
+// Split engine (grid 2): workgroup 0, the placer, runs the jobs; workgroup 1, the selector, runs each job's
+// node selection one job ahead. For job m the selector takes the sweep's keys, re-keys the rows job m-2
+// committed (final by then) and drops the nodes job m-1 can commit to (its selected set S, published by the
+// placer at job m-1's node setup), then publishes the T best of the rest in key order, each with its row and
+// static cache, and the job's command. The placer re-keys S of job m-1 from the final rows it kept and merges:
+// the T best of the union are the T best overall, since job m-1 touches only S. A no-fit rebuilds every key
+// for the histogram. Cycles with a job of more than one segment do not use the split engine.
+constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
 struct FedXchg {
-  uint32_t p_start[kJobSlots];  // placer -> selector: job number + 1 once the job's set is published
-  uint32_t p_done[kJobSlots];   //   job number + 1 once the job has committed (its commit list is final)
-  int32_t p_mode[kJobSlots];    //   0: the set p_node[0, p_n); 1: full path (patch its commit list); 2: skipped
-  int32_t p_n[kJobSlots];
-  uint32_t s_seq[kJobSlots];    // selector -> placer: job number + 1 once the job's candidates are published
-  int32_t s_n[kJobSlots];       //   candidates (-1: none, the full path)
-  int32_t p_node[kJobSlots][128];
-  int32_t s_node[kJobSlots][128];
-  uint32_t s_key[kJobSlots][128];
-  uint64_t sdiag[8];  // KB_DIAG builds: the selector's phase cycles (KB_FED_DIAG prints them at kb_fed_end)
+  uint64_t p_head[kJobSlots];        // placer -> selector (tagged, job number + 1): mode << 16 | count
+  uint64_t p_done[kJobSlots];        //   (tagged) the job's commit count, once its rows are written back
+  uint64_t p_node[kJobSlots][128];   //   the job's selected set (tagged)
+  uint64_t s_head[kJobSlots];        // selector -> placer: (job number + 1) << 32 | candidates (kSelExit: EXIT),
+                                     //   stored once the entries below are drained
+  uint64_t s_cmd[kJobSlots][8];      //   the job's command (FedCmd)
+  uint64_t s_ent[kJobSlots][128][2 + sizeof(Row) / 8];  //   candidates in key order (descending): key | node << 32,
+                                                        //   static cache, row
+  uint64_t sdiag[16];  // KB_DIAG builds: the selector's phase cycles, [8..] the placer's merge (KB_FED_DIAG)
 };
 
 // Thread 0: spin (sleeping) until *w reaches want, at most idle_ticks of s_memrealtime. ACQ: with an
@@ -2639,8 +2655,7 @@ template <int QN>
 __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits,
                                              const FedSlots& S, const FedCmd* ring, const uint32_t* ctr,
                                              uint64_t idle_ticks, int32_t* exit_flag, FedXchg* X, uint32_t* k32,
-                                             SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_mode,
-                                             int32_t& s_n1) {
+                                             SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_n1) {
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2649,11 +2664,11 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
   uint32_t tgt[kJobSlots];
 #pragma unroll
   for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
-  int slot1 = -1, slot2 = -1;  // slots of jobs m-1, m-2
+  int slot2 = -1, slot1 = -1;  // slots of jobs m-2, m-1
   int rp = 0;
 #ifdef KB_DIAG
-  // [0] wait for the command, [1] key load, [2] wait for the placer, [3] patch + exclusion, [4] selection,
-  // [5] publish, [6] jobs
+  // [0] wait for the command, [1] key load, [3] wait for job m-2 + patch, [2] wait for job m-1's set +
+  // exclusion, [4] selection, [5] publish, [6] jobs
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
 #define KB_SSTAMP(k) KB_STAMP(k)
@@ -2667,76 +2682,120 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     tgt[r] += blocks;
     fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
     KB_SSTAMP(0);
-    if (s_op != KB_ENG_RUN) break;
-    const int slot = cm.slot, spec = cm.spec;
-    if (cm.t_count > kSegMax) {  // more than one segment: the placer takes the full path
-      if (tid == 0) {
-        __hip_atomic_store(&X->s_n[r], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&X->s_seq[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
-      __syncthreads();
-      KB_SSTAMP(1);
-      const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
-      if (tid == 0) {
-        int mode = 2, n1 = 0;
-        bool ok = true;
-        if (m >= 1) {
-          ok = fed_wait_word<false>(&X->p_start[r1], m, idle_ticks);
-          if (ok) {
-            mode = __hip_atomic_load(&X->p_mode[r1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            n1 = __hip_atomic_load(&X->p_n[r1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (mode == 1) ok = fed_wait_word<false>(&X->p_done[r1], m, idle_ticks);
-          }
-          // the rows it re-keys were written back by the placer's publish of their job (a system-scope
-          // release before these words): drop any stale cached copies
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        if (!ok) *exit_flag = 1;
-        s_mode = ok ? mode : -1;
-        s_n1 = n1;
-      }
-      __syncthreads();
-      KB_SSTAMP(2);
-      if (s_mode < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
-      const kb_spec sp = P.specs[spec];
-      const uint64_t* stat = S.stat[slot];
-      // rows job m-2 committed (final), and job m-1's when it took the full path (final after p_done)
-      const int n2 = slot2 >= 0 ? S.js[slot2]->n_commit : 0;
-      const int n1c = s_mode == 1 && slot1 >= 0 ? S.js[slot1]->n_commit : 0;
-      fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, n2,
-                slot1 >= 0 ? S.commits[slot1] : nullptr, n1c);
-      if (s_mode == 0) {  // the nodes job m-1 can commit to are the placer's to re-key
-        if (tid < s_n1) k32[__hip_atomic_load(&X->p_node[r1][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = 0u;
-        __syncthreads();
-      }
-      KB_SSTAMP(3);
-      uint32_t cnt;
-#ifdef KB_DIAG
-      uint64_t dgp[7] = {0, 0, 0, 0, 0, 0, 0};  // sel_pick's own fine stamps (KB_DIAG_SEL) kept apart
-      sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, nullptr, dgp, dg_last);
-#else
-      sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, nullptr);
-#endif
-      __syncthreads();
-      KB_SSTAMP(4);
-      if (tid < (int)cnt) {
-        __hip_atomic_store(&X->s_node[r][tid], sh.node[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&X->s_key[r][tid], sh.key0[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();  // every wave's stores drained
-      if (tid == 0) {
-        __hip_atomic_store(&X->s_n[r], (int32_t)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&X->s_seq[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      KB_SSTAMP(5);
-#ifdef KB_DIAG
-      dg[6]++;
-#endif
+    if (s_op != KB_ENG_RUN) {
+      if (s_op == KB_ENG_EXIT && tid == 0)  // the placer takes EXIT from here
+        x_store64(&X->s_head[r], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
+      break;
     }
+    const int slot = cm.slot, spec = cm.spec;
+    load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+    __syncthreads();
+    KB_SSTAMP(1);
+    const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
+    const int r2 = r1 == 0 ? kJobSlots - 1 : r1 - 1;
+    const kb_spec sp = P.specs[spec];
+    const uint64_t* stat = S.stat[slot];
+    if (tid == 0) {  // job m-2 done: its commit count, after its rows were written back
+      int n2 = 0;
+      if (m >= 2) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const uint64_t h = x_load64(&X->p_done[r2]);
+          if ((uint32_t)(h >> 32) == m - 1) {
+            n2 = (int)(uint32_t)h;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            n2 = -1;
+            *exit_flag = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // its rows: no stale cached copies
+      }
+      s_n1 = n2;
+    }
+    __syncthreads();
+    if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
+    // rows job m-2 committed (final), while job m-1 may still be choosing its set
+    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1, nullptr, 0);
+    KB_SSTAMP(3);
+    if (tid == 0) {  // job m-1's set (published at its node setup)
+      int n1 = 0;
+      if (m >= 1) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const uint64_t h = x_load64(&X->p_head[r1]);
+          if ((uint32_t)(h >> 32) == m) {
+            n1 = (h >> 16 & 0xffffu) == kPubModeSet ? (int)(h & 0xffffu) : 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            n1 = -1;
+            *exit_flag = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      s_n1 = n1;
+    }
+    __syncthreads();
+    KB_SSTAMP(2);
+    if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
+    if (tid < s_n1) {  // job m-1's set is the placer's to re-key (every entry's tag checked: no store order)
+      uint64_t e;
+      do e = x_load64(&X->p_node[r1][tid]);
+      while ((uint32_t)(e >> 32) != m);
+      k32[(uint32_t)e] = 0u;
+    }
+    __syncthreads();
+    KB_SSTAMP(2);
+    uint32_t cnt;
+#ifdef KB_DIAG
+    uint64_t dgp[7] = {0, 0, 0, 0, 0, 0, 0};  // sel_pick's own fine stamps (KB_DIAG_SEL) kept apart
+    sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, dgp, dg_last);
+#else
+    sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt);
+#endif
+    __syncthreads();
+    KB_SSTAMP(4);
+    {  // rank by key (4 threads per candidate), then each candidate's entry at its rank
+      const int e = tid >> 2, part = tid & 3;
+      const uint32_t k = e < (int)cnt ? sh.key0[e] : 0u;
+      uint32_t rk = 0;
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const int o = part * 32 + q;
+        rk += sh.key0[o] > k;  // entries past cnt are 0 (sel_pick)
+      }
+      rk += dpp_src<0xb1>(0u, rk);  // quad_perm [1,0,3,2]
+      rk += dpp_src<0x4e>(0u, rk);  // quad_perm [2,3,0,1]
+      if (part == 0 && e < (int)cnt) sh.lmax[e] = (int)rk;
+    }
+    __syncthreads();
+    if (tid < (int)cnt) {
+      const int w = sh.node[tid];
+      const Row rw = load_row(N, w);  // final: job m-1 touches only its set
+      uint64_t* ent = X->s_ent[r][sh.lmax[tid]];
+      x_store64(&ent[0], (uint64_t)sh.key0[tid] | ((uint64_t)(uint32_t)w << 32));
+      x_store64(&ent[1], stat[w]);
+      uint64_t words[sizeof(Row) / 8];
+      __builtin_memcpy(words, &rw, sizeof(Row));
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q], words[q]);
+    } else if (tid >= 256 && tid < 256 + 8) {  // the command, for the placer
+      uint64_t words[8];
+      __builtin_memcpy(words, &cm, sizeof(FedCmd));
+      x_store64(&X->s_cmd[r][tid - 256], words[tid - 256]);
+    }
+    __syncthreads();  // every wave's stores drained
+    if (tid == 0) x_store64(&X->s_head[r], ((uint64_t)(m + 1) << 32) | cnt);
+    KB_SSTAMP(5);
+#ifdef KB_DIAG
+    dg[6]++;
+#endif
     slot2 = slot1;
     slot1 = slot;
     __syncthreads();  // cm reused by the next command
@@ -2746,6 +2805,22 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     for (int k = 0; k < 7; ++k) X->sdiag[k] = dg[k];
 #endif
 #undef KB_SSTAMP
+}
+
+// The row after c commits of the spec from r0 (min(c, A) Allocates, the rest Pipelines): store_back_row's
+// columns as a Row.
+__device__ __forceinline__ Row row_after(const kb_spec& sp, const Row& r0, int c, int A) {
+  const int64_t a = c < A ? c : A;
+  const int64_t p = c - a;
+  Row r = r0;
+  r.idle_cpu -= a * sp.req_cpu;
+  r.idle_mem -= a * sp.req_mem;
+  r.rel_cpu -= p * sp.req_cpu;
+  r.rel_mem -= p * sp.req_mem;
+  r.pod_count += c;
+  r.nz_cpu += (int64_t)c * sp.nz_cpu;
+  r.nz_mem += (int64_t)c * sp.nz_mem;
+  return r;
 }
 
 // SPLIT: grid 2, workgroup 0 the placer and 1 the selector (fed_selector); every job of the cycle one
@@ -2759,8 +2834,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
   __shared__ int32_t s_op, s_cand;
-  __shared__ int32_t bprev[128];  // the previous job's selected set (split engine)
-  __shared__ uint32_t bkey[128];
+  __shared__ int32_t bprev[128];  // split: the previous job's selected set, slot order
+  __shared__ uint32_t bkey[128];  //   its keys for this job
+  __shared__ int32_t s_feas;
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2769,14 +2845,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   if constexpr (SPLIT) {
     if (blockIdx.x == 1) {
-      __shared__ int32_t s_mode, s_n1;
-      fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_mode, s_n1);
+      fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand);
       return;
     }
   }
-  constexpr bool split = SPLIT;  // n_pad >= 4096: the candidates and their nodes fit k32
-  uint32_t* kc = k32;                        // split: candidate keys by position (QN = 1 layout)
-  int32_t* cn = (int32_t*)(k32 + 4 * kSelThreads);  // and their nodes
+  // split: the previous job's set's final rows, kept from its commit to this job's merge (the candidate
+  // lists' space is free between the two)
+  Row* brow = (Row*)cand;
   const uint32_t blocks = (uint32_t)((n + 63) / 64);
   uint32_t tgt[kJobSlots];
 #pragma unroll
@@ -2788,6 +2863,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   int nbprev = 0;
   int rp = 0;
 #ifdef KB_DIAG
+  uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
   // publish (fence + host writes)
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -2796,8 +2872,38 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
   uint32_t m = 0;
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
-    tgt[r] += blocks;
-    fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
+    if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
+      if (tid == 0) {
+        int c = -2;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t h;
+        for (;;) {
+          h = x_load64(&X->s_head[r]);
+          if ((uint32_t)(h >> 32) == m + 1) break;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if ((uint32_t)(h >> 32) == m + 1) {
+          c = (int32_t)(uint32_t)h;
+          if (c >= 0) {
+            uint64_t words[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) words[q] = x_load64(&X->s_cmd[r][q]);
+            __builtin_memcpy(&cm, words, sizeof(FedCmd));
+          }
+          // the sweep's static cache (another agent's release, which the selector has seen): fresh loads
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        } else {
+          *exit_flag = 1;
+        }
+        s_cand = c;
+        s_op = c >= 0 ? KB_ENG_RUN : (c == kSelExit ? KB_ENG_EXIT : KB_ENG_EXIT_IDLE);
+      }
+      __syncthreads();
+    } else {
+      tgt[r] += blocks;
+      fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
+    }
     if (s_op != KB_ENG_RUN) break;
     const int slot = cm.slot, spec = cm.spec;
     JobState* js = S.js[slot];
@@ -2808,12 +2914,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         js->stopped = 1;
         js->n_commit = 0;
         __hip_atomic_store(&hjs->seq, cm.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (split) {  // after the release above: n_commit = 0 is visible with them
-          __hip_atomic_store(&X->p_n[r], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&X->p_mode[r], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(&X->p_start[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&X->p_done[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (SPLIT) {
+          tag_store(&X->p_head[r], m + 1, kPubModeSkipped << 16);
+          tag_store(&X->p_done[r], m + 1, 0u);
         }
       }
       last_panic = 1;
@@ -2838,60 +2941,125 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
     if (tid == 0) {
       sh.n_commit = 0;
-      int c = -1;
-      if (split) {  // -1 from the selector: more than one segment, which the host never sends here
-        c = fed_wait_word<false>(&X->s_seq[r], m + 1, idle_ticks)
-                ? __hip_atomic_load(&X->s_n[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                : -2;
-        if (c < 0) *exit_flag = 1;
-      }
-      s_cand = c;
+      sh.need_hist = 0;
+      s_feas = 0;
     }
-    __syncthreads();
-    const int na = s_cand;
-    if (split && na < 0) break;  // the selector stopped answering: leave (the host sees the exit flag)
-    if (tid == 0) sh.need_hist = 0;
     if constexpr (SPLIT) {
-      // candidates: the selector's T best outside the previous job's set, and that set re-keyed from its final
-      // rows; merged in node order (both lists are) so positions order ties as node indices do
-      int an = 0, bw = -1;
-      uint32_t ak = 0;
+      // candidates: A, the selector's T best outside the previous job's set (key order, with their static cache
+      // and rows); B, that set re-keyed from the final rows kept in brow. Every rank below is a count over at
+      // most 128 LDS entries split across 4 threads (unrolled), never a per-thread loop over all of them.
+      const int na = s_cand, nb = nbprev;
+      const uint32_t T = (uint32_t)cm.t_count;  // one segment
+#ifdef KB_DIAG
+      uint64_t mt = __builtin_amdgcn_s_memtime();
+#define KB_MSTAMP(k)                                    \
+  do {                                                  \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    mg[k] += t_ - mt;                                   \
+    mt = t_;                                            \
+  } while (0)
+#else
+#define KB_MSTAMP(k) \
+  do {               \
+  } while (0)
+#endif
+      Row* crow = brow + 128;                    // the candidates' rows by candidate index (A, then B)
+      uint64_t* cst = (uint64_t*)(crow + 256);   // and static caches
+      int32_t* cnd = (int32_t*)(cst + 256);      // and nodes
+      uint32_t* ak = sh.key0;                    // A's keys (descending), then the slots' keys
       if (tid < na) {
-        an = __hip_atomic_load(&X->s_node[r][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ak = __hip_atomic_load(&X->s_key[r][tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t* ent = X->s_ent[r][tid];
+        const uint64_t e0 = x_load64(&ent[0]);
+        const uint64_t st = x_load64(&ent[1]);
+        uint64_t words[sizeof(Row) / 8];
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = x_load64(&ent[2 + q]);
+        __builtin_memcpy(&crow[tid], words, sizeof(Row));
+        cst[tid] = st;
+        cnd[tid] = (int)(e0 >> 32);
+        ak[tid] = (uint32_t)e0;
+      } else if (tid >= 128 && tid - 128 < nb) {
+        const int j = tid - 128, w = bprev[j];
+        const Row rw = brow[j];
+        const uint64_t st = stat[w];
+        const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, w);
+        // an infeasible key (its reason mask) gets the B index below it, so B's keys are distinct: their ranks
+        // are a permutation (still below every feasible key)
+        bkey[j] = rs ? (rs << 7) | (uint32_t)j
+                     : compress_key(make_key(0, row_score(C, sp, rw, st), w), w + N.base, idx_bits);
+        crow[na + j] = rw;
+        cst[na + j] = st;
+        cnd[na + j] = w;
+        if (rs == 0) atomicAdd(&s_feas, 1);
       }
-      if (tid >= 128 && tid - 128 < nbprev) {
-        bw = bprev[tid - 128];
-        const Row rr = load_row(N, bw);
-        const uint64_t st = stat[bw];
-        const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, bw);
-        bkey[tid - 128] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), bw), bw + N.base, idx_bits);
-      }
-      if (tid < na) sh.node[tid] = an;  // scratch until sel_pick: A's nodes for the B side's search
-      for (int i = tid; i < 4 * kSelThreads; i += kSelThreads)
-        if (i >= na + nbprev) kc[i] = 0u;
+      if (tid >= nb && tid < 128) bkey[tid] = 0u;  // padding ranks below every key
       __syncthreads();
-      if (tid < na) {  // position = own index + B nodes below it
-        int lo = 0, hi = nbprev;
+      KB_MSTAMP(0);
+      // B's keys in descending order (rank among B: 4 threads per entry; the keys are distinct)
+      {
+        const int j = tid >> 2, part = tid & 3;
+        const uint32_t k = j < nb ? bkey[j] : 0u;
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) c += bkey[part * 32 + q] > k;
+        c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
+        c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
+        if (part == 0 && j < nb) {
+          sh.emin[c] = k;  // scratch: B's keys sorted (descending)
+          sh.A[j] = (int)c;
+        }
+      }
+      __syncthreads();
+      KB_MSTAMP(1);
+      // rank in the union (keys carry the node: distinct), by binary search in the other sorted list
+      const int nc = na + nb;
+      int pos = -1;
+      uint32_t key = 0;
+      if (tid < nc) {
+        const bool in_a = tid < na;
+        key = in_a ? ak[tid] : bkey[tid - na];
+        const uint32_t* other = in_a ? sh.emin : ak;
+        int lo = 0, hi = in_a ? nb : na;  // entries of the other list above key
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
-          if (bprev[mid] < an) lo = mid + 1;
+          if (other[mid] > key) lo = mid + 1;
           else hi = mid;
         }
-        kc[tid + lo] = ak;
-        cn[tid + lo] = an;
+        pos = (in_a ? tid : sh.A[tid - na]) + lo;
       }
-      if (bw >= 0) {
-        int lo = 0, hi = na;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sh.node[mid] < bw) lo = mid + 1;
-          else hi = mid;
-        }
-        kc[tid - 128 + lo] = bkey[tid - 128];
-        cn[tid - 128 + lo] = bw;
+      // the T best feasible (A is all feasible; infeasible keys rank below every feasible one), slots in node
+      // order: the winners' tie rule on equal score fields takes lower slots first, which must be lower nodes
+      const int nsel = min((int)T, na + s_feas);
+      const bool sel = pos >= 0 && pos < nsel;
+      __syncthreads();  // the lists read
+      if (sel) bprev[pos] = cnd[tid];  // scratch: the selected nodes by rank
+      if (tid >= nsel && tid < 128) bprev[tid] = 0x7fffffff;  // padding: above every node
+      __syncthreads();
+      KB_MSTAMP(2);
+      {
+        const int e = tid >> 2, part = tid & 3;
+        const int w = e < nsel ? bprev[e] : 0;
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) c += bprev[part * 32 + q] < w;
+        c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
+        c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
+        if (part == 0 && e < nsel) sh.gen[e] = (int)c;  // scratch: slot of the rank-e node
       }
       __syncthreads();
+      if (sel) {
+        const int slot_s = sh.gen[pos];
+        sh.node[slot_s] = cnd[tid];
+        sh.key0[slot_s] = key;
+        sh.row[slot_s] = crow[tid];
+        sh.stat[slot_s] = cst[tid];
+        sh.lmax[slot_s] = (int)T - pos;
+        if (pos == nsel - 1) sh.theta0 = key;
+      }
+      if (tid == 0) sh.n_sel = nsel;
+      __syncthreads();
+      KB_MSTAMP(3);
+#undef KB_MSTAMP
     } else {
       // the previous two jobs' commits (final rows) re-keyed for this spec: their loads first
       const int np0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0;
@@ -2922,20 +3090,21 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     KB_SEL_PH(0);
     FedPub pub;
     if constexpr (SPLIT) {
+      pub.head = &X->p_head[r];
       pub.node = X->p_node[r];
-      pub.n = &X->p_n[r];
-      pub.mode = &X->p_mode[r];
-      pub.start = &X->p_start[r];
-      pub.val = m + 1;
+      pub.tag = m + 1;
     }
     sel_run<false, QN, SPLIT>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
                               gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
-                              S.commits[slot] SEL_DIAG_ARGS, SPLIT ? cn : nullptr, pub);
+                              S.commits[slot] SEL_DIAG_ARGS, pub);
     if constexpr (SPLIT) {
-      // the set published for the selector becomes the next job's B
       __syncthreads();
+      // this job's set, with its final rows, is the next job's B
       const int ns = sh.n_sel;
-      if (tid < ns) bprev[tid] = sh.node[tid];
+      if (tid < ns) {
+        bprev[tid] = sh.node[tid];
+        brow[tid] = row_after(sp, sh.row[tid], sh.fin[tid], sh.A[tid]);
+      }
       nbprev = ns;
       if (sh.need_hist) {  // no fit: every node's key at this point (the sweep's, then every row changed since)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
@@ -2963,8 +3132,6 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           hjs->hist[tid] = sh.hist[tid];
         }
       }
-    } else {
-      nbprev = 0;
     }
 #ifdef KB_DIAG
     // fed engine layout: [0] key load + patch, [1..4] as sel_run, [5] commit + the previous job's publish +
@@ -2984,8 +3151,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     if (tid == 0) {
       js->n_commit = ncommit;
       publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
-      // after that release (which wrote the job's rows and n_commit back): the selector may re-key them
-      if (split) __hip_atomic_store(&X->p_done[r], m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // after that release (the job's rows written back): the selector may re-key them
+      if (SPLIT) tag_store(&X->p_done[r], m + 1, (uint32_t)ncommit);
     }
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
     prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
@@ -2997,6 +3164,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     pub_prev = t_wait0 - t_pub;
 #endif
   }
+#ifdef KB_DIAG
+  if (SPLIT && tid == 0)
+    for (int k = 0; k < 4; ++k) X->sdiag[8 + k] = mg[k];
+#endif
 }
 
 int fed_lds_bytes(int n) {

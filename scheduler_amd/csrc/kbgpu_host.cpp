@@ -1206,12 +1206,15 @@ int kb_fed_end(kb_ctx* c) {
   if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
   if (c->timing) c->ev_collect(true);
   if (getenv("KB_FED_DIAG") && c->fed_xchg && c->stats.fed_split) {  // KB_DIAG builds: the selector's phases
-    uint64_t d[8] = {};
+    uint64_t d[16] = {};
     if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - sizeof(d), sizeof(d), hipMemcpyDeviceToHost) ==
-        hipSuccess && d[6])
-      fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_placer=%.0f "
-              "patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
+        hipSuccess && d[6]) {
+      fprintf(stderr, "kb_fed_placer_merge cycles/job loads=%.0f b_order=%.0f union_rank=%.0f slots=%.0f\n",
+              (double)d[8] / d[6], (double)d[9] / d[6], (double)d[10] / d[6], (double)d[11] / d[6]);
+      fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_set_exclude=%.0f "
+              "wait_done_patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
               (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6], (double)d[5] / d[6]);
+    }
   }
   // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;
