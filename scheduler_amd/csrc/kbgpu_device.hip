@@ -2596,7 +2596,7 @@ struct FedXchg {
   uint64_t p_node[kJobSlots][128];   //   the job's selected set (tagged)
   uint64_t s_head[kJobSlots];        // selector -> placer: (job number + 1) << 32 | candidates (kSelExit: EXIT),
                                      //   stored once the entries below are drained
-  uint64_t s_cmd[kJobSlots][8];      //   the job's command (FedCmd)
+  uint64_t s_cmd[kJobSlots][16];     //   the job's command (FedCmd), one tagged word per field
   uint64_t s_ent[kJobSlots][128][2 + sizeof(Row) / 8];  //   candidates in key order (descending): key | node << 32,
                                                         //   static cache, row
   uint64_t sdiag[16];  // KB_DIAG builds: the selector's phase cycles, [8..] the placer's merge (KB_FED_DIAG)
@@ -2785,12 +2785,12 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
       for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q], words[q]);
-    } else if (tid >= 256 && tid < 256 + 8) {  // the command, for the placer
-      uint64_t words[8];
-      __builtin_memcpy(words, &cm, sizeof(FedCmd));
-      x_store64(&X->s_cmd[r][tid - 256], words[tid - 256]);
+    } else if (tid >= 256 && tid < 256 + 16) {  // the command, for the placer (tagged: it may prefetch it)
+      tag_store(&X->s_cmd[r][tid - 256], m + 1, ((const uint32_t*)&cm)[tid - 256]);
     }
-    __syncthreads();  // every wave's stores drained
+    // every wave's entry stores drained before the head (a barrier alone waits for LDS only)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (tid == 0) x_store64(&X->s_head[r], ((uint64_t)(m + 1) << 32) | cnt);
     KB_SSTAMP(5);
 #ifdef KB_DIAG
@@ -2862,6 +2862,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   int prev_slot[2] = {-1, -1}, prev_ncommit[2] = {0, 0};
   int nbprev = 0;
   int rp = 0;
+  uint64_t pre[17];  // split, thread 0: the next job's command words and head, loaded at this job's end
+#pragma unroll
+  for (int q = 0; q < 17; ++q) pre[q] = 0;
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -2875,21 +2878,31 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
       if (tid == 0) {
         int c = -2;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint64_t h;
-        for (;;) {
-          h = x_load64(&X->s_head[r]);
-          if ((uint32_t)(h >> 32) == m + 1) break;
-          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-          __builtin_amdgcn_s_sleep(1);
+        // the head and command prefetched at the end of the previous job, when they were already there
+        bool have = (uint32_t)(pre[16] >> 32) == m + 1;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) have = have && (uint32_t)(pre[q] >> 32) == m + 1;
+        uint64_t h = pre[16];
+        if (!have) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            h = x_load64(&X->s_head[r]);
+            if ((uint32_t)(h >> 32) == m + 1) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
         }
         if ((uint32_t)(h >> 32) == m + 1) {
           c = (int32_t)(uint32_t)h;
           if (c >= 0) {
-            uint64_t words[8];
+            uint32_t fields[16];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) words[q] = x_load64(&X->s_cmd[r][q]);
-            __builtin_memcpy(&cm, words, sizeof(FedCmd));
+            for (int q = 0; q < 16; ++q) {
+              uint64_t w = have ? pre[q] : x_load64(&X->s_cmd[r][q]);
+              while ((uint32_t)(w >> 32) != m + 1) w = x_load64(&X->s_cmd[r][q]);  // the tag orders it
+              fields[q] = (uint32_t)w;
+            }
+            __builtin_memcpy(&cm, fields, sizeof(FedCmd));
           }
           // the sweep's static cache (another agent's release, which the selector has seen): fresh loads
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -3145,7 +3158,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #ifdef KB_DIAG
     const uint64_t t_pub = __builtin_amdgcn_s_memtime();
 #endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (SPLIT && tid == 0) {  // the next job's head and command: their latency hides in the drain below
+      const int rn = r + 1 == kJobSlots ? 0 : r + 1;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pre[q] = x_load64(&X->s_cmd[rn][q]);
+      pre[16] = x_load64(&X->s_head[rn]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a barrier alone waits for LDS only)
     __syncthreads();
     const int ncommit = sh.n_commit;
     if (tid == 0) {
