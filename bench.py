@@ -388,6 +388,8 @@ DIAG_PHASES = {
                          "nofit_hist"],
     "fed_engine_kernel": ["key_load_patch", "node_select", "node_setup", "e_sequences", "winners_order",
                           "commit_publish_nofit", "wait_for_command"],
+    "cls_place_kernel": ["prologue_rest", "minmax_keys_argmax", "commit", "rescan_counts", "prologue_loads",
+                         "stop_flush", "hot_switches_x1000"],
     "aff_place_kernel": ["prologue", "live_loads_minmax", "keys_argmax", "commit", "table_incr_fence", "stop_flush",
                          "nofit_hist"],
 }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 8
+#define KBGPU_ABI_VERSION 9
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -395,7 +395,8 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_KERNEL_SHARD_EXCHANGE 11 /* node sharding: the all-gather of the proposals (RCCL) */
 #define KB_KERNEL_SHARD_COMMIT 12  /* node sharding: global merge, stop rules, own commits */
 #define KB_KERNEL_FED_ENGINE 13    /* kb_allocate: resident selection workgroup fed by the sweeps, one launch per cycle */
-#define KB_NUM_KERNELS 14
+#define KB_KERNEL_CLS_PLACE 14      /* class loop: specs whose own commits move only their affinity histograms */
+#define KB_NUM_KERNELS 15
 typedef struct kb_stats {
   uint64_t launches[KB_NUM_KERNELS];
   double kernel_ms[KB_NUM_KERNELS];   /* summed event time per kernel kind */
@@ -407,6 +408,8 @@ typedef struct kb_stats {
                                          idle bound): finished on the launch path */
   uint64_t fed_cycles, fed_split;     /* kb_allocate cycles served by the resident engine; of those, by the
                                          split engine (node selection one job ahead on a second workgroup) */
+  uint64_t cap1_runs;                 /* runs of self-dependent specs taken as cap-1 selection runs */
+  uint64_t cls_runs;                  /* runs taken by the class loop (KB_KERNEL_CLS_PLACE) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

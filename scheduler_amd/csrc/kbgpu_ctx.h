@@ -28,6 +28,18 @@ struct kb_ctx {
   std::vector<char> spec_hist;  // per spec: has InterPodAffinity histograms
   std::vector<char> spec_incr;  // per spec: its commits update affinity tables
   std::vector<char> spec_aff_reg;  // per spec: its entry count when the register-resident loop takes it, else 0
+  std::vector<char> spec_cap1;     // per spec: kSpecCap1 (a selection run with at most one Allocate per node)
+  std::vector<int32_t> spec_cls;   // per spec: the class loop's finest dynamic slot (-1: not eligible)
+  std::vector<int64_t> aff_slot_D;  // per topology slot: its domain count
+  uint64_t* cls_lvl = nullptr;  // [kClsLevels][n] class loop scratch: keys after 1..kClsLevels commits
+  int32_t* cls_amax = nullptr;  // [n] class loop scratch: Allocates before Idle stops fitting
+  // per topology slot that is some spec's class slot: its classes as member lists (offsets [K + 1], node ids
+  // by class [n]; device copies in aff_mem), else null
+  std::vector<uint32_t*> cls_coff;
+  std::vector<uint16_t*> cls_mem;
+  bool use_cap1 = true, use_cls = true;  // KB_NO_CAP1 / KB_NO_CLS unset
+  bool cap1(int spec) const { return use_cap1 && spec < (int)spec_cap1.size() && spec_cap1[spec]; }
+  int cls_slot(int spec) const { return use_cls && spec < (int)spec_cls.size() ? spec_cls[spec] : -1; }
   bool use_aff_reg = true;
   int64_t* mm_eval = nullptr;   // [2 * chunk] per-spec IPA min / max for kb_eval
   uint32_t mm_eval_cap = 0;

@@ -15,6 +15,20 @@ constexpr int64_t kScoreBias = 1ll << 38;
 constexpr uint32_t kIdxMask = (1u << 24) - 1;
 constexpr uint32_t kMaxNodes = 1u << 24;
 
+// Internal kb_spec.flags bits, set on the device copy by kb_upload_affinity (never part of the ABI).
+// kSpecCap1: the spec's only self-dependent affinity input is a required anti-affinity check over
+// single-node domains (hostname): after one Allocate of the spec on a node (a Pipelined task does not join
+// the lister) the check fails there, and nothing else moves. Its run is a selection run whose levels j >= 1
+// fail once A >= 1, with the reason of the first such check (kSpecCapAnti: "didn't match pod anti-affinity
+// rules", else "didn't satisfy existing pods anti-affinity rules").
+constexpr uint32_t kSpecCap1 = 1u << 30;
+constexpr uint32_t kSpecCapAnti = 1u << 29;
+// Class loop (cls_place_kernel): at most kClsE histograms per spec, kClsU of its own histogram increments
+// per commit, kClsMaxK classes (the F-domains + one class for the nodes without one).
+constexpr int kClsE = 4;
+constexpr int kClsU = 8;
+constexpr int kClsMaxK = 1024;
+
 struct DevNodes {
   int32_t n, S, K, P;
   int32_t base;  // canonical index of row 0 (node sharding across GPUs; 0 on one GPU)
@@ -153,6 +167,18 @@ bool aff_reg_fits(int n, int ne);
 void launch_aff_reg(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int ne, int t_begin,
                     int t_count, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
                     int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+// The class loop for specs whose own commits move only their histograms (kbgpu_host.cpp
+// classify_self_dynamic): F = the finest moving slot, K = its domain count + 1. cls_fits: the LDS plan
+// holds n nodes and K classes. The run's global table updates are left to launch_aff_commit.
+bool cls_fits(int n, int K);
+// Scratch: bk / stat [n], lvl [kClsLevels][n], amax [n] (the chip-wide prologue's base keys, static cache,
+// keys after 1..kClsLevels commits, Allocates before Idle stops fitting). coff [K + 1] / mem [n]: slot F's
+// classes as member lists (node ids by class, kb_upload_affinity).
+constexpr int kClsLevels = 8;
+void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int F, int K, int t_begin,
+                      int t_count, uint64_t* bk, uint64_t* stat, uint64_t* lvl, int32_t* amax, const uint32_t* coff,
+                      const uint16_t* mem, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout,
+                      JobState* hjs, uint32_t seq, SpecGuard g, void* stream);
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
 // keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.

@@ -941,6 +941,10 @@ __device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCf
         if (q.ip == 0 ? used : (used & (1ull | (1ull << q.ip)))) reasons = 1u << KB_R_HOST_PORTS;
       }
       if (!reasons) reasons = stat_post(st);
+      // a cap-1 spec's own anti-affinity check, after its first Allocate here (InterPodAffinityMatches is
+      // the last predicate; a node failing a static one never reaches level 1)
+      if (!reasons && j > 0 && A > 0 && (sp.flags & kSpecCap1))
+        reasons = (sp.flags & kSpecCapAnti) ? kAffAntiRules : kAffExistingAnti;
     }
   }
   if (reasons) return reasons;
@@ -2039,8 +2043,11 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   __shared__ SelShared sh;
   if ((!first && js->stopped) || guard_fails(g)) {
     if (threadIdx.x == 0) {
-      js->stopped = 1;  // later runs of a skipped speculative job skip too
-      js->n_commit = 0;  // nothing for the next job to patch
+      // a skipped speculative job: later runs skip too, nothing for the next job to patch, and n_placed
+      // (stale: an older job's) reads as nothing placed for the affinity table commit queued behind it
+      if (first) js->n_placed = -1;
+      js->stopped = 1;
+      js->n_commit = 0;
     }
     signal_skip(hjs, seq);
     return;
@@ -3314,7 +3321,46 @@ __global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, Dev
   int64_t mn = 0, mx = 0;
   if (sp.aff_class >= 0) {
     const kb_aff_spec as = P.A.specs[sp.aff_class];
-    if (as.hist_cnt) block_ipa_minmax<false>(P.A, as, N.n, rmin, rmax, &mn, &mx);
+    if (as.hist_cnt) {
+      // batches of 8 nodes per thread, every load of a batch issued before its use
+      const int tid = threadIdx.x, n = N.n;
+      constexpr int kB = 8;
+      for (int i0 = 0; i0 < n; i0 += kB * kAffThreads) {
+        int64_t c[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) c[j] = 0;
+        for (uint32_t e = 0; e < as.hist_cnt; ++e) {
+          const kb_ipa_hist h = P.A.hists[as.hist_off + e];
+          int32_t d[kB];
+#pragma unroll
+          for (int j = 0; j < kB; ++j) {
+            const int i = i0 + j * kAffThreads + tid;
+            d[j] = i < n ? P.A.topo_dom[(size_t)h.slot * P.A.n + i] : -1;
+          }
+#pragma unroll
+          for (int j = 0; j < kB; ++j)
+            if (d[j] >= 0) c[j] += P.A.h[h.h_off + d[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < kB; ++j)
+          if (i0 + j * kAffThreads + tid < n) {
+            mn = c[j] < mn ? c[j] : mn;
+            mx = c[j] > mx ? c[j] : mx;
+          }
+      }
+      mn = wave_min_i64(mn);
+      mx = wave_max_i64(mx);
+      if ((tid & 63) == 0) {
+        rmin[tid >> 6] = mn;
+        rmax[tid >> 6] = mx;
+      }
+      __syncthreads();
+      mn = 0, mx = 0;
+      for (int w = 0; w < kAffThreads / 64; ++w) {
+        mn = rmin[w] < mn ? rmin[w] : mn;
+        mx = rmax[w] > mx ? rmax[w] : mx;
+      }
+    }
   }
   if (threadIdx.x == 0) {
     mm[2 * blockIdx.x] = mn;
@@ -4003,6 +4049,515 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                      spec, t_begin, t_count, base, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
+// ---------------------------------------------------------------------------
+// Class loop: a spec whose own commits move only its InterPodAffinity histograms (preferred affinity to
+// its own job's pods, say "the rack of my job"), every check static. classify_self_dynamic (kbgpu_host.cpp)
+// found F, the finest moving slot, with every histogram's domain a function of the node's F-domain. A
+// class = the nodes of one F-domain (class K-1: the nodes without one). They share every histogram entry
+// all run long, hence the count, the InterPodAffinity score (interpod_affinity.go:221-238: min / max over
+// all nodes = over the non-empty classes) and the checks. Inside a class the order is that of the base key
+// (row + static predicates + LR / BRA / NodeAffinity, scheduler_helper.go:67-129 without the batch score),
+// so a task's argmax (scheduler_helper.go:147-158) is the best over classes of (class best + class score).
+// A commit changes the winner's row (its base key: a rescan of its class's members) and the counts of the
+// classes in the committed node's domains (nodeorder.go:161-172 AddPod). Per task: one wave, a few lane
+// ops per class and per member of the winner's class, no block barriers; aff_reg_kernel re-keys every node.
+// Prologue on the whole block: base keys, class member lists (CSR) and class state in LDS. The run's
+// global table updates come after it (aff_commit_kernel, from the placements).
+// ---------------------------------------------------------------------------
+// 4 waves: the task loop's wave gets the whole VGPR file of its SIMD (1024 threads cap it at 128 and spill)
+constexpr int kClsThreads = 256;
+static_assert(kClsMaxK <= 16 * 64 && kClsMaxK % kClsThreads == 0, "classes per lane: at most 16");
+
+// wave-uniform signed max / min on DPP (ordering-preserving bias to unsigned); |v| < 2^62
+__device__ __forceinline__ int64_t wave_max_i64_dpp(int64_t v) {
+  return (int64_t)(wave_max_dpp((uint64_t)v ^ (1ull << 63)) ^ (1ull << 63));
+}
+__device__ __forceinline__ int64_t wave_min_i64_dpp(int64_t v) { return -wave_max_i64_dpp(-v); }
+
+// One wave's LDS accesses complete in issue order (the LDS serves a wave's DS instructions in order), so a
+// lane's store is seen by every later load of the wave: only the compiler must not move accesses across.
+__device__ __forceinline__ void wave_sync_lds() { __builtin_amdgcn_wave_barrier(); }
+
+static size_t cls_lds_bytes(int n, int K, int pb_cap) {
+  return (size_t)n * 8 + (size_t)K * 8 + (size_t)K * 8 + (size_t)kClsE * K * 4 + (size_t)(K + 1) * 4 +
+         (size_t)K * 4 + (size_t)pb_cap * 4 + (size_t)n * 4 + 16;
+}
+
+bool cls_fits(int n, int K) {
+  return n > 0 && n < 65536 && K >= 1 && K <= kClsMaxK && cls_lds_bytes(n, K, 256) + 2048 <= (size_t)kLdsLimit;
+}
+
+// Chip-wide prologue of a class-loop run, grid (nodes, 1 + kClsL): level 0 -> the base key (allocate's
+// predicate with every static affinity check, then the host overlay, as aff_key orders them; LR / BRA /
+// NodeAffinity without the batch score), the static cache and A (Allocates before Idle stops fitting);
+// level j >= 1 -> the key after j commits of the spec (traj_key64's closed form: the first A Allocate, the
+// rest Pipeline). A node failing a static check at level 0 never commits, so levels >= 1 leave them out.
+constexpr int kClsL = kClsLevels;
+__global__ __launch_bounds__(256) void cls_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, uint64_t* bk,
+                                                        uint64_t* stat, uint64_t* lvl, int32_t* amax,
+                                                        const JobState* js, SpecGuard g) {
+  if ((js != nullptr && js->stopped) || guard_fails(g)) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y;
+  if (i >= N.n) return;
+  const DevAff& A = P.A;
+  const kb_spec sp = P.specs[spec];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  const Row r = load_row(N, i);
+  const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
+  if (j == 0) {
+    const kb_aff_spec as = A.specs[sp.aff_class];
+    const int32_t ov = ov_row(P, spec);
+    uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
+    if (!rs && C.predicates) rs = aff_reasons<false>(A, as, i);
+    if (!rs && ov >= 0 && P.ov_fail[(size_t)ov * N.n + i]) rs = kHostError;
+    bk[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
+    stat[i] = st;
+    amax[i] = allocs_before_full(N, sp, sci, scr, r, i);
+  } else {
+    const uint64_t k = traj_key64(N, P, C, sp, sci, scr, r, st, i, j, allocs_before_full(N, sp, sci, scr, r, i));
+    lvl[(size_t)(j - 1) * N.n + i] = (k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)i)) : k;
+  }
+}
+
+// lane j's key of the hot node: the key after j + 1 more commits (wave-uniform index)
+__device__ __forceinline__ uint64_t hk_at(uint64_t hk, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)hk, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(hk >> 32), j);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The class loop's deep-node path (rare: a node past the sweep's levels).
+__device__ __forceinline__ int cls_allocs_deep(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
+                                            const int64_t* scr, const Row& r, int n) {
+  return allocs_before_full(N, sp, sci, scr, r, n);
+}
+__device__ __forceinline__ uint64_t cls_key_deep(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
+                                              const kb_spec& sp, const int64_t* sci, const int64_t* scr,
+                                              const Row& r, uint64_t st, int n, int j, int A) {
+  return traj_key64(N, P, C, sp, sci, scr, r, st, n, j, A);
+}
+
+template <int KQ>
+__global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int K, int t_begin, int t_count, const uint64_t* bkg,
+    const uint64_t* stat, const uint64_t* lvl, const int32_t* amax, const uint32_t* coff_g, const uint16_t* mem_g,
+    JobState* js, int first,
+    int ready0, int minav0,
+    int gang0, int32_t* hout, JobState* hjs, int pb_cap, uint32_t seq, SpecGuard g) {
+  // dynamic LDS: bk u64[n] base keys | cbest u64[K] class best base key | cnt i64[K] class counts |
+  // cdom i32[kClsE][K] each histogram's domain per class | coff u32[K + 1] member offsets | cur u32[K]
+  // populations, then scatter cursors | pbs u32[pb_cap] placements | mem u16[n] members by class
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_cl[];
+  const int n = N.n;
+  uint64_t* bk = lds_cl;
+  uint64_t* cbest = bk + n;
+  int64_t* cnt = (int64_t*)(cbest + K);
+  int32_t* cdom = (int32_t*)(cnt + K);
+  uint32_t* coff = (uint32_t*)(cdom + kClsE * K);
+  uint32_t* cur = coff + K + 1;
+  uint32_t* pbs = cur + K;
+  uint16_t* mem = (uint16_t*)(pbs + pb_cap);
+  uint16_t* lv16 = mem + n;  // commits of this run per node
+  __shared__ uint32_t wsum[kClsThreads / 64];
+  if ((!first && js->stopped) || guard_fails(g)) {
+    if (threadIdx.x == 0) {
+      if (first) js->n_placed = -1;  // a skipped speculative job (see sel_place_kernel)
+      js->stopped = 1;
+      js->n_commit = 0;
+    }
+    signal_skip(hjs, seq);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#ifdef KB_DIAG_AFF
+  // phases: 0 prologue, 1 min / max + class keys + argmax, 2 commit (lane 0), 3 class rescan + counts,
+  // 5 stop rules / flush, 6 no-fit histogram
+  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_last = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  const DevAff& A = P.A;
+  const kb_spec sp = P.specs[spec];
+  const kb_aff_spec as = A.specs[sp.aff_class];
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  const int ne = (int)as.hist_cnt;  // <= kClsE (host)
+  int32_t e_slot[kClsE], e_off[kClsE];
+#pragma unroll
+  for (int e = 0; e < kClsE; ++e) {
+    e_slot[e] = 0, e_off[e] = -1;
+    if (e < ne) {
+      const kb_ipa_hist h = A.hists[as.hist_off + e];
+      e_slot[e] = h.slot, e_off[e] = (int32_t)h.h_off;
+    }
+  }
+  // the class member lists (static per topology slot: built at kb_upload_affinity) into LDS
+  for (int c = tid; c <= K; c += kClsThreads) coff[c] = coff_g[c];
+  for (int c = tid; c < K; c += kClsThreads) cbest[c] = 0;
+  for (int j = tid; j < n; j += kClsThreads) {
+    mem[j] = mem_g[j];
+    lv16[j] = 0;
+  }
+  __syncthreads();
+  // base keys into LDS and each class's best: every thread a contiguous stretch of the member list, a
+  // running max per class, flushed at class boundaries (atomics only where stretches share a class)
+  {
+    const int ch = (n + kClsThreads - 1) / kClsThreads;
+    const int j0 = tid * ch < n ? tid * ch : n, j1 = j0 + ch < n ? j0 + ch : n;
+    int lo = 0, hi = K;  // the class of position j0: the last c with coff[c] <= j0
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if ((int)coff[mid] <= j0) lo = mid;
+      else hi = mid;
+    }
+    int c = lo;
+    uint64_t run = 0;
+    constexpr int kB = 16;
+    for (int jb = j0; jb < j1; jb += kB) {
+      uint64_t kk[kB];
+      int nd[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) nd[q] = jb + q < j1 ? mem[jb + q] : 0;
+#pragma unroll
+      for (int q = 0; q < kB; ++q) kk[q] = jb + q < j1 ? bkg[nd[q]] : 0;
+#pragma unroll
+      for (int q = 0; q < kB; ++q) {
+        const int j = jb + q;
+        if (j < j1) {
+          while (j >= (int)coff[c + 1]) {
+            if (run) atomicMax((unsigned long long*)&cbest[c], (unsigned long long)run);
+            run = 0;
+            ++c;
+          }
+          bk[nd[q]] = kk[q];
+          run = umax64(run, kk[q]);
+        }
+      }
+    }
+    if (run) atomicMax((unsigned long long*)&cbest[c], (unsigned long long)run);
+  }
+  __syncthreads();
+  // per class: each histogram's domain (class-uniform: read at the first member) and the count
+  for (int c = tid; c < K; c += kClsThreads) {
+    int64_t c0 = 0;
+    const bool any = coff[c + 1] > coff[c];
+    const int i0 = any ? mem[coff[c]] : 0;
+    int32_t dd[kClsE];
+#pragma unroll
+    for (int e = 0; e < kClsE; ++e) dd[e] = any && e < ne ? A.topo_dom[(size_t)e_slot[e] * n + i0] : -1;
+#pragma unroll
+    for (int e = 0; e < kClsE; ++e) {
+      cdom[e * K + c] = dd[e];
+      if (dd[e] >= 0) c0 += ld_cnt<false>(&A.h[e_off[e] + dd[e]]);
+    }
+    cnt[c] = c0;
+  }
+  __syncthreads();
+  if (wv != 0) return;  // the task loop is wave 0's: no block barrier below
+
+  // ---- task loop (wave 0) ----
+  // class c = q * 64 + lane: its count in registers
+  int64_t cq[KQ];
+  bool live[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int c = q * 64 + lane;
+    live[q] = c < K && coff[c + 1] > coff[c];
+    cq[q] = c < K ? cnt[c] : 0;
+  }
+  // the spec's increments of its own histograms (entry, weight); the others go to the global tables only
+  // (register arrays: every index a constant after unrolling, so nothing goes to scratch)
+  int32_t u_e[kClsU], u_w[kClsU];
+  int nu = 0;
+#pragma unroll
+  for (int v = 0; v < kClsU; ++v) u_e[v] = -1, u_w[v] = 0;
+  for (uint32_t i = 0; i < as.incr_cnt && nu < kClsU; ++i) {
+    const kb_ipa_incr u = A.incr[as.incr_off + i];
+#pragma unroll
+    for (int e = 0; e < kClsE; ++e)
+      if (e < ne && (int32_t)u.h_off == e_off[e] && nu < kClsU) {
+#pragma unroll
+        for (int v = 0; v < kClsU; ++v)
+          if (v == nu) u_e[v] = e, u_w[v] = u.weight;
+        ++nu;
+      }
+  }
+  const int64_t* scr = P.sc_req + (size_t)spec * N.S;
+  int ready = first ? ready0 : js->ready_num;
+  int minav = first ? minav0 : js->min_available;
+  int gang = first ? gang0 : js->gang_ready;
+  int placed = first ? 0 : js->n_placed;
+  int pb_n = 0, pb_base = t_begin;
+  int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
+  const bool ipa = C.nodeorder && ne > 0;
+  const int64_t c_wpa = C.w_pa;
+  // The hot node: the last winner, with its next keys one per lane (lane j: the key after j + 1 more
+  // commits), read from the sweep's level keys (a gather, prefetched for the winner's class's new best right
+  // after its rescan), or -- past kClsL levels -- computed from its row at once (traj_key64, 64 levels). Its
+  // first hot_A further commits are Allocates. Its row deltas go to HBM as atomics when another node turns
+  // hot and at the end (nothing waits for them; rows are read again only on the deep path, after a fence).
+  // A winner keeps its score for several pods (LR / BRA move in steps): most commits read a register.
+  int hot = -1, hot_c = 0, hot_A = 0, hot_n = 0, hot_lim = 0, p_node = -1, p_A = 0;
+  uint64_t hk = 0, pk = 0;
+  const auto flush_hot = [&]() {  // lane 0: the hot node's commits as row deltas (NodeInfo.AddTask)
+    if (hot < 0 || hot_c == 0) return;
+    if (lane == 0) {
+      const int64_t ac = hot_c < hot_A ? hot_c : hot_A, pc = hot_c - ac;
+      if (ac) {
+        atomicAdd((unsigned long long*)&N.idle_cpu[hot], (unsigned long long)(-ac * sp.req_cpu));
+        atomicAdd((unsigned long long*)&N.idle_mem[hot], (unsigned long long)(-ac * sp.req_mem));
+      }
+      if (pc) {
+        atomicAdd((unsigned long long*)&N.rel_cpu[hot], (unsigned long long)(-pc * sp.req_cpu));
+        atomicAdd((unsigned long long*)&N.rel_mem[hot], (unsigned long long)(-pc * sp.req_mem));
+      }
+      atomicAdd(&N.pod_count[hot], hot_c);
+      atomicAdd((unsigned long long*)&N.nz_cpu[hot], (unsigned long long)((int64_t)hot_c * sp.nz_cpu));
+      atomicAdd((unsigned long long*)&N.nz_mem[hot], (unsigned long long)((int64_t)hot_c * sp.nz_mem));
+      const uint32_t fl = N.flags[hot];
+      uint64_t m = sp.req_sc_mask;
+      while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
+        const int q = __builtin_ctzll(m);
+        m &= m - 1;
+        if (ac && (fl & KB_NODE_IDLE_HAS_MAP))
+          atomicAdd((unsigned long long*)&N.idle_sc[(size_t)q * n + hot], (unsigned long long)(-ac * scr[q]));
+        if (pc && (fl & KB_NODE_REL_HAS_MAP))
+          atomicAdd((unsigned long long*)&N.rel_sc[(size_t)q * n + hot], (unsigned long long)(-pc * scr[q]));
+      }
+      for (uint32_t i = 0; i < sp.port_cnt; ++i) {
+        const kb_port q = P.ports[sp.port_off + i];
+        atomicOr((unsigned long long*)&N.port_used[(size_t)q.slot * n + hot], 1ull << q.ip);
+      }
+      lv16[hot] = (uint16_t)(hot_n + hot_c);
+    }
+  };
+  AFF_STAMP(0);
+  for (int t = 0; t < t_count; ++t) {
+    int64_t mn = 0, mx = 0;
+    int64_t bp[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) bp[q] = INT64_MAX;
+    if (ipa) {
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        if (live[q]) {
+          mn = cq[q] < mn ? cq[q] : mn;
+          mx = cq[q] > mx ? cq[q] : mx;
+        }
+      mn = wave_min_i64_dpp(mn);
+      mx = wave_max_i64_dpp(mx);
+      // ipa_score is monotone in the count: its 10 breakpoints, exactly (as in aff_reg_kernel): a_s =
+      // ceil(s * b / 10) is the first offset with 10 a / b >= s; the float64 formula falls short of s only
+      // where 10 a / b == s exactly, and then a_s + 1 is it. Lane s - 1 computes a_s.
+      const int64_t bb = mx - mn;
+      int64_t as_ = INT64_MAX;
+      if (bb > 0 && lane < 10) {
+        const int64_t sb = (int64_t)(lane + 1) * bb;
+        as_ = (sb + 9) / 10;
+        if (sb % 10 == 0 && ipa_score(mn + as_, mn, mx) < lane + 1) ++as_;
+      }
+#pragma unroll
+      for (int q = 0; q < 10; ++q) {
+        const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)as_, q);
+        const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)((uint64_t)as_ >> 32), q);
+        bp[q] = (int64_t)(((uint64_t)hi32 << 32) | lo32);
+      }
+    }
+    uint64_t kq[KQ];
+    uint64_t best = 0;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const int c = q * 64 + lane;
+      uint64_t k = c < K ? cbest[c] : 0;
+      if ((k & kFeasible) && ipa) {
+        const int64_t off = cq[q] - mn;
+        int32_t sc = 0;  // == ipa_score(cq[q], mn, mx)
+#pragma unroll
+        for (int s = 0; s < 10; ++s) sc += off >= bp[s];
+        k += (uint64_t)((int64_t)sc * c_wpa) << 24;
+      }
+      kq[q] = k;
+      best = umax64(best, k);
+    }
+    best = wave_max_dpp(best);
+    if (!(best & kFeasible)) {
+      // PredicateNodes found nothing (allocate.go:150-153): FitErrors over every node's base reasons
+      uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+      for (int i = lane; i < n; i += 64) {
+        const uint64_t k = bk[i];
+#pragma unroll
+        for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (uint32_t)(k >> b) & 1u;
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) {
+        const uint32_t s = wave_sum_u32(h[b]);
+        if (lane == b) {
+          js->hist[b] = s;
+          hjs->hist[b] = s;
+        }
+      }
+      stop = KB_STOP_NO_FIT;
+      fail_task = t_begin + t;
+      stopped = 1;
+      AFF_STAMP(6);
+      break;
+    }
+    const int64_t score = (int64_t)((best >> 24) & ((1ull << 39) - 1)) - kScoreBias;
+    if (score <= -1) {  // SelectBestNode: no bucket with score > -1 -> the reference panics
+      fail_task = t_begin + t;
+      panic = 1;
+      stopped = 1;
+      break;
+    }
+    const int w = (int)(kIdxMask - (uint32_t)(best & kIdxMask));
+    int mine = -1;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+      if (kq[q] == best) mine = q * 64 + lane;
+    const uint64_t who = __ballot(mine >= 0);
+    const int cw = __builtin_amdgcn_readlane(mine, (int)__builtin_ctzll(who));
+    AFF_STAMP(1);
+    // commit: Session.Allocate / Pipeline on the winner's row (allocate.go:159-182). A new hot node (or the
+    // hot one past its keys) first.
+    if (w != hot || hot_c == hot_lim) {
+      const bool same = w == hot;
+      flush_hot();
+      wave_sync_lds();
+      const int l0 = same ? hot_n + hot_c : (int)lv16[w];
+      hot = w, hot_c = 0, hot_n = l0;
+      if (l0 < kClsL) {  // the sweep's level keys (lane j: level l0 + j + 1)
+        if (w == p_node) {
+          hk = pk, hot_A = p_A;
+        } else {
+          hk = l0 + lane < kClsL ? lvl[(size_t)(l0 + lane) * n + w] : 0;
+          const int a0 = amax[w];
+          hot_A = a0 > l0 ? a0 - l0 : 0;
+        }
+        hot_lim = kClsL - l0;
+      } else {  // deeper than the sweep went: from the row as it stands (this run's deltas applied)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        Row r;
+        r.flags = N.flags[w];
+        r.max_pods = N.max_pods[w];
+        r.alloc_cpu = N.alloc_cpu[w];
+        r.alloc_mem = N.alloc_mem[w];
+        r.pod_count = __hip_atomic_load(&N.pod_count[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.idle_cpu = __hip_atomic_load(&N.idle_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.idle_mem = __hip_atomic_load(&N.idle_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.rel_cpu = __hip_atomic_load(&N.rel_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.rel_mem = __hip_atomic_load(&N.rel_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.nz_cpu = __hip_atomic_load(&N.nz_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.nz_mem = __hip_atomic_load(&N.nz_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hot_A = cls_allocs_deep(N, sp, sci, scr, r, w);
+        const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[w], w, lane + 1, hot_A);
+        hk = (k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)w)) : k;
+        hot_lim = 64;
+      }
+      if (p_node == w) p_node = -1;
+    }
+    const int kind = hot_c < hot_A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+    const uint64_t nk = hk_at(hk, hot_c);
+    ++hot_c;
+    const int moved = nk != cbest[cw];  // w was its class's best; an unchanged key keeps it there
+    if (lane == 0) {
+      bk[w] = nk;
+      pbs[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
+    }
+    wave_sync_lds();
+    AFF_STAMP(2);
+    if (moved) {  // the winner's key fell: its class's best again
+      const uint32_t m0 = coff[cw], m1 = coff[cw + 1];
+      uint64_t b = 0;
+      for (uint32_t k = m0 + lane; k < m1; k += 64) b = umax64(b, bk[mem[k]]);
+      b = wave_max_dpp(b);
+      if (lane == 0) cbest[cw] = b;
+      const int bn = (int)(kIdxMask - (uint32_t)(b & kIdxMask));
+      if ((b & kFeasible) && bn != hot && bn != p_node) {  // prefetch its level keys (not waited for here)
+        const int l0 = lv16[bn];
+        if (l0 < kClsL) {
+          p_node = bn;
+          pk = l0 + lane < kClsL ? lvl[(size_t)(l0 + lane) * n + bn] : 0;
+          const int a0 = amax[bn];
+          p_A = a0 > l0 ? a0 - l0 : 0;
+        }
+      }
+    }
+    // the classes in the committed node's domains: this commit's increments of the spec's own histograms
+#pragma unroll
+    for (int u = 0; u < kClsU; ++u) {
+      if (u >= nu) break;
+      const int e = u_e[u];
+      const int32_t d = cdom[e * K + cw];
+      if (d < 0) continue;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        const int c = q * 64 + lane;
+        if (c < K && cdom[e * K + c] == d) cq[q] += u_w[u];
+      }
+    }
+    wave_sync_lds();
+    AFF_STAMP(3);
+    ++placed;
+    ++pb_n;
+    if (kind == KB_PLACE_ALLOCATE) ++ready;
+    if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+      stop = KB_STOP_READY;
+      stopped = 1;
+      break;
+    }
+    if (pb_n == pb_cap) {
+      for (int k = lane; k < pb_n; k += 64) {
+        const uint32_t e = pbs[k];
+        hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+        hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+      }
+      wave_sync_lds();
+      pb_base += pb_n;
+      pb_n = 0;
+    }
+    AFF_STAMP(5);
+  }
+  flush_hot();
+  for (int k = lane; k < pb_n; k += 64) {
+    const uint32_t e = pbs[k];
+    hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+    hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+  }
+#ifdef KB_DIAG_AFF
+  if (lane == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
+  __threadfence_system();
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, seq);
+}
+
+void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int F, int K, int t_begin,
+                      int t_count, uint64_t* bk, uint64_t* stat, uint64_t* lvl, int32_t* amax, const uint32_t* coff,
+                      const uint16_t* mem, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout,
+                      JobState* hjs, uint32_t seq, SpecGuard g, void* stream) {
+  hipLaunchKernelGGL(cls_sweep_kernel, dim3((N.n + 255) / 256, 1 + kClsL), dim3(256), 0, (hipStream_t)stream, N, P,
+                     C, spec, bk, stat, lvl, amax, first ? (const JobState*)nullptr : js, g);
+  int pb_cap = aff_pb_cap(t_count);
+  const size_t fixed = cls_lds_bytes(N.n, K, 0);
+  const size_t cap_max = ((size_t)kLdsLimit - 2048 - fixed) / 4;
+  if ((size_t)pb_cap > cap_max) pb_cap = (int)cap_max;
+  const size_t bytes = cls_lds_bytes(N.n, K, pb_cap);
+#define KB_CLS_Q(Q)                                                                                              \
+  hipLaunchKernelGGL(cls_place_kernel<Q>, dim3(1), dim3(kClsThreads), bytes, (hipStream_t)stream, N, P, C, spec, K, \
+                     t_begin, t_count, bk, stat, lvl, amax, coff, mem, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, \
+                     seq, g)
+  const int q = (K + 63) / 64;
+  if (q <= 1) KB_CLS_Q(1);
+  else if (q <= 2) KB_CLS_Q(2);
+  else if (q <= 4) KB_CLS_Q(4);
+  else if (q <= 8) KB_CLS_Q(8);
+  else KB_CLS_Q(16);
+#undef KB_CLS_Q
+}
+
 // LDS plan of one place-loop launch: chunk maxima + placement buffer (+ all keys when they fit).
 static void place_loop_lds_plan(int n, int t_count, int* bytes, int* pb_cap, bool* keys_in_lds) {
   const int M = (n + 63) >> 6;
@@ -4065,6 +4620,14 @@ int configure_kernels() {
   for (const void* f : kAffRegFns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - 4096);
     if (e != hipSuccess) return (int)e;
+  }
+  {
+    for (const void* f : {(const void*)cls_place_kernel<1>, (const void*)cls_place_kernel<2>,
+                          (const void*)cls_place_kernel<4>, (const void*)cls_place_kernel<8>,
+                          (const void*)cls_place_kernel<16>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - 2048);
+      if (e != hipSuccess) return (int)e;
+    }
   }
   for (const void* f :
        {(const void*)sel_place_kernel<0>, (const void*)sel_place_kernel<1>, (const void*)sel_place_kernel<2>,

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -81,6 +82,94 @@ void drop_affinity(kb_ctx* c) {
   c->spec_aff_err.clear();
   c->mm_eval = nullptr;
   c->mm_eval_cap = 0;
+  c->spec_cap1.clear();
+  c->spec_cls.clear();
+  c->cls_coff.clear();
+  c->cls_mem.clear();
+}
+
+// Which self-dependent specs (KB_AFF_SELF_DYNAMIC) leave the per-task re-sweep loops:
+//  * cap-1 (kSpecCap1 on the device copy of the spec): every self-dependent entry is a required
+//    anti-affinity check (EXISTING_ANTI / ANTI) of a table the spec's own Allocates join, over a slot whose
+//    domains are single nodes, and no histogram moves. A commit then changes one thing: that node fails the
+//    check for the rest of the run. The run is a selection run (traj_key64's cap).
+//  * class loop (spec_cls = its finest moving slot F): every check is static (the spec's commits join none
+//    of its tables) and at least one of its InterPodAffinity histograms moves. Every entry's domain is a
+//    function of the node's F-domain, so the nodes of one F-domain share their counts all run long, and a
+//    task ranks the F-domains' best nodes instead of every node (cls_place_kernel).
+void classify_self_dynamic(kb_ctx* c, const kb_affinity* a, const std::vector<int64_t>& D,
+                           std::vector<kb_spec>& specs) {
+  const size_t n = (size_t)c->N.n;
+  c->spec_cap1.assign(a->m, 0);
+  c->spec_cls.assign(a->m, -1);
+  for (auto& sp : specs) sp.flags &= ~(kbgpu::kSpecCap1 | kbgpu::kSpecCapAnti);
+  std::vector<signed char> single(a->n_slots, -1);  // slot: every node has its own domain
+  auto single_node = [&](int32_t sl) {
+    if (single[sl] < 0) {
+      bool ok = D[sl] == (int64_t)n;
+      std::vector<char> seen(ok ? n : 0, 0);
+      for (size_t i = 0; ok && i < n; ++i) {
+        const int32_t d = a->topo_dom[sl * n + i];
+        ok = d >= 0 && !seen[d];
+        if (ok) seen[d] = 1;
+      }
+      single[sl] = ok;
+    }
+    return single[sl] == 1;
+  };
+  std::map<std::pair<int32_t, int32_t>, bool> nests;  // (F, S): dom_S is a function of dom_F
+  auto nested = [&](int32_t F, int32_t S) {
+    auto it = nests.find({F, S});
+    if (it != nests.end()) return it->second;
+    std::vector<int32_t> map_(D[F] + 1, -2);  // index dom_F + 1
+    bool ok = true;
+    for (size_t i = 0; ok && i < n; ++i) {
+      int32_t& m = map_[a->topo_dom[F * n + i] + 1];
+      const int32_t s = a->topo_dom[S * n + i];
+      if (m == -2) m = s;
+      ok = m == s;
+    }
+    nests[{F, S}] = ok;
+    return ok;
+  };
+  for (uint32_t s = 0; s < a->m; ++s) {
+    const int32_t ac = specs[s].aff_class;
+    if (ac < 0 || !(a->specs[ac].flags & KB_AFF_SELF_DYNAMIC)) continue;
+    const kb_aff_spec& e = a->specs[ac];
+    auto joins = [&](int32_t table) {
+      for (uint32_t i = 0; i < e.lister_cnt; ++i)
+        if (a->lister[e.lister_off + i] == table) return true;
+      return false;
+    };
+    auto moves = [&](uint32_t h_off) {
+      for (uint32_t i = 0; i < e.incr_cnt; ++i)
+        if (a->incr[e.incr_off + i].h_off == h_off) return true;
+      return false;
+    };
+    int dyn_checks = 0, first_kind = -1;
+    bool cap_ok = true;
+    for (uint32_t i = 0; i < e.check_cnt; ++i) {
+      const kb_aff_check& ck = a->checks[e.check_off + i];
+      if (!joins(ck.table)) continue;
+      ++dyn_checks;
+      if (first_kind < 0) first_kind = ck.kind;
+      cap_ok = cap_ok && (ck.kind == KB_AFF_EXISTING_ANTI || ck.kind == KB_AFF_ANTI) &&
+               single_node(a->tables[ck.table].slot);
+    }
+    int32_t F = -1;
+    for (uint32_t i = 0; i < e.hist_cnt; ++i) {
+      const kb_ipa_hist& h = a->hists[e.hist_off + i];
+      if (moves(h.h_off) && (F < 0 || D[h.slot] > D[F])) F = h.slot;
+    }
+    if (dyn_checks && cap_ok && F < 0) {
+      c->spec_cap1[s] = 1;
+      specs[s].flags |= kbgpu::kSpecCap1 | (first_kind == KB_AFF_ANTI ? kbgpu::kSpecCapAnti : 0u);
+    } else if (!dyn_checks && F >= 0 && e.hist_cnt <= (uint32_t)kbgpu::kClsE) {
+      bool ok = true;
+      for (uint32_t i = 0; ok && i < e.hist_cnt; ++i) ok = nested(F, a->hists[e.hist_off + i].slot);
+      if (ok) c->spec_cls[s] = F;
+    }
+  }
 }
 
 }  // namespace
@@ -143,6 +232,8 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
   c->use_aff_reg = getenv("KB_NO_AFF_REG") == nullptr;  // testing: force the global-memory affinity loop
+  c->use_cap1 = getenv("KB_NO_CAP1") == nullptr;        // testing: cap-1 specs on the re-sweep loops
+  c->use_cls = getenv("KB_NO_CLS") == nullptr;          // testing: class-loop specs on the re-sweep loops
   c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
   c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
   c->timing_now = c->timing;
@@ -290,6 +381,12 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, n * sizeof(uint64_t)));
   c->work_mem.push_back(p);
   c->stat = (uint64_t*)p;
+  HIP_OK(c, hipMalloc(&p, (size_t)kClsLevels * n * sizeof(uint64_t)));  // class loop scratch
+  c->work_mem.push_back(p);
+  c->cls_lvl = (uint64_t*)p;
+  HIP_OK(c, hipMalloc(&p, n * sizeof(int32_t)));
+  c->work_mem.push_back(p);
+  c->cls_amax = (int32_t*)p;
   c->idx_bits = 1;  // key index field: global node indices when sharded
   const unsigned long long n_keys = c->sharded ? c->shard.n_total : n;
   while ((1ull << c->idx_bits) < n_keys) ++c->idx_bits;
@@ -453,6 +550,27 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
       c->spec_aff_reg[s] = ok && e.check_cnt + e.hist_cnt > 0 ? (char)(e.check_cnt + e.hist_cnt) : 0;  // entries (0: not eligible)
     }
   }
+  c->aff_slot_D = D;
+  classify_self_dynamic(c, a, D, specs);
+  // member lists of every class slot: class k = domain k, class D = the nodes without a domain
+  c->cls_coff.assign(a->n_slots, nullptr);
+  c->cls_mem.assign(a->n_slots, nullptr);
+  for (uint32_t s = 0; s < a->m; ++s) {
+    const int32_t F = c->spec_cls[s];
+    if (F < 0 || c->cls_coff[F] || n >= 65536) continue;
+    const size_t K = (size_t)D[F] + 1;
+    std::vector<uint32_t> off(K + 1, 0);
+    std::vector<uint16_t> mem(n);
+    auto cls_of = [&](size_t i) { const int32_t d = a->topo_dom[F * n + i]; return d >= 0 ? (size_t)d : K - 1; };
+    for (size_t i = 0; i < n; ++i) ++off[cls_of(i) + 1];
+    for (size_t k = 0; k < K; ++k) off[k + 1] += off[k];
+    std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < n; ++i) mem[cur[cls_of(i)]++] = (uint16_t)i;
+    int rc_;
+    if ((rc_ = upload(c, c->aff_mem, &c->cls_coff[F], off.data(), K + 1))) return rc_;
+    if ((rc_ = upload(c, c->aff_mem, &c->cls_mem[F], mem.data(), n))) return rc_;
+  }
+  if (a->m) HIP_OK(c, hipMemcpy(c->P.specs, specs.data(), a->m * sizeof(kb_spec), hipMemcpyHostToDevice));
   DevAff& A = c->P.A;
   int rc;
   if ((rc = upload(c, c->aff_mem, &A.topo_dom, a->topo_dom, (size_t)a->n_slots * n))) return rc;
@@ -930,6 +1048,13 @@ static uint32_t slots_cap(const kb_ctx* c) {
   return cap;
 }
 
+// A self-dependent spec the class loop takes (classify_self_dynamic; its LDS plan fits).
+static bool cls_run_ok(const kb_ctx* c, int spec) {
+  const int F = c->cls_slot(spec);
+  return F >= 0 && c->aff_ok && !c->spec_ipa_err[spec] && (size_t)F < c->cls_coff.size() && c->cls_coff[F] &&
+         cls_fits(c->N.n, (int)c->aff_slot_D[F] + 1);
+}
+
 // Launch every run of the job into slot `si`. The path per run: block-wide re-sweep (self-dependent
 // affinity), selection, trajectory, or rekey. `g` (first run only) guards a speculative job.
 static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard& g) {
@@ -952,18 +1077,30 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     int pbc;
     const int run = (int)(e - t);
     const bool aff = c->aff_ok && c->spec_needs_aff[spec];
-    const bool dyn = aff && c->spec_dyn[spec];
     const bool key32 = c->spec_traj_ok[spec] && c->traj != nullptr;
-    const bool sel = !dyn && c->use_sel && key32 && c->sel_ok;
+    const bool sel_fits = c->use_sel && key32 && c->sel_ok;
+    // self-dependent specs: cap-1 ones run as selection runs, the rest take a per-task loop
+    const bool dyn = aff && c->spec_dyn[spec] && !(sel_fits && c->cap1(spec));
+    const bool sel = !dyn && sel_fits;
     const bool traj = !sel && !dyn && c->use_traj && key32 && c->traj_full && traj_lds_bytes(c->N.n, run, &pbc) > 0;
-    if (first && g.prev && !sel) return fail(c, KB_E_INVALID, "guarded job does not take the selection path");
+    const bool cls = dyn && cls_run_ok(c, spec);
+    if (first && g.prev && !sel && !cls)
+      return fail(c, KB_E_INVALID, "guarded job takes neither the selection path nor the class loop");
     const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
     if (!dyn && c->aff_ok && c->spec_hist[spec]) {  // this run's InterPodAffinity normalisation
       c->ev_begin(&ea);
       launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, c->P.A.mm, first ? nullptr : js, c->stream);
       c->ev_end(ea, KB_KERNEL_IPA_MINMAX, (uint64_t)c->N.n);
     }
-    if (dyn) {
+    if (cls) {
+      const int cls_F = c->cls_slot(spec);
+      c->ev_begin(&ea);
+      launch_cls_place(c->N, c->P, c->cfg, spec, cls_F, (int)c->aff_slot_D[cls_F] + 1, (int)t, run, c->keys, c->stat,
+                       c->cls_lvl, c->cls_amax, c->cls_coff[cls_F], c->cls_mem[cls_F], js, first, job->ready_num,
+                       job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr, c->stream);
+      c->ev_end(ea, KB_KERNEL_CLS_PLACE, 0);
+      c->stats.cls_runs++;
+    } else if (dyn) {
       c->ev_begin(&ea);
       if (c->use_aff_reg && c->spec_aff_reg[spec] && aff_reg_fits(c->N.n, c->spec_aff_reg[spec]) &&
           !((size_t)spec < c->ov_slot.size() && c->ov_slot[spec] >= 0))
@@ -974,6 +1111,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                          job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream);
       c->ev_end(ea, KB_KERNEL_AFF_PLACE, 0);
     } else if (sel) {  // level-0 keys of every node, then the run as one top-T selection
+      if (aff && c->spec_dyn[spec]) c->stats.cap1_runs++;
       uint32_t* kt = c->sel_keys[si];
       uint64_t* st = c->sel_stat[si];
       // A job that is one run without inter-pod terms lists the rows it commits. When the previous job
@@ -1022,7 +1160,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                         c->stream);
       c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     }
-    if (aff && !dyn && c->spec_incr[spec])  // this run's commits update other specs' affinity tables
+    if (aff && (!dyn || cls) && c->spec_incr[spec])  // this run's commits update the affinity tables
       launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, c->stream);
     t = e;
   }
@@ -1065,7 +1203,7 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
     for (size_t k = S.ev_b; k < S.ev_e && k < c->pending.size(); ++k) {
       auto& p = c->pending[k];
       if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE ||
-          p.kind == KB_KERNEL_SEL_PLACE) {
+          p.kind == KB_KERNEL_SEL_PLACE || p.kind == KB_KERNEL_CLS_PLACE) {
         p.pairs = tasks * (uint64_t)c->N.n;
         tasks = 0;
       }
@@ -1109,7 +1247,7 @@ int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
   if (!c->use_sel || !c->sel_ok || !c->traj || job->n_tasks == 0) return 0;
   const int s0 = job->task_specs[0];
   if (s0 < 0 || s0 >= c->P.m || !c->spec_traj_ok[s0]) return 0;
-  if (c->aff_ok && c->spec_needs_aff[s0] && c->spec_dyn[s0]) return 0;
+  if (c->aff_ok && c->spec_needs_aff[s0] && c->spec_dyn[s0] && !c->cap1(s0) && !cls_run_ok(c, s0)) return 0;
   return 1;
 }
 

@@ -107,9 +107,10 @@ class kb_cycle_result(C.Structure):
 
 
 class kb_stats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 14), ("kernel_ms", C.c_double * 14), ("pairs", C.c_uint64 * 14),
+    _fields_ = [("launches", C.c_uint64 * 15), ("kernel_ms", C.c_double * 15), ("pairs", C.c_uint64 * 15),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8),
-                ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64)]
+                ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64),
+                ("cap1_runs", C.c_uint64), ("cls_runs", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -118,7 +119,7 @@ KB_OPT_NO_SELECT = 4
 KB_OPT_ENGINE = 8
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
-           "shard_propose_kernel", "shard_exchange", "shard_commit_kernel", "fed_engine_kernel")
+           "shard_propose_kernel", "shard_exchange", "shard_commit_kernel", "fed_engine_kernel", "cls_place_kernel")
 # device paths for a run of same-spec tasks (kb_place_job picks the first one that applies):
 #   select     - per-job launches of the level-0 sweep + the top-T selection kernel (default)
 #   engine     - the same selection served by one persistent workgroup (no launches; single-CU sweep)
@@ -127,7 +128,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 8  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 9  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -319,7 +320,8 @@ class Context:
         self._check(self.lib.kb_get_stats(self.ctx, C.byref(st), int(reset)))
         return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
                 "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag),
-                "fed_abandon": st.fed_abandon, "fed_cycles": st.fed_cycles, "fed_split": st.fed_split}
+                "fed_abandon": st.fed_abandon, "fed_cycles": st.fed_cycles, "fed_split": st.fed_split,
+                "cap1_runs": st.cap1_runs, "cls_runs": st.cls_runs}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
@@ -548,13 +550,16 @@ def host_reason_strings(snap: E.Snapshot, out: dict, job: int, task: int) -> dic
     return hist
 
 
-def allocate(cluster, device: int = 0, path: str = "select") -> dict:
-    """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle."""
+def allocate(cluster, device: int = 0, path: str = "select", stats_out: dict | None = None) -> dict:
+    """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle
+    (stats_out: filled with the context's kb_get_stats counters)."""
     snap = E.Snapshot(cluster)
     ctx = Context(device, path=path)
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)
+        if stats_out is not None:
+            stats_out.update(ctx.stats())
         return result_dict(snap, out)
     finally:
         ctx.close()

@@ -199,6 +199,71 @@ def affinity_edge_cluster(seed=11, n_nodes=40):
     return cl
 
 
+def self_affinity_cluster(seed=5, n_nodes=45, tight=False):
+    """Jobs whose own commits move their inter-pod affinity inputs, shaped for the cap-1 selection runs and
+    the class loop (kbgpu_host.cpp classify_self_dynamic): required anti-affinity to their own job on
+    hostname (one Allocate per node; Pipelined tasks do not join the lister, so nodes with only Releasing
+    room take several), preferred affinity to their own job on rack (+ zone: two moving histograms, racks
+    nested in zones), preferred anti-affinity to their own job on zone (negative counts), noisy pods that a
+    running pod's preferred anti-affinity scores down per zone (a static histogram beside the moving one),
+    nodes without a rack label (the class of nodes without a domain), a job whose own label a running pod
+    already carries (a static anti-affinity failure), and a job that fits nowhere (NO_FIT in the loop).
+    tight: small nodes with pods being deleted, so commits go Pipelined onto Releasing capacity."""
+    import random
+    rng = random.Random(seed)
+    cl = m.Cluster(tiers=m.default_tiers())
+    n_racks = 9
+    cpu = 6000 if tight else 24000
+    for i in range(n_nodes):
+        rack = i * n_racks // n_nodes
+        labels = {"kubernetes.io/hostname": f"n{i:02d}"}
+        if i % 9 == 4:
+            labels["zone"] = "z9"  # the rack-less nodes share a zone of their own (zone stays a function of rack)
+        else:
+            labels["rack"] = f"r{rack}"
+            labels["zone"] = f"z{rack // 3}"
+        cl.nodes.append(m.Node(name=f"n{i:02d}", alloc={m.CPU: cpu + 2000 * (i % 3), m.MEMORY: 64 * GI,
+                                                          m.PODS: 30}, labels=labels))
+    cl.queues.append(m.Queue(name="q", weight=1))
+    own = lambda job, key: dict({"labelSelector": {"matchLabels": {"job": job}}}, topologyKey=key)
+    # running pods: one noisy-averse (preferred anti-affinity per zone), some being deleted (Releasing room)
+    cl.pod_groups.append(m.PodGroup(ns="ns", name="run", queue="q", min_member=1, phase="Running"))
+    for t in range(12):
+        node = rng.randrange(n_nodes)
+        aff = None
+        if t == 0:
+            aff = {"podAntiAffinity": {"preferred": [{"weight": 10, "podAffinityTerm": dict(
+                {"labelSelector": {"matchLabels": {"noisy": "true"}}}, topologyKey="zone")}]}}
+        labels = {"app": "run"}
+        if t == 1:
+            labels["job"] = "spread-b"  # spread-b's own anti-affinity already fails on this node
+        cl.pods.append(m.Pod(ns="ns", name=f"run-{t}", uid=f"ns-run-{t}", group="run", node=f"n{node:02d}",
+                             phase="Running", deleting=tight and t % 2 == 1, labels=labels, affinity=aff,
+                             containers=[m.Container(req={m.CPU: 3000 if tight else 1000, m.MEMORY: 2 * GI})]))
+    pending = [
+        ("spread-a", 14, 14, {}, {"podAntiAffinity": {"required": [own("spread-a", "kubernetes.io/hostname")]}}),
+        ("pack-a", 16, 16, {}, {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": own("pack-a", "rack")}]}}),
+        ("spread-b", 10, 1, {}, {"podAntiAffinity": {"required": [own("spread-b", "kubernetes.io/hostname")]}}),
+        ("pack-noisy", 12, 12, {"noisy": "true"},
+         {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": own("pack-noisy", "rack")}]}}),
+        ("zone-spread", 12, 12, {}, {"podAntiAffinity": {"preferred": [
+            {"weight": 40, "podAffinityTerm": own("zone-spread", "zone")}]}}),
+        ("pack-two", 14, 7, {}, {"podAffinity": {"preferred": [
+            {"weight": 10, "podAffinityTerm": own("pack-two", "rack")},
+            {"weight": 5, "podAffinityTerm": own("pack-two", "zone")}]}}),
+        ("pack-huge", 3, 3, {}, {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": own("pack-huge", "rack")}]}}),
+        ("spread-c", 60, 60, {}, {"podAntiAffinity": {"required": [own("spread-c", "kubernetes.io/hostname")]}}),
+    ]
+    for name, n, minm, extra, aff in pending:
+        cl.pod_groups.append(m.PodGroup(ns="ns", name=name, queue="q", min_member=minm))
+        cpu_req = 40000 if name == "pack-huge" else (1000 + 500 * (len(name) % 3))
+        for t in range(n):
+            cl.pods.append(m.Pod(ns="ns", name=f"{name}-{t:02d}", uid=f"ns-{name}-{t:02d}", group=name,
+                                 labels=dict({"job": name}, **extra), affinity=aff,
+                                 containers=[m.Container(req={m.CPU: cpu_req, m.MEMORY: 2 * GI})]))
+    return cl
+
+
 def affinity_clusters():
     """(name, cluster) pairs with inter-pod (anti)affinity for parity tests."""
     return [
@@ -208,6 +273,8 @@ def affinity_clusters():
                               pre_job_size=20, seed=22)),
         ("aff-edge", affinity_edge_cluster()),
         ("aff-edge-b", affinity_edge_cluster(seed=12, n_nodes=25)),
+        ("self-aff", self_affinity_cluster()),
+        ("self-aff-tight", self_affinity_cluster(seed=6, n_nodes=30, tight=True)),
     ]
 
 

@@ -240,17 +240,28 @@ def test_driver_pipeline_parity(name, cluster, mode, monkeypatch):
     _compare(ref, got)
 
 
-@pytest.mark.parametrize("reg", [True, False], ids=["aff-reg", "aff-global"])
+AFF_VARIANTS = {"default": {}, "aff-reg": {"KB_NO_CAP1": "1", "KB_NO_CLS": "1"},
+                "aff-global": {"KB_NO_CAP1": "1", "KB_NO_CLS": "1", "KB_NO_AFF_REG": "1"}}
+
+
+@pytest.mark.parametrize("variant", sorted(AFF_VARIANTS))
 @pytest.mark.parametrize("name,cluster", affinity_clusters(), ids=[c[0] for c in affinity_clusters()])
-def test_affinity_loop_variants(name, cluster, reg, monkeypatch):
-    """Specs whose own commits move their inter-pod affinity inputs: the register-resident loop
-    (aff_reg_kernel, the default when n <= 10240) and the global-memory loop (aff_place_kernel) both match
-    the oracle."""
-    if not reg:
-        monkeypatch.setenv("KB_NO_AFF_REG", "1")
+def test_affinity_loop_variants(name, cluster, variant, monkeypatch):
+    """Specs whose own commits move their inter-pod affinity inputs. default: cap-1 specs (required
+    anti-affinity to their own pods over hostname) as selection runs and histogram-only specs on the class
+    loop (cls_place_kernel), the rest on the register-resident loop; aff-reg: every such spec on the
+    register-resident loop (aff_reg_kernel); aff-global: the global-memory loop (aff_place_kernel). All
+    match the oracle."""
+    for k, v in AFF_VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
     ref = pyoracle.allocate(cluster)
-    got = runtime.allocate(cluster)
+    ctx_stats = {}
+    got = runtime.allocate(cluster, stats_out=ctx_stats)
     _compare(ref, got)
+    if name.startswith("self-aff") or name == "C4-parity":
+        # the clusters built for them do reach the new paths (or, with them off, none of them)
+        on = variant == "default"
+        assert (ctx_stats["cap1_runs"] > 0) == on and (ctx_stats["cls_runs"] > 0) == on, ctx_stats
 
 
 def test_fed_engine_survives_a_host_stall(monkeypatch):
