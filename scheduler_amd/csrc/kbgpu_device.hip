@@ -4195,10 +4195,30 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
   // the class member lists (static per topology slot: built at kb_upload_affinity) into LDS
   for (int c = tid; c <= K; c += kClsThreads) coff[c] = coff_g[c];
   for (int c = tid; c < K; c += kClsThreads) cbest[c] = 0;
-  for (int j = tid; j < n; j += kClsThreads) {
-    mem[j] = mem_g[j];
-    lv16[j] = 0;
+  {  // the member list in 16-byte loads, all of a thread's in flight at once (mem_g is padded to 8 entries)
+    const uint4* mg = (const uint4*)mem_g;
+    const int nv = (n + 7) / 8;
+    constexpr int kV = 8;
+    for (int v0 = 0; v0 < nv; v0 += kV * kClsThreads) {
+      uint4 x[kV];
+#pragma unroll
+      for (int q = 0; q < kV; ++q) {
+        const int v = v0 + q * kClsThreads + tid;
+        x[q] = v < nv ? mg[v] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < kV; ++q) {
+        const int v = v0 + q * kClsThreads + tid;
+        if (v < nv) {
+          const uint32_t w4[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+          for (int h = 0; h < 8; ++h)
+            if (8 * v + h < n) mem[8 * v + h] = (uint16_t)(w4[h >> 1] >> (16 * (h & 1)));
+        }
+      }
+    }
   }
+  for (int j = tid; j < n; j += kClsThreads) lv16[j] = 0;
   __syncthreads();
   // base keys into LDS and each class's best: every thread a contiguous stretch of the member list, a
   // running max per class, flushed at class boundaries (atomics only where stretches share a class)
@@ -4347,6 +4367,8 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         }
       mn = wave_min_i64_dpp(mn);
       mx = wave_max_i64_dpp(mx);
+    }
+    if (ipa && KQ > 2) {
       // ipa_score is monotone in the count: its 10 breakpoints, exactly (as in aff_reg_kernel): a_s =
       // ceil(s * b / 10) is the first offset with 10 a / b >= s; the float64 formula falls short of s only
       // where 10 a / b == s exactly, and then a_s + 1 is it. Lane s - 1 computes a_s.
@@ -4371,10 +4393,15 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       const int c = q * 64 + lane;
       uint64_t k = c < K ? cbest[c] : 0;
       if ((k & kFeasible) && ipa) {
-        const int64_t off = cq[q] - mn;
-        int32_t sc = 0;  // == ipa_score(cq[q], mn, mx)
+        int32_t sc;
+        if (KQ > 2) {  // == ipa_score(cq[q], mn, mx) by the breakpoints
+          const int64_t off = cq[q] - mn;
+          sc = 0;
 #pragma unroll
-        for (int s = 0; s < 10; ++s) sc += off >= bp[s];
+          for (int s = 0; s < 10; ++s) sc += off >= bp[s];
+        } else {  // a division per class is cheaper than the breakpoints for a few classes per lane
+          sc = ipa_score(cq[q], mn, mx);
+        }
         k += (uint64_t)((int64_t)sc * c_wpa) << 24;
       }
       kq[q] = k;

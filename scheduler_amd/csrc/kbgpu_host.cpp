@@ -560,7 +560,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
     if (F < 0 || c->cls_coff[F] || n >= 65536) continue;
     const size_t K = (size_t)D[F] + 1;
     std::vector<uint32_t> off(K + 1, 0);
-    std::vector<uint16_t> mem(n);
+    std::vector<uint16_t> mem((n + 7) / 8 * 8, 0);  // padded: the kernel reads it in 16-byte loads
     auto cls_of = [&](size_t i) { const int32_t d = a->topo_dom[F * n + i]; return d >= 0 ? (size_t)d : K - 1; };
     for (size_t i = 0; i < n; ++i) ++off[cls_of(i) + 1];
     for (size_t k = 0; k < K; ++k) off[k + 1] += off[k];
@@ -568,7 +568,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
     for (size_t i = 0; i < n; ++i) mem[cur[cls_of(i)]++] = (uint16_t)i;
     int rc_;
     if ((rc_ = upload(c, c->aff_mem, &c->cls_coff[F], off.data(), K + 1))) return rc_;
-    if ((rc_ = upload(c, c->aff_mem, &c->cls_mem[F], mem.data(), n))) return rc_;
+    if ((rc_ = upload(c, c->aff_mem, &c->cls_mem[F], mem.data(), mem.size()))) return rc_;
   }
   if (a->m) HIP_OK(c, hipMemcpy(c->P.specs, specs.data(), a->m * sizeof(kb_spec), hipMemcpyHostToDevice));
   DevAff& A = c->P.A;
