@@ -207,8 +207,13 @@ def main():
                   "source": f"{per_job['source']}: sel_place_kernel per job (KB_NO_FED pass) x {jobs:.0f} jobs"}
     elif c2_default:
         tr = pmc_traffic(runtime.KERNELS[k])
+    elif (args.nodes, args.jobs, args.tasks_per_job) == (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
+        tr = pmc_traffic(runtime.KERNELS[k], args.config)  # that configuration's own committed PMC pass
+    roofline["measured_frac"] = None  # measured HBM bytes per launch / the launch time / peak
     if tr is not None:
         roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
+        if avg_ms > 0:
+            roofline["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
 
     workload = cfg["workload"]
     if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
@@ -367,11 +372,17 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, config=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md HBM section), or None when no summary for it is committed."""
+    MI355X_MICROARCH.md HBM section), or None when no summary for it is committed. config: a non-headline
+    configuration's own summaries (profiles/*_<config>_prof_summary.json); None: the C2 headline's."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*prof_summary.json")), reverse=True):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*prof_summary.json")), reverse=True)
+    if config is None:
+        files = [f for f in files if not any(f.endswith(f"_{c}_prof_summary.json") for c in CONFIGS)]
+    else:
+        files = [f for f in files if f.endswith(f"_{config}_prof_summary.json")]
+    for f in files:
         try:
             with open(f) as fh:
                 e = json.load(fh)["kernels"].get(kernel, {})
