@@ -111,12 +111,17 @@ def main():
     # replicas: each rank an independent cluster partition (different seed per rank); shard: one cluster
     seed = synth.SEED + (0 if shard else rank)
     cl = None
-    if args.config in ARRAY_CONFIGS:
+    e0 = time.perf_counter()
+    if args.config in ARRAY_CONFIGS:  # the numpy session builder (equal to the exporter: test_export.py)
         snap = synth.c2_snapshot(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=seed)
+        export_kind = "synth.c2_snapshot (numpy arrays)"
     else:
         cl = synth.CONFIGS[args.config](n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job,
                                         seed=seed)
+        e0 = time.perf_counter()
         snap = export.Snapshot(cl)
+        export_kind = "export.Snapshot (Python, per pod)"
+    export_ms = (time.perf_counter() - e0) * 1e3
     ctx = runtime.Context(device, timing=not args.no_timing, timing_every=args.timing_every, path=args.path)
     if shard:
         ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
@@ -235,6 +240,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "p50_cycle_ms": round(statistics.median(times), 3),
             **({"upload_ms": round(statistics.median(up), 3),
                 "p50_cycle_with_upload_ms": round(statistics.median(times) + statistics.median(up), 3)} if up else {}),
+            # session open: building the exported snapshot from the cluster objects (the Go shim's
+            # exportSnapshot twin) + its upload; the reference's counterpart is cache.Snapshot + OnSessionOpen
+            "session_open": {"export_ms": round(export_ms, 1), "export": export_kind,
+                             "upload_ms": round(statistics.median(up), 3) if up else None},
             "higher_is_better": True, "scaling": "strong" if shard else "weak", "vs_baseline": None,
             "dtype": "int64", "data": f"synthetic (seeded {args.config} generator, SURVEY.md §8 d2)",
             "config": {"workload": workload,

@@ -12,6 +12,7 @@ The device never sees a string; node index = position in name order.
 """
 from __future__ import annotations
 
+import functools
 import re
 
 import numpy as np
@@ -168,6 +169,7 @@ def new_requirement_error(key: str, op: str, vals) -> str | None:
     return None
 
 
+@functools.lru_cache(maxsize=4096)
 def is_scalar_resource_name(n: str) -> bool:  # core/v1/helper/helpers.go:36-104
     prefixed_native = "kubernetes.io/" in n
     native = "/" not in n or prefixed_native
@@ -216,6 +218,16 @@ class Res:
 
     def copy(self):
         return Res(self.cpu, self.mem, None if self.sc is None else dict(self.sc), self.max_task)
+
+    @classmethod
+    def of_request(cls, rl, memo):
+        """from_list for a request that is only read (container requests): one Res per distinct request in
+        `memo` (a session-open dict), so pods built from one template parse their quantities once."""
+        key = tuple(rl.items())
+        r = memo.get(key)
+        if r is None:
+            r = memo[key] = cls.from_list(rl)
+        return r
 
     def add(self, rr):  # Add (:131-143)
         self.cpu += rr.cpu
@@ -333,13 +345,14 @@ class Snapshot:
         node_pods = {n: [] for n in names}
         # tasks
         self.tasks = []
+        memo = {}
         for p in cl.pods:
             resreq = Res()
             for c in p.containers:
-                resreq.add(Res.from_list(c.req))
+                resreq.add(Res.of_request(c.req, memo))
             initreq = resreq.copy()
             for c in p.init:
-                initreq.set_max(Res.from_list(c.req))
+                initreq.set_max(Res.of_request(c.req, memo))
             t = {"pod": p, "uid": p.uid, "status": task_status(p), "resreq": resreq, "initreq": initreq,
                  "priority": p.priority if p.priority is not None else 1,
                  "job": f"{p.ns}/{p.group}" if p.group else ""}
@@ -463,6 +476,14 @@ class Snapshot:
         terms, reqs, vals, ports = [], [], [], []
         specs, sc_init, sc_req = [], [], []
         sig_index = {}
+        reprs = {}  # repr of a pod's affinity sub-dicts, by object (pods of one template share them)
+
+        def rp(x):
+            k = id(x)
+            v = reprs.get(k)
+            if v is None:
+                v = reprs[k] = (x, repr(x))  # keeps x alive: its id is not reused during the export
+            return v[1]
 
         def req_rows(exprs, allow_gtlt=True):
             """NodeSelectorRequirementsAsSelector (helpers.go:222-254) -> requirement rows, None if invalid."""
@@ -519,11 +540,11 @@ class Snapshot:
             best_effort = not any(M.CPU in c.req or M.MEMORY in c.req for c in list(p.containers) + list(p.init))
             sig = (ir.cpu, ir.mem, tuple(sorted((ir.sc or {}).items())) if ir.sc is not None else None,
                    rr.cpu, rr.mem, tuple(sorted((rr.sc or {}).items())) if rr.sc is not None else None,
-                   nzc, nzm, tuple(sorted(p.node_selector.items())), repr(nodeaff), tols, tuple(port_list),
+                   nzc, nzm, tuple(sorted(p.node_selector.items())), rp(nodeaff), tols, tuple(port_list),
                    best_effort)
             if self.aff_in_play:  # selectors and terms see the pod's namespace, labels and own terms
-                sig = sig + (p.ns, tuple(sorted(p.labels.items())), repr(aff.get("podAffinity")),
-                             repr(aff.get("podAntiAffinity")))
+                sig = sig + (p.ns, tuple(sorted(p.labels.items())), rp(aff.get("podAffinity")),
+                             rp(aff.get("podAntiAffinity")))
             if sig in sig_index:
                 t["spec"] = sig_index[sig]
                 continue
