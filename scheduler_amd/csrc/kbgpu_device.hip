@@ -4141,7 +4141,7 @@ __device__ __forceinline__ uint64_t cls_key_deep(const DevNodes& N, const DevSpe
 
 template <int KQ>
 __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
-    DevNodes N, DevSpecs P, DevCfg C, int spec, int K, int t_begin, int t_count, const uint64_t* bkg,
+    DevNodes N, DevSpecs P, DevCfg C, int spec, int F, int K, int t_begin, int t_count, const uint64_t* bkg,
     const uint64_t* stat, const uint64_t* lvl, const int32_t* amax, const uint32_t* coff_g, const uint16_t* mem_g,
     JobState* js, int first,
     int ready0, int minav0,
@@ -4290,6 +4290,8 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
   // (register arrays: every index a constant after unrolling, so nothing goes to scratch)
   int32_t u_e[kClsU], u_w[kClsU];
   int nu = 0;
+  int wsign = 0;       // 1: every own increment > 0, -1: every one < 0, else 2
+  bool only_f = true;  // every own increment is on the class slot itself: a commit updates its class only
 #pragma unroll
   for (int v = 0; v < kClsU; ++v) u_e[v] = -1, u_w[v] = 0;
   for (uint32_t i = 0; i < as.incr_cnt && nu < kClsU; ++i) {
@@ -4300,9 +4302,15 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #pragma unroll
         for (int v = 0; v < kClsU; ++v)
           if (v == nu) u_e[v] = e, u_w[v] = u.weight;
+        const int sg = u.weight > 0 ? 1 : (u.weight < 0 ? -1 : 2);
+        wsign = nu == 0 ? sg : (wsign == sg ? wsign : 2);
+        only_f = only_f && e_slot[e] == F;
         ++nu;
       }
   }
+  // Incremental min / max (interpod_affinity.go:221-238 over the classes): when every own increment has one
+  // sign, a commit moves counts one way only, so the new max (weights > 0; the min stays 0 if it was) or
+  // the new min (weights < 0) is the old one against the updated classes alone; otherwise a full pass.
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
   int ready = first ? ready0 : js->ready_num;
   int minav = first ? minav0 : js->min_available;
@@ -4353,12 +4361,14 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     }
   };
   AFF_STAMP(0);
+  int64_t mn = 0, mx = 0;
+  bool mm_ok = false;  // mn / mx hold the current min / max
   for (int t = 0; t < t_count; ++t) {
-    int64_t mn = 0, mx = 0;
     int64_t bp[10];
 #pragma unroll
     for (int q = 0; q < 10; ++q) bp[q] = INT64_MAX;
-    if (ipa) {
+    if (ipa && !mm_ok) {
+      mn = 0, mx = 0;
 #pragma unroll
       for (int q = 0; q < KQ; ++q)
         if (live[q]) {
@@ -4367,6 +4377,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         }
       mn = wave_min_i64_dpp(mn);
       mx = wave_max_i64_dpp(mx);
+      mm_ok = true;
     }
     if (ipa && KQ > 2) {
       // ipa_score is monotone in the count: its 10 breakpoints, exactly (as in aff_reg_kernel): a_s =
@@ -4513,6 +4524,9 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       }
     }
     // the classes in the committed node's domains: this commit's increments of the spec's own histograms
+    bool upd[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) upd[q] = false;
 #pragma unroll
     for (int u = 0; u < kClsU; ++u) {
       if (u >= nu) break;
@@ -4522,7 +4536,39 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
         const int c = q * 64 + lane;
-        if (c < K && cdom[e * K + c] == d) cq[q] += u_w[u];
+        if (c < K && cdom[e * K + c] == d) {
+          cq[q] += u_w[u];
+          upd[q] = true;
+        }
+      }
+    }
+    if (ipa) {
+      if (wsign == 1 && mn == 0) {  // counts only grew: the min stays 0, the max is the old one or an updated one
+        int64_t um = INT64_MIN;
+        if (only_f) {
+#pragma unroll
+          for (int q = 0; q < KQ; ++q)
+            if (q == (cw >> 6)) {
+              const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)cq[q], cw & 63);
+              const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)cq[q] >> 32), cw & 63);
+              um = (int64_t)(((uint64_t)hi << 32) | lo);
+            }
+        } else {
+#pragma unroll
+          for (int q = 0; q < KQ; ++q)
+            if (upd[q]) um = cq[q] > um ? cq[q] : um;
+          um = wave_max_i64_dpp(um);
+        }
+        mx = um > mx ? um : mx;
+      } else if (wsign == -1 && mx == 0) {  // counts only fell: the max stays 0
+        int64_t um = INT64_MAX;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+          if (upd[q]) um = cq[q] < um ? cq[q] : um;
+        um = wave_min_i64_dpp(um);
+        mn = um < mn ? um : mn;
+      } else {
+        mm_ok = false;
       }
     }
     wave_sync_lds();
@@ -4573,7 +4619,8 @@ void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   if ((size_t)pb_cap > cap_max) pb_cap = (int)cap_max;
   const size_t bytes = cls_lds_bytes(N.n, K, pb_cap);
 #define KB_CLS_Q(Q)                                                                                              \
-  hipLaunchKernelGGL(cls_place_kernel<Q>, dim3(1), dim3(kClsThreads), bytes, (hipStream_t)stream, N, P, C, spec, K, \
+  hipLaunchKernelGGL(cls_place_kernel<Q>, dim3(1), dim3(kClsThreads), bytes, (hipStream_t)stream, N, P, C, spec, F, \
+                     K, \
                      t_begin, t_count, bk, stat, lvl, amax, coff, mem, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, \
                      seq, g)
   const int q = (K + 63) / 64;
