@@ -199,7 +199,7 @@ def affinity_edge_cluster(seed=11, n_nodes=40):
     return cl
 
 
-def self_affinity_cluster(seed=5, n_nodes=45, tight=False):
+def self_affinity_cluster(seed=5, n_nodes=45, tight=False, n_racks=9):
     """Jobs whose own commits move their inter-pod affinity inputs, shaped for the cap-1 selection runs and
     the class loop (kbgpu_host.cpp classify_self_dynamic): required anti-affinity to their own job on
     hostname (one Allocate per node; Pipelined tasks do not join the lister, so nodes with only Releasing
@@ -208,11 +208,11 @@ def self_affinity_cluster(seed=5, n_nodes=45, tight=False):
     running pod's preferred anti-affinity scores down per zone (a static histogram beside the moving one),
     nodes without a rack label (the class of nodes without a domain), a job whose own label a running pod
     already carries (a static anti-affinity failure), and a job that fits nowhere (NO_FIT in the loop).
-    tight: small nodes with pods being deleted, so commits go Pipelined onto Releasing capacity."""
+    tight: small nodes with pods being deleted, so commits go Pipelined onto Releasing capacity. n_racks > 128:
+    more classes than two per lane (the class loop's breakpoint scores)."""
     import random
     rng = random.Random(seed)
     cl = m.Cluster(tiers=m.default_tiers())
-    n_racks = 9
     cpu = 6000 if tight else 24000
     for i in range(n_nodes):
         rack = i * n_racks // n_nodes
@@ -275,6 +275,7 @@ def affinity_clusters():
         ("aff-edge-b", affinity_edge_cluster(seed=12, n_nodes=25)),
         ("self-aff", self_affinity_cluster()),
         ("self-aff-tight", self_affinity_cluster(seed=6, n_nodes=30, tight=True)),
+        ("self-aff-racks", self_affinity_cluster(seed=8, n_nodes=420, n_racks=210)),
     ]
 
 
