@@ -2768,6 +2768,16 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
 #endif
     __syncthreads();
     KB_SSTAMP(4);
+    // the candidates' rows and static cache, loaded before the ranking so that their latency hides behind it
+    // (final: job m-1 touches only its set)
+    Row rw{};
+    uint64_t stw = 0;
+    int wn = 0;
+    if (tid < (int)cnt) {
+      wn = sh.node[tid];
+      rw = load_row(N, wn);
+      stw = stat[wn];
+    }
     {  // rank by key (4 threads per candidate), then each candidate's entry at its rank
       const int e = tid >> 2, part = tid & 3;
       const uint32_t k = e < (int)cnt ? sh.key0[e] : 0u;
@@ -2783,11 +2793,9 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     __syncthreads();
     if (tid < (int)cnt) {
-      const int w = sh.node[tid];
-      const Row rw = load_row(N, w);  // final: job m-1 touches only its set
       uint64_t* ent = X->s_ent[r][sh.lmax[tid]];
-      x_store64(&ent[0], (uint64_t)sh.key0[tid] | ((uint64_t)(uint32_t)w << 32));
-      x_store64(&ent[1], stat[w]);
+      x_store64(&ent[0], (uint64_t)sh.key0[tid] | ((uint64_t)(uint32_t)wn << 32));
+      x_store64(&ent[1], stw);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
