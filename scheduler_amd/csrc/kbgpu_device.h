@@ -242,10 +242,11 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
-                          ShardRec* rec, void* stream);
+                          ShardRec* rec, SpecGuard g, void* stream);
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
-                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g,
+                         void* stream);
 
 constexpr int kBitonicMin = 2048;  // == the sort's LDS tile
 // kb_sort_nodes: the spec's keys (PredicateFn + PrioritizeNodes) sorted descending into keys[0..n_pad), n_pad a

@@ -2299,10 +2299,13 @@ static_assert(kShardSegMax == kSegMax, "ShardRec holds one segment");
 __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec,
                                                                     int t_count, int idx_bits,
                                                                     const uint32_t* keys32, const uint64_t* stat,
-                                                                    const JobState* js, int first, ShardRec* rec) {
+                                                                    const JobState* js, int first, ShardRec* rec,
+                                                                    SpecGuard g) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
-  if (!first && js->stopped) return;  // the segment's commit kernel skips too
+  // the segment's commit kernel skips too (every rank sees the same job state: the exchange still runs, and
+  // its content is not read)
+  if ((!first && js->stopped) || guard_fails(g)) return;
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2338,14 +2341,19 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
                                                                    int t_begin, int t_count, int idx_bits,
                                                                    const ShardRec* recs, int world, JobState* js,
                                                                    int first, int ready0, int minav0, int gang0,
-                                                                   int32_t* hout, JobState* hjs, uint32_t seq) {
+                                                                   int32_t* hout, JobState* hjs, uint32_t seq,
+                                                                   SpecGuard g) {
   __shared__ ShardRec r[kShardMaxWorld];
   __shared__ uint64_t ord[128];
   __shared__ int32_t ordnk[128];
   __shared__ int32_t fin[128], fin_node[128];
   __shared__ int32_t s_cut, s_kind, s_alloc;
   __shared__ LoopOut lo;
-  if (!first && js->stopped) {
+  if ((!first && js->stopped) || guard_fails(g)) {
+    if (threadIdx.x == 0 && first) {  // a skipped speculative job (see sel_place_kernel)
+      js->stopped = 1;
+      js->n_placed = -1;
+    }
     signal_skip(hjs, seq);
     return;
   }
@@ -2477,16 +2485,17 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
 
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
-                          ShardRec* rec, void* stream) {
+                          ShardRec* rec, SpecGuard g, void* stream) {
   hipLaunchKernelGGL(shard_propose_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P,
-                     C, spec, t_count, idx_bits, keys32, stat, js, first, rec);
+                     C, spec, t_count, idx_bits, keys32, stat, js, first, rec, g);
 }
 
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
-                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream) {
+                         int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g,
+                         void* stream) {
   hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(kSelThreads), 0, (hipStream_t)stream, N, P, C, spec, t_begin,
-                     t_count, idx_bits, recs, world, js, first, ready0, minav0, gang0, hout, hjs, seq);
+                     t_count, idx_bits, recs, world, js, first, ready0, minav0, gang0, hout, hjs, seq, g);
 }
 
 int sel_lds_bytes(int n) {

@@ -874,22 +874,25 @@ int kb_set_shard_rccl(kb_ctx* c, const kb_shard* sh, const uint8_t id[KB_COMM_ID
 }
 
 // One job on a node-sharded table: per run segment, sweep + local proposal, one all-gather, merge + commit.
-static int shard_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t* placed_kind,
-                           kb_job_result* result) {
+// Node-sharded job: per run segment, the sweep and this rank's proposal, the all-gather (RCCL on the library
+// stream, or host-staged through the callback), the global merge + commit. Issued into job slot `si` like
+// place_issue (`g` guards a speculative job's first segment: every rank sees the same previous job, so every
+// rank skips alike, and the all-gather still runs); the host-staged exchange waits for the proposal here.
+static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard& g) {
   if (!c->sel_ok || !c->traj) return fail(c, KB_E_UNSUPPORTED, "sharded table does not fit the selection path");
   for (uint32_t i = 0; i < job->n_tasks; ++i) {
     const int s = job->task_specs[i];
     if (!c->spec_traj_ok[s] || c->spec_needs_aff[s])
       return fail(c, KB_E_UNSUPPORTED, "spec %d needs a path that does not run sharded", s);
   }
-  if (int rc = ensure_job_buffers(c, job->n_tasks)) return rc;
-  auto t0 = std::chrono::steady_clock::now();
-  c->pending_job_begin = c->pending.size();
-  c->timing_now = c->timing && (c->stats.job_calls % c->timing_every == 0);
-  memset(((JobState*)c->h_job)->diag, 0, sizeof(((JobState*)c->h_job)->diag));
-  JobState* js = (JobState*)c->d_job;
-  JobState* hjs_dev = (JobState*)c->h_job_dev;
-  int32_t* hout_dev = (int32_t*)(c->h_job_dev + sizeof(JobState));
+  kb_ctx::JobSlot& S = c->slot[si];
+  S.t_issue = std::chrono::steady_clock::now();
+  S.ev_b = c->pending.size();
+  c->timing_now = c->timing && (c->issue_count++ % c->timing_every == 0);
+  memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
+  JobState* js = (JobState*)S.d;
+  JobState* hjs_dev = (JobState*)S.hdev;
+  int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
   const size_t rb = sizeof(ShardRec);
   for (uint32_t t = 0; t < job->n_tasks;) {
     uint32_t e = t + 1;
@@ -898,13 +901,14 @@ static int shard_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_nod
     for (uint32_t seg = t; seg < e; seg += kShardSegMax) {
       const int T = (int)std::min<uint32_t>(kShardSegMax, e - seg);
       const int first = seg == 0;
+      const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
       hipEvent_t ea;
       c->ev_begin(&ea);
       launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, false,
-                       c->stream);
+                       c->stream, gr);
       c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
       c->ev_begin(&ea);
-      launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, c->traj, c->stat, js, first, c->d_rec,
+      launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, c->traj, c->stat, js, first, c->d_rec, gr,
                            c->stream);
       c->ev_end(ea, KB_KERNEL_SHARD_PROPOSE, 0);
       c->ev_begin(&ea);
@@ -922,41 +926,19 @@ static int shard_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_nod
       c->ev_end(ea, KB_KERNEL_SHARD_EXCHANGE, 0);
       c->ev_begin(&ea);
       launch_shard_commit(c->N, c->P, c->cfg, spec, (int)seg, T, c->idx_bits, c->d_rec_all, c->shard.world, js,
-                          first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq,
+                          first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr,
                           c->stream);
       c->ev_end(ea, KB_KERNEL_SHARD_COMMIT, 0);
     }
     t = e;
   }
   HIP_OK(c, hipGetLastError());
-  if (int rc = wait_seq(c)) return rc;
-  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  c->device_ms += wall;
-  c->stats.device_ms += wall;
-  c->stats.job_calls += 1;
-  const JobState* hs = (const JobState*)c->h_job;
-  if (c->timing) {
-    uint64_t tasks = (uint64_t)hs->n_placed + (hs->stop == KB_STOP_NO_FIT ? 1 : 0);
-    for (size_t k = c->pending_job_begin; k < c->pending.size(); ++k) {
-      auto& p = c->pending[k];
-      if (p.kind == KB_KERNEL_SHARD_PROPOSE) {
-        p.pairs = tasks * (uint64_t)c->N.n;
-        tasks = 0;
-      }
-    }
-    c->ev_collect(false);
-  }
-  const int32_t* ho = (const int32_t*)(c->h_job + sizeof(JobState));
-  result->n_placed = (uint32_t)hs->n_placed;
-  result->stop = hs->stop;
-  result->fail_task = hs->fail_task;
-  if (hs->stop == KB_STOP_NO_FIT)
-    for (int b = 0; b < KB_NUM_REASONS; ++b) result->reason_hist[b] = hs->hist[b];
-  for (int i = 0; i < hs->n_placed; ++i) {
-    if (placed_node) placed_node[i] = ho[2 * i];
-    if (placed_kind) placed_kind[i] = ho[2 * i + 1];
-  }
-  if (hs->panic) return fail(c, KB_E_PANIC, "SelectBestNode: no node scored above -1 (task %d)", hs->fail_task);
+  c->prev_listed = false;
+  c->prev_slot = si;
+  S.seq = c->seq;
+  S.ev_e = c->pending.size();
+  S.busy = true;
+  S.issue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S.t_issue).count();
   return KB_OK;
 }
 
@@ -1203,7 +1185,7 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
     for (size_t k = S.ev_b; k < S.ev_e && k < c->pending.size(); ++k) {
       auto& p = c->pending[k];
       if (p.kind == KB_KERNEL_PLACE || p.kind == KB_KERNEL_TRAJ_PLACE || p.kind == KB_KERNEL_AFF_PLACE ||
-          p.kind == KB_KERNEL_SEL_PLACE || p.kind == KB_KERNEL_CLS_PLACE) {
+          p.kind == KB_KERNEL_SEL_PLACE || p.kind == KB_KERNEL_CLS_PLACE || p.kind == KB_KERNEL_SHARD_PROPOSE) {
         p.pairs = tasks * (uint64_t)c->N.n;
         tasks = 0;
       }
@@ -1232,7 +1214,12 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   if (int rc = validate_job(c, job)) return rc;
   if (job->n_tasks == 0) return KB_OK;
   c->prev_listed = false;
-  if (c->sharded) return shard_place_job(c, job, placed_node, placed_kind, result);
+  if (c->sharded) {
+    if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
+    if (int rc = ensure_slots(c, job->n_tasks, false)) return rc;
+    if (int rc = shard_issue(c, job, 0, SpecGuard{nullptr, 0, 0, 0})) return rc;
+    return place_finish(c, 0, placed_node, placed_kind, result, false);
+  }
   if (engine_ok(c, job)) return engine_place_job(c, job, placed_node, placed_kind, result);
   if (int rc = kb_engine_stop(c)) return rc;
   if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
@@ -1241,13 +1228,15 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
   return place_finish(c, 0, placed_node, placed_kind, result, false);
 }
 
-int kb_job_pipeline_ok(kb_ctx* c) { return c && !c->sharded && !c->use_engine && !c->broken; }
+// Sharded contexts pipeline with the RCCL exchange only (a host-staged exchange waits for the proposal).
+int kb_job_pipeline_ok(kb_ctx* c) { return c && (!c->sharded || c->comm) && !c->use_engine && !c->broken; }
 
 int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
   if (!c->use_sel || !c->sel_ok || !c->traj || job->n_tasks == 0) return 0;
   const int s0 = job->task_specs[0];
   if (s0 < 0 || s0 >= c->P.m || !c->spec_traj_ok[s0]) return 0;
   if (c->aff_ok && c->spec_needs_aff[s0] && c->spec_dyn[s0] && !c->cap1(s0) && !cls_run_ok(c, s0)) return 0;
+  if (c->sharded && c->spec_needs_aff[s0]) return 0;  // (refused by shard_issue anyway)
   return 1;
 }
 
@@ -1414,7 +1403,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     if (!kb_job_guardable(c, job)) return fail(c, KB_E_INVALID, "job cannot be issued speculatively");
     g = SpecGuard{(const JobState*)c->slot[pred->prev_slot].d, pred->stop, pred->placed, pred->ready};
   }
-  return place_issue(c, job, slot, g);
+  return c->sharded ? shard_issue(c, job, slot, g) : place_issue(c, job, slot, g);
 }
 
 int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kind, kb_job_result* result,

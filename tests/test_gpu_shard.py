@@ -129,6 +129,30 @@ def test_rccl_exchange_one_rank():
     assert got == ref
 
 
+@pytest.mark.parametrize("frac", [1.0, 0.5, 0.34])
+def test_rccl_pipelined_matches_oracle(frac):
+    """A sharded context with the RCCL exchange runs kb_allocate pipelined (job k+1 issued, guarded on job k's
+    predicted outcome, before job k is read). minMember below the job size makes jobs stop READY mid-way, so
+    predictions fail and guarded sharded jobs skip (sweep, proposal and commit no-ops; the exchange still runs).
+    One-rank communicator; placements, statuses and FitErrors equal the oracle's."""
+    from oracle import pyoracle
+    cl = synth.c2(n_nodes=160, n_jobs=36, tasks_per_job=20, seed=41)
+    for pg in cl.pod_groups:
+        pg.min_member = max(1, int(pg.min_member * frac))
+    ref = pyoracle.allocate(cl)
+    snap = E.Snapshot(cl)
+    ctx = runtime.Context(0)
+    try:
+        ctx.set_shard(0, 1, snap.n_nodes, rccl_id=runtime.comm_unique_id())
+        ctx.upload(snap)
+        got = runtime.result_dict(snap, ctx.allocate(snap))
+    finally:
+        ctx.close()
+    assert got["events"] == ref["events"]
+    assert got["binds"] == ref["binds"]
+    assert got["fit_errors"] == ref["fit_errors"]
+
+
 def _c5_rank(rank, world, port, q):
     import torch.distributed as dist
     import torch
