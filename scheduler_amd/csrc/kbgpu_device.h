@@ -242,11 +242,13 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
-                          ShardRec* rec, SpecGuard g, void* stream);
+                          ShardRec* rec, SpecGuard g, const int32_t* patch, const JobState* patch_js,
+                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream);
+// commit_out (single-segment jobs): the rank's rows this job committed, for the next job's overlapped sweep
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
                          int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g,
-                         void* stream);
+                         int32_t* commit_out, void* stream);
 
 constexpr int kBitonicMin = 2048;  // == the sort's LDS tile
 // kb_sort_nodes: the spec's keys (PredicateFn + PrioritizeNodes) sorted descending into keys[0..n_pad), n_pad a

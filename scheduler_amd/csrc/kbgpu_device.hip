@@ -2300,7 +2300,9 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
                                                                     int t_count, int idx_bits,
                                                                     const uint32_t* keys32, const uint64_t* stat,
                                                                     const JobState* js, int first, ShardRec* rec,
-                                                                    SpecGuard g) {
+                                                                    SpecGuard g, const int32_t* patch,
+                                                                    const JobState* patch_js, const uint32_t* wait_ctr,
+                                                                    uint32_t wait_target, JobState* hjs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   // the segment's commit kernel skips too (every rank sees the same job state: the exchange still runs, and
@@ -2313,7 +2315,35 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   const kb_spec sp = P.specs[spec];
+  // overlapped sweep (as sel_place_kernel): the previous job's committed rows of this rank load first, then
+  // the wait for this job's sweep on the other stream, then those rows are re-keyed from their stored state
+  const int np = patch != nullptr ? patch_js->n_commit : 0;
+  const int pw = tid < np ? patch[tid] : -1;
+  Row prow;
+  if (pw >= 0) prow = load_row(N, pw);
+  if (wait_ctr != nullptr) {
+    if (tid == 0) {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(wait_ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - wait_target > 0x7fffffffu) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == (1u << 26)) {
+          hjs->stall = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const uint64_t pst = pw >= 0 ? stat[pw] : 0;
   load_keys_lds(k32, keys32, n, n_pad);
+  if (patch != nullptr) {
+    __syncthreads();
+    const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+    if (pw >= 0) {
+      const uint32_t rs = row_reasons(N, P, C, sp, sci, prow, pst, pw);
+      k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
+    }
+  }
   int ready = 0, placed = 0, stop = 0, fail_task = -1, panic = 0, stopped = 0, rp = 0;
 #ifdef KB_DIAG
   uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -2342,17 +2372,18 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
                                                                    const ShardRec* recs, int world, JobState* js,
                                                                    int first, int ready0, int minav0, int gang0,
                                                                    int32_t* hout, JobState* hjs, uint32_t seq,
-                                                                   SpecGuard g) {
+                                                                   SpecGuard g, int32_t* commit_out) {
   __shared__ ShardRec r[kShardMaxWorld];
   __shared__ uint64_t ord[128];
   __shared__ int32_t ordnk[128];
   __shared__ int32_t fin[128], fin_node[128];
-  __shared__ int32_t s_cut, s_kind, s_alloc;
+  __shared__ int32_t s_cut, s_kind, s_alloc, s_ncommit;
   __shared__ LoopOut lo;
   if ((!first && js->stopped) || guard_fails(g)) {
     if (threadIdx.x == 0 && first) {  // a skipped speculative job (see sel_place_kernel)
       js->stopped = 1;
       js->n_placed = -1;
+      js->n_commit = 0;
     }
     signal_skip(hjs, seq);
     return;
@@ -2368,6 +2399,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
     const int words = world * (int)(sizeof(ShardRec) / 16);
     for (int i = tid; i < words; i += kSelThreads) dst[i] = src[i];
   }
+  if (tid == 0) s_ncommit = 0;
   if (tid < 128) fin[tid] = 0;
   const int ready_in = first ? ready0 : js->ready_num;
   const int minav = first ? minav0 : js->min_available;
@@ -2453,6 +2485,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
     const int w = fin_node[tid];
     const Row row = load_row(N, w);
     store_back_row(N, P, sp, scr, w, fin[tid], allocs_before_full(N, sp, sci, scr, row, w), row);
+    if (commit_out != nullptr) commit_out[atomicAdd(&s_ncommit, 1)] = w;  // for the next job's overlapped sweep
   }
   int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
   if (kind == 3) {
@@ -2478,6 +2511,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
+    if (commit_out != nullptr) js->n_commit = s_ncommit;
     __threadfence_system();
     publish_state(js, hjs, lo.stopped, lo.stop, lo.fail_task, lo.placed, lo.ready, lo.minav, lo.gang, lo.panic, seq);
   }
@@ -2485,17 +2519,19 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
 
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
-                          ShardRec* rec, SpecGuard g, void* stream) {
+                          ShardRec* rec, SpecGuard g, const int32_t* patch, const JobState* patch_js,
+                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream) {
   hipLaunchKernelGGL(shard_propose_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P,
-                     C, spec, t_count, idx_bits, keys32, stat, js, first, rec, g);
+                     C, spec, t_count, idx_bits, keys32, stat, js, first, rec, g, patch, patch_js, wait_ctr,
+                     wait_target, hjs);
 }
 
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,
                          int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g,
-                         void* stream) {
+                         int32_t* commit_out, void* stream) {
   hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(kSelThreads), 0, (hipStream_t)stream, N, P, C, spec, t_begin,
-                     t_count, idx_bits, recs, world, js, first, ready0, minav0, gang0, hout, hjs, seq, g);
+                     t_count, idx_bits, recs, world, js, first, ready0, minav0, gang0, hout, hjs, seq, g, commit_out);
 }
 
 int sel_lds_bytes(int n) {

@@ -894,22 +894,39 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
   JobState* hjs_dev = (JobState*)S.hdev;
   int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
   const size_t rb = sizeof(ShardRec);
+  bool listed = false;
   for (uint32_t t = 0; t < job->n_tasks;) {
     uint32_t e = t + 1;
     while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
     const int spec = job->task_specs[t];
+    // a job of one single-segment run lists the rows it commits; when the previous job (the other slot) did,
+    // this job's sweep runs on stream_b beside that job's kernels and the proposal re-keys those rows (as the
+    // one-GPU selection path does, place_issue)
+    const bool one_run = t == 0 && e == job->n_tasks && e - t <= (uint32_t)kShardSegMax;
+    const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1);
+    uint32_t* kt = one_run ? c->sel_keys[si] : c->traj;
+    uint64_t* st = one_run ? c->sel_stat[si] : c->stat;
     for (uint32_t seg = t; seg < e; seg += kShardSegMax) {
       const int T = (int)std::min<uint32_t>(kShardSegMax, e - seg);
       const int first = seg == 0;
       const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
       hipEvent_t ea;
+      if (ov) {
+        c->ev_begin(&ea, c->stream_b);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, false, c->stream_b,
+                         SpecGuard{nullptr, 0, 0, 0}, c->sweep_ctr + si);
+        c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
+        c->sweep_target[si] += (uint32_t)((c->N.n + 63) / 64);
+        c->n_overlap++;
+      } else {
+        c->ev_begin(&ea);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, false, c->stream, gr);
+        c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
+      }
       c->ev_begin(&ea);
-      launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, c->traj, c->stat, first ? nullptr : js, false,
-                       c->stream, gr);
-      c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
-      c->ev_begin(&ea);
-      launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, c->traj, c->stat, js, first, c->d_rec, gr,
-                           c->stream);
+      launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, kt, st, js, first, c->d_rec, gr,
+                           ov ? c->commits[si ^ 1] : nullptr, ov ? (const JobState*)c->slot[si ^ 1].d : nullptr,
+                           ov ? c->sweep_ctr + si : nullptr, c->sweep_target[si], hjs_dev, c->stream);
       c->ev_end(ea, KB_KERNEL_SHARD_PROPOSE, 0);
       c->ev_begin(&ea);
       if (c->comm) {
@@ -927,13 +944,14 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
       c->ev_begin(&ea);
       launch_shard_commit(c->N, c->P, c->cfg, spec, (int)seg, T, c->idx_bits, c->d_rec_all, c->shard.world, js,
                           first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr,
-                          c->stream);
+                          one_run ? c->commits[si] : nullptr, c->stream);
       c->ev_end(ea, KB_KERNEL_SHARD_COMMIT, 0);
     }
+    listed = one_run;
     t = e;
   }
   HIP_OK(c, hipGetLastError());
-  c->prev_listed = false;
+  c->prev_listed = listed;
   c->prev_slot = si;
   S.seq = c->seq;
   S.ev_e = c->pending.size();
