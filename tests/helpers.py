@@ -253,10 +253,12 @@ def self_affinity_cluster(seed=5, n_nodes=45, tight=False, n_racks=9):
             {"weight": 5, "podAffinityTerm": own("pack-two", "zone")}]}}),
         ("pack-huge", 3, 3, {}, {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": own("pack-huge", "rack")}]}}),
         ("spread-c", 60, 60, {}, {"podAntiAffinity": {"required": [own("spread-c", "kubernetes.io/hostname")]}}),
+        # small pods packing one rack: a node takes more than the class loop's 8 precomputed levels
+        ("pack-deep", 60, 60, {}, {"podAffinity": {"preferred": [{"weight": 50, "podAffinityTerm": own("pack-deep", "rack")}]}}),
     ]
     for name, n, minm, extra, aff in pending:
         cl.pod_groups.append(m.PodGroup(ns="ns", name=name, queue="q", min_member=minm))
-        cpu_req = 40000 if name == "pack-huge" else (1000 + 500 * (len(name) % 3))
+        cpu_req = 40000 if name == "pack-huge" else (100 if name == "pack-deep" else 1000 + 500 * (len(name) % 3))
         for t in range(n):
             cl.pods.append(m.Pod(ns="ns", name=f"{name}-{t:02d}", uid=f"ns-{name}-{t:02d}", group=name,
                                  labels=dict({"job": name}, **extra), affinity=aff,
