@@ -4339,6 +4339,15 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     live[q] = c < K && coff[c + 1] > coff[c];
     cq[q] = c < K ? cnt[c] : 0;
   }
+  // each histogram's domain of the lane's classes, in registers (a commit compares them with the winner's)
+  int32_t cd[kClsE][KQ];
+#pragma unroll
+  for (int e = 0; e < kClsE; ++e)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const int c = q * 64 + lane;
+      cd[e][q] = e < ne && c < K ? cdom[e * K + c] : -1;
+    }
   // the spec's increments of its own histograms (entry, weight); the others go to the global tables only
   // (register arrays: every index a constant after unrolling, so nothing goes to scratch)
   int32_t u_e[kClsU], u_w[kClsU];
@@ -4360,6 +4369,17 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         only_f = only_f && e_slot[e] == F;
         ++nu;
       }
+  }
+  // the spec's own increments summed per histogram (a commit adds them to the classes sharing the winner's
+  // domain in that histogram; integer sums, so the order of the increments does not matter)
+  int32_t e_w[kClsE];
+  bool e_has[kClsE];
+#pragma unroll
+  for (int e = 0; e < kClsE; ++e) {
+    e_w[e] = 0, e_has[e] = false;
+#pragma unroll
+    for (int v = 0; v < kClsU; ++v)
+      if (v < nu && u_e[v] == e) e_w[e] += u_w[v], e_has[e] = true;
   }
   // Incremental min / max (interpod_affinity.go:221-238 over the classes): when every own increment has one
   // sign, a commit moves counts one way only, so the new max (weights > 0; the min stays 0 if it was) or
@@ -4385,6 +4405,8 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     if (hot < 0 || hot_c == 0) return;
     if (lane == 0) {
       const int64_t ac = hot_c < hot_A ? hot_c : hot_A, pc = hot_c - ac;
+      // read before the atomics: a load issued after them would wait for them too (in-order vmcnt)
+      const uint32_t fl = sp.req_sc_mask ? N.flags[hot] : 0u;
       if (ac) {
         atomicAdd((unsigned long long*)&N.idle_cpu[hot], (unsigned long long)(-ac * sp.req_cpu));
         atomicAdd((unsigned long long*)&N.idle_mem[hot], (unsigned long long)(-ac * sp.req_mem));
@@ -4396,7 +4418,6 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       atomicAdd(&N.pod_count[hot], hot_c);
       atomicAdd((unsigned long long*)&N.nz_cpu[hot], (unsigned long long)((int64_t)hot_c * sp.nz_cpu));
       atomicAdd((unsigned long long*)&N.nz_mem[hot], (unsigned long long)((int64_t)hot_c * sp.nz_mem));
-      const uint32_t fl = N.flags[hot];
       uint64_t m = sp.req_sc_mask;
       while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
         const int q = __builtin_ctzll(m);
@@ -4515,20 +4536,29 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     // hot one past its keys) first.
     if (w != hot || hot_c == hot_lim) {
       const bool same = w == hot;
-      flush_hot();
-      wave_sync_lds();
+      // lv16[w] before the flush: the flush writes the old hot node's entry (w's own only when same)
       const int l0 = same ? hot_n + hot_c : (int)lv16[w];
-      hot = w, hot_c = 0, hot_n = l0;
       if (l0 < kClsL) {  // the sweep's level keys (lane j: level l0 + j + 1)
+        // the new node's loads go out before the old node's atomics, so waiting for them does not wait
+        // for the atomics
+        uint64_t nhk;
+        int nA;
         if (w == p_node) {
-          hk = pk, hot_A = p_A;
+          nhk = pk, nA = p_A;
         } else {
-          hk = l0 + lane < kClsL ? lvl[(size_t)(l0 + lane) * n + w] : 0;
+          nhk = l0 + lane < kClsL ? lvl[(size_t)(l0 + lane) * n + w] : 0;
           const int a0 = amax[w];
-          hot_A = a0 > l0 ? a0 - l0 : 0;
+          nA = a0 > l0 ? a0 - l0 : 0;
         }
+        flush_hot();
+        wave_sync_lds();
+        hot = w, hot_c = 0, hot_n = l0;
+        hk = nhk, hot_A = nA;
         hot_lim = kClsL - l0;
       } else {  // deeper than the sweep went: from the row as it stands (this run's deltas applied)
+        flush_hot();
+        wave_sync_lds();
+        hot = w, hot_c = 0, hot_n = l0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
         Row r;
         r.flags = N.flags[w];
@@ -4581,19 +4611,19 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #pragma unroll
     for (int q = 0; q < KQ; ++q) upd[q] = false;
 #pragma unroll
-    for (int u = 0; u < kClsU; ++u) {
-      if (u >= nu) break;
-      const int e = u_e[u];
-      const int32_t d = cdom[e * K + cw];
+    for (int e = 0; e < kClsE; ++e) {
+      if (!e_has[e]) continue;
+      int32_t d = -1;  // the winner's domain: lane cw % 64 of register q = cw / 64
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        if (q == (cw >> 6)) d = (int32_t)__builtin_amdgcn_readlane((uint32_t)cd[e][q], cw & 63);
       if (d < 0) continue;
 #pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        const int c = q * 64 + lane;
-        if (c < K && cdom[e * K + c] == d) {
-          cq[q] += u_w[u];
+      for (int q = 0; q < KQ; ++q)
+        if (cd[e][q] == d) {  // -1 (no class / no domain) never equals d >= 0
+          cq[q] += e_w[e];
           upd[q] = true;
         }
-      }
     }
     if (ipa) {
       if (wsign == 1 && mn == 0) {  // counts only grew: the min stays 0, the max is the old one or an updated one
