@@ -428,7 +428,8 @@ int kb_read_nodes(kb_ctx* ctx, int64_t* idle_cpu, int64_t* idle_mem, int64_t* re
  * (scheduler_helper.go:74-78). Scores must be integral (every in-tree node-order fn is) and
  * |NodeAffinity * weight + score_add| < 2^26. Either array may be NULL; both NULL clears the overlay.
  * The overlay stays until replaced: a plugin whose answer depends on this cycle's commits is re-set by
- * the caller between kb_place_job calls (device layer). n = this context's node rows.
+ * the caller between kb_place_job calls (device layer). n = this context's node rows. KB_E_UNSUPPORTED on a
+ * node-sharded context (the verdicts and the NO_FIT hook's masks would be rank-local).
  */
 int kb_set_host_overlay(kb_ctx* ctx, int32_t spec, const uint8_t* fail, const int64_t* score_add);
 

@@ -621,7 +621,7 @@ struct Driver {
     if (pipe)
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
     // every job one selection run of an eligible spec: the fed engine serves the whole cycle
-    bool fed = pipe;
+    bool fed = pipe && kb_fed_cycle_ok(ctx, max_pending);
     std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
     for (uint32_t j = 0; fed && j < s.n_jobs; ++j) {
       int sp0 = -1;
@@ -657,10 +657,8 @@ struct Driver {
     // KB_HOST_TRACE=1: per-job host timings on stderr at the end of the cycle (speculative issue, wait in
     // finish, bookkeeping after it)
     const bool trace = getenv("KB_HOST_TRACE") != nullptr;
-    const char* stall_env = getenv("KB_TEST_STALL_JOB");  // tests: sleep KB_TEST_STALL_MS before finishing job k
-    const int64_t stall_job = stall_env ? atoll(stall_env) : -1;
-    const char* stall_ms_env = getenv("KB_TEST_STALL_MS");
-    const int stall_ms = stall_ms_env ? atoi(stall_ms_env) : 1500;
+    const int64_t stall_job = ctx->test_stall_job;  // tests (read once at kb_create): a host stall before job k
+    const int stall_ms = ctx->test_stall_ms;
     uint64_t n_iter_all = 0;
     const auto loop0 = std::chrono::steady_clock::now();
     double t_spec = 0, t_fin = 0, t_apply = 0;

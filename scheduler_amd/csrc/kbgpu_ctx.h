@@ -136,6 +136,15 @@ struct kb_ctx {
   int32_t* fed_exit = nullptr;
   void* fed_xchg = nullptr;   // split engine exchange (fed_xchg_bytes)
   bool use_fed_split = true;  // KB_NO_FED_SPLIT unset
+  // The resident engine waits for sweeps issued on stream_b: they must never queue behind it on one hardware queue.
+  // The engine is a cooperative launch (the device's own cooperative queue, every workgroup co-resident) and
+  // stream_b a CU-masked stream (a hardware queue of its own, never shared with other streams of the process).
+  // KB_FED_SHARED_QUEUES=1 (tests): plain launch and plain stream, the hazard these remove.
+  bool fed_dedicated = true;
+  // tests only (KB_TEST_STALL_JOB / KB_TEST_STALL_MS, read once at kb_create): kb_allocate's driver sleeps before
+  // finishing job test_stall_job, a host stall longer than the engine's idle bound
+  int64_t test_stall_job = -1;
+  int test_stall_ms = 1500;
   uint32_t fed_count[kbgpu::kJobSlots] = {};
   int fed_r = 0;
   uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)
@@ -193,6 +202,9 @@ extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, u
 // (kb_spec_fed_ok): kb_fed_begin after kb_job_reserve, then kb_job_issue / kb_job_finish as usual (each
 // issue launches only the job's sweep kernel), kb_fed_end before anything else runs on the context.
 extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, int spec);
+// the engine can serve a cycle whose jobs have at most max_job_tasks tasks (past one selector's key plan only the
+// split engine, whose jobs are one segment)
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks);
 // max_job_tasks: the most tasks any job of the cycle can place (the split engine takes one-segment jobs only)
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);

@@ -100,7 +100,8 @@ struct JobState {
   uint64_t t_recv, t_done;  // placement engine: s_memrealtime (100 MHz) at command receipt / completion
   uint32_t exit_seq;  // placement engine: the command it was waiting for when it exited idle (0: none)
   int32_t n_commit;   // selection place kernel: rows in its commit list (device copy only)
-  int32_t stall;      // host copy: 1 = the place kernel gave up waiting for its overlapped sweep
+  int32_t stall;      // host copy: 1 = the place kernel gave up waiting for its overlapped sweep; 2 = node-sharded
+                      //   ranks exchanged different segments (ShardRec::tag)
   uint32_t seq;       // host copy: sequence number of the last finished place launch (written last)
 };
 
@@ -120,7 +121,9 @@ struct ShardRec {
   int32_t pad1;
   uint64_t comp[kShardSegMax];     // pick-order composites (global node index inside)
   int32_t node_kind[kShardSegMax]; // global node | kind << 30
-  int32_t pad2[4];
+  // what the rank issued for this segment (launch sequence number, spec, segment start << 16 | tasks, guard
+  // prediction hash | skipped << 31): every rank must exchange the same tag, else the ranks diverged
+  uint32_t tag[4];
 };
 static_assert(sizeof(ShardRec) % 16 == 0, "ShardRec is exchanged as raw bytes");
 
@@ -234,16 +237,22 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 constexpr int kFedSplitMaxTasks = 100;  // one selection segment (kbgpu_device.hip kSegMax)
 size_t fed_xchg_bytes();
 bool fed_split_ok(int n);
-void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
-                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                       int32_t* exit_flag, void* xchg, void* stream);
+// selector workgroups of the split engine for n nodes (1: one holds every key; up to 4 node ranges past that;
+// 0: beyond the engine)
+int fed_nsel(int n);
+// coop: a cooperative launch (every workgroup co-resident, on the device's cooperative queue); returns the
+// launch's hipError_t.
+int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
+                      const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
                           ShardRec* rec, SpecGuard g, const int32_t* patch, const JobState* patch_js,
-                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream);
+                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream,
+                          const uint32_t* tag);
 // commit_out (single-segment jobs): the rank's rows this job committed, for the next job's overlapped sweep
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                          int idx_bits, const ShardRec* recs, int world, JobState* js, int first, int ready0,

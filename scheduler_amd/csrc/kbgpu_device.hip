@@ -2302,12 +2302,19 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
                                                                     const JobState* js, int first, ShardRec* rec,
                                                                     SpecGuard g, const int32_t* patch,
                                                                     const JobState* patch_js, const uint32_t* wait_ctr,
-                                                                    uint32_t wait_target, JobState* hjs) {
+                                                                    uint32_t wait_target, JobState* hjs, uint4 tag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   // the segment's commit kernel skips too (every rank sees the same job state: the exchange still runs, and
-  // its content is not read)
-  if ((!first && js->stopped) || guard_fails(g)) return;
+  // only its tag is read)
+  const bool skip = (!first && js->stopped) || guard_fails(g);
+  if (threadIdx.x == 0) {
+    rec->tag[0] = tag.x;
+    rec->tag[1] = tag.y;
+    rec->tag[2] = tag.z;
+    rec->tag[3] = tag.w | (skip ? 0x80000000u : 0u);
+  }
+  if (skip) return;
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2379,6 +2386,12 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
   __shared__ int32_t fin[128], fin_node[128];
   __shared__ int32_t s_cut, s_kind, s_alloc, s_ncommit;
   __shared__ LoopOut lo;
+  if (threadIdx.x == 0) {  // every rank exchanged the same segment (a divergence would otherwise hang later)
+    bool same = true;
+    for (int w = 1; w < world; ++w)
+      for (int q = 0; q < 4; ++q) same = same && recs[w].tag[q] == recs[0].tag[q];
+    if (!same) hjs->stall = 2;
+  }
   if ((!first && js->stopped) || guard_fails(g)) {
     if (threadIdx.x == 0 && first) {  // a skipped speculative job (see sel_place_kernel)
       js->stopped = 1;
@@ -2520,10 +2533,11 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
 void launch_shard_propose(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_count,
                           int idx_bits, const uint32_t* keys32, const uint64_t* stat, const JobState* js, int first,
                           ShardRec* rec, SpecGuard g, const int32_t* patch, const JobState* patch_js,
-                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream) {
+                          const uint32_t* wait_ctr, uint32_t wait_target, JobState* hjs, void* stream,
+                          const uint32_t* tag) {
   hipLaunchKernelGGL(shard_propose_kernel, dim3(1), dim3(kSelThreads), sel_lds_bytes(N.n), (hipStream_t)stream, N, P,
                      C, spec, t_count, idx_bits, keys32, stat, js, first, rec, g, patch, patch_js, wait_ctr,
-                     wait_target, hjs);
+                     wait_target, hjs, make_uint4(tag[0], tag[1], tag[2], tag[3]));
 }
 
 void launch_shard_commit(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
@@ -2642,15 +2656,23 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
 // the T best of the union are the T best overall, since job m-1 touches only S. A no-fit rebuilds every key
 // for the histogram. Cycles with a job of more than one segment do not use the split engine.
 constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
+// Past one workgroup's key plan (fed_fits), the node table is split into kFedMaxSel ranges at most, one selector
+// workgroup each (grid 1 + nsel): each publishes the T best of its range, and the placer merges the lists. Every
+// range is a multiple of 4 nodes (16-byte key loads) and holds at most kFedSelNodes keys.
+constexpr int kFedMaxSel = 4;
+constexpr int kFedSelQ = 10;                          // key groups per thread of a range selector
+constexpr int kFedSelNodes = 4 * kSelThreads * kFedSelQ;  // 20480
+__host__ __device__ __forceinline__ int fed_sel_chunk(int n, int nsel) { return ((n + nsel - 1) / nsel + 3) & ~3; }
 struct FedXchg {
   uint64_t p_head[kJobSlots];        // placer -> selector (tagged, job number + 1): mode << 16 | count
   uint64_t p_done[kJobSlots];        //   (tagged) the job's commit count, once its rows are written back
   uint64_t p_node[kJobSlots][128];   //   the job's selected set (tagged)
-  uint64_t s_head[kJobSlots];        // selector -> placer: (job number + 1) << 32 | candidates (kSelExit: EXIT),
-                                     //   stored once the entries below are drained
-  uint64_t s_cmd[kJobSlots][16];     //   the job's command (FedCmd), one tagged word per field
-  uint64_t s_ent[kJobSlots][128][2 + sizeof(Row) / 8];  //   candidates in key order (descending): key | node << 32,
-                                                        //   static cache, row
+  uint64_t s_head[kJobSlots][kFedMaxSel];  // selector k -> placer: (job number + 1) << 32 | candidates (selector
+                                           //   0: kSelExit on EXIT), stored once the entries below are drained
+  uint64_t s_cmd[kJobSlots][16];     //   (selector 0) the job's command (FedCmd), one tagged word per field
+  uint64_t s_ent[kJobSlots][kFedMaxSel][128][2 + sizeof(Row) / 8];  //   selector k's candidates in key order
+                                                                    //   (descending): key | node << 32, static
+                                                                    //   cache, row
   uint64_t sdiag[16];  // KB_DIAG builds: the selector's phase cycles, [8..] the placer's merge (KB_FED_DIAG)
 };
 
@@ -2669,19 +2691,20 @@ __device__ __forceinline__ bool fed_wait_word(const uint32_t* w, uint32_t want, 
   }
 }
 
-// Re-key the rows on two commit lists (n0 entries of l0, then n1 of l1) for `spec` into k32 (node positions).
-// Ends after a barrier.
+// Re-key the rows on two commit lists (n0 entries of l0, then n1 of l1) for `spec` into k32 (positions node - base;
+// nodes outside [base, base + nk) are another selector's). Ends after a barrier.
 __device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
                           int spec, const uint64_t* stat, int idx_bits, const int32_t* l0, int n0, const int32_t* l1,
-                          int n1) {
+                          int n1, int base, int nk) {
   const int np = n0 + n1;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = threadIdx.x; i < np; i += kSelThreads) {
     const int w = i < n0 ? l0[i] : l1[i - n0];
+    if ((uint32_t)(w - base) >= (uint32_t)nk) continue;
     const Row rr = load_row(N, w);
     const uint64_t st = stat[w];
     const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
-    k32[w] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+    k32[w - base] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
   }
   __syncthreads();
 }
@@ -2701,18 +2724,22 @@ __device__ __forceinline__ void fed_wait_cmd(const uint32_t* ctr, uint32_t tgt, 
   __syncthreads();
 }
 
-// The split engine's selector: the second workgroup of the engine's launch (one dispatch, so both are resident
-// together; separate kernels on separate streams are not guaranteed separate hardware queues).
+// The split engine's selector `sel` of nsel: a workgroup of the engine's launch after the placer (one dispatch, so
+// all are resident together; separate kernels on separate streams are not guaranteed separate hardware queues).
+// It serves the nodes [base, base + nk) of the table (all of them when nsel == 1).
 template <int QN>
 __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits,
                                              const FedSlots& S, const FedCmd* ring, const uint32_t* ctr,
                                              uint64_t idle_ticks, int32_t* exit_flag, FedXchg* X, uint32_t* k32,
-                                             SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_n1) {
+                                             SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_n1, int sel,
+                                             int nsel) {
   const int tid = threadIdx.x;
-  const int n = N.n;
+  const int chunk = fed_sel_chunk(N.n, nsel);
+  const int base = sel * chunk;
+  const int n = N.n - base < chunk ? N.n - base : chunk;  // this selector's nodes
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const int n_pad = 4 * kSelThreads * Q4;
-  const uint32_t blocks = (uint32_t)((n + 63) / 64);
+  const uint32_t blocks = (uint32_t)((N.n + 63) / 64);  // the sweep's blocks over the whole table
   uint32_t tgt[kJobSlots];
 #pragma unroll
   for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
@@ -2735,12 +2762,12 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
     KB_SSTAMP(0);
     if (s_op != KB_ENG_RUN) {
-      if (s_op == KB_ENG_EXIT && tid == 0)  // the placer takes EXIT from here
-        x_store64(&X->s_head[r], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
+      if (s_op == KB_ENG_EXIT && tid == 0 && sel == 0)  // the placer takes EXIT from here
+        x_store64(&X->s_head[r][0], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
       break;
     }
     const int slot = cm.slot, spec = cm.spec;
-    load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
+    load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot] + base, n, n_pad);
     __syncthreads();
     KB_SSTAMP(1);
     const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
@@ -2771,7 +2798,8 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     __syncthreads();
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
     // rows job m-2 committed (final), while job m-1 may still be choosing its set
-    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1, nullptr, 0);
+    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1, nullptr, 0,
+              base, n);
     KB_SSTAMP(3);
     if (tid == 0) {  // job m-1's set (published at its node setup)
       int n1 = 0;
@@ -2800,7 +2828,8 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       uint64_t e;
       do e = x_load64(&X->p_node[r1][tid]);
       while ((uint32_t)(e >> 32) != m);
-      k32[(uint32_t)e] = 0u;
+      const uint32_t w = (uint32_t)e - (uint32_t)base;
+      if (w < (uint32_t)n) k32[w] = 0u;
     }
     __syncthreads();
     KB_SSTAMP(2);
@@ -2819,7 +2848,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     uint64_t stw = 0;
     int wn = 0;
     if (tid < (int)cnt) {
-      wn = sh.node[tid];
+      wn = sh.node[tid] + base;
       rw = load_row(N, wn);
       stw = stat[wn];
     }
@@ -2838,20 +2867,20 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     __syncthreads();
     if (tid < (int)cnt) {
-      uint64_t* ent = X->s_ent[r][sh.lmax[tid]];
+      uint64_t* ent = X->s_ent[r][sel][sh.lmax[tid]];
       x_store64(&ent[0], (uint64_t)sh.key0[tid] | ((uint64_t)(uint32_t)wn << 32));
       x_store64(&ent[1], stw);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
       for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q], words[q]);
-    } else if (tid >= 256 && tid < 256 + 16) {  // the command, for the placer (tagged: it may prefetch it)
+    } else if (sel == 0 && tid >= 256 && tid < 256 + 16) {  // the command, for the placer (tagged: prefetched)
       tag_store(&X->s_cmd[r][tid - 256], m + 1, ((const uint32_t*)&cm)[tid - 256]);
     }
     // every wave's entry stores drained before the head (a barrier alone waits for LDS only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) x_store64(&X->s_head[r], ((uint64_t)(m + 1) << 32) | cnt);
+    if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | cnt);
     KB_SSTAMP(5);
 #ifdef KB_DIAG
     dg[6]++;
@@ -2861,7 +2890,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     __syncthreads();  // cm reused by the next command
   }
 #ifdef KB_DIAG
-  if (tid == 0)
+  if (tid == 0 && sel == 0)
     for (int k = 0; k < 7; ++k) X->sdiag[k] = dg[k];
 #endif
 #undef KB_SSTAMP
@@ -2883,13 +2912,60 @@ __device__ __forceinline__ Row row_after(const kb_spec& sp, const Row& r0, int c
   return r;
 }
 
-// SPLIT: grid 2, workgroup 0 the placer and 1 the selector (fed_selector); every job of the cycle one
-// segment (the host checks). Otherwise one workgroup with every node's key in LDS.
+// The no-fit FitErrors histogram (allocate.go:150-153, unschedule_info.go:57-79) of a table too large for the
+// placer's LDS: every node's key is the sweep's (keys, read from memory) unless its row changed since, on one of
+// the three commit lists; those are re-keyed. bits (LDS, n bits) marks them, so a node listed twice counts once
+// and the streamed pass skips it. Ends after a barrier with the histogram in sh.hist.
+__device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
+                                const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
+                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int n = N.n, nw = (n + 31) >> 5;
+  const int64_t* sci = P.sc_init + (size_t)spec * N.S;
+  for (int i = tid; i < nw; i += kSelThreads) bits[i] = 0u;
+  if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
+    const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : l2[i - n0 - n1]);
+    const uint32_t b = 1u << (w & 31);
+    if (atomicOr(&bits[w >> 5], b) & b) continue;  // listed twice: its row is the same final row
+    const uint32_t rs = row_reasons(N, P, C, sp, sci, load_row(N, w), stat[w], w);
+    for (uint32_t m = rs; m; m &= m - 1) atomicAdd(&sh.hist[__builtin_ctz(m)], 1u);
+  }
+  __syncthreads();
+  uint32_t h[KB_NUM_REASONS];
+#pragma unroll
+  for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] = 0;
+  for (int i0 = 0; i0 < n; i0 += 4 * kSelThreads) {
+    uint32_t k[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // the loads first: one memory latency per four keys
+      const int i = i0 + q * kSelThreads + tid;
+      k[q] = i < n ? keys[i] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + q * kSelThreads + tid;
+      if (i >= n || (k[q] >> 31) || ((bits[i >> 5] >> (i & 31)) & 1u)) continue;
+#pragma unroll
+      for (int b = 0; b < KB_NUM_REASONS; ++b) h[b] += (k[q] >> b) & 1u;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < KB_NUM_REASONS; ++b) {
+    const uint32_t v = wave_sum_u32(h[b]);
+    if (lane == 0 && v) atomicAdd(&sh.hist[b], v);
+  }
+  __syncthreads();
+}
+
+// SPLIT: grid 1 + nsel, workgroup 0 the placer and 1.. the selectors (fed_selector) of nsel node ranges; every
+// job of the cycle one segment (the host checks). Otherwise one workgroup with every node's key in LDS.
 template <int QN, bool SPLIT>
 __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
-                                                                 int32_t* exit_flag, FedXchg* X) {
+                                                                 int32_t* exit_flag, FedXchg* X, int nsel) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
@@ -2897,6 +2973,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   __shared__ int32_t bprev[128];  // split: the previous job's selected set, slot order
   __shared__ uint32_t bkey[128];  //   its keys for this job
   __shared__ int32_t s_feas;
+  __shared__ int32_t s_na[kFedMaxSel];  // split: the selectors' candidate counts for this job
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2904,8 +2981,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   if constexpr (SPLIT) {
-    if (blockIdx.x == 1) {
-      fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand);
+    if (blockIdx.x >= 1) {
+      fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
+                       (int)blockIdx.x - 1, nsel);
       return;
     }
   }
@@ -2922,9 +3000,11 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   int prev_slot[2] = {-1, -1}, prev_ncommit[2] = {0, 0};
   int nbprev = 0;
   int rp = 0;
-  uint64_t pre[17];  // split, thread 0: the next job's command words and head, loaded at this job's end
+  // split, thread 0: the next job's command words and selector 0's head, then the other selectors' heads, loaded
+  // at this job's end
+  uint64_t pre[16 + kFedMaxSel];
 #pragma unroll
-  for (int q = 0; q < 17; ++q) pre[q] = 0;
+  for (int q = 0; q < 16 + kFedMaxSel; ++q) pre[q] = 0;
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -2946,7 +3026,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         if (!have) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
-            h = x_load64(&X->s_head[r]);
+            h = x_load64(&X->s_head[r][0]);
             if ((uint32_t)(h >> 32) == m + 1) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
             __builtin_amdgcn_s_sleep(1);
@@ -2954,6 +3034,22 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         }
         if ((uint32_t)(h >> 32) == m + 1) {
           c = (int32_t)(uint32_t)h;
+          s_na[0] = c;
+#pragma unroll
+          for (int k = 1; k < kFedMaxSel; ++k) {  // the other selectors' lists of this job (unrolled: pre in VGPRs)
+            if (k >= nsel || c < 0) continue;
+            uint64_t hk = pre[16 + k];
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while ((uint32_t)(hk >> 32) != m + 1) {
+              if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                c = -2;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+              hk = x_load64(&X->s_head[r][k]);
+            }
+            s_na[k] = (int32_t)(uint32_t)hk;
+          }
           if (c >= 0) {
             uint32_t fields[16];
 #pragma unroll
@@ -2966,9 +3062,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           }
           // the sweep's static cache (another agent's release, which the selector has seen): fresh loads
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        } else {
-          *exit_flag = 1;
         }
+        if (c == -2) *exit_flag = 1;
         s_cand = c;
         s_op = c >= 0 ? KB_ENG_RUN : (c == kSelExit ? KB_ENG_EXIT : KB_ENG_EXIT_IDLE);
       }
@@ -3021,7 +3116,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       // candidates: A, the selector's T best outside the previous job's set (key order, with their static cache
       // and rows); B, that set re-keyed from the final rows kept in brow. Every rank below is a count over at
       // most 128 LDS entries split across 4 threads (unrolled), never a per-thread loop over all of them.
-      const int na = s_cand, nb = nbprev;
+      // lists: the selectors' (k < nsel, s_na[k] entries each, keys descending), then B (nb)
+      const int nb = nbprev;
       const uint32_t T = (uint32_t)cm.t_count;  // one segment
 #ifdef KB_DIAG
       uint64_t mt = __builtin_amdgcn_s_memtime();
@@ -3036,12 +3132,22 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   do {               \
   } while (0)
 #endif
-      Row* crow = brow + 128;                    // the candidates' rows by candidate index (A, then B)
-      uint64_t* cst = (uint64_t*)(crow + 256);   // and static caches
-      int32_t* cnd = (int32_t*)(cst + 256);      // and nodes
-      uint32_t* ak = sh.key0;                    // A's keys (descending), then the slots' keys
-      if (tid < na) {
-        const uint64_t* ent = X->s_ent[r][tid];
+      // the lists' keys (A_k at akey[128 k], descending); one selector: its rows and static caches beside the
+      // previous set's rows in the candidate space, else (up to 4 * 128 + 128 rows) in the key space, which a
+      // split placer does not otherwise use
+      uint32_t* akey = k32;
+      Row* crow = nsel == 1 ? brow + 128 : (Row*)(k32 + kFedMaxSel * 128);
+      uint64_t* cst = (uint64_t*)(crow + (nsel == 1 ? 256 : 128 * (kFedMaxSel + 1)));
+      int32_t* cnd = (int32_t*)(cst + 128 * (kFedMaxSel + 1));
+      int na = 0, list = -1, idx = 0;
+#pragma unroll
+      for (int k = 0; k < kFedMaxSel; ++k) {
+        const int c = k < nsel ? s_na[k] : 0;
+        if (tid >= na && tid < na + c) list = k, idx = tid - na;
+        na += c;
+      }
+      if (list >= 0) {
+        const uint64_t* ent = X->s_ent[r][list][idx];
         const uint64_t e0 = x_load64(&ent[0]);
         const uint64_t st = x_load64(&ent[1]);
         uint64_t words[sizeof(Row) / 8];
@@ -3050,9 +3156,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         __builtin_memcpy(&crow[tid], words, sizeof(Row));
         cst[tid] = st;
         cnd[tid] = (int)(e0 >> 32);
-        ak[tid] = (uint32_t)e0;
-      } else if (tid >= 128 && tid - 128 < nb) {
-        const int j = tid - 128, w = bprev[j];
+        akey[list * 128 + idx] = (uint32_t)e0;
+      } else if (tid >= na && tid - na < nb) {
+        const int j = tid - na, w = bprev[j];
         const Row rw = brow[j];
         const uint64_t st = stat[w];
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, w);
@@ -3084,40 +3190,46 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       }
       __syncthreads();
       KB_MSTAMP(1);
-      // rank in the union (keys carry the node: distinct), by binary search in the other sorted list
+      // rank in the union (keys carry the node: distinct): the own index plus, in every other list, the entries
+      // above the key (binary search)
       const int nc = na + nb;
       int pos = -1;
       uint32_t key = 0;
-      if (tid < nc) {
-        const bool in_a = tid < na;
-        key = in_a ? ak[tid] : bkey[tid - na];
-        const uint32_t* other = in_a ? sh.emin : ak;
-        int lo = 0, hi = in_a ? nb : na;  // entries of the other list above key
+      const auto count_gt = [](const uint32_t* l, int len, uint32_t v) {
+        int lo = 0, hi = len;
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
-          if (other[mid] > key) lo = mid + 1;
+          if (l[mid] > v) lo = mid + 1;
           else hi = mid;
         }
-        pos = (in_a ? tid : sh.A[tid - na]) + lo;
+        return lo;
+      };
+      if (tid < nc) {
+        const bool in_a = tid < na;
+        const int j = tid - na;
+        key = in_a ? akey[list * 128 + idx] : bkey[j];
+        pos = in_a ? idx + count_gt(sh.emin, nb, key) : sh.A[j];
+        for (int k = 0; k < nsel; ++k)
+          if (k != list) pos += count_gt(akey + k * 128, s_na[k], key);
       }
       // the T best feasible (A is all feasible; infeasible keys rank below every feasible one), slots in node
       // order: the winners' tie rule on equal score fields takes lower slots first, which must be lower nodes
-      const int nsel = min((int)T, na + s_feas);
-      const bool sel = pos >= 0 && pos < nsel;
+      const int nsel_t = min((int)T, na + s_feas);
+      const bool sel = pos >= 0 && pos < nsel_t;
       __syncthreads();  // the lists read
       if (sel) bprev[pos] = cnd[tid];  // scratch: the selected nodes by rank
-      if (tid >= nsel && tid < 128) bprev[tid] = 0x7fffffff;  // padding: above every node
+      if (tid >= nsel_t && tid < 128) bprev[tid] = 0x7fffffff;  // padding: above every node
       __syncthreads();
       KB_MSTAMP(2);
       {
         const int e = tid >> 2, part = tid & 3;
-        const int w = e < nsel ? bprev[e] : 0;
+        const int w = e < nsel_t ? bprev[e] : 0;
         uint32_t c = 0;
 #pragma unroll
         for (int q = 0; q < 32; ++q) c += bprev[part * 32 + q] < w;
         c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
         c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
-        if (part == 0 && e < nsel) sh.gen[e] = (int)c;  // scratch: slot of the rank-e node
+        if (part == 0 && e < nsel_t) sh.gen[e] = (int)c;  // scratch: slot of the rank-e node
       }
       __syncthreads();
       if (sel) {
@@ -3127,9 +3239,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         sh.row[slot_s] = crow[tid];
         sh.stat[slot_s] = cst[tid];
         sh.lmax[slot_s] = (int)T - pos;
-        if (pos == nsel - 1) sh.theta0 = key;
+        if (pos == nsel_t - 1) sh.theta0 = key;
       }
-      if (tid == 0) sh.n_sel = nsel;
+      if (tid == 0) sh.n_sel = nsel_t;
       __syncthreads();
       KB_MSTAMP(3);
 #undef KB_MSTAMP
@@ -3179,7 +3291,18 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         brow[tid] = row_after(sp, sh.row[tid], sh.fin[tid], sh.A[tid]);
       }
       nbprev = ns;
-      if (sh.need_hist) {  // no fit: every node's key at this point (the sweep's, then every row changed since)
+      if (sh.need_hist && nsel > 1) {  // no fit, the table past one key plan: the histogram streamed (below)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
+        __syncthreads();
+        const int32_t* l0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
+        const int32_t* l1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
+        fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, S.keys[slot], l0, prev_slot[0] >= 0 ? prev_ncommit[0] : 0,
+                        l1, prev_slot[1] >= 0 ? prev_ncommit[1] : 0, S.commits[slot], sh.n_commit);
+        if (tid < KB_NUM_REASONS) {
+          js->hist[tid] = sh.hist[tid];
+          hjs->hist[tid] = sh.hist[tid];
+        }
+      } else if (sh.need_hist) {  // no fit: every node's key at this point (the sweep's, then every row changed since)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
         __syncthreads();
         load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
@@ -3222,7 +3345,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       const int rn = r + 1 == kJobSlots ? 0 : r + 1;
 #pragma unroll
       for (int q = 0; q < 16; ++q) pre[q] = x_load64(&X->s_cmd[rn][q]);
-      pre[16] = x_load64(&X->s_head[rn]);
+#pragma unroll
+      for (int k = 0; k < kFedMaxSel; ++k) pre[16 + k] = k < nsel ? x_load64(&X->s_head[rn][k]) : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a barrier alone waits for LDS only)
     __syncthreads();
@@ -3270,12 +3394,20 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
 size_t fed_xchg_bytes() { return sizeof(FedXchg); }
+// Selector workgroups of the split engine for n nodes: one when every key fits one workgroup's plan, else the
+// fewest ranges of at most kFedSelNodes (kFedMaxSel at most); 0: the table is beyond the engine.
+int fed_nsel(int n) {
+  if (fed_fits(n) && sel_qn(n) > 0) return 1;  // (the run-time group count instance spills when split)
+  for (int k = 2; k <= kFedMaxSel; ++k)
+    if (fed_sel_chunk(n, k) <= kFedSelNodes) return k;
+  return 0;
+}
 // the placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096
-bool fed_split_ok(int n) { return fed_fits(n) && n > 4 * kSelThreads; }
+bool fed_split_ok(int n) { return fed_nsel(n) > 0 && n > 4 * kSelThreads; }
 
-void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
-                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                       int32_t* exit_flag, void* xchg, void* stream) {
+int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
+                      const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop) {
   FedSlots S;
   for (int s = 0; s < kJobSlots; ++s) {
     S.tgt[s] = tgt[s];
@@ -3286,17 +3418,21 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
     S.hjs[s] = sp.hjs[s];
     S.hout[s] = sp.hout[s];
   }
-  const int qn = sel_qn(N.n);
-  const int bytes = fed_lds_bytes(N.n);
+  // past one workgroup's key plan: nsel range selectors of kFedSelQ key groups each (split engine only)
+  int nsel = xchg ? fed_nsel(N.n) : 1;
+  const int qn = nsel > 1 ? kFedSelQ : sel_qn(N.n);
+  const int bytes = nsel > 1 ? 4 * (4 * kSelThreads * kFedSelQ) + 8 * kCandCap : fed_lds_bytes(N.n);
+  const FedCmd* ring_c = (const FedCmd*)ring;
+  FedXchg* X = (FedXchg*)xchg;
+  void* args[] = {(void*)&N, (void*)&P, (void*)&C, (void*)&idx_bits, (void*)&S, (void*)&ring_c, (void*)&ctr,
+                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel};
   // (no split instance for one key group: fed_split_ok needs n > 4 * kSelThreads)
-#define KB_FED_QN(Q)                                                                                              \
-  case Q:                                                                                                        \
-    if (xchg && Q != 1)                                                                                          \
-      hipLaunchKernelGGL((fed_engine_kernel<Q, Q != 1>), dim3(2), dim3(kSelThreads), bytes, (hipStream_t)stream, \
-                         N, P, C, idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag, (FedXchg*)xchg);   \
-    else                                                                                                         \
-      hipLaunchKernelGGL((fed_engine_kernel<Q, false>), dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream,   \
-                         N, P, C, idx_bits, S, (const FedCmd*)ring, ctr, idle_ticks, exit_flag, (FedXchg*)xchg);   \
+  const void* f = nullptr;
+  bool split = false;
+#define KB_FED_QN(Q)                                                               \
+  case Q:                                                                         \
+    split = xchg && Q != 1;                                                       \
+    f = split ? (const void*)fed_engine_kernel<Q, Q != 1> : (const void*)fed_engine_kernel<Q, false>; \
     break;
   switch (qn) {
     KB_FED_QN(1)
@@ -3311,6 +3447,10 @@ void launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
       KB_FED_QN(0)
   }
 #undef KB_FED_QN
+  if (!split) nsel = 1;
+  const dim3 grid(split ? 1 + nsel : 1), block(kSelThreads);
+  if (coop) return (int)hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)bytes, (hipStream_t)stream);
+  return (int)hipLaunchKernel(f, grid, block, args, (size_t)bytes, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -236,6 +236,9 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->use_cls = getenv("KB_NO_CLS") == nullptr;          // testing: class-loop specs on the re-sweep loops
   c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
   c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
+  c->fed_dedicated = getenv("KB_FED_SHARED_QUEUES") == nullptr;  // testing: the shared-queue hazard
+  if (const char* e = getenv("KB_TEST_STALL_JOB")) c->test_stall_job = atoll(e);
+  if (const char* e = getenv("KB_TEST_STALL_MS")) c->test_stall_ms = atoi(e);
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
@@ -923,10 +926,15 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
         launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, false, c->stream, gr);
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
       }
+      // the segment's identity, compared across ranks after the exchange (ShardRec::tag)
+      const uint32_t gh = gr.prev ? (uint32_t)(0x40000000u ^ ((uint32_t)gr.stop * 0x9e3779b1u) ^
+                                               ((uint32_t)gr.placed * 0x85ebca77u) ^ ((uint32_t)gr.ready * 0xc2b2ae3du))
+                                  : 0u;
+      const uint32_t tag[4] = {c->seq + 1, (uint32_t)spec, (seg << 16) | (uint32_t)T, gh & 0x7fffffffu};
       c->ev_begin(&ea);
       launch_shard_propose(c->N, c->P, c->cfg, spec, T, c->idx_bits, kt, st, js, first, c->d_rec, gr,
                            ov ? c->commits[si ^ 1] : nullptr, ov ? (const JobState*)c->slot[si ^ 1].d : nullptr,
-                           ov ? c->sweep_ctr + si : nullptr, c->sweep_target[si], hjs_dev, c->stream);
+                           ov ? c->sweep_ctr + si : nullptr, c->sweep_target[si], hjs_dev, c->stream, tag);
       c->ev_end(ea, KB_KERNEL_SHARD_PROPOSE, 0);
       c->ev_begin(&ea);
       if (c->comm) {
@@ -1004,7 +1012,16 @@ static int ensure_sel_bufs(kb_ctx* c) {
     HIP_OK(c, hipMalloc((void**)&c->sweep_ctr, 2 * sizeof(uint32_t)));
     HIP_OK(c, hipMemset(c->sweep_ctr, 0, 2 * sizeof(uint32_t)));
     c->sweep_target[0] = c->sweep_target[1] = 0;
-    HIP_OK(c, hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+    if (c->fed_dedicated) {  // a hardware queue of its own (kb_ctx::fed_dedicated): a mask of every CU
+      hipDeviceProp_t prop;
+      HIP_OK(c, hipGetDeviceProperties(&prop, c->device));
+      const int cus = std::max(prop.multiProcessorCount, 1);
+      std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+      HIP_OK(c, hipExtStreamCreateWithCUMask(&c->stream_b, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIP_OK(c, hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+    }
   }
   return KB_OK;
 }
@@ -1186,6 +1203,8 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
   // pipelined, so issue-to-finish walls would count the overlap twice)
   const double wall =
       S.issue_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count();
+  if (hs->stall == 2)
+    return fail(c, KB_E_STATE, "node-sharded ranks exchanged different segments (their drivers diverged)");
   if (hs->stall)
     return fail(c, KB_E_HIP, "place kernel gave up waiting for its overlapped level-0 sweep");
   if (skipped) {  // a speculative job whose guard failed: nothing ran, nothing to count
@@ -1250,6 +1269,7 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
 int kb_job_pipeline_ok(kb_ctx* c) { return c && (!c->sharded || c->comm) && !c->use_engine && !c->broken; }
 
 int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
+  if (c->fed) return job->n_tasks > 0 && kb_spec_fed_ok(c, job->task_specs[0]);  // the engine's own guard
   if (!c->use_sel || !c->sel_ok || !c->traj || job->n_tasks == 0) return 0;
   const int s0 = job->task_specs[0];
   if (s0 < 0 || s0 >= c->P.m || !c->spec_traj_ok[s0]) return 0;
@@ -1266,8 +1286,10 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 
 int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
-  if (c->sharded || c->use_engine || !c->use_sel || !c->sel_ok || !c->traj || !c->spec_traj_ok[spec]) return 0;
-  if (!fed_fits(c->N.n)) return 0;
+  if (c->sharded || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
+  const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
+  if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
+  if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
   if (c->aff_ok && c->spec_needs_aff[spec]) return 0;
   if (c->host_reasons(spec)) return 0;  // its NO_FIT needs a mid-cycle kb_node_reasons (not beside the engine)
   return c->use_fed ? 1 : 0;
@@ -1280,9 +1302,17 @@ static uint64_t fed_idle_ticks() {
   return ms > 0 ? (uint64_t)ms * 100000ull : 100000000ull;
 }
 
+int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
+  if (!c) return 0;
+  const int ns = fed_nsel(c->N.n);
+  return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
+}
+
 int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return KB_E_INVALID;
   if (c->fed) return fail(c, KB_E_STATE, "fed engine already running");
+  if (!kb_fed_cycle_ok(c, max_job_tasks))
+    return fail(c, KB_E_UNSUPPORTED, "fed engine: %d nodes need the split engine with one-segment jobs", c->N.n);
   if (c->any_busy()) return fail(c, KB_E_STATE, "a pipelined job is still in flight");
   if (!c->slot[kJobSlots - 1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
   if (!c->fed_ring) {
@@ -1319,8 +1349,9 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     c->stats.fed_split++;
   }
   c->stats.fed_cycles++;
-  launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr, c->fed_count, fed_idle_ticks(),
-                    c->fed_exit, xchg, c->stream);
+  HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
+                                          c->fed_count, fed_idle_ticks(), c->fed_exit, xchg, c->stream,
+                                          c->fed_dedicated));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1613,6 +1644,9 @@ int kb_set_host_overlay(kb_ctx* c, int32_t spec, const uint8_t* fail_in, const i
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
   if (c->fed || c->any_busy()) return fail(c, KB_E_STATE, "a job is in flight");
   if (spec < 0 || spec >= c->P.m) return fail(c, KB_E_INVALID, "spec %d out of range", spec);
+  // node sharding: the overlay's verdicts, its score bound (key width) and the NO_FIT hook's node masks are
+  // rank-local, so ranks could take different paths for one job and break the collective sequence
+  if (c->sharded) return fail(c, KB_E_UNSUPPORTED, "host overlay on a node-sharded context");
   HIP_OK(c, hipSetDevice(c->device));
   const size_t n = (size_t)c->N.n, m = (size_t)c->P.m;
   if (c->ov_slot.size() != m) {

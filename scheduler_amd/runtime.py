@@ -193,6 +193,7 @@ class Context:
         self.lib = load_library()
         self._keep = []
         self.overlay_reason = {}
+        self.overlay_fail = {}
         opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | PATHS[path], timing_every)
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
@@ -290,8 +291,10 @@ class Context:
         self._check(self.lib.kb_set_host_overlay(self.ctx, int(spec), _ptr(f), _ptr(sc)))
         if f is None and sc is None:
             self.overlay_reason.pop(int(spec), None)
+            self.overlay_fail.pop(int(spec), None)
         else:
             self.overlay_reason[int(spec)] = reason
+            self.overlay_fail[int(spec)] = None if f is None else f.copy()
 
     def apply(self, deltas, sc=None, ports=None):
         """kb_apply: rows changed by commits made outside the device (ROW_DELTA_DTYPE records; see
@@ -398,6 +401,7 @@ class Context:
             raise KbError(KB_E_INVALID, "NO_FIT hook failed")
         out["nofit"] = dict(self._nofit)
         out["overlay_reason"] = dict(self.overlay_reason)
+        out["overlay_fail"] = dict(self.overlay_fail)
         out["n_events"] = res.n_events
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
@@ -473,8 +477,24 @@ class Context:
                             for u in allocated:
                                 st[u] = E.ST["Binding"]
                             allocated = []
-                    for t in be[k + len(placed):e]:  # the run's failed task and the rest of the run
-                        fit.setdefault(j, {})[t] = np.array(res.reason_hist, np.uint32)
+                    if len(placed) < e - k:  # the run's failed task and the rest of the run
+                        hist = {E.REASONS[b]: int(c) for b, c in enumerate(res.reason_hist)
+                                if c and b != KB_R_HOST_ERROR}
+                        reasons = None
+                        if res.reason_hist[KB_R_HOST_ERROR]:
+                            # host-evaluated failures (overlay plugins, affinity errors): the reference records
+                            # each node's own error (fe.SetNodeError, backfill.go:84-86). Every node's mask at
+                            # this state (the run's commits applied), mapped per task as allocate's NO_FIT hook
+                            # does (the strings name the pod)
+                            reasons = self.eval([spec])[0][0]
+                        for t in be[k + len(placed):e]:
+                            h = dict(hist)
+                            if reasons is not None:
+                                view = dict(out, nofit={j: (t, n_ev, reasons)}, overlay_fail=dict(self.overlay_fail),
+                                            overlay_reason=dict(self.overlay_reason))
+                                for key, c in host_reason_strings(snap, view, j, t).items():
+                                    h[key] = h.get(key, 0) + c
+                            fit.setdefault(j, {})[t] = h
                     k = e
         finally:
             self._check(self.lib.kb_set_config(self.ctx, C.byref(kb_config(**cfg))))
@@ -538,14 +558,23 @@ def host_reason_strings(snap: E.Snapshot, out: dict, job: int, task: int) -> dic
         u = int(out["event_task"][i])
         if out["task_status"][u] != E.ST["Pipelined"]:
             before.append((snap.session_tasks[u]["uid"], int(snap.session_tasks[u]["spec"])))
-    aff_err = snap.aff is not None and (spec in snap.aff.own_err or snap.aff.xb_pods or snap.aff.xb_spec)
+    # the inter-pod predicate errors at every node that reaches it when the spec's own terms are invalid or an
+    # invalid lister pod exists by now (at session open, or one of the cycle's commits before this task)
+    aff_err = snap.aff is not None and (spec in snap.aff.own_err or bool(snap.aff.xb_pods) or
+                                        any(sp in snap.aff.xb_spec for _, sp in before))
     ov = out.get("overlay_reason", {}).get(spec)
+    ov_fail = out.get("overlay_fail", {}).get(spec)
     hist = {}
     for i in np.nonzero((reasons >> KB_R_HOST_ERROR) & 1)[0]:
+        # per node, in chain order: the inter-pod predicate's error, else the overlay plugin's verdict (the
+        # overlay is the chain's last stage)
         if aff_err:
             s = snap.aff.host_error_string(t["pod"], spec, names[i], before)
-        else:
+        elif ov is not None and (ov_fail is None or ov_fail[i]):
             s = ov(names[i]) if callable(ov) else str(ov)
+        else:
+            raise KbError(KB_E_STATE, f"job {job}: node {names[i]} failed a host-evaluated stage that neither the "
+                                      f"overlay nor the affinity tables account for")
         hist[s] = hist.get(s, 0) + 1
     return hist
 
@@ -576,8 +605,7 @@ def allocate_backfill(cluster, device: int = 0, path: str = "select") -> dict:
         d = result_dict(snap, out)
         ts = snap.session_tasks
         d["backfill_fit_errors"] = {
-            snap.jobs[j]["uid"]: {ts[t]["uid"]: {E.REASONS[b]: int(c) for b, c in enumerate(h) if c}
-                                  for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
+            snap.jobs[j]["uid"]: {ts[t]["uid"]: dict(h) for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
         return d
     finally:
         ctx.close()

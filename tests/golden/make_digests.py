@@ -30,18 +30,21 @@ from scheduler_amd import synth  # noqa: E402
 KIND = {"allocate": 1, "pipeline": 2}
 
 
-# BASELINE.json configs[4] (C5: 50k nodes) has no single-GPU selection path; its sharded test compares the
-# first placements of a 300-job C5-shaped cluster with this prefix of the oracle's cycle
+# C5-head: the first placements of a 300-job C5-shaped cluster (the sharded 3-rank test compares a prefix)
 HEADS = {"C5-head": (dict(n_nodes=50000, n_jobs=300, tasks_per_job=100), 3000)}
+# BASELINE.json configs[4] at full size: the C2 shape at 50k nodes x 1M pods (10k jobs)
+SHAPES = {"C5": dict(n_nodes=50000, n_jobs=10000, tasks_per_job=100)}
 
 
 def cluster_of(cfg):
     if cfg in HEADS:
         return synth.c2(**HEADS[cfg][0])
+    if cfg in SHAPES:
+        return synth.c2(**SHAPES[cfg])
     return synth.CONFIGS[cfg]()
 
 
-def make(cfg, workers=8):
+def make(cfg, workers=int(os.environ.get("DIGEST_WORKERS", "8"))):
     cl = cluster_of(cfg)
     snap = E.Snapshot(cl)
     max_tasks = HEADS[cfg][1] if cfg in HEADS else -1
@@ -61,7 +64,8 @@ def make(cfg, workers=8):
             job_fail[jidx[ju]] = uid[tu]
     np.savez_compressed(os.path.join(HERE, f"digest-{cfg}.npz"), event_task=event_task, event_node=event_node,
                         event_kind=event_kind, job_fail=job_fail)
-    meta = {"config": cfg, "generator": ("synth.c2(**%r)" % (HEADS[cfg][0],) if cfg in HEADS else
+    shape = HEADS[cfg][0] if cfg in HEADS else SHAPES.get(cfg)
+    meta = {"config": cfg, "generator": ("synth.c2(**%r)" % (shape,) if shape is not None else
                                          "synth.CONFIGS[%r]() defaults" % cfg) + " (seed %d)" % synth.SEED,
             "max_tasks": max_tasks,
             "nodes": snap.n_nodes, "pods": len(snap.session_tasks), "events": len(ev),

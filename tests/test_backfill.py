@@ -9,7 +9,7 @@ from oracle import pyoracle
 from scheduler_amd import model as m
 from scheduler_amd import runtime
 
-from helpers import GI, affinity_clusters, backfill_cluster, parity_clusters
+from helpers import GI, affinity_clusters, affinity_error_clusters, backfill_cluster, parity_clusters
 
 
 def _first_fit_cluster():
@@ -46,8 +46,25 @@ def test_oracle_backfill_skips_invalid_and_nonempty():
     assert len(ports) == len(set(ports))  # one hostPort 9090 per node
 
 
+def _with_best_effort(cl, n=6, sel=None):
+    """cl plus a job of BestEffort pods (backfill candidates)."""
+    cl.pod_groups.append(m.PodGroup(ns="ns", name="be", queue=cl.queues[0].name, min_member=1))
+    for i in range(n):
+        cl.pods.append(m.Pod(ns="ns", name=f"be-{i}", uid=f"ns-be-{i}", group="be", labels={"role": "be"},
+                             node_selector=dict(sel or {}), containers=[m.Container(req={})]))
+    return cl
+
+
+def _error_backfill_cases():
+    """Inputs where backfill's PredicateFn returns the inter-pod predicate's error on nodes (the device's
+    host-evaluated bucket): an invalid lister pod at session open, and one arising from the cycle's commits."""
+    errs = dict(affinity_error_clusters())
+    return [("be-err-existing-anti", _with_best_effort(errs["err-existing-anti"])),
+            ("be-err-dynamic", _with_best_effort(errs["err-existing-anti-dynamic"]))]
+
+
 CASES = [("first-fit", _first_fit_cluster()), ("backfill-edge", backfill_cluster())] + \
-    parity_clusters()[-2:] + affinity_clusters()[:2]
+    parity_clusters()[-2:] + affinity_clusters()[:2] + _error_backfill_cases()
 
 
 @pytest.mark.gpu
@@ -62,3 +79,29 @@ def test_backfill_parity(name, cluster):
     assert got["backfill_fit_errors"] == ref["backfill_fit_errors"]
     for uid, st in got["status"].items():  # the oracle also lists pods outside any job
         assert ref["status"][uid] == st, uid
+
+
+@pytest.mark.gpu
+def test_backfill_overlay_strings():
+    """A node the host overlay rejects fails a backfill task with the overlay plugin's own reason string
+    (fe.SetNodeError, backfill.go:84-86), never an unnamed bucket."""
+    from scheduler_amd import export as E
+    cl = _with_best_effort(_first_fit_cluster(), n=3, sel=None)
+    snap = E.Snapshot(cl)
+    names = snap.node_names()
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        fail = [1, 1, 0]  # a, b rejected; c is unschedulable: nothing fits
+        for sp in range(len(snap.spec_arr)):
+            ctx.set_host_overlay(sp, fail=fail, reason=lambda node: f"plugin says no to {node}")
+        out = ctx.backfill(snap, ctx.allocate(snap))
+    finally:
+        ctx.close()
+    fit = out["backfill_fit"]
+    assert fit, "every BestEffort task fails"
+    for tasks in fit.values():
+        for h in tasks.values():
+            assert None not in h
+            assert h == {"plugin says no to a": 1, "plugin says no to b": 1, "node(s) were unschedulable": 1}, h
+    assert names == ["a", "b", "c"]

@@ -185,8 +185,8 @@ def _c5_rank(rank, world, port, q):
 def test_c5_sharded_matches_one_gpu_and_oracle_prefix():
     """BASELINE.json configs[4] shape (C5: C2 nodes at 50k) with 300 jobs: 3 ranks sharing the GPU (each
     ~16.7k rows, the selection path per shard, one exchange per run segment over gloo) give the placements
-    of one GPU holding all 50k rows (the per-commit re-key path, the only one that fits 50k nodes), and
-    that cycle's first 3000 placements are the oracle's (tests/golden/digest-C5-head)."""
+    of one GPU holding all 50k rows (the split fed engine with three range selectors), and that cycle's
+    first 3000 placements are the oracle's (tests/golden/digest-C5-head)."""
     import json
     import torch.multiprocessing as mp
     from helpers import digest_arrays
@@ -225,3 +225,63 @@ def test_c5_sharded_matches_one_gpu_and_oracle_prefix():
         summary, exchanges = got[r]
         assert summary == ref, r
         assert exchanges >= 300  # at least one all-gather per job
+
+
+def _diverge_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+    res = {}
+    try:
+        snap = synth.c2_snapshot(n_nodes=400, n_jobs=6, tasks_per_job=10, seed=17)
+        ctx = runtime.Context(0)
+        try:
+            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+            ctx.upload(snap)
+            try:  # the overlay's verdicts would be rank-local
+                ctx.set_host_overlay(0, fail=np.zeros(ctx.n_nodes, np.uint8))
+                res["overlay"] = "accepted"
+            except runtime.KbError as e:
+                res["overlay"] = e.code
+            try:  # rank r issues a job of spec r: the exchanged segment tags differ
+                ctx.place_job([rank % len(snap.spec_arr)] * 5, ready_num=0, min_available=5)
+                res["diverged"] = "no error"
+            except runtime.KbError as e:
+                res["diverged"] = e.code
+        finally:
+            ctx.close()
+        q.put((rank, res, None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ranks_that_diverge_fail_loudly():
+    """every rank must issue the same segments. Ranks whose drivers issue different jobs get
+    KB_E_STATE from the exchanged segment tags (ShardRec::tag) instead of committing a mixed merge (or, with a
+    collective count mismatch, hanging later); the host overlay is refused on a sharded context."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_diverge_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=240)
+        assert err is None, f"rank {rank}: {err}"
+        got[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert got[r] == {"overlay": runtime.KB_E_UNSUPPORTED, "diverged": runtime.KB_E_STATE}, (r, got[r])
