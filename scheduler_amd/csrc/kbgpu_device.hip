@@ -1463,10 +1463,13 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
 // by score field, ties to the lower position. sh.node / sh.key0 [0, S) get node_of(position) and the key, in
 // position order (the position is the node). Returns the feasible count (0: nothing fits, S = 0). No barrier
 // after the LDS writes.
+// no / ko (cap entries, default sh.node / sh.key0): where the selected nodes and keys go.
 template <int QN>
 __device__ __forceinline__ uint32_t sel_pick(SelShared& sh, const uint32_t* k32, int n, int idx_bits, uint32_t T,
-                                             int& rp, uint32_t& S_out SEL_DIAG_PARAMS) {
+                                             int& rp, uint32_t& S_out SEL_DIAG_PARAMS, int32_t* no = nullptr,
+                                             uint32_t* ko = nullptr, int cap = 128) {
   const int tid = threadIdx.x;
+  if (no == nullptr) no = sh.node, ko = sh.key0;
   constexpr int QU = QN > 0 ? QN : kSelQ4;  // unroll bound of the key passes
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
   const uint4* k32v = (const uint4*)k32;
@@ -1548,13 +1551,13 @@ __device__ __forceinline__ uint32_t sel_pick(SelShared& sh, const uint32_t* k32,
       bool take = h > sstar;
       if (h == sstar) take = le++ < selE;
       if (take) {
-        sh.node[slot] = ki;
-        sh.key0[slot] = k;
+        no[slot] = ki;
+        ko[slot] = k;
         ++slot;
       }
     })
   }
-  if (tid >= (int)S_out && tid < 128) sh.key0[tid] = 0u;  // the rank loops read all 128 entries
+  if (tid >= (int)S_out && tid < cap) ko[tid] = 0u;  // the rank loops read all cap entries
 #undef SEL_EACH_KEY
   return F;
 }
@@ -2670,9 +2673,9 @@ struct FedXchg {
   uint64_t s_head[kJobSlots][kFedMaxSel];  // selector k -> placer: (job number + 1) << 32 | candidates (selector
                                            //   0: kSelExit on EXIT), stored once the entries below are drained
   uint64_t s_cmd[kJobSlots][16];     //   (selector 0) the job's command (FedCmd), one tagged word per field
-  uint64_t s_ent[kJobSlots][kFedMaxSel][128][2 + sizeof(Row) / 8];  //   selector k's candidates in key order
-                                                                    //   (descending): key | node << 32, static
-                                                                    //   cache, row
+  // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
+  // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
+  uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
   uint64_t sdiag[16];  // KB_DIAG builds: the selector's phase cycles, [8..] the placer's merge (KB_FED_DIAG)
 };
 
@@ -2732,8 +2735,13 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
                                              const FedSlots& S, const FedCmd* ring, const uint32_t* ctr,
                                              uint64_t idle_ticks, int32_t* exit_flag, FedXchg* X, uint32_t* k32,
                                              SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_n1, int sel,
-                                             int nsel) {
+                                             int nsel, uint32_t* scratch) {
   const int tid = threadIdx.x;
+  // candidate lists (scratch: 4 x 256 words of the candidate space, unused by a selector): by position, by rank
+  int32_t* cnode = (int32_t*)scratch;
+  uint32_t* ckey = scratch + 256;
+  int32_t* rnode = (int32_t*)scratch + 512;
+  uint32_t* rkey = scratch + 768;
   const int chunk = fed_sel_chunk(N.n, nsel);
   const int base = sel * chunk;
   const int n = N.n - base < chunk ? N.n - base : chunk;  // this selector's nodes
@@ -2801,6 +2809,42 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1, nullptr, 0,
               base, n);
     KB_SSTAMP(3);
+    // the T best of this range outside job m-1's set are among its T + kSegMax best (the set holds at most kSegMax
+    // nodes): chosen, ranked and their rows loaded before the set is known -- only the exclusion waits for it
+    const uint32_t T = (uint32_t)cm.t_count;
+    uint32_t cnt;
+#ifdef KB_DIAG
+    uint64_t dgp[7] = {0, 0, 0, 0, 0, 0, 0};  // sel_pick's own fine stamps (KB_DIAG_SEL) kept apart
+    sel_pick<QN>(sh, k32, n, idx_bits, T + kSegMax, rp, cnt, dgp, dg_last, cnode, ckey, 2 * 128);
+#else
+    sel_pick<QN>(sh, k32, n, idx_bits, T + kSegMax, rp, cnt, cnode, ckey, 2 * 128);
+#endif
+    __syncthreads();
+    {  // rank by key (2 threads per candidate; entries past cnt are 0)
+      const int e = tid >> 1, part = tid & 1;
+      const uint32_t k = e < (int)cnt ? ckey[e] : 0u;
+      uint32_t rk = 0;
+#pragma unroll 16
+      for (int q = 0; q < 128; ++q) rk += ckey[part * 128 + q] > k;
+      rk += dpp_src<0xb1>(0u, rk);  // quad_perm [1,0,3,2]: the pair's other half
+      if (part == 0 && e < (int)cnt) {
+        rnode[rk] = cnode[e];
+        rkey[rk] = k;
+      }
+    }
+    __syncthreads();
+    KB_SSTAMP(4);
+    // thread i: the rank-i candidate's row and static cache (final: job m-1 touches only its set)
+    Row rw{};
+    uint64_t stw = 0;
+    int wp = 0;
+    uint32_t wk = 0;
+    if (tid < (int)cnt) {
+      wp = rnode[tid];
+      wk = rkey[tid];
+      rw = load_row(N, wp + base);
+      stw = stat[wp + base];
+    }
     if (tid == 0) {  // job m-1's set (published at its node setup)
       int n1 = 0;
       if (m >= 1) {
@@ -2832,55 +2876,26 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       if (w < (uint32_t)n) k32[w] = 0u;
     }
     __syncthreads();
-    KB_SSTAMP(2);
-    uint32_t cnt;
-#ifdef KB_DIAG
-    uint64_t dgp[7] = {0, 0, 0, 0, 0, 0, 0};  // sel_pick's own fine stamps (KB_DIAG_SEL) kept apart
-    sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt, dgp, dg_last);
-#else
-    sel_pick<QN>(sh, k32, n, idx_bits, (uint32_t)cm.t_count, rp, cnt);
-#endif
-    __syncthreads();
-    KB_SSTAMP(4);
-    // the candidates' rows and static cache, loaded before the ranking so that their latency hides behind it
-    // (final: job m-1 touches only its set)
-    Row rw{};
-    uint64_t stw = 0;
-    int wn = 0;
-    if (tid < (int)cnt) {
-      wn = sh.node[tid] + base;
-      rw = load_row(N, wn);
-      stw = stat[wn];
-    }
-    {  // rank by key (4 threads per candidate), then each candidate's entry at its rank
-      const int e = tid >> 2, part = tid & 3;
-      const uint32_t k = e < (int)cnt ? sh.key0[e] : 0u;
-      uint32_t rk = 0;
-#pragma unroll
-      for (int q = 0; q < 32; ++q) {
-        const int o = part * 32 + q;
-        rk += sh.key0[o] > k;  // entries past cnt are 0 (sel_pick)
-      }
-      rk += dpp_src<0xb1>(0u, rk);  // quad_perm [1,0,3,2]
-      rk += dpp_src<0x4e>(0u, rk);  // quad_perm [2,3,0,1]
-      if (part == 0 && e < (int)cnt) sh.lmax[e] = (int)rk;
-    }
-    __syncthreads();
-    if (tid < (int)cnt) {
-      uint64_t* ent = X->s_ent[r][sel][sh.lmax[tid]];
-      x_store64(&ent[0], (uint64_t)sh.key0[tid] | ((uint64_t)(uint32_t)wn << 32));
-      x_store64(&ent[1], stw);
+    // candidates outside the set (a zeroed key: inside), in rank order; the first T go out
+    uint32_t pos = tid < (int)cnt && k32[wp] != 0u ? 1u : 0u, zero = 0, kept, ztot;
+    const bool keep = pos != 0;
+    sel_excl_scan2(sh, rp, pos, zero, &kept, &ztot);
+    const uint32_t nout = kept < T ? kept : T;
+    if (keep && pos < T) {
+      uint64_t(*ent)[128] = X->s_ent[r][sel];
+      x_store64(&ent[0][pos], (uint64_t)wk | ((uint64_t)(uint32_t)(wp + base) << 32));
+      x_store64(&ent[1][pos], stw);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
-      for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q], words[q]);
+      for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q][pos], words[q]);
     } else if (sel == 0 && tid >= 256 && tid < 256 + 16) {  // the command, for the placer (tagged: prefetched)
       tag_store(&X->s_cmd[r][tid - 256], m + 1, ((const uint32_t*)&cm)[tid - 256]);
     }
     // every wave's entry stores drained before the head (a barrier alone waits for LDS only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | cnt);
+    if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | nout);
     KB_SSTAMP(5);
 #ifdef KB_DIAG
     dg[6]++;
@@ -2983,7 +2998,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   if constexpr (SPLIT) {
     if (blockIdx.x >= 1) {
       fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
-                       (int)blockIdx.x - 1, nsel);
+                       (int)blockIdx.x - 1, nsel, (uint32_t*)cand);
       return;
     }
   }
@@ -3147,12 +3162,12 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         na += c;
       }
       if (list >= 0) {
-        const uint64_t* ent = X->s_ent[r][list][idx];
-        const uint64_t e0 = x_load64(&ent[0]);
-        const uint64_t st = x_load64(&ent[1]);
+        const uint64_t(*ent)[128] = X->s_ent[r][list];
+        const uint64_t e0 = x_load64(&ent[0][idx]);
+        const uint64_t st = x_load64(&ent[1][idx]);
         uint64_t words[sizeof(Row) / 8];
 #pragma unroll
-        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = x_load64(&ent[2 + q]);
+        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = x_load64(&ent[2 + q][idx]);
         __builtin_memcpy(&crow[tid], words, sizeof(Row));
         cst[tid] = st;
         cnd[tid] = (int)(e0 >> 32);
@@ -3195,22 +3210,29 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       const int nc = na + nb;
       int pos = -1;
       uint32_t key = 0;
-      const auto count_gt = [](const uint32_t* l, int len, uint32_t v) {
-        int lo = 0, hi = len;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (l[mid] > v) lo = mid + 1;
-          else hi = mid;
-        }
-        return lo;
-      };
       if (tid < nc) {
-        const bool in_a = tid < na;
-        const int j = tid - na;
-        key = in_a ? akey[list * 128 + idx] : bkey[j];
-        pos = in_a ? idx + count_gt(sh.emin, nb, key) : sh.A[j];
-        for (int k = 0; k < nsel; ++k)
-          if (k != list) pos += count_gt(akey + k * 128, s_na[k], key);
+        key = tid < na ? akey[list * 128 + idx] : bkey[tid - na];
+        // entries above the key in every list (its own list included: there that is its index), all searches
+        // at once: branch-free halving steps over lists of at most 128 (padding past a list's length unread)
+        int c[kFedMaxSel + 1];
+#pragma unroll
+        for (int k = 0; k <= kFedMaxSel; ++k) c[k] = 0;
+        int len[kFedMaxSel + 1];
+#pragma unroll
+        for (int k = 0; k <= kFedMaxSel; ++k) len[k] = k < kFedMaxSel ? (k < nsel ? s_na[k] : 0) : nb;
+#pragma unroll
+        for (int step = 64; step >= 1; step >>= 1) {
+#pragma unroll
+          for (int k = 0; k <= kFedMaxSel; ++k) {
+            if (k < kFedMaxSel && k >= nsel) continue;  // (uniform) lists past the selectors
+            const uint32_t* l = k < kFedMaxSel ? akey + k * 128 : sh.emin;
+            const int p = c[k] + step;
+            if (p <= len[k] && l[p - 1] > key) c[k] = p;
+          }
+        }
+        pos = 0;
+#pragma unroll
+        for (int k = 0; k <= kFedMaxSel; ++k) pos += c[k];
       }
       // the T best feasible (A is all feasible; infeasible keys rank below every feasible one), slots in node
       // order: the winners' tie rule on equal score fields takes lower slots first, which must be lower nodes
