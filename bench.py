@@ -6,13 +6,15 @@ step   : one allocateAction.Execute (actions/allocate/allocate.go:42-193) over t
          then kb_allocate (host ordering plugins + per-job device sweep/argmax/commit). The snapshot is
          uploaded once before the timed region; value = pods placed / second over the timed steps.
 
-Multi-GPU (N > 1, one process per GPU): BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped
-nodes x 1M pods whose node table is sharded across the N ranks (each rank holds a contiguous block; per run
-segment the ranks exchange their proposals with one RCCL all-gather over xGMI; every rank commits its own
-rows). `value` = the cycle's pods / the max-over-ranks time. A rank holds at most SEL_NODES_PER_GPU rows
-on the selection path, so at N = 2 the cluster is 2 x that (stated in config.nodes). The replicas line
-(every rank an independent C2 cluster, no collective) is reported beside it under "replicas".
+Multi-GPU (N > 1, one process per GPU): every rank schedules its own independent C2 cluster (a partition of the
+fleet with its own seed; no collective on the data path: torch.distributed only for the barriers and the
+max-over-ranks time) -- `value` = all ranks' pods / the max-over-ranks time, scaling "weak", the same per-GPU
+workload as the N = 1 line. One allocate cycle is a sequential chain of jobs, so GPUs add throughput by serving
+partitions. Beside it, "sharded": BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M pods
+whose node table is split across the N ranks (one RCCL all-gather per run segment over xGMI), reported with its
+exchange latency (the north star's scaling limiter). `--mode shard` makes that the line instead.
 `python bench.py --gpus N` without torchrun's environment starts the N ranks itself (before any GPU call).
+One GPU also runs C5 whole: `--config C5` (the split fed engine with range selectors).
 
 Extra JSON fields: roofline (dominant kernel, HIP events on the library's stream during the timed region),
 eval_roofline (the fit/score sweep kb_eval at 256 specs x 50k nodes: the HBM-bound kernel), and cpu_baseline
@@ -76,6 +78,7 @@ def main():
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP events around the launches of every Nth job call of the timed region")
     args = ap.parse_args()
+    args.mode_auto = args.mode == "auto"
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)  # torchrun's environment is missing: start the ranks (no GPU touched yet)
@@ -83,7 +86,7 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
-    mode = args.mode if args.mode != "auto" else ("shard" if world > 1 else "replicas")
+    mode = args.mode if args.mode != "auto" else "replicas"
     args.mode = mode
     args.config = args.config or ("C5" if mode == "shard" and world > 1 else "C2")
     cfg = CONFIGS[args.config]
@@ -173,52 +176,15 @@ def main():
             total_placed = int(p.item())
     side = None
     if world > 1 and mode == "shard":
-        side = replicas_side(args, dist, rank, world, device)
+        side = {"replicas": replicas_side(args, dist, rank, world, device)}
+    elif world > 1 and args.mode_auto:
+        side = {"sharded": shard_side(args, dist, rank, world, device)}
     ev = None
     if world == 1 and rank == 0 and not args.no_eval:
         ev = eval_side(device)
 
-    # roofline: dominant kernel by summed event time
-    kern_ms = [0.0 if runtime.KERNELS[i] == "shard_exchange" else v for i, v in enumerate(st["kernel_ms"])]
-    k = int(np.argmax(kern_ms)) if any(kern_ms) else 0  # the collective is reported on its own
-    launches = max(1, st["launches"][k])
-    avg_ms = st["kernel_ms"][k] / launches
-    bytes_per_launch = st["pairs"][k] * cfg["row_bytes"] / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    roofline = {"bound": "hbm", "kernel": runtime.KERNELS[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None, "traffic_source": None,
-                "avg_launch_us": round(avg_ms * 1e3, 3), "timed_launches": launches,
-                "timing": ("HIP events on the library stream around the resident engine's one launch per "
-                           "allocate cycle, every cycle of the timed region"
-                           if runtime.KERNELS[k] == "fed_engine_kernel" else
-                           f"HIP events on the library stream around every launch of every {args.timing_every}th "
-                           f"job call in the timed region"),
-                "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
-                "avg_us_per_launch": {runtime.KERNELS[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
-                                      for i in range(len(runtime.KERNELS)) if st["launches"][i]}}
-
-    # the committed PMC pass was taken on the default C2 line: its bytes apply to that workload only
-    c2_default = (args.config, args.nodes, args.jobs, args.tasks_per_job) == ("C2", 10000, 1000, 100)
-    tr = None
-    if c2_default and runtime.KERNELS[k] == "fed_engine_kernel":
-        # counter collection serialises dispatches, under which the resident engine cannot be fed: its HBM
-        # bytes are the launch path's per-job selection kernel bytes (same work, KB_NO_FED PMC pass) times
-        # the jobs it serves per launch
-        per_job = pmc_traffic("sel_place_kernel")
-        jobs = st["job_calls"] / max(1, st["launches"][k])
-        if per_job is not None:
-            tr = {"bytes_per_launch": round(per_job["bytes_per_launch"] * jobs, 1),
-                  "source": f"{per_job['source']}: sel_place_kernel per job (KB_NO_FED pass) x {jobs:.0f} jobs"}
-    elif c2_default:
-        tr = pmc_traffic(runtime.KERNELS[k])
-    elif (args.nodes, args.jobs, args.tasks_per_job) == (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
-        tr = pmc_traffic(runtime.KERNELS[k], args.config)  # that configuration's own committed PMC pass
-    roofline["measured_frac"] = None  # measured HBM bytes per launch / the launch time / peak
-    if tr is not None:
-        roofline["traffic"], roofline["traffic_source"] = tr["bytes_per_launch"], tr["source"]
-        if avg_ms > 0:
-            roofline["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+    roofline = roofline_of(st, args, cfg)
+    engine = engine_of(st, args) if st["launches"][runtime.KERNELS.index("fed_engine_kernel")] else None
 
     workload = cfg["workload"]
     if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
@@ -233,7 +199,7 @@ def main():
             if cl is None:  # the oracle runs on the cluster objects of the same workload
                 cl = synth.CONFIGS.get(args.config, synth.c2)(n_nodes=args.nodes, n_jobs=args.jobs,
                                                             tasks_per_job=args.tasks_per_job, seed=seed)
-            cpu = cpu_baseline(cl, args.cpu_sample_tasks)
+            cpu = cpu_baseline(cl, args.cpu_sample_tasks, args.config)
         result = {
             "metric": "pods placed/sec + p50 allocate-cycle ms at 10k nodes x 100k pods",
             "value": round(total_placed / elapsed, 1), "unit": "pods/s", "n_gpus": world, "steps": args.steps,
@@ -251,21 +217,90 @@ def main():
                        "pods_placed_per_cycle": placed // max(1, args.steps),
                        "parallelism": f"node_shard{world}" if shard else f"replicas{world}"},
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
-            **({"diag_place_phases": diag_summary(st["diag"], placed, runtime.KERNELS[k])}
+            **({"diag_place_phases": diag_summary(st["diag"], placed, "fed_engine_kernel" if engine is not None
+                                                  else roofline["kernel"])}
                if any(st["diag"]) else {}),
             "job_calls_per_step": st["job_calls"] / args.steps,
             "roofline": roofline,
+            **({"engine": engine} if engine is not None else {}),
             "cpu_baseline": cpu,
             **({"shard_exchange_us_per_segment": exchange_us(st),
                 "shard_segments_per_step": st["launches"][runtime.KERNELS.index("shard_exchange")] / args.steps}
                if shard else {}),
-            **({"replicas": side} if side is not None else {}),
+            **(side if side is not None else {}),
             **({"eval_roofline": ev} if ev is not None else {}),
         }
         print(json.dumps(result), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+SWEEP_OUT_BYTES = 12  # the level-0 sweep's output per node: 4 B key + 8 B static cache
+
+
+def roofline_of(st, args, cfg, streaming=False):
+    """The roofline of the cycle's HBM-streaming kernel. Fed-engine cycles: the per-job level-0 sweep
+    (sel_sweep_kernel on the sweep stream: every node's row read and its key written once per job -- the hot
+    path's fit/score evaluation of every (job spec, node) pair); the resident engine itself is a latency-bound
+    chain and is reported beside it ("engine"). Other cycles: the kernel with the most event time. achieved =
+    algorithmic bytes per launch (the row bytes of each (task, node) evaluation the launch makes,
+    plus the sweep's output) / the launch's average HIP-event duration on the stream it runs on; traffic = the
+    same kernel's measured HBM bytes per launch from this configuration's committed rocprofv3 PMC pass."""
+    from scheduler_amd import runtime
+    K = runtime.KERNELS
+    fed = st["launches"][K.index("fed_engine_kernel")] > 0
+    if fed or (streaming and st["launches"][K.index("sel_sweep_kernel")]):  # streaming: node-sharded cycles
+        k = K.index("sel_sweep_kernel")
+    else:
+        kern_ms = [0.0 if K[i] in ("shard_exchange", "fed_engine_kernel") else v for i, v in enumerate(st["kernel_ms"])]
+        k = int(np.argmax(kern_ms)) if any(kern_ms) else 0
+    launches = max(1, st["launches"][k])
+    avg_ms = st["kernel_ms"][k] / launches
+    per_eval = cfg["row_bytes"] + (SWEEP_OUT_BYTES if K[k] == "sel_sweep_kernel" else 0)
+    bytes_per_launch = st["pairs"][k] * per_eval / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    out = {"bound": "hbm", "kernel": K[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "traffic_source": None,
+           "avg_launch_us": round(avg_ms * 1e3, 3), "timed_launches": st["launches"][k],
+           "timing": (f"HIP events on the sweep stream around every {args.timing_every}th job's sweep launch in the "
+                      f"timed region" if K[k] == "sel_sweep_kernel" else
+                      f"HIP events on the library stream around every launch of every {args.timing_every}th job "
+                      f"call in the timed region"),
+           "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
+           "algorithmic_bytes_note": (f"{cfg['row_bytes']} B row read + {SWEEP_OUT_BYTES} B key/static cache written "
+                                      f"per node, every node once per job" if K[k] == "sel_sweep_kernel" else
+                                      f"{cfg['row_bytes']} B row per (task, node) evaluation (SURVEY.md §8 d3)"),
+           "avg_us_per_launch": {K[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
+                                 for i in range(len(K)) if st["launches"][i]},
+           "measured_frac": None}
+    full = (args.nodes, args.jobs, args.tasks_per_job) == (cfg["nodes"], cfg["jobs"], cfg["tasks"])
+    tr = pmc_traffic(K[k], args.config) if full else None
+    if tr is not None:
+        out["traffic"] = tr["bytes_per_launch"]
+        out["traffic_source"] = tr["source"] + f": {K[k]} " + (
+            "(the same kernel and launch size; counters taken on the per-job launch path, KB_NO_FED=1, because "
+            "counter collection serialises dispatches and the resident engine waits on the sweeps)" if fed else
+            "(this kernel, this configuration)")
+        if avg_ms > 0:
+            out["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+    return out
+
+
+def engine_of(st, args):
+    """The resident fed engine (one launch per allocate cycle): a latency-bound chain of dependent LDS round
+    trips per job inside one placer workgroup fed by selector workgroups -- not an HBM roofline kernel. Its
+    launch spans the cycle; the per-job time and the committed KB_DIAG phase split (busy vs waiting) are what
+    bound it."""
+    from scheduler_amd import runtime
+    K = runtime.KERNELS
+    k = K.index("fed_engine_kernel")
+    launches = max(1, st["launches"][k])
+    us = st["kernel_ms"][k] * 1e3 / launches
+    jobs = st["job_calls"] / launches
+    return {"kernel": "fed_engine_kernel", "bound": "latency (per-job dependent chain in one workgroup)",
+            "avg_launch_us": round(us, 3), "launches": st["launches"][k], "jobs_per_launch": round(jobs, 1),
+            "us_per_job": round(us / max(1.0, jobs), 3)}
 
 
 def tensor_device(dist, device):
@@ -331,6 +366,51 @@ def replicas_side(args, dist, rank, world, device):
         return {"error": repr(e)[:300]}
 
 
+def shard_side(args, dist, rank, world, device):
+    """Beside the replicas line (N > 1): BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M
+    pods whose node table is split across the N ranks (contiguous blocks; per run segment one all-gather of the
+    ranks' proposals, RCCL over xGMI, and every rank commits its own rows). `side_steps` cycles after one warm-up;
+    pods/s at the max-over-ranks time. A rank's block runs on the selection path (at most SEL_NODES_PER_GPU rows),
+    so at N = 2 the cluster is 2 x that, stated in the workload."""
+    import torch
+    from scheduler_amd import runtime, synth
+    try:
+        c = CONFIGS["C5"]
+        nodes = min(c["nodes"], SEL_NODES_PER_GPU * world)
+        snap = synth.c2_snapshot(n_nodes=nodes, n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED)
+        ctx = runtime.Context(device, timing=True, timing_every=args.timing_every)
+        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+        ctx.upload(snap)
+        ctx.allocate(snap)  # warm-up cycle
+        ctx.stats(reset=True)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        placed = 0
+        for _ in range(args.side_steps):
+            ctx.restore()
+            placed = int(ctx.allocate(snap)["n_events"])
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=tensor_device(dist, device))
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        st = ctx.stats()
+        ctx.close()
+        a = argparse.Namespace(**vars(args))
+        a.config, a.nodes, a.jobs, a.tasks_per_job = "C5", nodes, c["jobs"], c["tasks"]
+        work = (c["workload"] if nodes == c["nodes"] else
+                f"C5 shape at {nodes} nodes x {c['jobs'] * c['tasks']} pods (node table sharded {world} ways, at most "
+                f"{SEL_NODES_PER_GPU} rows per GPU)")
+        elapsed = float(el.item())
+        return {"workload": work, "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
+                "steps": args.side_steps, "scaling": "strong", "ms_per_step": round(elapsed / args.side_steps * 1e3, 3),
+                "exchange_us_per_segment": exchange_us(st),
+                "segments_per_step": st["launches"][runtime.KERNELS.index("shard_exchange")] / args.side_steps,
+                "roofline": roofline_of(st, a, c, streaming=True)}
+    except Exception as e:  # the side measurement never takes the main line down
+        return {"error": repr(e)[:300]}
+
+
 EVAL_SPECS, EVAL_NODES = 256, 50000
 
 
@@ -359,7 +439,7 @@ def eval_side(device):
                "avg_launch_us": round(us, 3), "algorithmic_bytes_per_launch": alg,
                "achieved": round(alg / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None, "measured_frac": None}
-        tr = pmc_traffic("eval_kernel")
+        tr = pmc_traffic("eval_kernel", "C2")  # the C2 PMC pass carries this side measurement
         if tr is not None:
             out["traffic"], out["traffic_source"] = tr["bytes_per_launch"], tr["source"]
             out["measured_frac"] = round(tr["bytes_per_launch"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
@@ -381,16 +461,12 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
-def pmc_traffic(kernel, config=None):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md HBM section), or None when no summary for it is committed. config: a non-headline
-    configuration's own summaries (profiles/*_<config>_prof_summary.json); None: the C2 headline's."""
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass of this configuration
+    (profiles/*_<config>_prof_summary.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or
+    None when none is committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*prof_summary.json")), reverse=True)
-    if config is None:
-        files = [f for f in files if not any(f.endswith(f"_{c}_prof_summary.json") for c in CONFIGS)]
-    else:
-        files = [f for f in files if f.endswith(f"_{config}_prof_summary.json")]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_prof_summary.json")), reverse=True)
     for f in files:
         try:
             with open(f) as fh:
@@ -424,7 +500,7 @@ def diag_summary(d, tasks, kernel):
             "clock_mhz": round(clock_mhz, 1) if clock_mhz else None}
 
 
-def cpu_baseline(cluster, sample_tasks):
+def cpu_baseline(cluster, sample_tasks, config):
     """The oracle (C++ restatement of the reference, ParallelizeUntil-style pool) on the first
     `sample_tasks` placements of the same workload."""
     from oracle import pyoracle
@@ -438,7 +514,7 @@ def cpu_baseline(cluster, sample_tasks):
     placed = len(out["events"])
     secs = out["elapsed_ms"] / 1e3
     return {"value": round(placed / secs, 1) if secs > 0 else None, "unit": "pods/s", "cores": cores,
-            "kind": "port", "sample": f"first {out['attempts']} task placements of the C2 cycle "
+            "kind": "port", "sample": f"first {out['attempts']} task placements of the {config} cycle "
                                       f"({placed} placed in {secs:.2f} s, {cores} worker threads, "
                                       f"reference-structured full predicate+score sweep per task)"}
 

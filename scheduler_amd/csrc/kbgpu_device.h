@@ -183,6 +183,13 @@ void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                       const uint16_t* mem, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout,
                       JobState* hjs, uint32_t seq, SpecGuard g, void* stream);
 
+// A fed-engine job command (launch_sel_sweep's `fed` / launch_fed_cmd).
+struct FedCmdArgs {
+  int32_t op, spec, t_begin, t_count, ready0, minav0, gang0, slot;
+  int32_t g_valid, g_stop, g_placed, g_ready;
+  uint32_t seq;
+};
+
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
 // keys of launch_sel_sweep. sel_lds_bytes(n) < 0: the node count does not fit its LDS plan.
 int sel_lds_bytes(int n);
@@ -191,9 +198,11 @@ int sel_lds_bytes(int n);
 // run re-keys after loading keys32 (its sweep ran concurrently with that job). done_ctr: the sweep's
 // blocks each add 1 when their keys are written; wait_ctr / wait_target: the place kernel waits for the
 // counter to reach the target first.
+// fed / ring (the fed engine): the job's command, written to the ring entry before block 0's release.
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
                       uint64_t* stat, const JobState* js, bool aff, void* stream,
-                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, uint32_t* done_ctr = nullptr);
+                      SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, uint32_t* done_ctr = nullptr,
+                      const FedCmdArgs* fed = nullptr, void* ring = nullptr);
 void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
@@ -212,11 +221,6 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
 // kernel (launch_fed_cmd, on the sweep stream) also posts the job's command to a kJobSlots-entry device ring and
 // counts its blocks in ctr[ring entry]; the engine serves commands in order until an EXIT command (or
 // idle_ticks without one: *exit_flag = 1).
-struct FedCmdArgs {
-  int32_t op, spec, t_begin, t_count, ready0, minav0, gang0, slot;
-  int32_t g_valid, g_stop, g_placed, g_ready;
-  uint32_t seq;
-};
 // Job slots: the fed engine keeps up to kJobSlots jobs in flight (the running one and two speculative ones);
 // the per-job launch path uses two of them.
 constexpr int kJobSlots = 3;

@@ -2257,10 +2257,23 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
 
 // Level-0 keys for the selection path: one node per thread, 64-thread blocks (a 10k-node table is
 // ~160 workgroups, spread over the chip), no trajectory levels.
+// A fed-engine job command (fed_engine_kernel): written by the job's level-0 sweep into a device ring entry.
+struct FedCmd {
+  int32_t op;  // KB_ENG_RUN / KB_ENG_EXIT
+  int32_t spec, t_begin, t_count, ready0, minav0, gang0, slot;
+  int32_t g_valid, g_stop, g_placed, g_ready;  // SpecGuard on the previous job's outcome
+  uint32_t seq;
+  int32_t pad[3];
+};
+static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
+
+// The level-0 sweep of a selection run: every node's 32-bit key and static cache for `spec`. done_ctr: each block
+// adds 1 with an agent-scope release once its keys are written (the overlapped sweep of the launch path; the fed
+// engine's ring counter). ring (fed engine): block 0 also writes the job's command there before its release.
 template <bool AFF>
 __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int idx_bits,
                                                       uint32_t* keys32, uint64_t* stat, const JobState* js,
-                                                      SpecGuard g, uint32_t* done_ctr) {
+                                                      SpecGuard g, uint32_t* done_ctr, FedCmd cmd, FedCmd* ring) {
   if ((js != nullptr && js->stopped) || guard_fails(g)) return;
   const int n = blockIdx.x * 64 + threadIdx.x;
   if (n < N.n) {
@@ -2272,21 +2285,28 @@ __global__ __launch_bounds__(64) void sel_sweep_kernel(DevNodes N, DevSpecs P, D
     keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, r, st), n), n + N.base, idx_bits);
   }
   // overlapped sweep (stream_b): one release per block (the wave's stores, written back to memory for
-  // the place kernel on another XCD), counted by the place kernel of the same job
-  if (done_ctr != nullptr && threadIdx.x == 0)
-    __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // the place kernel on another XCD), counted by the place kernel of the same job (or the fed engine)
+  if (threadIdx.x == 0) {
+    if (ring != nullptr && blockIdx.x == 0) *ring = cmd;
+    if (done_ctr != nullptr) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int idx_bits, uint32_t* keys32,
                       uint64_t* stat, const JobState* js, bool aff, void* stream, SpecGuard g,
-                      uint32_t* done_ctr) {
+                      uint32_t* done_ctr, const FedCmdArgs* fed, void* ring) {
   const int blocks = (N.n + 63) / 64;
+  FedCmd cmd{};
+  if (fed)
+    cmd = FedCmd{fed->op, fed->spec, fed->t_begin, fed->t_count, fed->ready0, fed->minav0, fed->gang0, fed->slot,
+                 fed->g_valid, fed->g_stop, fed->g_placed, fed->g_ready, fed->seq, {0, 0, 0}};
+  FedCmd* rg = fed ? (FedCmd*)ring : nullptr;
   if (aff)
     hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
-                       keys32, stat, js, g, done_ctr);
+                       keys32, stat, js, g, done_ctr, cmd, rg);
   else
     hipLaunchKernelGGL(sel_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec,
-                       idx_bits, keys32, stat, js, g, done_ctr);
+                       idx_bits, keys32, stat, js, g, done_ctr, cmd, rg);
 }
 
 // ===========================================================================
@@ -2602,8 +2622,8 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 
 // ===========================================================================
 // Fed engine: the selection place kernel as ONE resident workgroup for a whole allocate cycle, fed through
-// device memory. Per job (one selection run) the host launches only fed_cmd_sweep_kernel on the sweep
-// stream: it computes the run's level-0 keys and static cache into the job slot's buffers, block 0
+// device memory. Per job (one selection run) the host launches only the run's level-0 sweep (sel_sweep_kernel,
+// the launch path's own) on the sweep stream: it computes the keys and static cache into the job slot's buffers, block 0
 // writes the run's command into a kJobSlots-entry ring, and every block adds one to the ring entry's
 // counter with an agent-scope release. The engine waits for the counter (acquire), checks the command's
 // guard against the previous job's outcome, re-keys the rows the previous two jobs committed (its sweep may
@@ -2611,14 +2631,6 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // sel_place_kernel does. No per-job kernel boundary on the place stream: the launch gap, the end-of-
 // kernel release and the next kernel's acquire (5.6 us median between place kernels) go away.
 // ===========================================================================
-struct FedCmd {
-  int32_t op;  // KB_ENG_RUN / KB_ENG_EXIT
-  int32_t spec, t_begin, t_count, ready0, minav0, gang0, slot;
-  int32_t g_valid, g_stop, g_placed, g_ready;  // SpecGuard on the previous job's outcome
-  uint32_t seq;
-  int32_t pad[3];
-};
-static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
 
 struct FedSlots {
   uint32_t* keys[kJobSlots];
@@ -2630,6 +2642,7 @@ struct FedSlots {
   uint32_t tgt[kJobSlots];   // ring counters' targets at launch
 };
 
+// A command without a sweep (EXIT): the ring entry and the whole block count at once.
 template <bool AFF>
 __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                           uint32_t* keys32, uint64_t* stat, FedCmd cmd, FedCmd* ring,

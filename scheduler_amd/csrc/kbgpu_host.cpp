@@ -1361,8 +1361,17 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
 // Post a command to the engine (sweep: the job's level-0 keys into its slot buffers first).
 static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
   const int r = c->fed_r;
-  launch_fed_cmd(c->N, c->P, c->cfg, c->idx_bits, c->sel_keys[si], c->sel_stat[si], a,
-                 (char*)c->fed_ring + r * (fed_ring_bytes() / kJobSlots), c->fed_ctr + r, sweep, c->stream_b);
+  void* entry = (char*)c->fed_ring + r * (fed_ring_bytes() / kJobSlots);
+  if (sweep) {  // the job's level-0 sweep (the launch path's own sweep kernel) carries the command
+    hipEvent_t ea;
+    c->ev_begin(&ea, c->stream_b);
+    launch_sel_sweep(c->N, c->P, c->cfg, a.spec, c->idx_bits, c->sel_keys[si], c->sel_stat[si], nullptr, false,
+                     c->stream_b, SpecGuard{nullptr, 0, 0, 0}, c->fed_ctr + r, &a, entry);
+    c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
+  } else {
+    launch_fed_cmd(c->N, c->P, c->cfg, c->idx_bits, c->sel_keys[si], c->sel_stat[si], a, entry, c->fed_ctr + r,
+                   false, c->stream_b);
+  }
   HIP_OK(c, hipGetLastError());
   c->fed_count[r] += (uint32_t)((c->N.n + 63) / 64);
   c->fed_r = r + 1 == kJobSlots ? 0 : r + 1;
@@ -1436,12 +1445,14 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     if (!kb_spec_fed_ok(c, job->task_specs[0])) return fail(c, KB_E_INVALID, "fed engine: spec not eligible");
     kb_ctx::JobSlot& S = c->slot[slot];
     S.t_issue = std::chrono::steady_clock::now();
-    S.ev_b = S.ev_e = c->pending.size();
+    c->timing_now = c->timing && (c->issue_count++ % c->timing_every == 0);  // the job's sweep
     memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
     FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
                  job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
                  pred ? pred->ready : 0, ++c->seq};
+    S.ev_b = c->pending.size();
     if (int rc = fed_post(c, a, slot, true)) return rc;
+    S.ev_e = c->pending.size();
     S.seq = c->seq;
     S.busy = true;
     S.issue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S.t_issue).count();
