@@ -139,8 +139,10 @@ struct kb_ctx {
   // The resident engine waits for sweeps issued on stream_b: they must never queue behind it on one hardware queue.
   // The engine is a cooperative launch (the device's own cooperative queue, every workgroup co-resident) and
   // stream_b a CU-masked stream (a hardware queue of its own, never shared with other streams of the process).
-  // KB_FED_SHARED_QUEUES=1 (tests): plain launch and plain stream, the hazard these remove.
+  // KB_FED_SHARED_QUEUES=1 (tests): plain launch and plain stream, the hazard these remove; KB_FED_PLAIN_LAUNCH=1:
+  // plain launch only (the dedicated sweep stream alone already separates the two).
   bool fed_dedicated = true;
+  bool fed_coop = true;
   // tests only (KB_TEST_STALL_JOB / KB_TEST_STALL_MS, read once at kb_create): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;

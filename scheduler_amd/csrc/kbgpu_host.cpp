@@ -237,6 +237,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
   c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
   c->fed_dedicated = getenv("KB_FED_SHARED_QUEUES") == nullptr;  // testing: the shared-queue hazard
+  c->fed_coop = c->fed_dedicated && getenv("KB_FED_PLAIN_LAUNCH") == nullptr;
   if (const char* e = getenv("KB_TEST_STALL_JOB")) c->test_stall_job = atoll(e);
   if (const char* e = getenv("KB_TEST_STALL_MS")) c->test_stall_ms = atoi(e);
   c->timing_now = c->timing;
@@ -1351,7 +1352,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   c->stats.fed_cycles++;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
                                           c->fed_count, fed_idle_ticks(), c->fed_exit, xchg, c->stream,
-                                          c->fed_dedicated));
+                                          c->fed_coop));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;

@@ -14,6 +14,9 @@ CONFIGS=${*:-C2 C3 C4 C5}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
+# rocprofv3 (ROCm 7.2) segfaults in its exit handlers after a cooperative launch: under the profiler the engine
+# takes a plain launch (same kernel, same grid; the CU-masked sweep stream still keeps the sweeps off its queue)
+export KB_FED_PLAIN_LAUNCH=1
 run() {  # run <name> <timeout> <cmd...>: stop the script on a crash / timeout
   local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
