@@ -30,8 +30,10 @@ for C in $CONFIGS; do
   run ${C}_trace 300 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/${C}_trace" -o run --output-format csv -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-eval
   NOFED=""
   [ "$C" != C4 ] && NOFED=1
-  KB_NO_FED=$NOFED run ${C}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/${C}_fetch" -o run --output-format csv -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline $EVAL
-  KB_NO_FED=$NOFED run ${C}_write 300 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/${C}_write" -o run --output-format csv -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline $EVAL
+  # (the PMC passes keep the sweep stream in the shared queue pool: with a dedicated CU-masked queue the profiler's
+  # serialisation leaves the launch path's place kernel waiting for its overlapped sweep)
+  KB_FED_SHARED_QUEUES=1 KB_NO_FED=$NOFED run ${C}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/${C}_fetch" -o run --output-format csv -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline $EVAL
+  KB_FED_SHARED_QUEUES=1 KB_NO_FED=$NOFED run ${C}_write 300 rocprofv3 --pmc WRITE_SIZE -d "$PWD/$OUT/${C}_write" -o run --output-format csv -- python3 bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline $EVAL
   python3 scripts/prof_summary.py "$OUT/${C}_trace" "$OUT/${C}_fetch" "$OUT/${C}_write" "$OUT/${TAG}_${C}_prof_summary.json" > "$OUT/sum_${C}.log" 2>&1
   rm -rf "$OUT/${C}_fetch" "$OUT/${C}_write"  # raw per-dispatch CSVs: large, summarised above
 done

@@ -285,3 +285,63 @@ def test_sharded_ranks_that_diverge_fail_loudly():
         p.join(timeout=60)
     for r in range(world):
         assert got[r] == {"overlay": runtime.KB_E_UNSUPPORTED, "diverged": runtime.KB_E_STATE}, (r, got[r])
+
+
+def _c5_full_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from helpers import digest_arrays
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+    try:
+        snap = synth.c2_snapshot(n_nodes=50000, n_jobs=10000, tasks_per_job=100, seed=synth.SEED)
+        ctx = runtime.Context(0)
+        try:
+            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+            ctx.upload(snap)
+            out = ctx.allocate(snap)
+        finally:
+            ctx.close()
+        k = int(out["n_events"])
+        et = out["event_task"][:k].astype(np.int32)
+        en = out["task_node"][et].astype(np.int32)
+        ek = np.where(out["task_status"][et] == E.ST["Pipelined"], 2, 1).astype(np.int8)
+        jf = out["job_fail_task"][:10000].astype(np.int32)
+        q.put((rank, (k, digest_arrays(et, en, ek, jf)), None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_full_eight_ranks_match_oracle_digest():
+    """BASELINE.json configs[4] at its stated size and split: 50k nodes x 1M pods, the node table sharded 8 ways
+    (8 ranks sharing the GPU, one host-staged all-gather over gloo per run segment). Every rank's whole cycle
+    equals the oracle's (tests/golden/digest-C5: 1,000,000 placements, 7,373 s of oracle time)."""
+    import json
+    import torch.multiprocessing as mp
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(golden, "digest-C5.json")) as f:
+        meta = json.load(f)
+    world = 8
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_c5_full_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=600)
+        assert err is None, f"rank {rank}: {err}"
+        got[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert got[r] == (meta["events"], meta["sha256"]), r
