@@ -212,13 +212,9 @@ class Tables:
         if s is not None:
             return s
         s = self.slot_ids[keys] = len(self.slot_doms)
-        ids, dom = {}, np.full(self.n, -1, np.int32)
-        for i, nd in enumerate(self.snap.nodes):
-            labels = nd["node"].labels
-            if all(k in labels for k in keys):
-                dom[i] = ids.setdefault(tuple(labels[k] for k in keys), len(ids))
+        dom, d = self.snap.slot_domains(keys)
         self.slot_doms.append(dom)
-        self.slot_D.append(len(ids))
+        self.slot_D.append(d)
         return s
 
     def table(self, key, keys, kind):
@@ -230,22 +226,15 @@ class Tables:
         return t
 
     def build(self):
+        """The snapshot supplies its pods grouped (a group: pods with one spec template -- namespace, labels,
+        (anti)affinity -- and their session nodes): snap.aff_groups() -> (lister, existing, spec_pod) with
+        lister  : [(pod, nodes, uids)] the allocated-status session tasks (NewPodLister, util.go:57-82),
+        existing: [(pod, nodes)] the pods on session nodes (schedulercache NodeInfo pods, for the score),
+        spec_pod: the first pending pod of every spec; and snap.slot_domains(keys) -> (domain id per node, D)."""
         snap, U = self.snap, self.U
-        node_index = snap.node_index
-        # lister pods: allocated-status session tasks (NewPodLister, util.go:57-82)
-        from .export import allocated_status, has_pod_affinity
-        lister = [t for t in snap.session_tasks if allocated_status(t["status"])]
-        for t in lister:
-            if t["pod"].node not in node_index:
-                raise U("lister pod on a node outside the session (predicates.go: failed to find node)")
-        # existing pods per session node (schedulercache NodeInfo pods, for the score)
-        existing = [(t, i) for i, nd in enumerate(snap.nodes) for t in nd["tasks"]]
-        pending_specs = {}
-        for t in snap.session_tasks:
-            if "spec" in t and t["status"] == 1:
-                pending_specs.setdefault(t["spec"], t["pod"])
-        m = len(snap.spec_arr)
-        spec_pod = [pending_specs[s] for s in range(m)]
+        from .export import has_pod_affinity
+        lister, existing, spec_pod = snap.aff_groups(U)
+        m = len(spec_pod)
         aff_cache = {}
 
         def paff(pod):
@@ -268,8 +257,8 @@ class Tables:
         self_match = [0] * m
         # XB: lister pods with an invalid required anti-affinity selector; every spec checks it first
         # (satisfiesExistingPodsAntiAffinity errors before it looks at any term, predicates.go:1302-1313)
-        self.xb_pods = sorted((t["uid"], first_invalid(paff(t["pod"]).req_anti)) for t in lister
-                              if first_invalid(paff(t["pod"]).req_anti))
+        self.xb_pods = sorted((u, first_invalid(paff(pod).req_anti)) for pod, _, uids in lister
+                              if first_invalid(paff(pod).req_anti) for u in uids)
         self.xb_spec = {s: first_invalid(paff(spec_pod[s]).req_anti) for s in range(m)
                         if first_invalid(paff(spec_pod[s]).req_anti)}
         if self.xb_pods or self.xb_spec:
@@ -279,8 +268,8 @@ class Tables:
             for s in self.xb_spec:
                 lister_incr[s].append(xb)
         e_classes = {}  # (ns, sel, key) -> table id
-        for t in lister:
-            for term in paff(t["pod"]).req_anti:
+        for pod, _, _ in lister:
+            for term in paff(pod).req_anti:
                 if term.key and not term.invalid:
                     e_classes.setdefault((term.ns, term.sel, term.key), None)
         for s in range(m):
@@ -338,8 +327,8 @@ class Tables:
             checks[s] += aff_chk
         # identities of lister pods (with their nodes) and of pending specs
         lid = defaultdict(list)
-        for t in lister:
-            lid[pod_ident(t["pod"])].append(node_index[t["pod"].node])
+        for pod, nodes, _ in lister:
+            lid[pod_ident(pod)].extend(nodes)
         index = defaultdict(set)
         for ident in set(lid) | set(spec_ids):
             for k, v in ident[1]:
@@ -359,15 +348,15 @@ class Tables:
             np.add.at(counters, cnt_off[tid] + dom[ok], 1)
             totals[tid] += len(nodes)
 
-        for t in lister:  # existing-anti classes carried by lister pods
-            for term in paff(t["pod"]).req_anti:
+        for pod, nodes, _ in lister:  # existing-anti classes carried by lister pods
+            for term in paff(pod).req_anti:
                 if term.key and not term.invalid:
-                    add_nodes(e_classes[(term.ns, term.sel, term.key)], [node_index[t["pod"].node]])
+                    add_nodes(e_classes[(term.ns, term.sel, term.key)], nodes)
         if self.xb_pods:
-            add_nodes(self.tables[("XB",)], [node_index[t["pod"].node] for t in lister
-                                            if first_invalid(paff(t["pod"]).req_anti)])
+            add_nodes(self.tables[("XB",)], [i for pod, nodes, _ in lister if first_invalid(paff(pod).req_anti)
+                                            for i in nodes])
         if all_t is not None:
-            add_nodes(all_t, [node_index[t["pod"].node] for t in lister])
+            add_nodes(all_t, [i for _, nodes, _ in lister for i in nodes])
             for s in range(m):
                 lister_incr[s].append(all_t)
         spec_by_ident = defaultdict(list)
@@ -395,10 +384,10 @@ class Tables:
                     repr((pod.affinity or {}).get("podAntiAffinity")))
         e_nodes = defaultdict(list)
         e_pod = {}
-        for t, i in existing:
-            k = sid(t["pod"])
-            e_nodes[k].append(i)
-            e_pod.setdefault(k, t["pod"])
+        for pod, nodes in existing:
+            k = sid(pod)
+            e_nodes[k].extend(nodes)
+            e_pod.setdefault(k, pod)
         spec_sid = [sid(p) for p in spec_pod]
         for s, k in enumerate(spec_sid):
             e_pod.setdefault(k, spec_pod[s])

@@ -322,6 +322,211 @@ class _Interner:
         return i
 
 
+class SpecTable:
+    """Pending pods deduplicated into task specs (kb_spec rows) with their compiled selector / affinity terms,
+    toleration sets and host ports, in first-occurrence order. Export.Snapshot feeds it every pending task;
+    the columnar exporter (columns.py) feeds it one pod per distinct template (pods of one template share
+    every field the signature reads)."""
+
+    def __init__(self, scalars, aff_in_play):
+        self.scalars = list(scalars)
+        if len(self.scalars) > 64:
+            raise Unsupported("more than 64 scalar resources")
+        self.slot = {n: i for i, n in enumerate(self.scalars)}
+        self.aff_in_play = aff_in_play
+        self.label_keys = _Interner()
+        self.values = _Interner()
+        self.gtlt_keys = set()
+        self.port_slots = _Interner()
+        self.port_ips = {}  # slot -> Interner of ips (0.0.0.0 first)
+        self.tol_sets = _Interner()
+        self.tol_list = []
+        self.terms, self.reqs, self.vals, self.ports = [], [], [], []
+        self.specs, self.sc_init, self.sc_req = [], [], []
+        self.sig_index = {}
+        self.reprs = {}  # repr of a pod's affinity sub-dicts, by object (pods of one template share them)
+
+    def rp(self, x):
+        k = id(x)
+        v = self.reprs.get(k)
+        if v is None:
+            v = self.reprs[k] = (x, repr(x))  # keeps x alive: its id is not reused during the export
+        return v[1]
+
+    def req_rows(self, exprs, allow_gtlt=True):
+        """NodeSelectorRequirementsAsSelector (helpers.go:222-254) -> requirement rows, None if invalid."""
+        rows = []
+        for e in exprs:
+            op = {"In": OP_IN, "NotIn": OP_NOTIN, "Exists": OP_EXISTS, "DoesNotExist": OP_DNE,
+                  "Gt": OP_GT, "Lt": OP_LT}.get(e.get("operator"))
+            key, vs = e.get("key", ""), list(e.get("values") or [])
+            if op is None or not is_qualified_name(key):
+                return None
+            if op in (OP_IN, OP_NOTIN) and not vs:
+                return None
+            if op in (OP_EXISTS, OP_DNE) and vs:
+                return None
+            ival = 0
+            if op in (OP_GT, OP_LT):
+                if len(vs) != 1 or parse_int64(vs[0]) is None:
+                    return None
+                ival = parse_int64(vs[0])
+                self.gtlt_keys.add(key)
+            if not all(is_valid_label_value(v) for v in vs):
+                return None
+            rows.append((self.label_keys(key), op, tuple(self.values(v) for v in vs) if op < OP_EXISTS else (),
+                         ival))
+        return rows
+
+    def add_term(self, rows, weight=0):
+        off = len(self.reqs)
+        for key, op, vv, ival in rows:
+            self.reqs.append((key, op, len(self.vals), len(vv), ival))
+            self.vals.extend(vv)
+        self.terms.append((off, len(rows), weight, 0))
+        return len(self.terms) - 1
+
+    def add(self, p, ir, rr) -> int:
+        """The spec id of a pending pod with InitResreq ir and Resreq rr (a new spec for a new signature)."""
+        nzc = nzm = 0
+        for c in p.containers:
+            a, b = nonzero(c.req)
+            nzc += a
+            nzm += b
+        aff = p.affinity or {}
+        nodeaff = aff.get("nodeAffinity") if p.affinity is not None else None
+        tols = tuple(sorted((d.get("key", ""), d.get("operator", ""), d.get("value", ""), d.get("effect", ""))
+                            for d in p.tolerations))
+        port_list = []
+        for c in p.containers:
+            for pt in c.ports:
+                hp = int(pt.get("hostPort", 0) or 0)
+                if hp <= 0:
+                    continue
+                port_list.append(((pt.get("protocol") or "TCP"), hp, pt.get("hostIP") or "0.0.0.0"))
+        best_effort = not any(M.CPU in c.req or M.MEMORY in c.req for c in list(p.containers) + list(p.init))
+        sig = (ir.cpu, ir.mem, tuple(sorted((ir.sc or {}).items())) if ir.sc is not None else None,
+               rr.cpu, rr.mem, tuple(sorted((rr.sc or {}).items())) if rr.sc is not None else None,
+               nzc, nzm, tuple(sorted(p.node_selector.items())), self.rp(nodeaff), tols, tuple(port_list),
+               best_effort)
+        if self.aff_in_play:  # selectors and terms see the pod's namespace, labels and own terms
+            sig = sig + (p.ns, tuple(sorted(p.labels.items())), self.rp(aff.get("podAffinity")),
+                         self.rp(aff.get("podAntiAffinity")))
+        if sig in self.sig_index:
+            return self.sig_index[sig]
+        slot = self.slot
+        flags = 0
+        if ir.sc is not None:
+            flags |= SPEC_INIT_HAS_MAP
+        if rr.sc is not None:
+            flags |= SPEC_REQ_HAS_MAP
+        if best_effort:
+            flags |= SPEC_BEST_EFFORT
+        if self.aff_in_play:
+            flags |= SPEC_POD_AFFINITY
+        imask = sum(1 << slot[k] for k in (ir.sc or {}))
+        rmask = sum(1 << slot[k] for k in (rr.sc or {}))
+        si = [0] * len(self.scalars)
+        sr = [0] * len(self.scalars)
+        for k, v in (ir.sc or {}).items():
+            si[slot[k]] = v
+        for k, v in (rr.sc or {}).items():
+            sr[slot[k]] = v
+        # nodeSelector: SelectorFromSet, any invalid pair => Everything (labels/selector.go:849-866)
+        sel_term = 0
+        if p.node_selector:
+            ok = all(is_qualified_name(k) and is_valid_label_value(v) for k, v in p.node_selector.items())
+            if ok:
+                sel_term = self.add_term([(self.label_keys(k), OP_IN, (self.values(v),), 0)
+                                          for k, v in sorted(p.node_selector.items())])
+                flags |= SPEC_HAS_SELECTOR
+        # required node affinity (MatchNodeSelectorTerms, helpers.go:302-333)
+        req_off, req_cnt = len(self.terms), 0
+        if nodeaff is not None and nodeaff.get("required") is not None:
+            flags |= SPEC_HAS_REQUIRED
+            built = []
+            for term in nodeaff["required"]:
+                exprs = term.get("matchExpressions") or []
+                fields = term.get("matchFields") or []
+                if not exprs and not fields:
+                    built.append([])  # empty term: matches nothing
+                    continue
+                rows = []
+                if exprs:
+                    r = self.req_rows(exprs)
+                    rows.extend(r if r is not None else [(0, OP_FALSE, (), 0)])
+                if fields:  # NodeSelectorRequirementsAsFieldSelector over {metadata.name: node.Name}
+                    for e in fields:
+                        op, vs = e.get("operator"), list(e.get("values") or [])
+                        if op not in ("In", "NotIn") or len(vs) != 1:
+                            rows = [(0, OP_FALSE, (), 0)]
+                            break
+                        if e.get("key") == "metadata.name":
+                            rows.append((self.label_keys("\x00metadata.name"), OP_IN if op == "In" else OP_NOTIN,
+                                         (self.values(vs[0]),), 0))
+                        else:
+                            truth = (vs[0] == "") if op == "In" else (vs[0] != "")
+                            rows.append((0, OP_TRUE if truth else OP_FALSE, (), 0))
+                built.append(rows)
+            req_off = len(self.terms)
+            for rows in built:
+                self.add_term(rows)
+            req_cnt = len(built)
+        # preferred node affinity (node_affinity.go:47-67)
+        pref_rows = []
+        if nodeaff is not None:
+            for pt in nodeaff.get("preferred") or []:
+                w = int(pt.get("weight", 0))
+                if w == 0:
+                    continue
+                exprs = (pt.get("preference") or {}).get("matchExpressions") or []
+                rows = self.req_rows(exprs) if exprs else []
+                if rows is None:
+                    flags |= SPEC_NA_ERROR
+                    pref_rows = []
+                    break
+                pref_rows.append((rows, w))
+        pref_off = len(self.terms)
+        for rows, w in pref_rows:
+            self.add_term(rows, w)
+        # tolerations
+        tol_id = self.tol_sets(tols)
+        if tol_id == len(self.tol_list):
+            self.tol_list.append([{"key": a, "operator": b, "value": c, "effect": d} for a, b, c, d in tols])
+        # ports
+        port_off = len(self.ports)
+        for proto, hp, ip in port_list:
+            s_id = self.port_slots((proto, hp))
+            ipi = self.port_ips.setdefault(s_id, _Interner())
+            if not ipi.ids:
+                ipi("0.0.0.0")
+            self.ports.append((s_id, ipi(ip)))
+        specs = self.specs
+        specs.append((ir.cpu, ir.mem, rr.cpu, rr.mem, nzc, nzm, imask, rmask, flags, tol_id,
+                      len(self.sc_init) * len(self.scalars), sel_term, req_off, req_cnt, pref_off, len(pref_rows),
+                      port_off, len(self.ports) - port_off, len(specs) if self.aff_in_play else -1, 0))
+        self.sc_init.extend(si)
+        self.sc_req.extend(sr)
+        self.sig_index[sig] = len(specs) - 1
+        return len(specs) - 1
+
+    def finish(self, snap):
+        """The spec arrays and interners onto the snapshot."""
+        for s_id, ipi in self.port_ips.items():
+            if len(ipi.ids) > 63:
+                raise Unsupported("more than 62 host IPs for one (protocol, port)")
+        snap.scalars = self.scalars
+        for k in ("label_keys", "values", "gtlt_keys", "port_slots", "port_ips", "tol_sets", "tol_list"):
+            setattr(snap, k, getattr(self, k))
+        snap.spec_arr = np.array(self.specs, dtype=SPEC_DTYPE) if self.specs else np.zeros(0, SPEC_DTYPE)
+        snap.sc_init = np.array(self.sc_init, dtype=np.int64)
+        snap.sc_req = np.array(self.sc_req, dtype=np.int64)
+        snap.term_arr = np.array(self.terms, dtype=TERM_DTYPE) if self.terms else np.zeros(0, TERM_DTYPE)
+        snap.req_arr = np.array(self.reqs, dtype=REQ_DTYPE) if self.reqs else np.zeros(0, REQ_DTYPE)
+        snap.val_arr = np.array(self.vals, dtype=np.int32)
+        snap.port_arr = np.array(self.ports, dtype=PORT_DTYPE) if self.ports else np.zeros(0, PORT_DTYPE)
+
+
 class Snapshot:
     """Session-open view of a Cluster, exported as kb_nodes / kb_specs / kb_session arrays."""
 
@@ -462,195 +667,10 @@ class Snapshot:
         for t in pending:
             scal.update((t["initreq"].sc or {}).keys())
             scal.update((t["resreq"].sc or {}).keys())
-        self.scalars = sorted(scal)
-        if len(self.scalars) > 64:
-            raise Unsupported("more than 64 scalar resources")
-        slot = {n: i for i, n in enumerate(self.scalars)}
-        self.label_keys = _Interner()
-        self.values = _Interner()
-        self.gtlt_keys = set()
-        self.port_slots = _Interner()
-        self.port_ips = {}  # slot -> Interner of ips (0.0.0.0 first)
-        self.tol_sets = _Interner()
-        self.tol_list = []
-        terms, reqs, vals, ports = [], [], [], []
-        specs, sc_init, sc_req = [], [], []
-        sig_index = {}
-        reprs = {}  # repr of a pod's affinity sub-dicts, by object (pods of one template share them)
-
-        def rp(x):
-            k = id(x)
-            v = reprs.get(k)
-            if v is None:
-                v = reprs[k] = (x, repr(x))  # keeps x alive: its id is not reused during the export
-            return v[1]
-
-        def req_rows(exprs, allow_gtlt=True):
-            """NodeSelectorRequirementsAsSelector (helpers.go:222-254) -> requirement rows, None if invalid."""
-            rows = []
-            for e in exprs:
-                op = {"In": OP_IN, "NotIn": OP_NOTIN, "Exists": OP_EXISTS, "DoesNotExist": OP_DNE,
-                      "Gt": OP_GT, "Lt": OP_LT}.get(e.get("operator"))
-                key, vs = e.get("key", ""), list(e.get("values") or [])
-                if op is None or not is_qualified_name(key):
-                    return None
-                if op in (OP_IN, OP_NOTIN) and not vs:
-                    return None
-                if op in (OP_EXISTS, OP_DNE) and vs:
-                    return None
-                ival = 0
-                if op in (OP_GT, OP_LT):
-                    if len(vs) != 1 or parse_int64(vs[0]) is None:
-                        return None
-                    ival = parse_int64(vs[0])
-                    self.gtlt_keys.add(key)
-                if not all(is_valid_label_value(v) for v in vs):
-                    return None
-                rows.append((self.label_keys(key), op, tuple(self.values(v) for v in vs) if op < OP_EXISTS else (),
-                             ival))
-            return rows
-
-        def add_term(rows, weight=0):
-            off = len(reqs)
-            for key, op, vv, ival in rows:
-                reqs.append((key, op, len(vals), len(vv), ival))
-                vals.extend(vv)
-            terms.append((off, len(rows), weight, 0))
-            return len(terms) - 1
-
+        tab = SpecTable(sorted(scal), self.aff_in_play)
         for t in pending:
-            p = t["pod"]
-            ir, rr = t["initreq"], t["resreq"]
-            nzc = nzm = 0
-            for c in p.containers:
-                a, b = nonzero(c.req)
-                nzc += a
-                nzm += b
-            aff = p.affinity or {}
-            nodeaff = aff.get("nodeAffinity") if p.affinity is not None else None
-            tols = tuple(sorted((d.get("key", ""), d.get("operator", ""), d.get("value", ""), d.get("effect", ""))
-                                for d in p.tolerations))
-            port_list = []
-            for c in p.containers:
-                for pt in c.ports:
-                    hp = int(pt.get("hostPort", 0) or 0)
-                    if hp <= 0:
-                        continue
-                    port_list.append(((pt.get("protocol") or "TCP"), hp, pt.get("hostIP") or "0.0.0.0"))
-            best_effort = not any(M.CPU in c.req or M.MEMORY in c.req for c in list(p.containers) + list(p.init))
-            sig = (ir.cpu, ir.mem, tuple(sorted((ir.sc or {}).items())) if ir.sc is not None else None,
-                   rr.cpu, rr.mem, tuple(sorted((rr.sc or {}).items())) if rr.sc is not None else None,
-                   nzc, nzm, tuple(sorted(p.node_selector.items())), rp(nodeaff), tols, tuple(port_list),
-                   best_effort)
-            if self.aff_in_play:  # selectors and terms see the pod's namespace, labels and own terms
-                sig = sig + (p.ns, tuple(sorted(p.labels.items())), rp(aff.get("podAffinity")),
-                             rp(aff.get("podAntiAffinity")))
-            if sig in sig_index:
-                t["spec"] = sig_index[sig]
-                continue
-            flags = 0
-            if ir.sc is not None:
-                flags |= SPEC_INIT_HAS_MAP
-            if rr.sc is not None:
-                flags |= SPEC_REQ_HAS_MAP
-            if best_effort:
-                flags |= SPEC_BEST_EFFORT
-            if self.aff_in_play:
-                flags |= SPEC_POD_AFFINITY
-            imask = sum(1 << slot[k] for k in (ir.sc or {}))
-            rmask = sum(1 << slot[k] for k in (rr.sc or {}))
-            si = [0] * len(self.scalars)
-            sr = [0] * len(self.scalars)
-            for k, v in (ir.sc or {}).items():
-                si[slot[k]] = v
-            for k, v in (rr.sc or {}).items():
-                sr[slot[k]] = v
-            # nodeSelector: SelectorFromSet, any invalid pair => Everything (labels/selector.go:849-866)
-            sel_term = 0
-            if p.node_selector:
-                ok = all(is_qualified_name(k) and is_valid_label_value(v) for k, v in p.node_selector.items())
-                if ok:
-                    sel_term = add_term([(self.label_keys(k), OP_IN, (self.values(v),), 0)
-                                         for k, v in sorted(p.node_selector.items())])
-                    flags |= SPEC_HAS_SELECTOR
-            # required node affinity (MatchNodeSelectorTerms, helpers.go:302-333)
-            req_off, req_cnt = len(terms), 0
-            if nodeaff is not None and nodeaff.get("required") is not None:
-                flags |= SPEC_HAS_REQUIRED
-                built = []
-                for term in nodeaff["required"]:
-                    exprs = term.get("matchExpressions") or []
-                    fields = term.get("matchFields") or []
-                    if not exprs and not fields:
-                        built.append([])  # empty term: matches nothing
-                        continue
-                    rows = []
-                    if exprs:
-                        r = req_rows(exprs)
-                        rows.extend(r if r is not None else [(0, OP_FALSE, (), 0)])
-                    if fields:  # NodeSelectorRequirementsAsFieldSelector over {metadata.name: node.Name}
-                        for e in fields:
-                            op, vs = e.get("operator"), list(e.get("values") or [])
-                            if op not in ("In", "NotIn") or len(vs) != 1:
-                                rows = [(0, OP_FALSE, (), 0)]
-                                break
-                            if e.get("key") == "metadata.name":
-                                rows.append((self.label_keys("\x00metadata.name"), OP_IN if op == "In" else OP_NOTIN,
-                                             (self.values(vs[0]),), 0))
-                            else:
-                                truth = (vs[0] == "") if op == "In" else (vs[0] != "")
-                                rows.append((0, OP_TRUE if truth else OP_FALSE, (), 0))
-                    built.append(rows)
-                req_off = len(terms)
-                for rows in built:
-                    add_term(rows)
-                req_cnt = len(built)
-            # preferred node affinity (node_affinity.go:47-67)
-            pref_rows = []
-            if nodeaff is not None:
-                for pt in nodeaff.get("preferred") or []:
-                    w = int(pt.get("weight", 0))
-                    if w == 0:
-                        continue
-                    exprs = (pt.get("preference") or {}).get("matchExpressions") or []
-                    rows = req_rows(exprs) if exprs else []
-                    if rows is None:
-                        flags |= SPEC_NA_ERROR
-                        pref_rows = []
-                        break
-                    pref_rows.append((rows, w))
-            pref_off = len(terms)
-            for rows, w in pref_rows:
-                add_term(rows, w)
-            # tolerations
-            tol_id = self.tol_sets(tols)
-            if tol_id == len(self.tol_list):
-                self.tol_list.append([{"key": a, "operator": b, "value": c, "effect": d} for a, b, c, d in tols])
-            # ports
-            port_off = len(ports)
-            for proto, hp, ip in port_list:
-                s_id = self.port_slots((proto, hp))
-                ipi = self.port_ips.setdefault(s_id, _Interner())
-                if not ipi.ids:
-                    ipi("0.0.0.0")
-                ports.append((s_id, ipi(ip)))
-            specs.append((ir.cpu, ir.mem, rr.cpu, rr.mem, nzc, nzm, imask, rmask, flags, tol_id,
-                          len(sc_init) * len(self.scalars), sel_term, req_off, req_cnt, pref_off, len(pref_rows),
-                          port_off, len(ports) - port_off, len(specs) if self.aff_in_play else -1, 0))
-            sc_init.extend(si)
-            sc_req.extend(sr)
-            sig_index[sig] = len(specs) - 1
-            t["spec"] = sig_index[sig]
-        for s_id, ipi in self.port_ips.items():
-            if len(ipi.ids) > 63:
-                raise Unsupported("more than 62 host IPs for one (protocol, port)")
-        self.spec_arr = np.array(specs, dtype=SPEC_DTYPE) if specs else np.zeros(0, SPEC_DTYPE)
-        self.sc_init = np.array(sc_init, dtype=np.int64)
-        self.sc_req = np.array(sc_req, dtype=np.int64)
-        self.term_arr = np.array(terms, dtype=TERM_DTYPE) if terms else np.zeros(0, TERM_DTYPE)
-        self.req_arr = np.array(reqs, dtype=REQ_DTYPE) if reqs else np.zeros(0, REQ_DTYPE)
-        self.val_arr = np.array(vals, dtype=np.int32)
-        self.port_arr = np.array(ports, dtype=PORT_DTYPE) if ports else np.zeros(0, PORT_DTYPE)
+            t["spec"] = tab.add(t["pod"], t["initreq"], t["resreq"])
+        tab.finish(self)
 
     # ---------------- node SoA ----------------
     def _node_table(self):
@@ -806,6 +826,31 @@ class Snapshot:
                                 dtype=np.dtype([("tier", "<i4"), ("plugin", "<i4"), ("enable", "<u4"),
                                                 ("pad", "<i4")])) if self.tier_plugins else \
             np.zeros(0, dtype=np.dtype([("tier", "<i4"), ("plugin", "<i4"), ("enable", "<u4"), ("pad", "<i4")]))
+
+    # ---------------- inputs of the affinity tables (affinity.Tables.build) ----------------
+    def slot_domains(self, keys):
+        """Topology domain of every session node for the key tuple (-1: a key missing) and the domain count."""
+        ids, dom = {}, np.full(self.n_nodes, -1, np.int32)
+        for i, nd in enumerate(self.nodes):
+            labels = nd["node"].labels
+            if all(k in labels for k in keys):
+                dom[i] = ids.setdefault(tuple(labels[k] for k in keys), len(ids))
+        return dom, len(ids)
+
+    def aff_groups(self, unsupported):
+        """Lister pods, existing pods and every spec's pending pod, one pod per group here."""
+        lister = []
+        for t in self.session_tasks:
+            if allocated_status(t["status"]):
+                if t["pod"].node not in self.node_index:
+                    raise unsupported("lister pod on a node outside the session (predicates.go: failed to find node)")
+                lister.append((t["pod"], [self.node_index[t["pod"].node]], [t["uid"]]))
+        existing = [(t["pod"], [i]) for i, nd in enumerate(self.nodes) for t in nd["tasks"]]
+        pending = {}
+        for t in self.session_tasks:
+            if "spec" in t and t["status"] == ST["Pending"]:
+                pending.setdefault(t["spec"], t["pod"])
+        return lister, existing, [pending[s] for s in range(len(self.spec_arr))]
 
     # ---------------- helpers ----------------
     def node_names(self):

@@ -15,7 +15,8 @@ from oracle import pyoracle
 from scheduler_amd import model as m
 
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.json"))
-                if not os.path.basename(p).startswith("digest-"))  # full-size digests: test_gpu_digest.py
+                if not os.path.basename(p).startswith(("digest-", "ref-e2e-")))  # own formats: test_gpu_digest.py,
+# test_e2e_ref.py
 IDS = [os.path.basename(p)[:-5] for p in GOLDEN]
 
 
