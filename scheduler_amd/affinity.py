@@ -280,10 +280,14 @@ class Tables:
             e_classes[ck] = self.table(("E",) + ck, (ck[2],), AFF_EXISTING_ANTI)
         # which specs match each existing-anti class (the incoming pod is matched against the term)
         spec_ids = [pod_ident(p) for p in spec_pod]
+        spec_lab = defaultdict(set)  # (label key, value) -> specs: candidates of a term's In requirements
+        for s, p in enumerate(spec_pod):
+            for lk, lv in p.labels.items():
+                spec_lab[(lk, lv)].add(s)
         for (ns, sel, key), tid in e_classes.items():
             term = Term.__new__(Term)
             term.ns, term.sel, term.key = ns, sel, key
-            for s in range(m):
+            for s in sorted(_candidates([term], spec_lab, range(m))):
                 if term.matches(spec_pod[s].ns, spec_pod[s].labels):
                     checks[s].append((tid, AFF_EXISTING_ANTI))
         # the pod's own terms (satisfiesPodsAffinityAntiAffinity, :1401-1457): an affinity error comes from

@@ -78,10 +78,12 @@ def _qname_fmt(s):
     return bool(s) and _alnum(s[0]) and _alnum(s[-1]) and all(_alnum(c) or c in "-_." for c in s)
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def is_qualified_name(v: str) -> bool:
     return not qualified_name_errors(v)
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def is_valid_label_value(v: str) -> bool:
     return not label_value_errors(v)
 
