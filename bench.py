@@ -422,29 +422,30 @@ def shard_side(args, dist, rank, world, device):
 
 
 EVAL_SPECS, EVAL_NODES = 256, 50000
+EVAL_OUT_BYTES = 8  # kb_eval32: u32 reason mask + i32 score per (spec, node)
 
 
 def eval_side(device):
     """The fit/score sweep on its own (kb_eval): reasons + scores of EVAL_SPECS specs x
-    EVAL_NODES nodes (a C2-shaped table, one spec per job). HIP events around the kernel; algorithmic bytes
-    = the output (4 B reason mask + 8 B score per pair) + one read of every node row (76 B), the least HBM
-    traffic the sweep needs. Measured HBM bytes come from the committed rocprofv3 PMC pass (pmc_traffic)."""
+    EVAL_NODES nodes (a C2-shaped table, one spec per job), through kb_eval32. HIP events around the kernel;
+    algorithmic bytes = the output (4 B reason mask + 4 B score per pair) + one read of every node row (76 B),
+    the least HBM traffic the sweep needs. Measured HBM bytes come from the committed rocprofv3 PMC pass."""
     from scheduler_amd import runtime, synth
     try:
         snap = synth.c2_snapshot(n_nodes=EVAL_NODES, n_jobs=EVAL_SPECS, tasks_per_job=1, seed=synth.SEED)
         ctx = runtime.Context(device, timing=True)
         ctx.upload(snap)
         ids = (np.arange(EVAL_SPECS) % len(snap.spec_arr)).astype(np.int32)  # (equal requests share a spec)
-        ctx.eval(ids)  # warm-up
+        ctx.eval32(ids)  # warm-up
         ctx.stats(reset=True)
         for _ in range(5):
-            ctx.eval(ids)
+            ctx.eval32(ids)
         st = ctx.stats()
         ctx.close()
         k = runtime.KERNELS.index("eval_kernel")
         us = st["kernel_ms"][k] * 1e3 / max(1, st["launches"][k])
         pairs = len(ids) * EVAL_NODES
-        alg = pairs * 12 + EVAL_NODES * 76
+        alg = pairs * EVAL_OUT_BYTES + EVAL_NODES * 76
         out = {"kernel": "eval_kernel", "bound": "hbm", "specs": len(ids), "nodes": EVAL_NODES,
                "avg_launch_us": round(us, 3), "algorithmic_bytes_per_launch": alg,
                "achieved": round(alg / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

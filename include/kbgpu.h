@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 9
+#define KBGPU_ABI_VERSION 10
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -350,6 +350,14 @@ int kb_place_job(kb_ctx* ctx, const kb_job_req* job, int32_t* placed_node, int32
  * scheduler_helper.go:107-127).
  */
 int kb_eval(kb_ctx* ctx, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores);
+
+/*
+ * kb_eval with 32-bit scores: 8 B per (spec, node) pair instead of 12 (the sweep's output is most of its HBM
+ * traffic). KB_E_UNSUPPORTED when a spec's score cannot be held in int32: its |score| bound (the weighted
+ * LeastRequested / Balanced / NodeAffinity / InterPodAffinity maxima plus the overlay's) reaches 2^31, or its
+ * InterPodAffinity batch score errors (kb_eval reports those with a score below every int32).
+ */
+int kb_eval32(kb_ctx* ctx, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int32_t* scores);
 
 /*
  * preempt's use of the sweep (actions/preempt/preempt.go:189-195): PredicateNodes with Session.PredicateFn

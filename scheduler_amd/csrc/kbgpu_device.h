@@ -150,6 +150,8 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream);
+void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, void* stream);
 int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;

@@ -785,9 +785,9 @@ done:
 // scalar loads), writing one coalesced 4 B + 8 B pair per spec. HBM traffic is the 12 B/pair of output; the
 // 76 B row is read once per kEvalSpecs specs.
 constexpr int kEvalSpecs = 16;
-template <bool AFF>
+template <bool AFF, class SCORE>
 __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids, int t,
-                                                   uint32_t* reasons, int64_t* scores, const int64_t* mm) {
+                                                   uint32_t* reasons, SCORE* scores, const int64_t* mm) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N.n) return;
   const int j0 = blockIdx.y * kEvalSpecs;
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
     const kb_spec sp = P.specs[s];
     const uint64_t st = static_eval<AFF>(N, P, C, sp, s, r.flags, n, AFF ? mm + 2 * j : nullptr);
     reasons[(size_t)j * N.n + n] = row_reasons(N, P, C, sp, P.sc_init + (size_t)s * N.S, r, st, n);
-    scores[(size_t)j * N.n + n] = row_score_inv(C, sp, r, st, ic, im);
+    scores[(size_t)j * N.n + n] = (SCORE)row_score_inv(C, sp, r, st, ic, im);
   }
 }
 
@@ -5022,15 +5022,24 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                      J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
-void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
+template <class SCORE>
+static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
+                          uint32_t* reasons, SCORE* scores, const int64_t* mm, void* stream) {
   dim3 grid((N.n + 255) / 256, (t + kEvalSpecs - 1) / kEvalSpecs);
   if (mm)
-    hipLaunchKernelGGL(eval_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, reasons,
-                       scores, mm);
+    hipLaunchKernelGGL((eval_kernel<true, SCORE>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+                       reasons, scores, mm);
   else
-    hipLaunchKernelGGL(eval_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, reasons,
-                       scores, mm);
+    hipLaunchKernelGGL((eval_kernel<false, SCORE>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+                       reasons, scores, mm);
+}
+void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, stream);
+}
+void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, stream);
 }
 
 // kb_apply: one thread per row delta of a commit made outside the device -- NodeInfo.AddTask / RemoveTask

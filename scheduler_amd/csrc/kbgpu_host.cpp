@@ -1475,7 +1475,33 @@ int kb_job_finish(kb_ctx* c, int slot, int32_t* placed_node, int32_t* placed_kin
   return place_finish(c, slot, placed_node, placed_kind, result, skipped != 0);
 }
 
-static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores);
+extern "C++" {
+template <class SCORE>
+static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, SCORE* scores);
+}
+
+int kb_eval32(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int32_t* scores) {
+  if (c) c->timing_now = c->timing;
+  if (c) c->prev_listed = false;
+  if (!c || (!spec_ids && t)) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
+  if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs first");
+  const DevCfg& C = c->cfg;
+  for (uint32_t i = 0; i < t; ++i) {
+    const int s = spec_ids[i];
+    if (s < 0 || s >= c->P.m) return fail(c, KB_E_INVALID, "spec id %d", s);
+    if (c->spec_needs_aff[s] && !c->aff_ok)
+      return fail(c, KB_E_UNSUPPORTED, "spec %d has pod (anti)affinity: upload the affinity tables first", s);
+    const int64_t ov = (size_t)s < c->ov_absmax.size() ? c->ov_absmax[s] : 0;
+    const long double bound = 10.0L * std::llabs((long long)C.w_lr) + 10.0L * std::llabs((long long)C.w_bra) +
+                              (long double)c->spec_pref_weight[s] * std::llabs((long long)C.w_na) + (long double)ov +
+                              10.0L * std::llabs((long long)C.w_pa);
+    if (bound >= 2147483647.0L || ((size_t)s < c->spec_ipa_err.size() && c->spec_ipa_err[s]))
+      return fail(c, KB_E_UNSUPPORTED, "spec %d: its score does not fit int32 (use kb_eval)", s);
+  }
+  HIP_OK(c, hipSetDevice(c->device));
+  return eval_impl(c, spec_ids, t, reasons, scores);
+}
 
 int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
   if (c) c->timing_now = c->timing;
@@ -1496,21 +1522,23 @@ int kb_eval(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, i
 int kb_node_reasons(kb_ctx* c, int spec, uint32_t* reasons) {
   const bool tn = c->timing_now;
   c->timing_now = false;
-  const int rc = eval_impl(c, &spec, 1, reasons, nullptr);
+  const int rc = eval_impl<int64_t>(c, &spec, 1, reasons, nullptr);
   c->timing_now = tn;
   return rc;
 }
 
-static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, int64_t* scores) {
+extern "C++" {
+template <class SCORE>
+static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* reasons, SCORE* scores) {
   const size_t n = (size_t)c->N.n;
   const uint32_t chunk = 8192;
   int32_t* d_ids;
   uint32_t* d_r;
-  int64_t* d_s;
+  SCORE* d_s;
   const uint32_t tc = std::min(t, chunk);
   HIP_OK(c, hipMalloc(&d_ids, std::max<uint32_t>(tc, 1) * 4));
   HIP_OK(c, hipMalloc(&d_r, std::max<size_t>(tc * n, 1) * 4));
-  HIP_OK(c, hipMalloc(&d_s, std::max<size_t>(tc * n, 1) * 8));
+  HIP_OK(c, hipMalloc(&d_s, std::max<size_t>(tc * n, 1) * sizeof(SCORE)));
   int rc = KB_OK;
   for (uint32_t b = 0; b < t && rc == KB_OK; b += chunk) {
     const uint32_t cnt = std::min(chunk, t - b);
@@ -1527,12 +1555,16 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
       launch_ipa_minmax(c->N, c->P, d_ids, 0, (int)cnt, c->mm_eval, nullptr, c->stream);
     }
     c->ev_begin(&ea);
-    launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
+    if constexpr (sizeof(SCORE) == 8)
+      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
+    else
+      launch_eval32(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
     c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
     if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
     if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))
       rc = KB_E_HIP;
-    if (scores && hipMemcpyAsync(scores + (size_t)b * n, d_s, cnt * n * 8, hipMemcpyDeviceToHost, c->stream))
+    if (scores && hipMemcpyAsync(scores + (size_t)b * n, d_s, cnt * n * sizeof(SCORE), hipMemcpyDeviceToHost,
+                                 c->stream))
       rc = KB_E_HIP;
     if (hipStreamSynchronize(c->stream) != hipSuccess) rc = KB_E_HIP;
   }
@@ -1543,6 +1575,7 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
   if (rc) return fail(c, rc, "kb_eval: HIP failure");
   return KB_OK;
 }
+}  // extern "C++"
 
 // The keys of kb_sort_nodes / kb_predicate_nodes (PredicateFn without allocate's resource check +
 // PrioritizeNodes) into h, sorted descending or in node order.

@@ -128,10 +128,10 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 9  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 10  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
-           "kb_upload_specs", "kb_place_job", "kb_eval", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
+           "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
            "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl",
            "kb_set_host_overlay", "kb_apply", "kb_set_nofit_hook", "kb_sort_nodes", "kb_predicate_nodes"]
 
@@ -166,6 +166,7 @@ def load_library(path: str = LIB_PATH):
     lib.kb_upload_affinity.argtypes = [P, C.POINTER(kb_affinity)]
     lib.kb_place_job.argtypes = [P, C.POINTER(kb_job_req), P, P, C.POINTER(kb_job_result)]
     lib.kb_eval.argtypes = [P, P, C.c_uint32, P, P]
+    lib.kb_eval32.argtypes = [P, P, C.c_uint32, P, P]
     lib.kb_read_nodes.argtypes = [P] + [P] * 7
     lib.kb_allocate.argtypes = [P, C.POINTER(kb_session), C.POINTER(kb_cycle_result)]
     lib.kb_restore_nodes.argtypes = [P]
@@ -332,6 +333,15 @@ class Context:
         reasons = np.zeros((len(ids), n), np.uint32)
         scores = np.zeros((len(ids), n), np.int64)
         self._check(self.lib.kb_eval(self.ctx, _ptr(ids), len(ids), _ptr(reasons), _ptr(scores)))
+        return reasons, scores
+
+    def eval32(self, spec_ids):
+        """kb_eval32: the same with 32-bit scores (KbError KB_E_UNSUPPORTED when a spec's scores do not fit)."""
+        ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
+        n = self.n_nodes
+        reasons = np.zeros((len(ids), n), np.uint32)
+        scores = np.zeros((len(ids), n), np.int32)
+        self._check(self.lib.kb_eval32(self.ctx, _ptr(ids), len(ids), _ptr(reasons), _ptr(scores)))
         return reasons, scores
 
     def sort_nodes(self, spec: int):

@@ -18,11 +18,11 @@ def main():
     ctx = runtime.Context(0, timing=True)
     ctx.upload(snap)
     ids = (np.arange(SPECS) % len(snap.spec_arr)).astype(np.int32)
-    ctx.eval(ids)
+    ctx.eval32(ids)
     ctx.stats(reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
-        ctx.eval(ids)
+        ctx.eval32(ids)
     el = time.perf_counter() - t0
     st = ctx.stats()
     k = runtime.KERNELS.index("eval_kernel")

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "kbgpu.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(kb_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(kb_[a-z_0-9]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 9
+    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 10
 
 
 def test_struct_layouts_match_header():

@@ -70,6 +70,26 @@ def test_eval_masks_and_scores(name, cluster):
         assert list(scores[i]) == rt["score"], s
 
 
+@pytest.mark.parametrize("name,cluster", CLUSTERS, ids=[c[0] for c in CLUSTERS])
+def test_eval32_equals_eval(name, cluster):
+    """kb_eval32 (int32 scores, 8 B per pair) returns kb_eval's reasons and scores wherever they fit."""
+    snap = E.Snapshot(cluster)
+    ids = list(range(len(snap.spec_arr)))
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        r64, s64 = ctx.eval(ids)
+        try:
+            r32, s32 = ctx.eval32(ids)
+        except runtime.KbError as e:  # only for scores beyond int32 (IPA batch errors)
+            assert e.code == runtime.KB_E_UNSUPPORTED and (np.abs(s64) >= 2 ** 31).any()
+            return
+    finally:
+        ctx.close()
+    assert np.array_equal(r32, r64)
+    assert np.array_equal(s32.astype(np.int64), s64)
+
+
 def test_full_size_c2_properties():
     """BASELINE configs[1] at full size (10k x 100k): size-independent invariants, determinism, and
     identical placements from the two device paths."""
