@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 10
+#define KBGPU_ABI_VERSION 11
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -467,6 +467,27 @@ typedef struct kb_row_delta {
 } kb_row_delta;
 int kb_apply(kb_ctx* ctx, const kb_row_delta* deltas, uint32_t k, const int64_t* sc, uint32_t n_sc,
              const kb_port* ports, uint32_t n_ports);
+
+/*
+ * Inter-pod affinity table updates for a pod that is not one of the session's pending specs (kb_row_delta.spec
+ * cannot name it): a pod bound or deleted by the Go side (schedulercache AddPod / RemovePod reach the
+ * InterPodAffinity priority's NodeInfo pods, cache/node_info.go:498-630), or a session task entering or leaving
+ * the predicate lister (PodLister.UpdateTask, plugins/util/util.go:108-130: an eviction makes a Running task
+ * Releasing, so it leaves the lister but stays on its node). table >= 0: the count table's counter at the node's
+ * domain of the table's slot (none when the node has no domain there) and the table's total, both += weight.
+ * table == -1: the InterPodAffinity histogram entry h[h_off + the node's domain of `slot`] += weight.
+ * scheduler_amd/affinity.py Tables.pod_deltas derives the entries from the pod's labels and terms; a pod whose
+ * terms would need a table or histogram the session's specs do not have is refused there (re-export instead).
+ */
+typedef struct kb_aff_delta {
+  int32_t node;   /* canonical index */
+  int32_t table;  /* count table id, or -1: a histogram entry */
+  int32_t slot;   /* histogram: its topology slot (single-key) */
+  uint32_t h_off; /* histogram: its offset into kb_affinity.h */
+  int32_t weight;
+  int32_t pad;
+} kb_aff_delta;
+int kb_apply_affinity(kb_ctx* ctx, const kb_aff_delta* deltas, uint32_t k);
 
 /*
  * Called by kb_allocate when a task of a spec with host-evaluated stages (an overlay, or KB_AFF_ERROR

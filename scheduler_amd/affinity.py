@@ -517,11 +517,69 @@ class Tables:
         self.h = H.astype(np.int32)
         self.incr_arr = np.array(inc, IPA_INCR_DTYPE) if inc else np.zeros(0, IPA_INCR_DTYPE)
         self.n_self_dynamic = sum(1 for f in flags if f & AFF_SELF_DYNAMIC)
+        # what pod_deltas needs to place a pod outside the pending specs into these tables
+        self._paff, self._bc, self._e_classes, self._all_t, self._spec_pod, self._h_off = \
+            paff, bc, e_classes, all_t, spec_pod, h_off
+        self._incoming_bad = any(first_invalid(incoming_terms(paff(p))) is not None for p in spec_pod)
+        self._nodeorder = bool(snap.config["nodeorder_enabled"])
         from .export import SPEC_IPA_ERROR
         for s in range(m):
             if self.ipa_error[s]:
                 snap.spec_arr["flags"][s] |= SPEC_IPA_ERROR
         return self
+
+    def pod_deltas(self, pod, node, lister=0, existing=0):
+        """kb_apply_affinity entries (node, table, slot, h_off, weight) for a pod that is not one of the session's
+        pending specs, on session node `node`: `lister` = +1 / -1 when it joins / leaves the predicate lister (an
+        allocated-status session task, util.go:57-130), `existing` = +1 / -1 when it is bound to / removed from the
+        node (the InterPodAffinity priority's NodeInfo pods, interpod_affinity.go:150-187). The entries are the
+        counts build() would have made with the pod there. Unsupported when the pod would need a table or a
+        histogram the pending specs do not have, or would change the error paths (invalid selectors)."""
+        U = self.U
+        a = PodAff(pod, U)  # (build's cache is keyed by object id: only for pods it keeps alive)
+        out = []
+        if lister:
+            if any(t.invalid for t in a.req_anti):
+                raise U("a lister pod with an invalid anti-affinity selector changes the error strings")
+            for term in a.req_anti:
+                if not term.key:
+                    continue
+                tid = self._e_classes.get((term.ns, term.sel, term.key))
+                if tid is None:
+                    if any(term.matches(p.ns, p.labels) for p in self._spec_pod):
+                        raise U("the pod's required anti-affinity term is a class no table holds")
+                    continue  # no pending spec matches the term: no check reads it
+                out.append((node, tid, -1, 0, lister))
+            if self._all_t is not None:
+                out.append((node, self._all_t, -1, 0, lister))
+            for tid, terms in self._bc.items():
+                if _all_match(terms, pod.ns, pod.labels):
+                    out.append((node, tid, -1, 0, lister))
+        if existing and self._nodeorder:
+            own = (a.req_aff + [t for _, t in a.pref_aff] if a.has_pod else []) + \
+                  ([t for _, t in a.pref_anti] if a.has_anti else [])
+            if any(t.invalid for t in own) or self._incoming_bad:
+                raise U("invalid inter-pod affinity score terms: the batch score error depends on the pods present")
+            mine = ([(1, t) for t in a.req_aff] + list(a.pref_aff) if a.has_pod else []) + \
+                   ([(-w, t) for w, t in a.pref_anti] if a.has_anti else [])
+            for s, sp in enumerate(self._spec_pod):
+                b = self._paff(sp)
+                W = defaultdict(int)
+                theirs = (list(b.pref_aff) if b.has_pod else []) + ([(-w, t) for w, t in b.pref_anti] if b.has_anti else [])
+                for w, term in theirs:  # the incoming spec's terms against this pod
+                    if term.key and w and term.matches(pod.ns, pod.labels):
+                        W[term.key] += w
+                for w, term in mine:  # this pod's own terms against the spec's pod
+                    if term.key and w and term.matches(sp.ns, sp.labels):
+                        W[term.key] += w
+                for key, w in sorted(W.items()):
+                    if not w:
+                        continue
+                    h = self._h_off.get((s, key))
+                    if h is None:
+                        raise U("the pod's score terms need a histogram the spec does not have")
+                    out.append((node, -1, self.slot_ids[(key,)], h, w * existing))
+        return out
 
     def host_error_string(self, pod, spec, node_name, allocated_before):
         """The FitErrors string of a node the device failed with KB_R_HOST_ERROR at the affinity stage: the

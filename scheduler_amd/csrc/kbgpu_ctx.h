@@ -31,6 +31,7 @@ struct kb_ctx {
   std::vector<char> spec_cap1;     // per spec: kSpecCap1 (a selection run with at most one Allocate per node)
   std::vector<int32_t> spec_cls;   // per spec: the class loop's finest dynamic slot (-1: not eligible)
   std::vector<int64_t> aff_slot_D;  // per topology slot: its domain count
+  uint32_t aff_n_tables = 0, aff_n_h = 0;  // kb_apply_affinity's bounds
   uint64_t* cls_lvl = nullptr;  // [kClsLevels][n] class loop scratch: keys after 1..kClsLevels commits
   int32_t* cls_amax = nullptr;  // [n] class loop scratch: Allocates before Idle stops fitting
   // per topology slot that is some spec's class slot: its classes as member lists (offsets [K + 1], node ids

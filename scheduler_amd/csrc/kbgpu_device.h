@@ -270,6 +270,8 @@ constexpr int kBitonicMin = 2048;  // == the sort's LDS tile
 // power of two >= max(n, 2048); mm: the spec's InterPodAffinity min / max (affinity tables) or null.
 void launch_sort_nodes(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, const int64_t* mm,
                        uint64_t* keys, int n_pad, void* stream, bool sort = true);
+// kb_apply_affinity: table / histogram entries of a pod outside the session's specs (indices checked by the host).
+void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, void* stream);
 // kb_apply: row deltas of commits made outside the device (one thread per delta, atomics).
 void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
                   const kb_port* ports, void* stream);

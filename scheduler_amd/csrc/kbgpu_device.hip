@@ -5090,6 +5090,26 @@ void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, i
     hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, N, P, d, k, sc, ports, pass);
 }
 
+// kb_apply_affinity: one thread per table / histogram entry of a pod outside the session's pending specs.
+__global__ __launch_bounds__(256) void apply_aff_kernel(DevAff A, const kb_aff_delta* d, int k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  const kb_aff_delta e = d[i];
+  if (e.table >= 0) {
+    const kb_aff_table tb = A.tables[e.table];
+    const int32_t dom = A.topo_dom[(size_t)tb.slot * A.n + e.node];
+    if (dom >= 0) atomicAdd(&A.counters[tb.cnt_off + dom], e.weight);
+    atomicAdd(&A.totals[e.table], e.weight);
+  } else {
+    const int32_t dom = A.topo_dom[(size_t)e.slot * A.n + e.node];
+    if (dom >= 0) atomicAdd(&A.h[e.h_off + dom], e.weight);
+  }
+}
+
+void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, void* stream) {
+  hipLaunchKernelGGL(apply_aff_kernel, dim3((k + 255) / 256), dim3(256), 0, (hipStream_t)stream, A, d, k);
+}
+
 // ---- preempt's sweep (actions/preempt/preempt.go:189-195): PredicateNodes with Session.PredicateFn (no
 // resource check), PrioritizeNodes, SortNodes (util/scheduler_helper.go:132-144): every feasible node by score,
 // descending, lowest index first among equal scores. The 64-bit keys (score << 24 | ~index) sort in exactly

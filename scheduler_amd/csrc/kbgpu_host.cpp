@@ -555,6 +555,8 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
     }
   }
   c->aff_slot_D = D;
+  c->aff_n_tables = a->n_tables;
+  c->aff_n_h = a->n_h;
   classify_self_dynamic(c, a, D, specs);
   // member lists of every class slot: class k = domain k, class D = the nodes without a domain
   c->cls_coff.assign(a->n_slots, nullptr);
@@ -1791,6 +1793,39 @@ int kb_apply(kb_ctx* c, const kb_row_delta* d, uint32_t k, const int64_t* sc, ui
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   free_all(tmp);
   if (e != hipSuccess) return fail(c, KB_E_HIP, "kb_apply: %s", hipGetErrorString(e));
+  return KB_OK;
+}
+
+int kb_apply_affinity(kb_ctx* c, const kb_aff_delta* d, uint32_t k) {
+  if (!c || (!d && k)) return KB_E_INVALID;
+  if (int rc_ = kb_engine_stop(c)) return rc_;
+  if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
+  if (!c->aff_ok) return fail(c, KB_E_STATE, "upload the affinity tables first");
+  if (c->fed || c->any_busy()) return fail(c, KB_E_STATE, "a job is in flight");
+  if (k == 0) return KB_OK;
+  const auto& D = c->aff_slot_D;
+  for (uint32_t i = 0; i < k; ++i) {  // every index the kernel follows
+    const kb_aff_delta& e = d[i];
+    if (e.node < 0 || e.node >= c->N.n) return fail(c, KB_E_INVALID, "affinity delta %u: node %d", i, e.node);
+    if (e.table >= 0) {
+      if ((uint32_t)e.table >= c->aff_n_tables) return fail(c, KB_E_INVALID, "affinity delta %u: table %d", i, e.table);
+    } else if (e.table != -1 || e.slot < 0 || (size_t)e.slot >= D.size() ||
+               (int64_t)e.h_off + D[e.slot] > (int64_t)c->aff_n_h) {
+      return fail(c, KB_E_INVALID, "affinity delta %u: histogram (slot %d, h_off %u)", i, e.slot, e.h_off);
+    }
+  }
+  HIP_OK(c, hipSetDevice(c->device));
+  std::vector<void*> tmp;
+  kb_aff_delta* dd;
+  if (int rc = upload(c, tmp, &dd, d, k)) {
+    free_all(tmp);
+    return rc;
+  }
+  launch_apply_aff(c->P.A, dd, (int)k, c->stream);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  free_all(tmp);
+  if (e != hipSuccess) return fail(c, KB_E_HIP, "kb_apply_affinity: %s", hipGetErrorString(e));
   return KB_OK;
 }
 

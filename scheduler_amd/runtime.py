@@ -67,6 +67,18 @@ ROW_DELTA_DTYPE = np.dtype([("node", "<i4"), ("pods", "<i4"), ("idle_cpu", "<i8"
                             ("flags_set", "<u4"), ("flags_clear", "<u4"), ("spec", "<i4"), ("kind", "<i4"),
                             ("sc_off", "<u4"), ("port_off", "<u4"), ("port_cnt", "<u4"), ("pad", "<i4")], align=True)
 assert ROW_DELTA_DTYPE.itemsize == 88
+# kb_aff_delta (kb_apply_affinity)
+AFF_DELTA_DTYPE = np.dtype([("node", "<i4"), ("table", "<i4"), ("slot", "<i4"), ("h_off", "<u4"), ("weight", "<i4"),
+                            ("pad", "<i4")])
+assert AFF_DELTA_DTYPE.itemsize == 24
+
+
+def aff_delta_array(entries):
+    """Pack (node, table, slot, h_off, weight) entries (affinity.Tables.pod_deltas) into kb_aff_delta records."""
+    d = np.zeros(len(entries), AFF_DELTA_DTYPE)
+    for i, (node, table, slot, h_off, weight) in enumerate(entries):
+        d[i] = (node, table, slot, h_off, weight, 0)
+    return d
 
 
 def shard_range(n_total: int, rank: int, world: int):
@@ -128,12 +140,12 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 10  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 11  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
            "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl",
-           "kb_set_host_overlay", "kb_apply", "kb_set_nofit_hook", "kb_sort_nodes", "kb_predicate_nodes"]
+           "kb_set_host_overlay", "kb_apply", "kb_apply_affinity", "kb_set_nofit_hook", "kb_sort_nodes", "kb_predicate_nodes"]
 
 _lib = None
 
@@ -176,6 +188,7 @@ def load_library(path: str = LIB_PATH):
     lib.kb_set_shard_rccl.argtypes = [P, C.POINTER(kb_shard), P]
     lib.kb_set_host_overlay.argtypes = [P, C.c_int32, P, P]
     lib.kb_apply.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32]
+    lib.kb_apply_affinity.argtypes = [P, P, C.c_uint32]
     lib.kb_set_nofit_hook.argtypes = [P, NOFIT_FN, P]
     lib.kb_sort_nodes.argtypes = [P, C.c_int32, P, P, C.POINTER(C.c_uint32)]
     lib.kb_predicate_nodes.argtypes = [P, C.c_int32, P, C.POINTER(C.c_uint32), P]
@@ -304,6 +317,12 @@ class Context:
         sc = np.ascontiguousarray(np.asarray(sc if sc is not None else [], dtype=np.int64))
         pt = np.ascontiguousarray(np.asarray(ports if ports is not None else [], dtype=E.PORT_DTYPE))
         self._check(self.lib.kb_apply(self.ctx, _ptr(d), len(d), _ptr(sc), len(sc), _ptr(pt), len(pt)))
+
+    def apply_affinity(self, deltas):
+        """kb_apply_affinity: inter-pod affinity table / histogram entries of pods outside the session's pending
+        specs (AFF_DELTA_DTYPE records; affinity.Tables.pod_deltas derives them)."""
+        d = np.ascontiguousarray(np.asarray(deltas, dtype=AFF_DELTA_DTYPE))
+        self._check(self.lib.kb_apply_affinity(self.ctx, _ptr(d), len(d)))
 
     def _hook(self):
         """Collect the per-node reason masks kb_allocate hands over at a NO_FIT with host-evaluated stages."""

@@ -109,3 +109,101 @@ def test_apply_removal_is_the_inverse():
     assert any(not np.array_equal(before[k], mid[k]) for k in before)
     for k in before:
         assert np.array_equal(before[k], after[k]), k
+
+
+# ---- kb_apply_affinity: inter-pod affinity tables for pods outside the pending specs ----
+def _aff_pair(seed):
+    """(A, B, bound, evicted): A = affinity_edge_cluster(seed) plus loose pods (no PodGroup: scored, not listed)
+    that copy the running pods' labels and terms, with one running lister task of B evicted (Releasing: it leaves
+    the lister, stays on its node); B is A without the loose pods and without the eviction."""
+    from helpers import affinity_edge_cluster
+    b = affinity_edge_cluster(seed)
+    a = copy.deepcopy(b)
+    rng = np.random.default_rng(seed)
+    names = sorted(n.name for n in a.nodes)
+    src = [p for p in a.pods if p.node and p.affinity]
+    bound = []
+    for i in range(8):
+        s = src[int(rng.integers(0, len(src)))]
+        p = m.Pod(ns=s.ns, name=f"loose-x{i}", uid=f"{s.ns}-loose-x{i}", node=names[int(rng.integers(0, len(names)))],
+                  phase="Running", labels=dict(s.labels), affinity=copy.deepcopy(s.affinity),
+                  containers=[m.Container(req={m.CPU: 100, m.MEMORY: GI // 8})])
+        bound.append(p)
+    a.pods = list(a.pods) + bound
+    victim = next(p for p in a.pods if p.group == "db")
+    victim.deleting = True
+    before = next(p for p in b.pods if p.uid == victim.uid)
+    return a, b, bound, (before, victim)
+
+
+def _aff_deltas(sb, bound, evicted):
+    tb = sb.aff
+    rows, ad = [], []
+    for p in bound:
+        w = sb.node_index[p.node]
+        rows.append(E.pod_delta(sb, p, w))
+        ad += tb.pod_deltas(p, w, existing=1)
+    before, after = evicted
+    w = sb.node_index[before.node]
+    rows += [E.pod_delta(sb, before, w, remove=True), E.pod_delta(sb, after, w)]
+    ad += tb.pod_deltas(before, w, lister=-1)  # Running -> Releasing: out of the lister, still on the node
+    return rows, runtime.aff_delta_array(ad)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_pod_affinity_deltas_rebuild_the_tables(seed):
+    a, b, bound, evicted = _aff_pair(seed)
+    sa, sb = E.Snapshot(a), E.Snapshot(b)
+    for f in ("topo_dom", "table_arr", "spec_arr", "check_arr", "lister_arr", "hist_arr", "incr_arr"):
+        assert np.array_equal(getattr(sa.aff, f), getattr(sb.aff, f)), f  # the same layout
+    _, ad = _aff_deltas(sb, bound, evicted)
+    assert len(ad) and (ad["table"] >= 0).any() and (ad["table"] < 0).any()
+    cnt, tot, h = sb.aff.counters.copy(), sb.aff.totals.copy(), sb.aff.h.copy()
+    for e in ad:  # what apply_aff_kernel does, in numpy
+        if e["table"] >= 0:
+            slot, off = sb.aff.table_arr[e["table"]]
+            d = sb.aff.topo_dom[slot, e["node"]]
+            if d >= 0:
+                cnt[off + d] += e["weight"]
+            tot[e["table"]] += e["weight"]
+        else:
+            d = sb.aff.topo_dom[e["slot"], e["node"]]
+            if d >= 0:
+                h[e["h_off"] + d] += e["weight"]
+    assert np.array_equal(cnt, sa.aff.counters)
+    assert np.array_equal(tot, sa.aff.totals)
+    assert np.array_equal(h, sa.aff.h)
+    assert not np.array_equal(h, sb.aff.h) and not np.array_equal(tot, sb.aff.totals)
+
+
+def test_pod_affinity_deltas_refuse_new_tables():
+    """A bound pod whose terms score a spec on a topology key the spec has no histogram for is refused."""
+    b = __import__("helpers").affinity_edge_cluster(11)
+    sb = E.Snapshot(b)
+    p = m.Pod(ns="ns", name="odd", uid="ns-odd", node=sb.node_names()[0], phase="Running", labels={"app": "odd"},
+              affinity={"podAffinity": {"preferred": [{"weight": 5, "podAffinityTerm": {
+                  "labelSelector": {"matchLabels": {"job": "plain"}}, "topologyKey": "brand-new-key"}}]}},
+              containers=[m.Container(req={m.CPU: 100})])
+    with pytest.raises(E.Unsupported):
+        sb.aff.pod_deltas(p, 0, existing=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_apply_affinity_then_allocate_matches_oracle(seed):
+    a, b, bound, evicted = _aff_pair(seed)
+    ref = pyoracle.allocate(a)
+    sa, sb = E.Snapshot(a), E.Snapshot(b)
+    rows, ad = _aff_deltas(sb, bound, evicted)
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(sb)
+        ctx.apply(*E.row_deltas(rows))
+        ctx.apply_affinity(ad)
+        out = ctx.allocate(sa)  # the host's session state is A's (the eviction changed the job's ready count)
+    finally:
+        ctx.close()
+    got = runtime.result_dict(sa, out)
+    assert got["events"] == ref["events"]
+    assert got["binds"] == ref["binds"]
+    assert got["fit_errors"] == ref["fit_errors"]
