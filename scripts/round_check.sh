@@ -14,7 +14,8 @@ step() {  # step <name> <timeout> <cmd...>: a crash / timeout ends the script (t
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step tests 900 python -u -m pytest -m gpu -q -p no:cacheprovider --timeout 600 --timeout-method thread tests
+  # -v -s: every test's name as it starts, and the long tests' heartbeats (a silent call is taken to be hung)
+  step tests 1000 python -u -m pytest -m gpu -v -s -rf -p no:cacheprovider --timeout 900 --timeout-method thread tests
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench_C2 400 python bench.py --steps 20 --warmup 2
