@@ -271,7 +271,7 @@ constexpr int kBitonicMin = 2048;  // == the sort's LDS tile
 void launch_sort_nodes(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, const int64_t* mm,
                        uint64_t* keys, int n_pad, void* stream, bool sort = true);
 // kb_apply_affinity: table / histogram entries of a pod outside the session's specs (indices checked by the host).
-void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, void* stream);
+void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, int base, void* stream);
 // kb_apply: row deltas of commits made outside the device (one thread per delta, atomics).
 void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
                   const kb_port* ports, void* stream);
@@ -283,8 +283,9 @@ void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        uint32_t* traj, uint32_t* cmax32, uint32_t* amax, uint64_t* stat, const JobState* js,
                        bool aff, void* stream);
 // Table increments of a run placed by the trajectory / re-key loops (affinity specs with increments).
+// base: the placements' node ids minus base index this context's rows (node-sharded: global ids, A.topo_dom offset)
 void launch_aff_commit(const DevSpecs& P, int spec, int t_begin, int run, const JobState* js, const int32_t* hout,
-                       void* stream);
+                       int base, void* stream);
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        int J, int idx_bits, const uint32_t* traj, const uint32_t* cmax32, const uint32_t* amax,
                        const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,

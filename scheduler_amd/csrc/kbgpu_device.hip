@@ -241,7 +241,7 @@ __device__ __forceinline__ int32_t ipa_score(int64_t c, int64_t mn, int64_t mx) 
 __device__ void apply_commit_tables(const DevAff& A, const kb_spec& sp, int w, int n_alloc, int n_commit) {
   if (!A.enabled || sp.aff_class < 0) return;
   const kb_aff_spec as = A.specs[sp.aff_class];
-  if (n_alloc > 0)
+  if (n_alloc != 0)  // (negative: kb_apply taking a pod back)
     for (uint32_t i = 0; i < as.lister_cnt; ++i) {
       const int32_t t = A.lister[as.lister_off + i];
       const kb_aff_table tb = A.tables[t];
@@ -249,7 +249,7 @@ __device__ void apply_commit_tables(const DevAff& A, const kb_spec& sp, int w, i
       if (d >= 0) atomicAdd(&A.counters[tb.cnt_off + d], n_alloc);
       atomicAdd(&A.totals[t], n_alloc);
     }
-  if (n_commit > 0)
+  if (n_commit != 0)
     for (uint32_t i = 0; i < as.incr_cnt; ++i) {
       const kb_ipa_incr e = A.incr[as.incr_off + i];
       const int32_t d = A.topo_dom[(size_t)e.slot * A.n + w];
@@ -3599,11 +3599,11 @@ __global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, Dev
 // The table increments of a run placed by the trajectory / re-key loops (whose spec's own affinity
 // inputs do not move): one thread per placement of the run, read back from the placement buffer.
 __global__ __launch_bounds__(256) void aff_commit_kernel(DevSpecs P, int spec, int t_begin, int run,
-                                                         const JobState* js, const int32_t* hout) {
+                                                         const JobState* js, const int32_t* hout, int base) {
   const int placed = js->n_placed - t_begin;  // placements of this run (tasks t_begin .. t_begin + run)
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= run || k >= placed) return;
-  const int w = hout[2 * (t_begin + k)];
+  const int w = hout[2 * (t_begin + k)] - base;  // (node-sharded: possibly another rank's row; A.topo_dom is global)
   const int kind = hout[2 * (t_begin + k) + 1];
   apply_commit_tables(P.A, P.specs[spec], w, kind == KB_PLACE_ALLOCATE, 1);
 }
@@ -5006,9 +5006,9 @@ void launch_traj_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 }
 
 void launch_aff_commit(const DevSpecs& P, int spec, int t_begin, int run, const JobState* js, const int32_t* hout,
-                       void* stream) {
+                       int base, void* stream) {
   hipLaunchKernelGGL(aff_commit_kernel, dim3((run + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, spec, t_begin,
-                     run, js, hout);
+                     run, js, hout, base);
 }
 
 void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
@@ -5052,6 +5052,10 @@ __global__ __launch_bounds__(256) void apply_kernel(DevNodes N, DevSpecs P, cons
   if (i >= k) return;
   const kb_row_delta e = d[i];
   const int w = e.node - N.base;
+  if (pass == 0 && e.spec >= 0) {  // the replicated affinity tables: every rank (A.topo_dom covers every node)
+    const int sign = e.pods < 0 ? -1 : 1;
+    apply_commit_tables(P.A, P.specs[e.spec], w, e.kind == KB_PLACE_ALLOCATE ? sign : 0, sign);
+  }
   if (w < 0 || w >= N.n) return;  // another rank's row
   if (pass == 1) {
     if (e.flags_clear) atomicAnd(&N.flags[w], ~e.flags_clear);
@@ -5077,10 +5081,6 @@ __global__ __launch_bounds__(256) void apply_kernel(DevNodes N, DevSpecs P, cons
     if (e.pods >= 0) atomicOr(used, 1ull << p.ip);
     else atomicAnd(used, ~(1ull << p.ip));
   }
-  if (e.spec >= 0) {
-    const int sign = e.pods < 0 ? -1 : 1;
-    apply_commit_tables(P.A, P.specs[e.spec], w, e.kind == KB_PLACE_ALLOCATE ? sign : 0, sign);
-  }
 }
 
 void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, int k, const int64_t* sc,
@@ -5091,23 +5091,24 @@ void launch_apply(const DevNodes& N, const DevSpecs& P, const kb_row_delta* d, i
 }
 
 // kb_apply_affinity: one thread per table / histogram entry of a pod outside the session's pending specs.
-__global__ __launch_bounds__(256) void apply_aff_kernel(DevAff A, const kb_aff_delta* d, int k) {
+__global__ __launch_bounds__(256) void apply_aff_kernel(DevAff A, const kb_aff_delta* d, int k, int base) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k) return;
   const kb_aff_delta e = d[i];
+  const int w = e.node - base;  // canonical id -> A.topo_dom's view (offset by the rank's first row when sharded)
   if (e.table >= 0) {
     const kb_aff_table tb = A.tables[e.table];
-    const int32_t dom = A.topo_dom[(size_t)tb.slot * A.n + e.node];
+    const int32_t dom = A.topo_dom[(size_t)tb.slot * A.n + w];
     if (dom >= 0) atomicAdd(&A.counters[tb.cnt_off + dom], e.weight);
     atomicAdd(&A.totals[e.table], e.weight);
   } else {
-    const int32_t dom = A.topo_dom[(size_t)e.slot * A.n + e.node];
+    const int32_t dom = A.topo_dom[(size_t)e.slot * A.n + w];
     if (dom >= 0) atomicAdd(&A.h[e.h_off + dom], e.weight);
   }
 }
 
-void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, void* stream) {
-  hipLaunchKernelGGL(apply_aff_kernel, dim3((k + 255) / 256), dim3(256), 0, (hipStream_t)stream, A, d, k);
+void launch_apply_aff(const DevAff& A, const kb_aff_delta* d, int k, int base, void* stream) {
+  hipLaunchKernelGGL(apply_aff_kernel, dim3((k + 255) / 256), dim3(256), 0, (hipStream_t)stream, A, d, k, base);
 }
 
 // ---- preempt's sweep (actions/preempt/preempt.go:189-195): PredicateNodes with Session.PredicateFn (no

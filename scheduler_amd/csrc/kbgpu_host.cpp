@@ -99,7 +99,7 @@ void drop_affinity(kb_ctx* c) {
 //    task ranks the F-domains' best nodes instead of every node (cls_place_kernel).
 void classify_self_dynamic(kb_ctx* c, const kb_affinity* a, const std::vector<int64_t>& D,
                            std::vector<kb_spec>& specs) {
-  const size_t n = (size_t)c->N.n;
+  const size_t n = c->sharded ? (size_t)c->shard.n_total : (size_t)c->N.n;  // rows of topo_dom
   c->spec_cap1.assign(a->m, 0);
   c->spec_cls.assign(a->m, -1);
   for (auto& sp : specs) sp.flags &= ~(kbgpu::kSpecCap1 | kbgpu::kSpecCapAnti);
@@ -494,10 +494,11 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   if (int rc_ = kb_engine_stop(c)) return rc_;
   if (c->broken) return fail(c, KB_E_HIP, "context unusable: %s", c->err.c_str());
   if (!c->nodes_ok || !c->specs_ok) return fail(c, KB_E_STATE, "upload nodes and specs before affinity");
-  if (c->sharded) return fail(c, KB_E_UNSUPPORTED, "inter-pod affinity tables do not run node-sharded");
   HIP_OK(c, hipSetDevice(c->device));
   drop_affinity(c);
-  const size_t n = (size_t)c->N.n;
+  // node-sharded: topo_dom holds every node of the cluster (a commit on another rank's row moves the
+  // replicated count tables at that node's domains); the device sees it from this rank's first row
+  const size_t n = c->sharded ? (size_t)c->shard.n_total : (size_t)c->N.n;
   if (a->m != (uint32_t)c->P.m) return fail(c, KB_E_INVALID, "affinity specs %u != specs %d", a->m, c->P.m);
   // every index the kernels follow is checked here (no out-of-bounds device access)
   std::vector<int64_t> D(a->n_slots, 0);  // domains per slot
@@ -563,7 +564,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   c->cls_mem.assign(a->n_slots, nullptr);
   for (uint32_t s = 0; s < a->m; ++s) {
     const int32_t F = c->spec_cls[s];
-    if (F < 0 || c->cls_coff[F] || n >= 65536) continue;
+    if (F < 0 || c->cls_coff[F] || n >= 65536 || c->sharded) continue;
     const size_t K = (size_t)D[F] + 1;
     std::vector<uint32_t> off(K + 1, 0);
     std::vector<uint16_t> mem((n + 7) / 8 * 8, 0);  // padded: the kernel reads it in 16-byte loads
@@ -593,6 +594,7 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   if ((rc = upload(c, c->aff_mem, &mm, (const int64_t*)nullptr, 2, false))) return rc;
   A.mm = mm;
   A.n = (int32_t)n;
+  if (c->sharded) A.topo_dom += c->N.base;  // (aff_mem keeps the allocation's own pointer)
   // pristine copies of the mutable tables (kb_restore_nodes re-opens the session)
   auto keep = [&](void* col, size_t bytes) -> int {
     void* q;
@@ -884,12 +886,42 @@ int kb_set_shard_rccl(kb_ctx* c, const kb_shard* sh, const uint8_t id[KB_COMM_ID
 // stream, or host-staged through the callback), the global merge + commit. Issued into job slot `si` like
 // place_issue (`g` guards a speculative job's first segment: every rank sees the same previous job, so every
 // rank skips alike, and the all-gather still runs); the host-staged exchange waits for the proposal here.
+// This run's InterPodAffinity normalisation over the whole cluster (interpod_affinity.go:221-238: min / max
+// count over every node): each rank's over its own rows, then min of the minima and max of the maxima.
+static int shard_ipa_minmax(kb_ctx* c, int spec, const JobState* js) {
+  int64_t* mm = c->P.A.mm;
+  launch_ipa_minmax(c->N, c->P, nullptr, spec, 1, mm, js, c->stream);
+  if (c->comm) {
+    ncclResult_t r = ncclAllReduce(mm, mm, 1, ncclInt64, ncclMin, (ncclComm_t)c->comm, c->stream);
+    if (r == ncclSuccess) r = ncclAllReduce(mm + 1, mm + 1, 1, ncclInt64, ncclMax, (ncclComm_t)c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, KB_E_HIP, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return KB_OK;
+  }
+  const int W = c->shard.world;
+  std::vector<int64_t> h(2 * (size_t)(W + 1));
+  HIP_OK(c, hipMemcpyAsync(h.data(), mm, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (int rc = c->ag_fn(c->ag_user, h.data(), h.data() + 2, 16))
+    return fail(c, KB_E_HIP, "all-gather callback failed (%d)", rc);
+  int64_t mn = h[2], mx = h[3];
+  for (int w = 1; w < W; ++w) {
+    mn = std::min(mn, h[2 + 2 * w]);
+    mx = std::max(mx, h[3 + 2 * w]);
+  }
+  h[0] = mn;
+  h[1] = mx;
+  HIP_OK(c, hipMemcpyAsync(mm, h.data(), 16, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));  // (h is pageable and local)
+  return KB_OK;
+}
+
 static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard& g) {
   if (!c->sel_ok || !c->traj) return fail(c, KB_E_UNSUPPORTED, "sharded table does not fit the selection path");
   for (uint32_t i = 0; i < job->n_tasks; ++i) {
     const int s = job->task_specs[i];
-    if (!c->spec_traj_ok[s] || c->spec_needs_aff[s])
-      return fail(c, KB_E_UNSUPPORTED, "spec %d needs a path that does not run sharded", s);
+    if (!c->spec_traj_ok[s]) return fail(c, KB_E_UNSUPPORTED, "spec %d needs a path that does not run sharded", s);
+    if (c->spec_needs_aff[s] && (!c->aff_ok || c->spec_aff_err[s]))
+      return fail(c, KB_E_UNSUPPORTED, "spec %d: inter-pod affinity error paths do not run sharded", s);
   }
   kb_ctx::JobSlot& S = c->slot[si];
   S.t_issue = std::chrono::steady_clock::now();
@@ -905,18 +937,30 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     uint32_t e = t + 1;
     while (e < job->n_tasks && job->task_specs[e] == job->task_specs[t]) ++e;
     const int spec = job->task_specs[t];
+    // inter-pod affinity: the count tables and histograms are replicated on every rank and every rank applies
+    // every commit's increments (global node ids, whole-cluster topo_dom). A spec whose inputs stay put during
+    // its run (or a cap-1 spec, whose key sequence stays closed-form) runs in segments as above, after a
+    // whole-cluster min / max; a spec whose own commits move its inputs runs one task per segment.
+    const bool aff = c->spec_needs_aff[spec];
+    const bool per_task = aff && c->spec_dyn[spec] && !c->cap1(spec);
+    const uint32_t seg_max = per_task ? 1u : (uint32_t)kShardSegMax;
     // a job of one single-segment run lists the rows it commits; when the previous job (the other slot) did,
     // this job's sweep runs on stream_b beside that job's kernels and the proposal re-keys those rows (as the
     // one-GPU selection path does, place_issue)
-    const bool one_run = t == 0 && e == job->n_tasks && e - t <= (uint32_t)kShardSegMax;
+    const bool one_run = !aff && t == 0 && e == job->n_tasks && e - t <= (uint32_t)kShardSegMax;
     const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1);
     uint32_t* kt = one_run ? c->sel_keys[si] : c->traj;
     uint64_t* st = one_run ? c->sel_stat[si] : c->stat;
-    for (uint32_t seg = t; seg < e; seg += kShardSegMax) {
-      const int T = (int)std::min<uint32_t>(kShardSegMax, e - seg);
+    for (uint32_t seg = t; seg < e; seg += seg_max) {
+      const int T = (int)std::min<uint32_t>(seg_max, e - seg);
       const int first = seg == 0;
       const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
       hipEvent_t ea;
+      if (aff && c->spec_hist[spec]) {
+        c->ev_begin(&ea);
+        if (int rc = shard_ipa_minmax(c, spec, first ? nullptr : js)) return rc;
+        c->ev_end(ea, KB_KERNEL_IPA_MINMAX, (uint64_t)c->N.n);
+      }
       if (ov) {
         c->ev_begin(&ea, c->stream_b);
         launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, false, c->stream_b,
@@ -926,7 +970,7 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
         c->n_overlap++;
       } else {
         c->ev_begin(&ea);
-        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, false, c->stream, gr);
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, aff, c->stream, gr);
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n);
       }
       // the segment's identity, compared across ranks after the exchange (ShardRec::tag)
@@ -957,6 +1001,8 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                           first, job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr,
                           one_run ? c->commits[si] : nullptr, c->stream);
       c->ev_end(ea, KB_KERNEL_SHARD_COMMIT, 0);
+      if (aff && c->spec_incr[spec])  // every rank: the segment's placements (global ids) into the tables
+        launch_aff_commit(c->P, spec, (int)seg, T, js, hout_dev, c->N.base, c->stream);
     }
     listed = one_run;
     t = e;
@@ -1181,7 +1227,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
       c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     }
     if (aff && (!dyn || cls) && c->spec_incr[spec])  // this run's commits update the affinity tables
-      launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, c->stream);
+      launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, 0, c->stream);
     t = e;
   }
   HIP_OK(c, hipGetLastError());
@@ -1277,7 +1323,7 @@ int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
   const int s0 = job->task_specs[0];
   if (s0 < 0 || s0 >= c->P.m || !c->spec_traj_ok[s0]) return 0;
   if (c->aff_ok && c->spec_needs_aff[s0] && c->spec_dyn[s0] && !c->cap1(s0) && !cls_run_ok(c, s0)) return 0;
-  if (c->sharded && c->spec_needs_aff[s0]) return 0;  // (refused by shard_issue anyway)
+  if (c->sharded && c->spec_needs_aff[s0]) return 0;  // sharded affinity runs issue serially
   return 1;
 }
 
@@ -1806,7 +1852,7 @@ int kb_apply_affinity(kb_ctx* c, const kb_aff_delta* d, uint32_t k) {
   const auto& D = c->aff_slot_D;
   for (uint32_t i = 0; i < k; ++i) {  // every index the kernel follows
     const kb_aff_delta& e = d[i];
-    if (e.node < 0 || e.node >= c->N.n) return fail(c, KB_E_INVALID, "affinity delta %u: node %d", i, e.node);
+    if (e.node < 0 || e.node >= c->P.A.n) return fail(c, KB_E_INVALID, "affinity delta %u: node %d", i, e.node);
     if (e.table >= 0) {
       if ((uint32_t)e.table >= c->aff_n_tables) return fail(c, KB_E_INVALID, "affinity delta %u: table %d", i, e.table);
     } else if (e.table != -1 || e.slot < 0 || (size_t)e.slot >= D.size() ||
@@ -1821,7 +1867,7 @@ int kb_apply_affinity(kb_ctx* c, const kb_aff_delta* d, uint32_t k) {
     free_all(tmp);
     return rc;
   }
-  launch_apply_aff(c->P.A, dd, (int)k, c->stream);
+  launch_apply_aff(c->P.A, dd, (int)k, c->N.base, c->stream);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   free_all(tmp);

@@ -278,8 +278,7 @@ class Context:
                          tol.shape[0], tol.shape[1], _ptr(tol))
         self._check(self.lib.kb_upload_specs(self.ctx, C.byref(specs)))
         if snap.aff is not None:
-            if hasattr(self, "rows"):
-                raise KbError(KB_E_UNSUPPORTED, "inter-pod affinity tables do not run node-sharded")
+            # (node-sharded: every rank holds the whole topo_dom and the replicated count tables)
             a = snap.aff
             arrs = [np.ascontiguousarray(x) for x in (a.topo_dom, a.table_arr, a.totals, a.counters, a.spec_arr,
                                                       a.check_arr, a.lister_arr, a.hist_arr, a.h, a.incr_arr)]

@@ -353,3 +353,67 @@ def test_c5_full_eight_ranks_match_oracle_digest():
         p.join(timeout=60)
     for r in range(world):
         assert got[r] == (meta["events"], meta["sha256"]), r
+
+
+# ---- inter-pod affinity, node-sharded (SURVEY.md §8 e1 with interpod_affinity.go:119-241) ----
+def _aff_cases():
+    from helpers import affinity_clusters
+    return dict(affinity_clusters())
+
+
+def _aff_rank_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+
+    res = {}
+    try:
+        for name, cl in _aff_cases().items():
+            snap = E.Snapshot(cl)
+            ctx = runtime.Context(0)
+            try:
+                ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+                ctx.upload(snap)
+                r = runtime.result_dict(snap, ctx.allocate(snap))
+                res[name] = {k: r[k] for k in ("events", "binds", "fit_errors")}
+            finally:
+                ctx.close()
+        q.put((rank, res, None))
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_affinity_matches_oracle(world):
+    """Replicated count tables and histograms, one whole-cluster IPA min / max per run (or per task), every
+    commit applied on every rank: the oracle's events, binds and FitErrors on every affinity cluster (C4 shapes,
+    the edge clusters, the self-affinity clusters whose specs run one task per segment or as cap-1 runs)."""
+    import torch.multiprocessing as mp
+    from oracle import pyoracle
+    ref = {name: pyoracle.allocate(cl) for name, cl in _aff_cases().items()}
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_aff_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=300)
+        assert err is None, f"rank {rank}: {err}"
+        got[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        for name, o in ref.items():
+            for k in ("events", "binds", "fit_errors"):
+                assert got[r][name][k] == o[k], (world, r, name, k)
