@@ -31,7 +31,7 @@ def _summary(out):
          "task_status": out["task_status"].tolist(), "job_fail_task": out["job_fail_task"].tolist(),
          "job_reason_hist": out["job_reason_hist"].tolist()}
     if "backfill_fit" in out:  # backfill: first fit with every score equal; FitErrors merged over the ranks
-        s["backfill_fit"] = {j: {t: h.tolist() for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
+        s["backfill_fit"] = {j: {t: dict(h) for t, h in tf.items()} for j, tf in out["backfill_fit"].items()}
     return s
 
 
