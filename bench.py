@@ -11,8 +11,9 @@ fleet with its own seed; no collective on the data path: torch.distributed only 
 max-over-ranks time) -- `value` = all ranks' pods / the max-over-ranks time, scaling "weak", the same per-GPU
 workload as the N = 1 line. One allocate cycle is a sequential chain of jobs, so GPUs add throughput by serving
 partitions. Beside it, "sharded": BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M pods
-whose node table is split across the N ranks (one RCCL all-gather per run segment over xGMI), reported with its
-exchange latency (the north star's scaling limiter). `--mode shard` makes that the line instead.
+whose node table is split across the N ranks: every rank's resident engine proposes its first T picks per job and
+writes them into every rank's inbox over xGMI (kb_set_shard_peer: device memory mapped across the GPUs), then
+merges them on the device -- no host round trip or collective launch per job. `--mode shard` makes that the line.
 `python bench.py --gpus N` without torchrun's environment starts the N ranks itself (before any GPU call).
 One GPU also runs C5 whole: `--config C5` (the split fed engine with range selectors).
 
@@ -51,7 +52,6 @@ CONFIGS = {
                workload="C5: 50k nodes x 1M pods (C2 shape), node table sharded across the GPUs"),
 }
 ARRAY_CONFIGS = ("C2", "C5")  # built by synth.c2_snapshot (numpy) instead of per-pod objects
-SEL_NODES_PER_GPU = 24576  # the selection kernel's LDS plan (kbgpu_device.hip kSelQ4: 512 threads x 48 keys)
 
 
 def main():
@@ -91,13 +91,12 @@ def main():
     args.config = args.config or ("C5" if mode == "shard" and world > 1 else "C2")
     cfg = CONFIGS[args.config]
     args.nodes = args.nodes or cfg["nodes"]
-    if mode == "shard" and world > 1:
-        args.nodes = min(args.nodes, SEL_NODES_PER_GPU * world)  # every rank's block on the selection path
     args.jobs = args.jobs or cfg["jobs"]
     args.tasks_per_job = args.tasks_per_job or cfg["tasks"]
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # KB_BENCH_SAME_GPU=1: rehearse N ranks on one GPU (gloo process group, host-staged shard exchange)
+    # KB_BENCH_SAME_GPU=1: rehearse N ranks on one GPU (gloo process group; with KB_FED_PLAIN_LAUNCH=1, see
+    # scripts/rehearse_multi.sh)
     same_gpu = os.environ.get("KB_BENCH_SAME_GPU") == "1"
     device = 0 if same_gpu else local_rank
     dist = None
@@ -195,8 +194,6 @@ def main():
     workload = cfg["workload"]
     if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
         workload = f"{args.config} shape at {args.nodes} nodes x {args.jobs * args.tasks_per_job} pods"
-        if shard and args.nodes < cfg["nodes"]:
-            workload += f" (node table sharded {world} ways, at most {SEL_NODES_PER_GPU} rows per GPU)"
     result = None
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -318,24 +315,19 @@ def tensor_device(dist, device):
 
 
 def shard_exchange(dist, rank, device):
-    """Context.set_shard keyword: the RCCL id made on rank 0 and broadcast over the torch process group, or
-    (gloo group: ranks sharing one GPU in a rehearsal) a host-staged all-gather over that group."""
+    """Context.set_shard keywords: the node-sharded fed engine's device exchange (kb_set_shard_peer), whose inbox
+    IPC handles travel once through an all-gather over the torch process group (RCCL, or gloo when the ranks share
+    one GPU in a rehearsal); that all-gather also serves any job the engine does not run."""
     import torch
-    from scheduler_amd import runtime
-    if dist.get_backend() == "gloo":
-        world = dist.get_world_size()
+    world = dist.get_world_size()
+    dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{device}"
 
-        def allgather(b):
-            t = torch.tensor(list(b), dtype=torch.uint8)
-            outs = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(outs, t)
-            return b"".join(bytes(o.tolist()) for o in outs)
-        return {"allgather": allgather}
-    t = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{device}")
-    if rank == 0:
-        t.copy_(torch.tensor(list(runtime.comm_unique_id()), dtype=torch.uint8))
-    dist.broadcast(t, 0)
-    return {"rccl_id": bytes(t.cpu().tolist())}
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8, device=dev)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.cpu().tolist()) for o in outs)
+    return {"allgather": allgather, "peer": True}
 
 
 def exchange_us(st):
@@ -378,15 +370,14 @@ def replicas_side(args, dist, rank, world, device):
 
 def shard_side(args, dist, rank, world, device):
     """Beside the replicas line (N > 1): BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M
-    pods whose node table is split across the N ranks (contiguous blocks; per run segment one all-gather of the
-    ranks' proposals, RCCL over xGMI, and every rank commits its own rows). `side_steps` cycles after one warm-up;
-    pods/s at the max-over-ranks time. A rank's block runs on the selection path (at most SEL_NODES_PER_GPU rows),
-    so at N = 2 the cluster is 2 x that, stated in the workload."""
+    pods whose node table is split across the N ranks (contiguous blocks; per job every rank's engine proposes,
+    writes its proposal into every rank's inbox over xGMI and merges all of them; every rank commits its own rows).
+    `side_steps` cycles after one warm-up; pods/s at the max-over-ranks time."""
     import torch
     from scheduler_amd import runtime, synth
     try:
         c = CONFIGS["C5"]
-        nodes = min(c["nodes"], SEL_NODES_PER_GPU * world)
+        nodes = c["nodes"]
         snap = synth.c2_snapshot(n_nodes=nodes, n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED)
         ctx = runtime.Context(device, timing=True, timing_every=args.timing_every)
         ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
@@ -408,15 +399,15 @@ def shard_side(args, dist, rank, world, device):
         ctx.close()
         a = argparse.Namespace(**vars(args))
         a.config, a.nodes, a.jobs, a.tasks_per_job = "C5", nodes, c["jobs"], c["tasks"]
-        work = (c["workload"] if nodes == c["nodes"] else
-                f"C5 shape at {nodes} nodes x {c['jobs'] * c['tasks']} pods (node table sharded {world} ways, at most "
-                f"{SEL_NODES_PER_GPU} rows per GPU)")
         elapsed = float(el.item())
-        return {"workload": work, "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
-                "steps": args.side_steps, "scaling": "strong", "ms_per_step": round(elapsed / args.side_steps * 1e3, 3),
-                "exchange_us_per_segment": exchange_us(st),
-                "segments_per_step": st["launches"][runtime.KERNELS.index("shard_exchange")] / args.side_steps,
-                "roofline": roofline_of(st, a, c, streaming=True)}
+        out = {"workload": c["workload"], "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
+               "steps": args.side_steps, "scaling": "strong", "ms_per_step": round(elapsed / args.side_steps * 1e3, 3),
+               "sharded_engine_cycles": st["fed_sharded"], "roofline": roofline_of(st, a, c, streaming=True)}
+        if st["launches"][runtime.KERNELS.index("fed_engine_kernel")]:
+            out["engine"] = engine_of(st, a)
+        else:  # (a cycle the engine does not serve: the per-job launch path with the host-staged exchange)
+            out["exchange_us_per_segment"] = exchange_us(st)
+        return out
     except Exception as e:  # the side measurement never takes the main line down
         return {"error": repr(e)[:300]}
 

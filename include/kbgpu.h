@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 11
+#define KBGPU_ABI_VERSION 12
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -418,6 +418,8 @@ typedef struct kb_stats {
                                          split engine (node selection one job ahead on a second workgroup) */
   uint64_t cap1_runs;                 /* runs of self-dependent specs taken as cap-1 selection runs */
   uint64_t cls_runs;                  /* runs taken by the class loop (KB_KERNEL_CLS_PLACE) */
+  uint64_t fed_sharded;               /* of the fed cycles, node-sharded ones (kb_set_shard_peer: the device
+                                         exchange between the ranks' engines) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 
@@ -523,6 +525,14 @@ int kb_set_shard(kb_ctx* ctx, const kb_shard* shard, kb_allgather_fn fn, void* u
 #define KB_COMM_ID_BYTES 128
 int kb_comm_unique_id(uint8_t id[KB_COMM_ID_BYTES]);
 int kb_set_shard_rccl(kb_ctx* ctx, const kb_shard* shard, const uint8_t id[KB_COMM_ID_BYTES]);
+/* Device exchange between the ranks' resident engines (ABI 12): every rank's inbox lives in its own GPU's memory
+ * and is mapped into every other rank's GPU (IPC handles, all-gathered once through fn); per job each rank's
+ * engine writes its proposal into every inbox over xGMI and merges all of them from its own, with no host or
+ * collective launch on the path. kb_allocate cycles whose jobs are all fed-engine runs (one <= 100-task selection
+ * run each, no inter-pod terms) take it; other jobs use fn as kb_set_shard's host-staged exchange, unpipelined.
+ * Replaces the per-task argmax all-reduce of SURVEY.md §8 e1 (scheduler_helper.go:147-158 over every rank's
+ * nodes); ranks must run the same cycles (a divergence fails with KB_E_STATE). */
+int kb_set_shard_peer(kb_ctx* ctx, const kb_shard* shard, kb_allgather_fn fn, void* user);
 
 /* ---- layer 2: session (allocate action + ordering plugins on the host) ---- */
 

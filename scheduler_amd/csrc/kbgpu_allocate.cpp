@@ -617,7 +617,7 @@ struct Driver {
     pk.resize(max_pending);
     // Pipelined: job k+1 is launched (guarded) before job k's result is read, so the device runs the jobs
     // back to back while the host does the bookkeeping. Otherwise one kb_place_job per job.
-    const bool pipe = kb_job_pipeline_ok(ctx) && getenv("KB_NO_PIPELINE") == nullptr;
+    bool pipe = kb_job_pipeline_ok(ctx) && getenv("KB_NO_PIPELINE") == nullptr;
     if (pipe)
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
     // every job one selection run of an eligible spec: the fed engine serves the whole cycle
@@ -642,6 +642,9 @@ struct Driver {
         sp0 = sp;
       }
     }
+    // node-sharded with the peer exchange only: the fed engine pipelines; any other cycle's jobs go one at a time
+    // through the host-staged exchange
+    if (!fed && ctx->sharded && !ctx->comm) pipe = false;
     if (fed)
       if (int rc = kb_fed_begin(ctx, max_pending)) return rc;
     struct FedEnd {  // the engine is stopped on every way out of the loop

@@ -55,6 +55,8 @@ struct kb_ctx {
   std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
   std::vector<int64_t> spec_pref_weight;
   std::vector<char> spec_ipa_err;   // per spec: KB_SPEC_IPA_ERROR (the batch score errors: 64-bit keys)
+  std::vector<char> spec_plain;     // per spec: no selector / node affinity / ports / scalars / inter-pod terms, and
+                                    //   one taint set it tolerates (kb_eval's row-only kernel; an overlay excludes it)
   std::vector<char> spec_aff_err;   // per spec: its affinity checks include KB_AFF_ERROR
   // host overlay (kb_set_host_overlay): per spec the slot of its rows (-1 none), per slot the rows
   std::vector<int32_t> ov_slot;
@@ -87,6 +89,12 @@ struct kb_ctx {
   kbgpu::ShardRec* d_rec = nullptr;     // this rank's proposal
   kbgpu::ShardRec* d_rec_all = nullptr; // [world] all proposals
   kbgpu::ShardRec* h_rec = nullptr;     // host staging (host exchange): [1 + world]
+  // kb_set_shard_peer: the node-sharded fed engine's inboxes (this rank's allocation, and every rank's as this GPU
+  // addresses it: IPC-mapped for the peers), and the cycle counter its tags carry
+  bool peer = false;
+  void* inbox = nullptr;
+  void* peer_inbox[kbgpu::kShardMaxWorld] = {};
+  uint32_t shard_epoch = 0;
   bool traj_full = false;  // trajectory buffers (kTrajMaxJ + 1 levels): chunk maxima fit the place loop
   bool sel_ok = false;     // the node count fits the selection kernel's LDS plan (level-0 keys buffer)
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
@@ -132,6 +140,7 @@ struct kb_ctx {
   // sweep kernels through a kJobSlots-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
   bool fed = false;
   bool use_fed = true;  // KB_NO_FED unset
+  bool use_eval_plain = true;  // KB_NO_EVAL_PLAIN unset
   void* fed_ring = nullptr;
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;

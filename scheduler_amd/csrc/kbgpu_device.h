@@ -148,10 +148,11 @@ void launch_sweep_keys(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
+// plain: every spec of the batch is plain (kb_ctx::spec_plain): the row-only kernel (eval_plain_kernel)
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream);
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, void* stream);
 void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                   uint32_t* reasons, int32_t* scores, const int64_t* mm, void* stream);
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, void* stream);
 int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;
@@ -246,11 +247,24 @@ bool fed_split_ok(int n);
 // selector workgroups of the split engine for n nodes (1: one holds every key; up to 4 node ranges past that;
 // 0: beyond the engine)
 int fed_nsel(int n);
+// Node-sharded fed engine (kb_set_shard_peer): per job every rank's placer writes its proposal into every rank's
+// inbox (device memory of each GPU, the peers' mapped through IPC handles: stores over xGMI) and merges all of
+// them from its own inbox. Inbox: [2 cycle halves][kJobSlots][kShardMaxWorld][kShardRecW] tagged 64-bit words
+// (tag = epoch << 20 | job + 1 in the high half, so every word validates itself and needs no store order).
+constexpr int kShardMaxWorld = 16;
+constexpr int kShardRecW = 3 * kShardSegMax + 24;  // 3 words per pick + kp + 3 header words + the histogram
+static_assert(3 * kShardSegMax + 4 + KB_NUM_REASONS <= kShardRecW, "inbox record layout");
+struct ShardPeers {
+  uint64_t* inbox[kShardMaxWorld];  // every rank's inbox as this GPU addresses it (its own included)
+  int32_t rank, world;              // world 0: not sharded
+  uint32_t epoch;                   // this cycle's number (the same on every rank)
+};
+size_t shard_inbox_bytes();
 // coop: a cooperative launch (every workgroup co-resident, on the device's cooperative queue); returns the
-// launch's hipError_t.
+// launch's hipError_t. shard.world > 0: the node-sharded engine (split engine only).
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                      int32_t* exit_flag, void* xchg, void* stream, bool coop);
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.

@@ -803,6 +803,67 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
   }
 }
 
+// kb_eval over a batch of plain specs (the host checks, kb_ctx::spec_plain: no nodeSelector, node affinity, host
+// ports, scalar requests, inter-pod terms or overlay, and one taint set that every spec tolerates). The chain then
+// reads only the row: resource fit, pod count, the node's conditions and pressure, LeastRequested + Balanced. The
+// node-only parts are computed once per node; the specs' four requests and BestEffort bit are staged in LDS once
+// per block, so the per-spec loop has no dependent scalar loads and no spec-dependent branches. Same values as
+// eval_kernel on such specs (tests/test_gpu_parity.py::test_eval_plain_equals_general).
+constexpr int kEvalPlainSpecs = 32;
+template <class SCORE>
+__global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
+                                                         int t, uint32_t* reasons, SCORE* scores) {
+  __shared__ int64_t s_req[4][kEvalPlainSpecs];  // init cpu, init mem, non-zero cpu, non-zero mem
+  __shared__ uint32_t s_be[kEvalPlainSpecs];
+  const int j0 = blockIdx.y * kEvalPlainSpecs;
+  const int nj = t - j0 < kEvalPlainSpecs ? t - j0 : kEvalPlainSpecs;
+  if ((int)threadIdx.x < nj) {
+    const kb_spec sp = P.specs[spec_ids[j0 + threadIdx.x]];
+    s_req[0][threadIdx.x] = sp.init_cpu;
+    s_req[1][threadIdx.x] = sp.init_mem;
+    s_req[2][threadIdx.x] = sp.nz_cpu;
+    s_req[3][threadIdx.x] = sp.nz_mem;
+    s_be[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? 1u : 0u;
+  }
+  __syncthreads();
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N.n) return;
+  const Row r = load_row(N, n);
+  const double ic = 1.0 / (double)r.alloc_cpu, im = 1.0 / (double)r.alloc_mem;
+  // row_reasons after the resource check, per node: pod count, conditions (static_eval's pre), then the post
+  // reasons (no taints: the one taint set is tolerated) -- memory pressure for BestEffort specs only
+  uint32_t after = 0, post_be = 0;
+  if (C.predicates) {
+    const uint32_t f = r.flags;
+    const uint32_t pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
+                              (1u << KB_R_UNSCHEDULABLE));
+    uint32_t post = 0;
+    if (C.disk_pressure && (f & KB_NODE_DISK_PRESSURE)) post = 1u << KB_R_DISK_PRESSURE;
+    else if (C.pid_pressure && (f & KB_NODE_PID_PRESSURE)) post = 1u << KB_R_PID_PRESSURE;
+    post_be = (C.mem_pressure && (f & KB_NODE_MEM_PRESSURE)) ? 1u << KB_R_MEMORY_PRESSURE : post;
+    after = r.max_pods <= r.pod_count ? 1u << KB_R_POD_NUMBER : (pre ? pre : post);
+    if (r.max_pods <= r.pod_count || pre) post_be = after;
+  }
+  uint32_t* rout = reasons + n;
+  SCORE* sout = scores + n;
+  const size_t stride = (size_t)N.n;
+#pragma unroll 4
+  for (int j = 0; j < nj; ++j) {
+    const int64_t icpu = s_req[0][j], imem = s_req[1][j];
+    const bool fit = (le_tol(icpu, r.idle_cpu, 10) && le_tol(imem, r.idle_mem, 10ll * 1024 * 1024)) ||
+                     (le_tol(icpu, r.rel_cpu, 10) && le_tol(imem, r.rel_mem, 10ll * 1024 * 1024));
+    const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
+    int64_t score = 0;
+    if (C.nodeorder) {  // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term
+      const int64_t rc = s_req[2][j] + r.nz_cpu, rm = s_req[3][j] + r.nz_mem;
+      const int64_t lr = (lr_score_inv(rc, r.alloc_cpu, ic) + lr_score_inv(rm, r.alloc_mem, im)) / 2;
+      score = lr * C.w_lr + bra_score_inv(rc, r.alloc_cpu, rm, r.alloc_mem, ic, im) * C.w_bra;
+    }
+    rout[(size_t)(j0 + j) * stride] = rs;
+    sout[(size_t)(j0 + j) * stride] = (SCORE)score;
+  }
+}
+
 // ===========================================================================
 // Trajectory path (N <= kTrajMaxNodes, scores that fit a 32-bit key).
 //
@@ -1643,7 +1704,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
   const int64_t bias32 = 1ll << (30 - idx_bits);
   const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
   const uint64_t lt = (1ull << lane) - 1;
-  if (PROPOSE && tid == 0) rec->kp = 0;
+  if (PROPOSE && !CAND && tid == 0) rec->kp = 0;
   int done_tasks = 0;
   while (done_tasks < t_count) {
     const uint32_t T = (uint32_t)(t_count - done_tasks < kSegMax ? t_count - done_tasks : kSegMax);
@@ -1868,7 +1929,15 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
       __syncthreads();
       KB_SEL_PH(4);
-      if constexpr (PROPOSE) {
+      if constexpr (PROPOSE && CAND) {
+        // the node-sharded fed engine's placer: the proposal stays in sh.ord[0..s_count) for the caller's exchange
+        // and merge; with fewer picks than tasks, sh.fin counts every one of them (the local no-fit histogram
+        // applies them all)
+        const int Kp = sh.s_count;
+        if (tid < Kp && Kp < (int)T) atomicAdd(&sh.fin[sel_slot(sh.ord[tid])], 1);
+        __syncthreads();
+        break;
+      } else if constexpr (PROPOSE) {
         // the rank's proposal: its best picks in order with their global nodes and commit kinds; when it runs
         // out of feasible picks, the reason histogram of its rows after all of them (the no-fit case)
         const int Kp = sh.s_count;
@@ -1981,7 +2050,10 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
     }
     if (no_fit) {
       if constexpr (CAND) {  // the caller rebuilds every node's key for the histogram (sh.need_hist)
-        if (tid == 0) sh.need_hist = 1;
+        if (tid == 0) {
+          sh.need_hist = 1;
+          if (PROPOSE) sh.s_count = 0;  // (sharded placer: an empty proposal)
+        }
         stop = KB_STOP_NO_FIT;
         fail_task = t_begin + done_tasks;
         stopped = 1;
@@ -2395,7 +2467,6 @@ __device__ __forceinline__ int shard_count_gt(const uint64_t* list, int len, uin
   return lo;
 }
 
-constexpr int kShardMaxWorld = 16;
 
 __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec,
                                                                    int t_begin, int t_count, int idx_bits,
@@ -2462,8 +2533,8 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
   if (wv == 0) {  // stop rules in pick order (as the one-GPU selection kernel applies them)
     const bool va = lane < Kp, vb = lane + 64 < Kp;
     const uint64_t oa = va ? ord[lane] : 0, ob = vb ? ord[lane + 64] : 0;
-    const bool aa = va && (ordnk[lane] >> 30) == KB_PLACE_ALLOCATE;
-    const bool ab = vb && (ordnk[lane + 64] >> 30) == KB_PLACE_ALLOCATE;
+    const bool aa = va && ((uint32_t)ordnk[lane] >> 30) == KB_PLACE_ALLOCATE;
+    const bool ab = vb && ((uint32_t)ordnk[lane + 64] >> 30) == KB_PLACE_ALLOCATE;
     const auto neg = [&](uint64_t o) {
       const uint32_t e32 = (uint32_t)(o >> 14);
       return (int64_t)((e32 >> idx_bits) & score_mask) - bias32 <= -1;
@@ -2506,7 +2577,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_commit_kernel(DevNodes N, D
     const int nk = ordnk[tid];
     const int node = nk & 0x3fffffff;
     hout[2 * (t_begin + tid)] = node;
-    hout[2 * (t_begin + tid) + 1] = nk >> 30;
+    hout[2 * (t_begin + tid) + 1] = (int32_t)((uint32_t)nk >> 30);
     if (node >= N.base && node < N.base + N.n) {
       const int s = sel_slot(ord[tid]);
       atomicAdd(&fin[s], 1);
@@ -2944,15 +3015,29 @@ __device__ __forceinline__ Row row_after(const kb_spec& sp, const Row& r0, int c
 // placer's LDS: every node's key is the sweep's (keys, read from memory) unless its row changed since, on one of
 // the three commit lists; those are re-keyed. bits (LDS, n bits) marks them, so a node listed twice counts once
 // and the streamed pass skips it. Ends after a barrier with the histogram in sh.hist.
+// sset (the node-sharded placer, before its commits): the selected nodes with sh.fin > 0 are keyed at their level
+// after those picks from their segment-start rows first (traj_key64), the rest as above.
 __device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                                 const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
-                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2) {
+                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2,
+                                bool sset = false) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int n = N.n, nw = (n + 31) >> 5;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = tid; i < nw; i += kSelThreads) bits[i] = 0u;
   if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
   __syncthreads();
+  if (sset) {
+    if (tid < sh.n_sel && sh.fin[tid] > 0) {
+      const int w = sh.node[tid];
+      const uint64_t k = traj_key64(N, P, C, sp, sci, P.sc_req + (size_t)spec * N.S, sh.row[tid], sh.stat[tid], w,
+                                    sh.fin[tid], sh.A[tid]);
+      atomicOr(&bits[w >> 5], 1u << (w & 31));
+      if (!(k & kFeasible))
+        for (uint32_t m = (uint32_t)k; m; m &= m - 1) atomicAdd(&sh.hist[__builtin_ctz(m)], 1u);
+    }
+    __syncthreads();
+  }
   for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
     const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : l2[i - n0 - n1]);
     const uint32_t b = 1u << (w & 31);
@@ -2987,13 +3072,260 @@ __device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N
   __syncthreads();
 }
 
+// ---- node-sharded fed engine: the placer's exchange and global merge ----
+// Per job every rank's placer proposes its first T picks (the selection of its own rows), writes the proposal into
+// every rank's inbox (stores over xGMI into the peers' HBM) and reads all W proposals from its own inbox. Every
+// word carries its tag (epoch << 20 | job + 1), so a reader takes a word once its tag matches: no store order, no
+// fence, and a stale word (an earlier job or cycle) reads as not there yet. Record i of rank w (L = 3T + 4 + R
+// words): 3 per pick (composite high / low, global node | kind << 30), then kp, three header words (the job's
+// spec, tasks and gang inputs: every rank must have issued the same job) and the no-fit histogram. Records are
+// numbered by exchange (xn: the cycle's jobs that ran, not skipped speculative ones, which exchange nothing), in
+// kJobSlots slots: a rank writes exchange xn + 1 only after every rank wrote exchange xn, so no rank is ever more
+// than one exchange ahead of another's reads.
+__device__ __forceinline__ uint64_t* shard_word(uint64_t* inbox, uint32_t epoch, int r, int w, int i) {
+  return inbox + ((((size_t)(epoch & 1u) * kJobSlots + r) * kShardMaxWorld + w) * kShardRecW + i);
+}
+__device__ __forceinline__ uint32_t shard_tag(uint32_t epoch, uint32_t m) {
+  return ((epoch & 0xfffu) << 20) | ((m + 1) & 0xfffffu);
+}
+// entries of rank h's proposal list (descending, high / low words in LDS) above v
+__device__ __forceinline__ int shard_gt(const uint32_t* ghi, const uint32_t* glo, int len, uint64_t v) {
+  int lo = 0, hi = len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((((uint64_t)ghi[mid] << 32) | glo[mid]) > v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+constexpr int kShardNoFitR = KB_NUM_REASONS;
+// gathered proposals in the placer's candidate space (free between sel_run and the next job's B rows)
+struct ShardGather {
+  uint32_t hi[kShardMaxWorld][128], lo[kShardMaxWorld][128];
+  int32_t nk[kShardMaxWorld][128];
+  int32_t kp[kShardMaxWorld];
+  uint32_t hdr[kShardMaxWorld][3];
+  uint32_t hist[kShardMaxWorld][kShardNoFitR];
+  int32_t fail, diverged, cut, kind, n_alloc;
+};
+static_assert(sizeof(ShardGather) <= 8 * kCandCap, "the gathered proposals fit the candidate space");
+
+// After sel_run<PROPOSE, QN, CAND> (sh.ord[0..s_count): this rank's proposal): the local no-fit histogram when the
+// rank ran out of picks, the exchange, the global first-T picks, the stop rules, and the commits on this rank's
+// rows. Returns 0, 1 (a peer's proposal did not arrive within idle_ticks) or 2 (the ranks issued different jobs).
+__device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const ShardPeers& SP, uint32_t xn,
+                           const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
+                           const uint64_t* stat, const uint32_t* keys, const int32_t* l0, int n0, const int32_t* l1,
+                           int n1, int t_begin, int t_count, int ready0, int minav, int gang, int idx_bits,
+                           int32_t* hout, JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
+                           int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int T = t_count, W = SP.world;
+  const int kp = sh.s_count;
+  stop = KB_STOP_DONE;  // (sel_run's local no-fit outcome is not the job's)
+  fail_task = -1;
+  panic = 0;
+  stopped = 0;
+  ShardGather& G = *(ShardGather*)cand;
+  // this rank's rows after all its picks, when it has fewer than T of them (a global no-fit needs every rank's)
+  if (kp < T)
+    fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, keys, l0, n0, l1, n1, nullptr, 0, true);
+  if (tid == 0) {
+    G.fail = 0;
+    G.diverged = 0;
+  }
+  const uint32_t tag = shard_tag(SP.epoch, xn);
+  const int r = (int)(xn % (uint32_t)kJobSlots);
+  const uint64_t th = (uint64_t)tag << 32;
+  const uint32_t hdr0 = (uint32_t)spec, hdr1 = (uint32_t)T;
+  const uint32_t hdr2 = (uint32_t)ready0 * 65599u + (uint32_t)minav * 31u + (uint32_t)gang;
+  const int L = 3 * T + 4 + kShardNoFitR;
+  // ---- write: this rank's record into every rank's inbox ----
+  for (int idx = tid; idx < W * L; idx += kSelThreads) {
+    const int w = idx / L, i = idx - w * L;
+    uint32_t v = 0;
+    if (i < 3 * T) {
+      const int e = i / 3, q = i - 3 * e;
+      if (e < kp) {
+        const uint64_t o = sh.ord[e];
+        if (q == 0) v = (uint32_t)(o >> 32);
+        else if (q == 1) v = (uint32_t)o;
+        else {
+          const int s = sel_slot(o), j = sel_level(o);
+          v = (uint32_t)(sh.node[s] + N.base) | ((uint32_t)(j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE) << 30);
+        }
+      }
+    } else if (i == 3 * T) {
+      v = (uint32_t)kp;
+    } else if (i < 3 * T + 4) {
+      v = i == 3 * T + 1 ? hdr0 : (i == 3 * T + 2 ? hdr1 : hdr2);
+    } else {
+      v = kp < T ? sh.hist[i - 3 * T - 4] : 0u;
+    }
+    __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // ---- read: every rank's record from this rank's inbox ----
+  {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    uint64_t* own = SP.inbox[SP.rank];
+    for (int idx = tid; idx < W * L && !late; idx += kSelThreads) {
+      const int w = idx / L, i = idx - w * L;
+      const uint64_t* p = shard_word(own, SP.epoch, r, w, i);
+      uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      while ((uint32_t)(x >> 32) != tag) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+          late = true;
+          // for the host's error text: the word waited for, the tag found there, and how many of rank w's words
+          // carry this job's tag
+          int have = 0;
+          for (int k = 0; k < L; ++k)
+            have += (uint32_t)(__hip_atomic_load(shard_word(own, SP.epoch, r, w, k), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM) >> 32) == tag;
+          hjs->t_recv = ((uint64_t)w << 56) | ((uint64_t)i << 40) | ((uint64_t)(uint32_t)have << 20) | 1ull;
+          hjs->t_done = ((uint64_t)(uint32_t)(x >> 32) << 32) | tag;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (late) break;
+      const uint32_t v = (uint32_t)x;
+      if (i < 3 * T) {
+        const int e = i / 3, q = i - 3 * e;
+        if (q == 0) G.hi[w][e] = v;
+        else if (q == 1) G.lo[w][e] = v;
+        else G.nk[w][e] = (int32_t)v;
+      } else if (i == 3 * T) {
+        G.kp[w] = (int32_t)v;
+      } else if (i < 3 * T + 4) {
+        G.hdr[w][i - 3 * T - 1] = v;
+      } else {
+        G.hist[w][i - 3 * T - 4] = v;
+      }
+    }
+    if (late) G.fail = 1;  // (benign race: every writer stores 1)
+  }
+  __syncthreads();
+  if (G.fail) return 1;
+  if (tid < W && (G.hdr[tid][0] != hdr0 || G.hdr[tid][1] != hdr1 || G.hdr[tid][2] != hdr2 || G.kp[tid] > T))
+    G.diverged = 1;
+  __syncthreads();
+  if (G.diverged) return 2;
+  // ---- the global pick order: proposal i of rank w ranks i + the larger proposals of every other rank ----
+  int K = 0;
+  for (int w = 0; w < W; ++w) K += G.kp[w];
+  int32_t* ordnk = sh.act;
+  for (int e = tid; e < W * T; e += kSelThreads) {
+    const int w = e / T, i = e - w * T;
+    if (i >= G.kp[w]) continue;
+    const uint64_t v = ((uint64_t)G.hi[w][i] << 32) | G.lo[w][i];
+    int rank = i;
+    for (int h = 0; h < W; ++h)
+      if (h != w) rank += shard_gt(G.hi[h], G.lo[h], G.kp[h], v);
+    if (rank < T) {
+      sh.ord[rank] = v;
+      ordnk[rank] = G.nk[w][i];
+    }
+  }
+  if (tid < sh.n_sel) sh.fin[tid] = 0;
+  __syncthreads();
+  const int Kp = K < T ? K : T;
+  if (wv == 0) {  // stop rules in pick order (as sel_run applies them on one GPU)
+    const int64_t bias32 = 1ll << (30 - idx_bits);
+    const uint32_t score_mask = (1u << (31 - idx_bits)) - 1;
+    const uint64_t lt = (1ull << lane) - 1;
+    const bool va = lane < Kp, vb = lane + 64 < Kp;
+    const uint64_t oa = va ? sh.ord[lane] : 0, ob = vb ? sh.ord[lane + 64] : 0;
+    const bool aa = va && ((uint32_t)ordnk[lane] >> 30) == KB_PLACE_ALLOCATE;
+    const bool ab = vb && ((uint32_t)ordnk[lane + 64] >> 30) == KB_PLACE_ALLOCATE;
+    const auto neg = [&](uint64_t o) {
+      const uint32_t e32 = (uint32_t)(o >> 14);
+      return (int64_t)((e32 >> idx_bits) & score_mask) - bias32 <= -1;
+    };
+    const uint64_t le_mask = lt | (1ull << lane);
+    const uint64_t ma = __ballot(aa), mb = __ballot(ab);
+    const int ra = ready0 + __popcll(ma & le_mask);
+    const int rb = ready0 + __popcll(ma) + __popcll(mb & le_mask);
+    const uint64_t sta = __ballot(va && (!gang || ra >= minav));
+    const uint64_t stb = __ballot(vb && (!gang || rb >= minav));
+    const uint64_t nga = __ballot(va && neg(oa)), ngb = __ballot(vb && neg(ob));
+    const int first_stop = sta ? __builtin_ctzll(sta) : (stb ? 64 + __builtin_ctzll(stb) : 128);
+    const int first_neg = nga ? __builtin_ctzll(nga) : (ngb ? 64 + __builtin_ctzll(ngb) : 128);
+    int cut, kind;
+    if (first_neg < Kp && first_neg <= first_stop) {
+      cut = first_neg;
+      kind = 3;
+    } else if (first_stop < Kp) {
+      cut = first_stop + 1;
+      kind = KB_STOP_READY;
+    } else if (Kp < T) {
+      cut = Kp;
+      kind = KB_STOP_NO_FIT;
+    } else {
+      cut = T;
+      kind = -1;
+    }
+    const int al = __popcll(cut >= 64 ? ma : (ma & ((1ull << cut) - 1))) +
+                   (cut > 64 ? __popcll(mb & ((1ull << (cut - 64)) - 1)) : 0);
+    if (lane == 0) {
+      G.cut = cut;
+      G.kind = kind;
+      G.n_alloc = al;
+    }
+  }
+  __syncthreads();
+  const int cut = G.cut, kind = G.kind;
+  // placements (every rank writes the whole sequence) and the picks on this rank's rows, per local slot
+  if (tid < cut) {
+    const int nk = ordnk[tid];
+    const int node = nk & 0x3fffffff;
+    hout[2 * (t_begin + tid)] = node;
+    hout[2 * (t_begin + tid) + 1] = (int32_t)((uint32_t)nk >> 30);
+    if (node >= N.base && node < N.base + N.n) atomicAdd(&sh.fin[sel_slot(sh.ord[tid])], 1);
+  }
+  __syncthreads();
+  if (tid < sh.n_sel && sh.fin[tid] > 0) {  // NodeInfo.AddTask x fin on this rank's row
+    const int w = sh.node[tid];
+    store_back_row(N, P, sp, P.sc_req + (size_t)spec * N.S, w, sh.fin[tid], sh.A[tid], sh.row[tid]);
+    commit_out[atomicAdd(&sh.n_commit, 1)] = w;
+  }
+  placed = cut;
+  ready = ready0 + G.n_alloc;
+  if (kind == 3) {
+    fail_task = t_begin + cut;
+    panic = 1;
+    stopped = 1;
+  } else if (kind == KB_STOP_READY) {
+    stop = KB_STOP_READY;
+    stopped = 1;
+  } else if (kind == KB_STOP_NO_FIT) {  // FitErrors over every rank's rows
+    if (tid < KB_NUM_REASONS) {
+      uint32_t h = 0;
+      for (int w = 0; w < W; ++w) h += G.hist[w][tid];
+      js->hist[tid] = h;
+      hjs->hist[tid] = h;
+    }
+    stop = KB_STOP_NO_FIT;
+    fail_task = t_begin + cut;
+    stopped = 1;
+  }
+  if (tid == 0) sh.need_hist = 0;
+  __syncthreads();
+  return 0;
+}
+
 // SPLIT: grid 1 + nsel, workgroup 0 the placer and 1.. the selectors (fed_selector) of nsel node ranges; every
 // job of the cycle one segment (the host checks). Otherwise one workgroup with every node's key in LDS.
-template <int QN, bool SPLIT>
+// SHARD (split only): the node-sharded engine -- the placer proposes, exchanges and merges (shard_place).
+template <int QN, bool SPLIT, bool SHARD = false>
 __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
-                                                                 int32_t* exit_flag, FedXchg* X, int nsel) {
+                                                                 int32_t* exit_flag, FedXchg* X, int nsel,
+                                                                 ShardPeers SP) {
+  static_assert(!SHARD || SPLIT, "the node-sharded engine is the split engine");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
@@ -3042,6 +3374,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t t_wait0 = dg_last, pub_prev = 0, rt_wait0 = __builtin_amdgcn_s_memrealtime();
 #endif
   uint32_t m = 0;
+  uint32_t xn = 0;  // SHARD: exchanges so far (the jobs that ran)
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
       if (tid == 0) {
@@ -3314,9 +3647,33 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       pub.node = X->p_node[r];
       pub.tag = m + 1;
     }
-    sel_run<false, QN, SPLIT>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
+    if constexpr (SHARD) {
+      sel_run<true, QN, true>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
                               gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
                               S.commits[slot] SEL_DIAG_ARGS, pub);
+      const int rc = shard_place(sh, k32, cand, SP, xn++, N, P, C, sp, spec, stat, S.keys[slot],
+                                 prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr,
+                                 prev_slot[0] >= 0 ? prev_ncommit[0] : 0,
+                                 prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr,
+                                 prev_slot[1] >= 0 ? prev_ncommit[1] : 0, cm.t_begin, cm.t_count, cm.ready0, minav,
+                                 gang, idx_bits, S.hout[slot], js, hjs, S.commits[slot], idle_ticks, stop, fail_task,
+                                 placed, ready, panic, stopped);
+      if (rc != 0) {  // a peer never answered (every rank's engine leaves), or the ranks issued different jobs
+        if (tid == 0) {
+          *exit_flag = 1;
+          if (rc == 2) {  // the host sees the job finish with the divergence flag (not a silent idle exit)
+            hjs->stall = 2;
+            js->n_commit = 0;
+            publish_state(js, hjs, 1, KB_STOP_DONE, -1, 0, ready, minav, gang, 0, cm.seq);
+          }
+        }
+        break;
+      }
+    } else {
+      sel_run<false, QN, SPLIT>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready,
+                                minav, gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp,
+                                nullptr, S.commits[slot] SEL_DIAG_ARGS, pub);
+    }
     if constexpr (SPLIT) {
       __syncthreads();
       // this job's set, with its final rows, is the next job's B
@@ -3440,9 +3797,11 @@ int fed_nsel(int n) {
 // the placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096
 bool fed_split_ok(int n) { return fed_nsel(n) > 0 && n > 4 * kSelThreads; }
 
+size_t shard_inbox_bytes() { return (size_t)2 * kJobSlots * kShardMaxWorld * kShardRecW * sizeof(uint64_t); }
+
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                      int32_t* exit_flag, void* xchg, void* stream, bool coop) {
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard) {
   FedSlots S;
   for (int s = 0; s < kJobSlots; ++s) {
     S.tgt[s] = tgt[s];
@@ -3459,15 +3818,19 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   const int bytes = nsel > 1 ? 4 * (4 * kSelThreads * kFedSelQ) + 8 * kCandCap : fed_lds_bytes(N.n);
   const FedCmd* ring_c = (const FedCmd*)ring;
   FedXchg* X = (FedXchg*)xchg;
+  ShardPeers SP = shard;
   void* args[] = {(void*)&N, (void*)&P, (void*)&C, (void*)&idx_bits, (void*)&S, (void*)&ring_c, (void*)&ctr,
-                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel};
+                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP};
+  const bool sharded = SP.world > 0;
+  if (sharded && !xchg) return (int)hipErrorInvalidValue;  // the node-sharded engine is the split engine
   // (no split instance for one key group: fed_split_ok needs n > 4 * kSelThreads)
   const void* f = nullptr;
   bool split = false;
-#define KB_FED_QN(Q)                                                               \
-  case Q:                                                                         \
-    split = xchg && Q != 1;                                                       \
-    f = split ? (const void*)fed_engine_kernel<Q, Q != 1> : (const void*)fed_engine_kernel<Q, false>; \
+#define KB_FED_QN(Q)                                                                                         \
+  case Q:                                                                                                   \
+    split = xchg && Q != 1;                                                                                 \
+    f = split ? (sharded ? (const void*)fed_engine_kernel<Q, Q != 1, Q != 1> : (const void*)fed_engine_kernel<Q, Q != 1>) \
+              : (const void*)fed_engine_kernel<Q, false>;                                                  \
     break;
   switch (qn) {
     KB_FED_QN(1)
@@ -3483,6 +3846,7 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   }
 #undef KB_FED_QN
   if (!split) nsel = 1;
+  if (sharded && !split) return (int)hipErrorInvalidValue;
   const dim3 grid(split ? 1 + nsel : 1), block(kSelThreads);
   if (coop) return (int)hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)bytes, (hipStream_t)stream);
   return (int)hipLaunchKernel(f, grid, block, args, (size_t)bytes, (hipStream_t)stream);
@@ -4970,7 +5334,8 @@ int configure_kernels() {
     if (e != hipSuccess) return (int)e;
   }
   // the fed engine's static block also holds its command and the split engine's merge lists: a smaller budget
-#define KB_FED_F(Q) (const void*)fed_engine_kernel<Q, false>, (const void*)fed_engine_kernel<Q, true>
+#define KB_FED_F(Q) \
+  (const void*)fed_engine_kernel<Q, false>, (const void*)fed_engine_kernel<Q, true>, (const void*)fed_engine_kernel<Q, true, true>
   for (const void* f : {KB_FED_F(0), (const void*)fed_engine_kernel<1, false>, KB_FED_F(2), KB_FED_F(3), KB_FED_F(4), KB_FED_F(5), KB_FED_F(6),
                         KB_FED_F(8), KB_FED_F(10)}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFedDynLimit);
@@ -5024,7 +5389,13 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 
 template <class SCORE>
 static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                          uint32_t* reasons, SCORE* scores, const int64_t* mm, void* stream) {
+                          uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, void* stream) {
+  if (plain) {
+    dim3 grid((N.n + 255) / 256, (t + kEvalPlainSpecs - 1) / kEvalPlainSpecs);
+    hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+                       reasons, scores);
+    return;
+  }
   dim3 grid((N.n + 255) / 256, (t + kEvalSpecs - 1) / kEvalSpecs);
   if (mm)
     hipLaunchKernelGGL((eval_kernel<true, SCORE>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
@@ -5034,12 +5405,12 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                        reasons, scores, mm);
 }
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, const int64_t* mm, void* stream) {
-  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, stream);
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, stream);
 }
 void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                   uint32_t* reasons, int32_t* scores, const int64_t* mm, void* stream) {
-  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, stream);
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, stream);
 }
 
 // kb_apply: one thread per row delta of a commit made outside the device -- NodeInfo.AddTask / RemoveTask

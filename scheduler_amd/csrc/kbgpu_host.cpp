@@ -235,6 +235,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->use_cap1 = getenv("KB_NO_CAP1") == nullptr;        // testing: cap-1 specs on the re-sweep loops
   c->use_cls = getenv("KB_NO_CLS") == nullptr;          // testing: class-loop specs on the re-sweep loops
   c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
+  c->use_eval_plain = getenv("KB_NO_EVAL_PLAIN") == nullptr;  // testing: kb_eval's general kernel on plain specs
   c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
   c->fed_dedicated = getenv("KB_FED_SHARED_QUEUES") == nullptr;  // testing: the shared-queue hazard
   c->fed_coop = c->fed_dedicated && getenv("KB_FED_PLAIN_LAUNCH") == nullptr;
@@ -300,6 +301,9 @@ void kb_destroy(kb_ctx* c) {
   if (c->d_rec) (void)hipFree(c->d_rec);
   if (c->d_rec_all) (void)hipFree(c->d_rec_all);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
+  for (int w = 0; w < kShardMaxWorld; ++w)
+    if (c->peer_inbox[w] && c->peer_inbox[w] != c->inbox) (void)hipIpcCloseMemHandle(c->peer_inbox[w]);
+  if (c->inbox) (void)hipFree(c->inbox);
   if (c->eng_dep) (void)hipEventDestroy(c->eng_dep);
   if (c->eng_stream) (void)hipStreamDestroy(c->eng_stream);
   for (auto& p : c->pending) {
@@ -474,6 +478,14 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   c->spec_ipa_err.assign(in->m, 0);
   c->ov_absmax.assign(in->m, 0);
   for (uint32_t i = 0; i < in->m; ++i) c->spec_ipa_err[i] = (in->specs[i].flags & KB_SPEC_IPA_ERROR) != 0;
+  c->spec_plain.assign(in->m, 0);
+  for (uint32_t i = 0; i < in->m; ++i) {
+    const kb_spec& s = in->specs[i];
+    const uint32_t not_plain = KB_SPEC_HAS_SELECTOR | KB_SPEC_HAS_REQUIRED | KB_SPEC_INIT_HAS_MAP | KB_SPEC_NA_ERROR |
+                               KB_SPEC_IPA_ERROR | KB_SPEC_POD_AFFINITY;
+    c->spec_plain[i] = !(s.flags & not_plain) && s.pref_term_cnt == 0 && s.port_cnt == 0 && s.aff_class < 0 &&
+                       in->n_taint_sets == 1 && in->tolerates[(size_t)s.tol_set] != 0;
+  }
   for (uint32_t i = 0; i < in->m; ++i)
     c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
   for (uint32_t i = 0; i < in->m; ++i) {
@@ -843,6 +855,7 @@ static int shard_common(kb_ctx* c, const kb_shard* sh) {
   HIP_OK(c, hipMemset(c->d_rec_all, 0, sizeof(ShardRec) * (size_t)sh->world));
   c->shard = *sh;
   c->sharded = true;
+  c->peer = false;  // (kb_set_shard_peer sets it after this)
   return KB_OK;
 }
 
@@ -855,6 +868,46 @@ int kb_set_shard(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) 
   HIP_OK(c, hipHostMalloc((void**)&c->h_rec, sizeof(ShardRec) * (size_t)(1 + sh->world), hipHostMallocDefault));
   c->ag_fn = fn;
   c->ag_user = user;
+  return KB_OK;
+}
+
+// The node-sharded fed engine's exchange: this rank's inbox in its GPU's memory (uncached: peers write it over
+// xGMI and the engine polls it), its IPC handle all-gathered through fn, the peers' inboxes opened. fn stays the
+// host-staged exchange of jobs the engine does not run.
+int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) {
+  if (int rc = kb_set_shard(c, sh, fn, user)) return rc;
+  const size_t bytes = shard_inbox_bytes();
+  if (!c->inbox) {
+    if (hipExtMallocWithFlags(&c->inbox, bytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      HIP_OK(c, hipMalloc(&c->inbox, bytes));
+    }
+  }
+  HIP_OK(c, hipMemset(c->inbox, 0, bytes));
+  HIP_OK(c, hipDeviceSynchronize());
+  for (int w = 0; w < kShardMaxWorld; ++w) {
+    if (c->peer_inbox[w] && c->peer_inbox[w] != c->inbox) (void)hipIpcCloseMemHandle(c->peer_inbox[w]);
+    c->peer_inbox[w] = nullptr;
+  }
+  const int W = sh->world;
+  std::vector<hipIpcMemHandle_t> h((size_t)W + 1);
+  if (W > 1) {
+    HIP_OK(c, hipIpcGetMemHandle(&h[0], c->inbox));
+    if (int rc = fn(user, &h[0], &h[1], sizeof(hipIpcMemHandle_t)))
+      return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the inbox handles", rc);
+  }
+  for (int w = 0; w < W; ++w) {
+    if (w == sh->rank) {
+      c->peer_inbox[w] = c->inbox;
+      continue;
+    }
+    void* p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, h[1 + w], hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return fail(c, KB_E_HIP, "hipIpcOpenMemHandle (rank %d's inbox): %s", w, hipGetErrorString(e));
+    c->peer_inbox[w] = p;
+  }
+  c->peer = true;
+  c->shard_epoch = 0;
   return KB_OK;
 }
 
@@ -1315,7 +1368,10 @@ int kb_place_job(kb_ctx* c, const kb_job_req* job, int32_t* placed_node, int32_t
 }
 
 // Sharded contexts pipeline with the RCCL exchange only (a host-staged exchange waits for the proposal).
-int kb_job_pipeline_ok(kb_ctx* c) { return c && (!c->sharded || c->comm) && !c->use_engine && !c->broken; }
+// (kb_set_shard_peer: the fed engine's cycles only; kb_allocate's driver drops pipelining for the others)
+int kb_job_pipeline_ok(kb_ctx* c) {
+  return c && (!c->sharded || c->comm || c->peer) && !c->use_engine && !c->broken;
+}
 
 int kb_job_guardable(kb_ctx* c, const kb_job_req* job) {
   if (c->fed) return job->n_tasks > 0 && kb_spec_fed_ok(c, job->task_specs[0]);  // the engine's own guard
@@ -1335,7 +1391,8 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 
 int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
-  if (c->sharded || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
+  if ((c->sharded && !c->peer) || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
+  if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n))) return 0;  // the sharded engine is the split one
   const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
   if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
   if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
@@ -1353,6 +1410,9 @@ static uint64_t fed_idle_ticks() {
 
 int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return 0;
+  if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n) &&
+                      max_job_tasks <= (uint32_t)kFedSplitMaxTasks))
+    return 0;
   const int ns = fed_nsel(c->N.n);
   return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
 }
@@ -1398,9 +1458,19 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     c->stats.fed_split++;
   }
   c->stats.fed_cycles++;
+  ShardPeers SP{};
+  if (c->sharded) {  // (kb_fed_cycle_ok: peer exchange, split engine)
+    if (!xchg) return fail(c, KB_E_STATE, "node-sharded fed engine without the split engine");
+    for (int w = 0; w < c->shard.world; ++w) SP.inbox[w] = (uint64_t*)c->peer_inbox[w];
+    SP.rank = c->shard.rank;
+    SP.world = c->shard.world;
+    SP.epoch = ++c->shard_epoch;
+    c->stats.fed_sharded++;
+  }
+  // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
+  const uint64_t idle = c->sharded ? 10 * fed_idle_ticks() : fed_idle_ticks();
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
-                                          c->fed_count, fed_idle_ticks(), c->fed_exit, xchg, c->stream,
-                                          c->fed_coop));
+                                          c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1464,6 +1534,25 @@ int kb_fed_end(kb_ctx* c) {
 int kb_fed_abandon(kb_ctx* c) {
   if (!c || !c->fed) return KB_OK;
   c->fed = false;
+  if (c->sharded) {  // every rank would have to leave at the same job: fail loudly instead
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream_b);
+    std::string why;
+    for (auto& sl : c->slot) {
+      sl.busy = false;
+      const JobState* hs = (const JobState*)sl.h;
+      if (hs && (hs->t_recv & 1)) {  // the placer's note (shard_place): the word it waited for
+        char b[200];
+        snprintf(b, sizeof(b), " (rank %d waited for rank %d's word %d: tag %08x there, %08x wanted; %d of the "
+                 "record's words current; epoch %u)", c->shard.rank, (int)(hs->t_recv >> 56),
+                 (int)((hs->t_recv >> 40) & 0xffff), (unsigned)(hs->t_done >> 32), (unsigned)hs->t_done,
+                 (int)((hs->t_recv >> 20) & 0xfffff), c->shard_epoch);
+        why = b;
+      }
+    }
+    return fail(c, KB_E_STATE, "node-sharded fed engine: a rank's proposal did not arrive (a peer stalled or left)%s",
+                why.c_str());
+  }
   if (c->fed_ev) {
     c->ev_end(c->fed_ev, KB_KERNEL_FED_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
     c->fed_ev = nullptr;
@@ -1496,6 +1585,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     S.t_issue = std::chrono::steady_clock::now();
     c->timing_now = c->timing && (c->issue_count++ % c->timing_every == 0);  // the job's sweep
     memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
+    ((JobState*)S.h)->t_recv = 0;  // (the sharded placer's timeout note)
     FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
                  job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
                  pred ? pred->ready : 0, ++c->seq};
@@ -1602,11 +1692,18 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
       }
       launch_ipa_minmax(c->N, c->P, d_ids, 0, (int)cnt, c->mm_eval, nullptr, c->stream);
     }
+    // a batch of plain specs (no overlay rows): the row-only kernel (KB_NO_EVAL_PLAIN: the general one, tests)
+    bool plain = c->use_eval_plain;
+    for (uint32_t i = 0; i < cnt && plain; ++i) {
+      const int s = spec_ids[b + i];
+      plain = c->spec_plain[s] && ((size_t)s >= c->ov_slot.size() || c->ov_slot[s] < 0);
+    }
     c->ev_begin(&ea);
     if constexpr (sizeof(SCORE) == 8)
-      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
+      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain, c->stream);
     else
-      launch_eval32(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, c->stream);
+      launch_eval32(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain,
+                    c->stream);
     c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
     if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
     if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))

@@ -122,7 +122,8 @@ class kb_stats(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 15), ("kernel_ms", C.c_double * 15), ("pairs", C.c_uint64 * 15),
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8),
                 ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64),
-                ("cap1_runs", C.c_uint64), ("cls_runs", C.c_uint64)]
+                ("cap1_runs", C.c_uint64), ("cls_runs", C.c_uint64),
+                ("fed_sharded", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -140,11 +141,12 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 11  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 12  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
            "kb_get_stats", "kb_upload_affinity", "kb_set_shard", "kb_comm_unique_id", "kb_set_shard_rccl",
+           "kb_set_shard_peer",
            "kb_set_host_overlay", "kb_apply", "kb_apply_affinity", "kb_set_nofit_hook", "kb_sort_nodes", "kb_predicate_nodes"]
 
 _lib = None
@@ -186,6 +188,7 @@ def load_library(path: str = LIB_PATH):
     lib.kb_set_shard.argtypes = [P, C.POINTER(kb_shard), ALLGATHER_FN, P]
     lib.kb_comm_unique_id.argtypes = [P]
     lib.kb_set_shard_rccl.argtypes = [P, C.POINTER(kb_shard), P]
+    lib.kb_set_shard_peer.argtypes = [P, C.POINTER(kb_shard), ALLGATHER_FN, P]
     lib.kb_set_host_overlay.argtypes = [P, C.c_int32, P, P]
     lib.kb_apply.argtypes = [P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32]
     lib.kb_apply_affinity.argtypes = [P, P, C.c_uint32]
@@ -233,10 +236,13 @@ class Context:
         if rc != KB_OK:
             raise KbError(rc, self.lib.kb_last_error(self.ctx).decode())
 
-    def set_shard(self, rank: int, world: int, n_total: int, allgather=None, rccl_id: bytes = None):
-        """Node sharding (kb_set_shard / kb_set_shard_rccl): this context holds shard_range(n_total, rank, world).
-        `allgather(send: bytes) -> bytes` (all ranks' records, rank order) for the host-staged exchange, or the
-        RCCL id from comm_unique_id() (the same bytes on every rank) for the device exchange."""
+    def set_shard(self, rank: int, world: int, n_total: int, allgather=None, rccl_id: bytes = None,
+                  peer: bool = False):
+        """Node sharding (kb_set_shard / kb_set_shard_rccl / kb_set_shard_peer): this context holds
+        shard_range(n_total, rank, world). `allgather(send: bytes) -> bytes` (all ranks' records, rank order) for the
+        host-staged exchange, or the RCCL id from comm_unique_id() (the same bytes on every rank) for the RCCL
+        exchange. peer=True (with allgather): the node-sharded fed engine's device exchange (inboxes mapped across
+        the ranks' GPUs; allgather carries their IPC handles once, then the jobs the engine does not run)."""
         begin, end = shard_range(n_total, rank, world)
         sh = kb_shard(n_total, begin, rank, world)
         self.rows = (begin, end)
@@ -255,7 +261,8 @@ class Context:
             except Exception:  # an error must not unwind through the C frames
                 return -1
         self._ag_cb = ALLGATHER_FN(cb)  # kept alive as long as the context
-        self._check(self.lib.kb_set_shard(self.ctx, C.byref(sh), self._ag_cb, None))
+        fn = self.lib.kb_set_shard_peer if peer else self.lib.kb_set_shard
+        self._check(fn(self.ctx, C.byref(sh), self._ag_cb, None))
 
     def upload(self, snap: E.Snapshot):
         cfg = kb_config(**snap.config)
@@ -343,7 +350,8 @@ class Context:
         return {"launches": list(st.launches), "kernel_ms": list(st.kernel_ms), "pairs": list(st.pairs),
                 "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag),
                 "fed_abandon": st.fed_abandon, "fed_cycles": st.fed_cycles, "fed_split": st.fed_split,
-                "cap1_runs": st.cap1_runs, "cls_runs": st.cls_runs}
+                "cap1_runs": st.cap1_runs, "cls_runs": st.cls_runs,
+                "fed_sharded": st.fed_sharded}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

@@ -1,10 +1,12 @@
 #!/bin/bash
-# Functional rehearsal of the multi-rank bench paths on ONE GPU (ranks share the card, gloo group,
-# host-staged shard exchange). Numbers are not meaningful; the 8-GPU runs belong to the driver.
+# Functional rehearsal of the multi-rank bench paths on ONE GPU (ranks share the card, gloo group for the
+# handle exchange, the engines' inboxes IPC-mapped between the processes). Numbers are not meaningful; the 8-GPU runs belong to the driver.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export KB_BENCH_SAME_GPU=1
+# ranks sharing the card: plain engine launches (cooperative launches from several processes take turns on it)
+export KB_FED_PLAIN_LAUNCH=1
 run() {  # run <name> <args...>: `bench.py --gpus 2` spawns its two ranks itself (as the driver's N=2 line)
   local name=$1; shift
   timeout -k 10 500 python bench.py --gpus 2 "$@" > gpurun_out/$name.log 2>&1

@@ -104,6 +104,38 @@ def edge_cluster(seed=7):
     return cl
 
 
+def plain_edge_cluster(seed=7):
+    """edge_cluster reduced to plain specs (kb_eval's row-only kernel): no taints, selectors, host ports, scalar
+    requests or affinity, one taint set -- but still not-ready / unschedulable / pressure nodes (memory pressure
+    for the BestEffort tasks, disk and PID pressure for all), full pod counts, releasing capacity and init
+    containers."""
+    cl = edge_cluster(seed)
+    for t in cl.tiers:
+        for p in t["plugins"]:
+            if p["name"] == "predicates":
+                p.setdefault("arguments", {})["predicate.PIDPressureEnable"] = "true"
+    for i, nd in enumerate(cl.nodes):
+        nd.taints = []
+        if i == 9:
+            nd.conditions.append({"type": "PIDPressure", "status": "True"})
+        if i == 11:
+            nd.conditions.append({"type": "MemoryPressure", "status": "True"})
+            nd.conditions.append({"type": "DiskPressure", "status": "True"})
+    keep = []
+    for p in cl.pods:
+        plain = not (p.node_selector or p.tolerations or p.affinity or
+                     any(c.ports for c in p.containers) or
+                     any(k not in (m.CPU, m.MEMORY) for c in p.containers + p.init for k in c.req))
+        if plain or p.node:
+            keep.append(p)
+    cl.pods = keep
+    for j in range(3):  # more BestEffort tasks (no requests at all)
+        cl.pod_groups.append(m.PodGroup(ns="e", name=f"be{j}", queue="q1", min_member=1))
+        cl.pods.append(m.Pod(ns="e", name=f"be{j}-0", uid=f"e-be{j}-0", group=f"be{j}",
+                             containers=[m.Container(req={})]))
+    return cl
+
+
 def backfill_cluster(seed=7, n_be=160):
     """edge_cluster plus jobs of BestEffort pods (empty InitResreq) for backfill (backfill.go:54-86): plain,
     with a node selector, with a host port (one per node), tolerating the dedicated taint, and one gang job

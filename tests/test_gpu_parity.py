@@ -12,7 +12,7 @@ from scheduler_amd import export as E
 from scheduler_amd import model as m
 from scheduler_amd import runtime, synth
 
-from helpers import affinity_clusters, parity_clusters
+from helpers import affinity_clusters, parity_clusters, plain_edge_cluster
 from test_oracle_kat import allocate_test_cases
 
 pytestmark = pytest.mark.gpu
@@ -88,6 +88,65 @@ def test_eval32_equals_eval(name, cluster):
         ctx.close()
     assert np.array_equal(r32, r64)
     assert np.array_equal(s32.astype(np.int64), s64)
+
+
+def _plain_spec(snap):
+    a = snap.spec_arr
+    bad = (E.SPEC_HAS_SELECTOR | E.SPEC_HAS_REQUIRED | E.SPEC_INIT_HAS_MAP | E.SPEC_NA_ERROR | E.SPEC_POD_AFFINITY |
+           E.SPEC_IPA_ERROR)
+    return ((a["flags"] & bad) == 0) & (a["pref_term_cnt"] == 0) & (a["port_cnt"] == 0) & (a["aff_class"] < 0) & \
+        (snap.tolerates.shape[1] == 1)
+
+
+def test_eval_plain_matches_oracle():
+    """kb_eval's row-only kernel (plain specs: resource fit, pod count, conditions, memory / disk / PID pressure,
+    BestEffort, LeastRequested + Balanced) against the oracle on every (spec, node) pair."""
+    cl = plain_edge_cluster()
+    snap = E.Snapshot(cl)
+    reps = {}
+    for t in snap.session_tasks:
+        if t["status"] == E.ST["Pending"] and t["spec"] not in reps:
+            reps[t["spec"]] = t["uid"]
+    spec_ids = sorted(reps)
+    assert _plain_spec(snap)[spec_ids].all() and (snap.spec_arr["flags"][spec_ids] & E.SPEC_BEST_EFFORT).any()
+    ref = pyoracle.evaluate(cl, [reps[s] for s in spec_ids])
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        reasons, scores = ctx.eval(spec_ids)
+        r32, s32 = ctx.eval32(spec_ids)
+    finally:
+        ctx.close()
+    for i, s in enumerate(spec_ids):
+        rt = ref["tasks"][i]
+        for n in range(snap.n_nodes):
+            got = sorted(E.REASONS[b] for b in range(16) if (int(reasons[i, n]) >> b) & 1)
+            assert got == sorted(rt["reasons"][n]), (s, n)
+        assert list(scores[i]) == rt["score"], s
+    assert np.array_equal(r32, reasons) and np.array_equal(s32.astype(np.int64), scores)
+
+
+@pytest.mark.parametrize("name", ["plain-edge", "C2-2000", "C1-parity"])
+def test_eval_plain_equals_general(name, monkeypatch):
+    """The row-only kernel returns the general eval_kernel's arrays (KB_NO_EVAL_PLAIN) on plain batches."""
+    cl = {"plain-edge": plain_edge_cluster, "C2-2000": lambda: synth.c2(n_nodes=2000, n_jobs=64, tasks_per_job=1,
+                                                                        seed=9),
+          "C1-parity": lambda: synth.c1(n_nodes=120, n_jobs=24, tasks_per_job=25, seed=1)}[name]()
+    snap = E.Snapshot(cl)
+    ids = [int(s) for s in np.nonzero(_plain_spec(snap))[0]]
+    assert ids
+    out = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("KB_NO_EVAL_PLAIN", env)
+        ctx = runtime.Context(0)
+        try:
+            ctx.upload(snap)
+            out.append(ctx.eval(ids) + ctx.eval32(ids))
+        finally:
+            ctx.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
 
 
 def test_full_size_c2_properties():

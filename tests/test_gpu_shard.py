@@ -287,7 +287,7 @@ def test_sharded_ranks_that_diverge_fail_loudly():
         assert got[r] == {"overlay": runtime.KB_E_UNSUPPORTED, "diverged": runtime.KB_E_STATE}, (r, got[r])
 
 
-def _c5_full_rank(rank, world, port, q):
+def _c5_full_rank(rank, world, port, q, peer=False):
     import torch
     import torch.distributed as dist
     from helpers import digest_arrays
@@ -303,9 +303,11 @@ def _c5_full_rank(rank, world, port, q):
         snap = synth.c2_snapshot(n_nodes=50000, n_jobs=10000, tasks_per_job=100, seed=synth.SEED)
         ctx = runtime.Context(0)
         try:
-            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
             ctx.upload(snap)
             out = ctx.allocate(snap)
+            if peer and ctx.stats()["fed_sharded"] != 1:
+                raise AssertionError("the cycle did not run on the node-sharded engine")
         finally:
             ctx.close()
         k = int(out["n_events"])
@@ -320,12 +322,17 @@ def _c5_full_rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_c5_full_eight_ranks_match_oracle_digest():
+@pytest.mark.parametrize("exchange", ["host", "peer"])
+def test_c5_full_eight_ranks_match_oracle_digest(exchange, monkeypatch):
     """BASELINE.json configs[4] at its stated size and split: 50k nodes x 1M pods, the node table sharded 8 ways
-    (8 ranks sharing the GPU, one host-staged all-gather over gloo per run segment). Every rank's whole cycle
-    equals the oracle's (tests/golden/digest-C5: 1,000,000 placements, 7,373 s of oracle time)."""
+    (8 ranks sharing the GPU). host: one host-staged all-gather over gloo per run segment; peer: the node-sharded
+    fed engine (kb_set_shard_peer), every job's proposals exchanged between the ranks' resident engines through
+    IPC-mapped inboxes. Every rank's whole cycle equals the oracle's (tests/golden/digest-C5: 1,000,000
+    placements, 7,373 s of oracle time)."""
     import json
     import torch.multiprocessing as mp
+    if exchange == "peer":  # ranks sharing one GPU: plain launches (cooperative ones from several processes
+        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")  # take turns on the card, DESIGN.md §5)
     golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     with open(os.path.join(golden, "digest-C5.json")) as f:
         meta = json.load(f)
@@ -333,7 +340,7 @@ def test_c5_full_eight_ranks_match_oracle_digest():
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_c5_full_rank, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctxm.Process(target=_c5_full_rank, args=(r, world, port, q, exchange == "peer")) for r in range(world)]
     for p in procs:
         p.start()
     import queue

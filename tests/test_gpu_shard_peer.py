@@ -1,0 +1,132 @@
+"""The node-sharded fed engine (kb_set_shard_peer): every rank's resident engine proposes its first T picks,
+writes them into every rank's inbox (device memory mapped across the ranks through IPC handles) and merges all of
+them on the device -- no host round trip and no collective launch per job. Parity bar: the placements, statuses
+and FitErrors of one unsharded GPU context on the same snapshot (itself oracle- and digest-checked), cycle after
+cycle (the engine's tags carry the cycle number). Multi-rank runs are processes sharing the one GPU of the box."""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+
+from scheduler_amd import runtime, synth
+
+from test_gpu_shard import _summary
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(world):
+    """Fed-eligible cycles (one <= 100-task run per job) with every rank's block over the split engine's 2048 nodes:
+    full gangs, half gangs whose jobs are popped again, a cycle that runs out of room (NO_FIT), BestEffort-free."""
+    n = 2100 * world + 300
+    half = synth.c2_snapshot(n_nodes=n, n_jobs=90, tasks_per_job=40, seed=23)
+    half.s_job_min = np.full_like(half.s_job_min, 20)  # ready at half the job: popped again for the rest
+    return {
+        "c2-gang": synth.c2_snapshot(n_nodes=n, n_jobs=120, tasks_per_job=60, seed=21),
+        "c2-nofit": synth.c2_snapshot(n_nodes=n, n_jobs=60, tasks_per_job=100, seed=22, fill=2.5),
+        "c2-halfgang": half,
+    }
+
+
+def _reference(snap, cycles):
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        out = []
+        for _ in range(cycles):
+            ctx.restore()
+            out.append(_summary(ctx.allocate(snap)))
+        return out
+    finally:
+        ctx.close()
+
+
+def _sharded(snap, rank, world, allgather, cycles, barrier=None):
+    ctx = runtime.Context(0)
+    try:
+        ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
+        ctx.upload(snap)
+        out = []
+        for c in range(cycles):
+            ctx.restore()
+            if barrier is not None:
+                barrier()
+            t0 = time.perf_counter()
+            out.append(_summary(ctx.allocate(snap)))
+            print(f"rank {rank}/{world} cycle {c}: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+        return out, ctx.stats()
+    finally:
+        ctx.close()
+
+
+def test_peer_engine_one_rank():
+    """world 1: the sharded engine's exchange through its own inbox; three cycles (the tags' cycle halves)."""
+    for name, snap in _cases(1).items():
+        ref = _reference(snap, 3)
+        got, st = _sharded(snap, 0, 1, lambda b: b, 3)
+        assert st["fed_sharded"] == 3 and st["fed_abandon"] == 0, (name, st)
+        assert got == ref, name
+
+
+def _rank_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    # ranks sharing one GPU: plain engine launches (cooperative launches from several processes take turns on the
+    # card -- 10 ms per job here; one process per GPU, as deployed, keeps the cooperative launch)
+    os.environ["KB_FED_PLAIN_LAUNCH"] = "1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+
+    res = {}
+    try:
+        for name, snap in _cases(world).items():
+            print(f"rank {rank}/{world}: {name}", flush=True)
+            got, st = _sharded(snap, rank, world, allgather, 2, barrier=dist.barrier)
+            res[name] = (got, st["fed_sharded"], st["fed_abandon"])
+        q.put((rank, res, None))
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_engine_ranks_equal_one_gpu(world):
+    """2 and 3 ranks (processes on the one GPU, inboxes IPC-mapped between them): every rank reports the one-GPU
+    outcome, two cycles each, and every cycle ran on the sharded engine."""
+    import torch.multiprocessing as mp
+    ref = {name: _reference(snap, 2) for name, snap in _cases(world).items()}
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, f"rank {rank}: {err}"
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        for name in ref:
+            out, n_sharded, n_abandon = got[r][name]
+            assert n_sharded == 2 and n_abandon == 0, (world, r, name)
+            assert out == ref[name], (world, r, name)
