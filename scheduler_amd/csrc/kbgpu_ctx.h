@@ -164,6 +164,7 @@ struct kb_ctx {
   bool prev_listed = false; // the last issued job was one selection run that lists its commits
   int prev_slot = -1;
   uint64_t n_overlap = 0;   // sweeps that ran overlapped
+  int32_t fed_exit_code = 0;   // the engine's exit flag when it left early (wait_seq)
   uint64_t n_fed_abandon = 0;  // cycles finished on the launch path after the engine idled out
   char* h_eval = nullptr;
 

@@ -804,16 +804,45 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
 }
 
 // kb_eval over a batch of plain specs (the host checks, kb_ctx::spec_plain: no nodeSelector, node affinity, host
-// ports, scalar requests, inter-pod terms or overlay, and one taint set that every spec tolerates). The chain then
-// reads only the row: resource fit, pod count, the node's conditions and pressure, LeastRequested + Balanced. The
-// node-only parts are computed once per node; the specs' four requests and BestEffort bit are staged in LDS once
-// per block, so the per-spec loop has no dependent scalar loads and no spec-dependent branches. Same values as
-// eval_kernel on such specs (tests/test_gpu_parity.py::test_eval_plain_equals_general).
+// ports, scalar requests, inter-pod terms or overlay, requests below 2^49, and one taint set that every spec
+// tolerates). The chain then reads only the row: resource fit, pod count, the node's conditions and pressure,
+// LeastRequested + Balanced. The node-only parts are computed once per node; the specs' requests are staged in LDS
+// once per block, so the per-spec loop has no dependent scalar loads and no spec-dependent branches. Rows whose
+// values lie below 2^49 (all real ones) take the loop in f64, which is exact there: every sum, difference and
+// tenfold product of such integers is an integer below 2^53, the LeastRequested quotient is floored from a
+// reciprocal estimate and corrected by one exact fma remainder, and Balanced keeps bra_score_inv's estimate with
+// its IEEE-division fallback near integers. Other rows take the int64 forms. Same values as eval_kernel on such
+// specs (tests/test_gpu_parity.py::test_eval_plain_equals_general, test_eval_plain_matches_oracle).
 constexpr int kEvalPlainSpecs = 32;
+constexpr double kPlainMax = 562949953421312.0;  // 2^49
+// leastRequestedScore (least_requested.go:36-53) on integers below 2^49 held in doubles: the quotient truncated
+// from a reciprocal estimate (the floor, or one off when num / cap lies within 2^-48 of an integer), then corrected
+// by the exact remainder (fma: num - q * cap is an integer below 2^53)
+__device__ __forceinline__ int lr_score_f64(double req, double cap, double inv) {
+  const double num = (cap - req) * 10.0;  // exact
+  const int qe = (int)(num * inv);
+  const double rem = fma(-(double)qe, cap, num);
+  const int q = qe + (rem >= cap ? 1 : 0) - (rem < 0.0 ? 1 : 0);
+  return (cap == 0.0 || req > cap) ? 0 : q;
+}
+// BalancedResourceAllocation (balanced_resource_allocation.go:41-77) as bra_score_inv, on such doubles (pos: the
+// node's capacities are positive; the requests here never are negative)
+__device__ __forceinline__ int bra_score_f64(double rc, double ac, double rm, double am, double ic, double im,
+                                             bool pos) {
+  if (pos) {
+    if (rc >= ac || rm >= am) return 0;
+    const double f = (1.0 - fabs(rc * ic - rm * im)) * 10.0;
+    const double fl = floor(f);
+    if (f - fl > 1e-9 && fl + 1.0 - f > 1e-9) return (int)fl;  // f in [0, 10]: truncation is the floor
+  }
+  const double cf = ac == 0.0 ? 1.0 : rc / ac, mf = am == 0.0 ? 1.0 : rm / am;
+  return (cf >= 1.0 || mf >= 1.0) ? 0 : (int)((1.0 - fabs(cf - mf)) * 10.0);
+}
 template <class SCORE>
 __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
                                                          int t, uint32_t* reasons, SCORE* scores) {
   __shared__ int64_t s_req[4][kEvalPlainSpecs];  // init cpu, init mem, non-zero cpu, non-zero mem
+  __shared__ double s_dreq[4][kEvalPlainSpecs];  // the same as doubles (exact: below 2^49)
   __shared__ uint32_t s_be[kEvalPlainSpecs];
   const int j0 = blockIdx.y * kEvalPlainSpecs;
   const int nj = t - j0 < kEvalPlainSpecs ? t - j0 : kEvalPlainSpecs;
@@ -823,13 +852,16 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     s_req[1][threadIdx.x] = sp.init_mem;
     s_req[2][threadIdx.x] = sp.nz_cpu;
     s_req[3][threadIdx.x] = sp.nz_mem;
+    s_dreq[0][threadIdx.x] = (double)sp.init_cpu;
+    s_dreq[1][threadIdx.x] = (double)sp.init_mem;
+    s_dreq[2][threadIdx.x] = (double)sp.nz_cpu;
+    s_dreq[3][threadIdx.x] = (double)sp.nz_mem;
     s_be[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? 1u : 0u;
   }
   __syncthreads();
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N.n) return;
   const Row r = load_row(N, n);
-  const double ic = 1.0 / (double)r.alloc_cpu, im = 1.0 / (double)r.alloc_mem;
   // row_reasons after the resource check, per node: pod count, conditions (static_eval's pre), then the post
   // reasons (no taints: the one taint set is tolerated) -- memory pressure for BestEffort specs only
   uint32_t after = 0, post_be = 0;
@@ -844,23 +876,51 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     after = r.max_pods <= r.pod_count ? 1u << KB_R_POD_NUMBER : (pre ? pre : post);
     if (r.max_pods <= r.pod_count || pre) post_be = after;
   }
-  uint32_t* rout = reasons + n;
-  SCORE* sout = scores + n;
   const size_t stride = (size_t)N.n;
+  const double d_ic = (double)r.idle_cpu, d_im = (double)r.idle_mem, d_rc = (double)r.rel_cpu,
+               d_rm = (double)r.rel_mem, d_nc = (double)r.nz_cpu, d_nm = (double)r.nz_mem,
+               d_ac = (double)r.alloc_cpu, d_am = (double)r.alloc_mem;
+  const double inv_c = 1.0 / d_ac, inv_m = 1.0 / d_am;
+  const bool fast = fabs(d_ic) < kPlainMax && fabs(d_im) < kPlainMax && fabs(d_rc) < kPlainMax &&
+                    fabs(d_rm) < kPlainMax && fabs(d_nc) < kPlainMax && fabs(d_nm) < kPlainMax &&
+                    fabs(d_ac) < kPlainMax && fabs(d_am) < kPlainMax;
+  if (fast) {
+    // LessEqual's tolerance folded into the node's side once: r - avail < tol <=> r < avail + tol (exact here)
+    const double t_ic = d_ic + 10.0, t_im = d_im + 10485760.0, t_rc = d_rc + 10.0, t_rm = d_rm + 10485760.0;
+    const bool pos = d_ac > 0.0 && d_am > 0.0;
 #pragma unroll 4
+    for (int j = 0; j < nj; ++j) {
+      const double icpu = s_dreq[0][j], imem = s_dreq[1][j];
+      const bool fit = (icpu < t_ic && imem < t_im) || (icpu < t_rc && imem < t_rm);
+      const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
+      SCORE score = 0;
+      if (C.nodeorder) {  // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term
+        const double rc = s_dreq[2][j] + d_nc, rm = s_dreq[3][j] + d_nm;
+        const int lr = (lr_score_f64(rc, d_ac, inv_c) + lr_score_f64(rm, d_am, inv_m)) >> 1;
+        // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
+        score = (SCORE)lr * (SCORE)C.w_lr + (SCORE)bra_score_f64(rc, d_ac, rm, d_am, inv_c, inv_m, pos) * (SCORE)C.w_bra;
+      }
+      // uniform row bases: the stores take a scalar base and the lane's offset
+      uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
+      SCORE* srow = scores + (size_t)(j0 + j) * stride;
+      rrow[n] = rs;
+      srow[n] = score;
+    }
+    return;
+  }
   for (int j = 0; j < nj; ++j) {
     const int64_t icpu = s_req[0][j], imem = s_req[1][j];
     const bool fit = (le_tol(icpu, r.idle_cpu, 10) && le_tol(imem, r.idle_mem, 10ll * 1024 * 1024)) ||
                      (le_tol(icpu, r.rel_cpu, 10) && le_tol(imem, r.rel_mem, 10ll * 1024 * 1024));
     const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
     int64_t score = 0;
-    if (C.nodeorder) {  // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term
+    if (C.nodeorder) {
       const int64_t rc = s_req[2][j] + r.nz_cpu, rm = s_req[3][j] + r.nz_mem;
-      const int64_t lr = (lr_score_inv(rc, r.alloc_cpu, ic) + lr_score_inv(rm, r.alloc_mem, im)) / 2;
-      score = lr * C.w_lr + bra_score_inv(rc, r.alloc_cpu, rm, r.alloc_mem, ic, im) * C.w_bra;
+      const int64_t lr = (lr_score_inv(rc, r.alloc_cpu, inv_c) + lr_score_inv(rm, r.alloc_mem, inv_m)) / 2;
+      score = lr * C.w_lr + bra_score_inv(rc, r.alloc_cpu, rm, r.alloc_mem, inv_c, inv_m) * C.w_bra;
     }
-    rout[(size_t)(j0 + j) * stride] = rs;
-    sout[(size_t)(j0 + j) * stride] = (SCORE)score;
+    reasons[(size_t)(j0 + j) * stride + n] = rs;
+    scores[(size_t)(j0 + j) * stride + n] = (SCORE)score;
   }
 }
 
@@ -2806,7 +2866,7 @@ __device__ __forceinline__ void fed_wait_cmd(const uint32_t* ctr, uint32_t tgt, 
       op = cm.op;
     }
     s_op = op;
-    if (op == KB_ENG_EXIT_IDLE) *exit_flag = 1;
+    if (op == KB_ENG_EXIT_IDLE) atomicMax(exit_flag, 1);
   }
   __syncthreads();
 }
@@ -2878,7 +2938,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
           }
           if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
             n2 = -1;
-            *exit_flag = 1;
+            atomicMax(exit_flag, 1);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -2941,7 +3001,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
           }
           if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
             n1 = -1;
-            *exit_flag = 1;
+            atomicMax(exit_flag, 1);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -2953,11 +3013,17 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     KB_SSTAMP(2);
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
     if (tid < s_n1) {  // job m-1's set is the placer's to re-key (every entry's tag checked: no store order)
-      uint64_t e;
-      do e = x_load64(&X->p_node[r1][tid]);
-      while ((uint32_t)(e >> 32) != m);
+      uint64_t e = x_load64(&X->p_node[r1][tid]);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((uint32_t)(e >> 32) != m) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {  // (cannot happen: the head is stored last)
+          atomicMax(exit_flag, 2);
+          break;
+        }
+        e = x_load64(&X->p_node[r1][tid]);
+      }
       const uint32_t w = (uint32_t)e - (uint32_t)base;
-      if (w < (uint32_t)n) k32[w] = 0u;
+      if ((uint32_t)(e >> 32) == m && w < (uint32_t)n) k32[w] = 0u;
     }
     __syncthreads();
     // candidates outside the set (a zeroed key: inside), in rank order; the first T go out
@@ -3140,38 +3206,52 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
   const uint32_t hdr0 = (uint32_t)spec, hdr1 = (uint32_t)T;
   const uint32_t hdr2 = (uint32_t)ready0 * 65599u + (uint32_t)minav * 31u + (uint32_t)gang;
   const int L = 3 * T + 4 + kShardNoFitR;
-  // ---- write: this rank's record into every rank's inbox ----
-  for (int idx = tid; idx < W * L; idx += kSelThreads) {
-    const int w = idx / L, i = idx - w * L;
-    uint32_t v = 0;
+  // record word i of this rank, and where a record word goes in the gathered arrays
+  const auto word = [&](int i) -> uint32_t {
     if (i < 3 * T) {
       const int e = i / 3, q = i - 3 * e;
-      if (e < kp) {
-        const uint64_t o = sh.ord[e];
-        if (q == 0) v = (uint32_t)(o >> 32);
-        else if (q == 1) v = (uint32_t)o;
-        else {
-          const int s = sel_slot(o), j = sel_level(o);
-          v = (uint32_t)(sh.node[s] + N.base) | ((uint32_t)(j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE) << 30);
-        }
-      }
-    } else if (i == 3 * T) {
-      v = (uint32_t)kp;
-    } else if (i < 3 * T + 4) {
-      v = i == 3 * T + 1 ? hdr0 : (i == 3 * T + 2 ? hdr1 : hdr2);
-    } else {
-      v = kp < T ? sh.hist[i - 3 * T - 4] : 0u;
+      if (e >= kp) return 0u;
+      const uint64_t o = sh.ord[e];
+      if (q == 0) return (uint32_t)(o >> 32);
+      if (q == 1) return (uint32_t)o;
+      const int s = sel_slot(o), j = sel_level(o);
+      return (uint32_t)(sh.node[s] + N.base) | ((uint32_t)(j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE) << 30);
     }
-    __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i == 3 * T) return (uint32_t)kp;
+    if (i < 3 * T + 4) return i == 3 * T + 1 ? hdr0 : (i == 3 * T + 2 ? hdr1 : hdr2);
+    return kp < T ? sh.hist[i - 3 * T - 4] : 0u;
+  };
+  const auto gput = [&](int w, int i, uint32_t v) {
+    if (i < 3 * T) {
+      const int e = i / 3, q = i - 3 * e;
+      if (q == 0) G.hi[w][e] = v;
+      else if (q == 1) G.lo[w][e] = v;
+      else G.nk[w][e] = (int32_t)v;
+    } else if (i == 3 * T) {
+      G.kp[w] = (int32_t)v;
+    } else if (i < 3 * T + 4) {
+      G.hdr[w][i - 3 * T - 1] = v;
+    } else {
+      G.hist[w][i - 3 * T - 4] = v;
+    }
+  };
+  // ---- write: this rank's record into every other rank's inbox (its own goes straight to LDS) ----
+  for (int idx = tid; idx < W * L; idx += kSelThreads) {
+    const int w = idx / L, i = idx - w * L;
+    const uint32_t v = word(i);
+    if (w == SP.rank) gput(w, i, v);
+    else
+      __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // ---- read: every rank's record from this rank's inbox ----
+  // ---- read: every other rank's record from this rank's inbox ----
   {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool late = false;
     uint64_t* own = SP.inbox[SP.rank];
     for (int idx = tid; idx < W * L && !late; idx += kSelThreads) {
       const int w = idx / L, i = idx - w * L;
+      if (w == SP.rank) continue;
       const uint64_t* p = shard_word(own, SP.epoch, r, w, i);
       uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       while ((uint32_t)(x >> 32) != tag) {
@@ -3191,19 +3271,7 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
         x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (late) break;
-      const uint32_t v = (uint32_t)x;
-      if (i < 3 * T) {
-        const int e = i / 3, q = i - 3 * e;
-        if (q == 0) G.hi[w][e] = v;
-        else if (q == 1) G.lo[w][e] = v;
-        else G.nk[w][e] = (int32_t)v;
-      } else if (i == 3 * T) {
-        G.kp[w] = (int32_t)v;
-      } else if (i < 3 * T + 4) {
-        G.hdr[w][i - 3 * T - 1] = v;
-      } else {
-        G.hist[w][i - 3 * T - 4] = v;
-      }
+      gput(w, i, (uint32_t)x);
     }
     if (late) G.fail = 1;  // (benign race: every writer stores 1)
   }
@@ -3416,7 +3484,15 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
               uint64_t w = have ? pre[q] : x_load64(&X->s_cmd[r][q]);
-              while ((uint32_t)(w >> 32) != m + 1) w = x_load64(&X->s_cmd[r][q]);  // the tag orders it
+              const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+              while ((uint32_t)(w >> 32) != m + 1) {  // the tag orders it
+                if (__builtin_amdgcn_s_memrealtime() - t1 > idle_ticks) {  // (cannot happen: the head is last)
+                  c = -2;
+                  atomicMax(exit_flag, 3);
+                  break;
+                }
+                w = x_load64(&X->s_cmd[r][q]);
+              }
               fields[q] = (uint32_t)w;
             }
             __builtin_memcpy(&cm, fields, sizeof(FedCmd));
@@ -3424,7 +3500,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           // the sweep's static cache (another agent's release, which the selector has seen): fresh loads
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        if (c == -2) *exit_flag = 1;
+        if (c == -2) atomicMax(exit_flag, 1);
         s_cand = c;
         s_op = c >= 0 ? KB_ENG_RUN : (c == kSelExit ? KB_ENG_EXIT : KB_ENG_EXIT_IDLE);
       }
@@ -3660,7 +3736,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                                  placed, ready, panic, stopped);
       if (rc != 0) {  // a peer never answered (every rank's engine leaves), or the ranks issued different jobs
         if (tid == 0) {
-          *exit_flag = 1;
+          atomicMax(exit_flag, 1);
           if (rc == 2) {  // the host sees the job finish with the divergence flag (not a silent idle exit)
             hjs->stall = 2;
             js->n_commit = 0;

@@ -483,8 +483,11 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
     const kb_spec& s = in->specs[i];
     const uint32_t not_plain = KB_SPEC_HAS_SELECTOR | KB_SPEC_HAS_REQUIRED | KB_SPEC_INIT_HAS_MAP | KB_SPEC_NA_ERROR |
                                KB_SPEC_IPA_ERROR | KB_SPEC_POD_AFFINITY;
+    const int64_t lim = 1ll << 49;  // (the row-only kernel's f64 loop: requests below 2^49)
     c->spec_plain[i] = !(s.flags & not_plain) && s.pref_term_cnt == 0 && s.port_cnt == 0 && s.aff_class < 0 &&
-                       in->n_taint_sets == 1 && in->tolerates[(size_t)s.tol_set] != 0;
+                       in->n_taint_sets == 1 && in->tolerates[(size_t)s.tol_set] != 0 && s.init_cpu >= 0 &&
+                       s.init_cpu < lim && s.init_mem >= 0 && s.init_mem < lim && s.nz_cpu >= 0 && s.nz_cpu < lim &&
+                       s.nz_mem >= 0 && s.nz_mem < lim;
   }
   for (uint32_t i = 0; i < in->m; ++i)
     c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
@@ -669,7 +672,10 @@ static int wait_seq(kb_ctx* c, const JobState* hs, uint32_t want) {
         if (c->fed) {  // the resident engine left: idle exit (a host stall longer than the idle bound)?
           int32_t idle = 0;
           if (hipMemcpy(&idle, c->fed_exit, sizeof(idle), hipMemcpyDeviceToHost) == hipSuccess && idle)
-            return fail(c, kFedIdleExit, "fed engine exited idle before command %u", want);
+          {
+            c->fed_exit_code = idle;  // 1 idle; 2 / 3: a selector / placer hand-off word never came (a bug)
+            return fail(c, kFedIdleExit, "fed engine exited (code %d) before command %u", idle, want);
+          }
         }
         return fail(c, KB_E_HIP, "place kernel finished without reporting (seq %u, want %u)", hs->seq, want);
       }
@@ -1550,8 +1556,8 @@ int kb_fed_abandon(kb_ctx* c) {
         why = b;
       }
     }
-    return fail(c, KB_E_STATE, "node-sharded fed engine: a rank's proposal did not arrive (a peer stalled or left)%s",
-                why.c_str());
+    return fail(c, KB_E_STATE, "node-sharded fed engine left (code %d): a rank's proposal did not arrive (a peer "
+                "stalled or left)%s", c->fed_exit_code, why.c_str());
   }
   if (c->fed_ev) {
     c->ev_end(c->fed_ev, KB_KERNEL_FED_ENGINE, c->fed_tasks * (uint64_t)c->N.n);

@@ -19,7 +19,7 @@ for d in ("p1", "p2", "p3", "p4"):
     for f in glob.glob(os.path.join(out, d, "**", "*counter_collection.csv"), recursive=True):
         per = {}
         for row in csv.DictReader(open(f)):
-            if "eval_kernel" not in row.get("Kernel_Name", ""):
+            if not any(k in row.get("Kernel_Name", "") for k in ("eval_kernel", "eval_plain_kernel")):
                 continue
             k = (row["Counter_Name"], row["Dispatch_Id"])
             per[k] = per.get(k, 0.0) + float(row["Counter_Value"])
@@ -30,7 +30,7 @@ for d in ("p1", "p2", "p3", "p4"):
             res[name] = sum(vs) / len(vs)
 for f in glob.glob(os.path.join(out, "trace", "**", "*kernel_stats.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "eval_kernel" in row["Name"]:
+        if "eval_kernel" in row["Name"] or "eval_plain_kernel" in row["Name"]:
             res["avg_ns"] = float(row["AverageNs"])
 pairs = 256 * 50000
 res["pairs"] = pairs

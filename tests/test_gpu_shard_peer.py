@@ -64,6 +64,7 @@ def _sharded(snap, rank, world, allgather, cycles, barrier=None):
 def test_peer_engine_one_rank():
     """world 1: the sharded engine's exchange through its own inbox; three cycles (the tags' cycle halves)."""
     for name, snap in _cases(1).items():
+        print(f"one rank: {name}", flush=True)
         ref = _reference(snap, 3)
         got, st = _sharded(snap, 0, 1, lambda b: b, 3)
         assert st["fed_sharded"] == 3 and st["fed_abandon"] == 0, (name, st)
