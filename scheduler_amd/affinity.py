@@ -591,4 +591,6 @@ class Tables:
         xb = list(self.xb_pods) + [(u, self.xb_spec[sp]) for u, sp in allocated_before if sp in self.xb_spec]
         if xb:
             return f"Failed to get all terms that pod {pn} matches, err: {min(xb)[1]}"
+        if spec not in self.own_err:  # (host_reason_strings asks only for specs with an error source)
+            raise self.U(f"spec {spec} has no inter-pod affinity error to report")
         return f"Cannot schedule pod {pn} onto node {node_name}, because of PodAffinity, err: {self.own_err[spec]}"

@@ -1,7 +1,8 @@
 """Probe: allocate cycles of C2 (10k x 100k) on a node-sharded context with one rank, per exchange kind:
   peer -- the node-sharded fed engine (kb_set_shard_peer): the resident engine proposes, exchanges through the
           inboxes and merges on the device, one launch per cycle plus one sweep per job;
-  rccl -- the pipelined launch path (sweep, proposal, ncclAllGather, merge + commit per job).
+  rccl -- the pipelined launch path (sweep, proposal, ncclAllGather, merge + commit per job);
+  none -- the unsharded fed engine on the same box, for comparison.
 Usage: python3 scripts/shard_pipeline_probe.py [peer|rccl ...]   (KB_NO_PIPELINE=1: the serial driver)"""
 import json
 import os
@@ -16,7 +17,7 @@ def probe(kind, snap):
     ctx = runtime.Context(0, timing=True)
     if kind == "peer":
         ctx.set_shard(0, 1, snap.n_nodes, allgather=lambda b: b, peer=True)
-    else:
+    elif kind == "rccl":
         ctx.set_shard(0, 1, snap.n_nodes, rccl_id=runtime.comm_unique_id())
     ctx.upload(snap)
     ctx.allocate(snap)
@@ -40,7 +41,7 @@ def probe(kind, snap):
 
 def main():
     snap = synth.c2_snapshot(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=synth.SEED)
-    for kind in sys.argv[1:] or ["peer", "rccl"]:
+    for kind in sys.argv[1:] or ["none", "peer", "rccl"]:
         probe(kind, snap)
 
 
