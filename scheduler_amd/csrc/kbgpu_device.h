@@ -258,6 +258,7 @@ struct ShardPeers {
   uint64_t* inbox[kShardMaxWorld];  // every rank's inbox as this GPU addresses it (its own included)
   int32_t rank, world;              // world 0: not sharded
   uint32_t epoch;                   // this cycle's number (the same on every rank)
+  int32_t self_inbox;               // testing (KB_SHARD_SELF_INBOX=1): the rank's own record through its inbox too
 };
 size_t shard_inbox_bytes();
 // coop: a cooperative launch (every workgroup co-resident, on the device's cooperative queue); returns the

@@ -815,25 +815,28 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
 // specs (tests/test_gpu_parity.py::test_eval_plain_equals_general, test_eval_plain_matches_oracle).
 constexpr int kEvalPlainSpecs = 32;
 constexpr double kPlainMax = 562949953421312.0;  // 2^49
-// leastRequestedScore (least_requested.go:36-53) on integers below 2^49 held in doubles: the quotient truncated
-// from a reciprocal estimate (the floor, or one off when num / cap lies within 2^-48 of an integer), then corrected
-// by the exact remainder (fma: num - q * cap is an integer below 2^53)
-__device__ __forceinline__ int lr_score_f64(double req, double cap, double inv) {
-  const double num = (cap - req) * 10.0;  // exact
+// leastRequestedScore (least_requested.go:36-53) on integers below 2^49 held in doubles. num = (cap - req) * 10
+// arrives as the node's (cap - nz_node) * 10 minus the spec's nz * 10 (exact), so req > cap is num < 0. The
+// quotient is truncated from a reciprocal estimate (the floor, or one off when num / cap lies within 2^-48 of an
+// integer) and corrected by the exact remainder (fma: num - q * cap is an integer below 2^53). cap == 0: the
+// caller's node flag.
+__device__ __forceinline__ int lr_score_f64(double num, double cap, double inv) {
   const int qe = (int)(num * inv);
   const double rem = fma(-(double)qe, cap, num);
   const int q = qe + (rem >= cap ? 1 : 0) - (rem < 0.0 ? 1 : 0);
-  return (cap == 0.0 || req > cap) ? 0 : q;
+  return num < 0.0 ? 0 : q;
 }
-// BalancedResourceAllocation (balanced_resource_allocation.go:41-77) as bra_score_inv, on such doubles (pos: the
-// node's capacities are positive; the requests here never are negative)
-__device__ __forceinline__ int bra_score_f64(double rc, double ac, double rm, double am, double ic, double im,
+// BalancedResourceAllocation (balanced_resource_allocation.go:41-77) as bra_score_inv, on such doubles: with
+// positive capacities (pos) f = 10 - |rc * 10/ac - rm * 10/am| estimates (1 - |cf - mf|) * 10 within 1e-14, which
+// decides the truncation unless f lies within 1e-9 of an integer; then (and for other capacities) the IEEE
+// divisions of the reference
+__device__ __forceinline__ int bra_score_f64(double rc, double ac, double rm, double am, double ic10, double im10,
                                              bool pos) {
   if (pos) {
     if (rc >= ac || rm >= am) return 0;
-    const double f = (1.0 - fabs(rc * ic - rm * im)) * 10.0;
-    const double fl = floor(f);
-    if (f - fl > 1e-9 && fl + 1.0 - f > 1e-9) return (int)fl;  // f in [0, 10]: truncation is the floor
+    const double f = 10.0 - fabs(fma(rc, ic10, -(rm * im10)));
+    const double fr = f - floor(f);
+    if (fr > 1e-9 && fr < 1.0 - 1e-9) return (int)f;  // f in [0, 10]: truncation is the floor
   }
   const double cf = ac == 0.0 ? 1.0 : rc / ac, mf = am == 0.0 ? 1.0 : rm / am;
   return (cf >= 1.0 || mf >= 1.0) ? 0 : (int)((1.0 - fabs(cf - mf)) * 10.0);
@@ -842,8 +845,10 @@ template <class SCORE>
 __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
                                                          int t, uint32_t* reasons, SCORE* scores) {
   __shared__ int64_t s_req[4][kEvalPlainSpecs];  // init cpu, init mem, non-zero cpu, non-zero mem
-  __shared__ double s_dreq[4][kEvalPlainSpecs];  // the same as doubles (exact: below 2^49)
+  __shared__ double s_dreq[4][kEvalPlainSpecs];  // init cpu, init mem as doubles; non-zero cpu, mem x 10 (exact)
+  __shared__ double s_dnz[2][kEvalPlainSpecs];   // non-zero cpu, mem as doubles
   __shared__ uint32_t s_be[kEvalPlainSpecs];
+  __shared__ SCORE s_tab[11 * 11];  // lr * w_lr + bra * w_bra for lr, bra in 0..10
   const int j0 = blockIdx.y * kEvalPlainSpecs;
   const int nj = t - j0 < kEvalPlainSpecs ? t - j0 : kEvalPlainSpecs;
   if ((int)threadIdx.x < nj) {
@@ -854,9 +859,15 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     s_req[3][threadIdx.x] = sp.nz_mem;
     s_dreq[0][threadIdx.x] = (double)sp.init_cpu;
     s_dreq[1][threadIdx.x] = (double)sp.init_mem;
-    s_dreq[2][threadIdx.x] = (double)sp.nz_cpu;
-    s_dreq[3][threadIdx.x] = (double)sp.nz_mem;
+    s_dreq[2][threadIdx.x] = (double)sp.nz_cpu * 10.0;
+    s_dreq[3][threadIdx.x] = (double)sp.nz_mem * 10.0;
+    s_dnz[0][threadIdx.x] = (double)sp.nz_cpu;
+    s_dnz[1][threadIdx.x] = (double)sp.nz_mem;
     s_be[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? 1u : 0u;
+  }
+  if (threadIdx.x >= 128 && threadIdx.x < 128 + 121) {
+    const int q = (int)threadIdx.x - 128;
+    s_tab[q] = (SCORE)(q / 11) * (SCORE)C.w_lr + (SCORE)(q % 11) * (SCORE)C.w_bra;
   }
   __syncthreads();
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -888,17 +899,21 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     // LessEqual's tolerance folded into the node's side once: r - avail < tol <=> r < avail + tol (exact here)
     const double t_ic = d_ic + 10.0, t_im = d_im + 10485760.0, t_rc = d_rc + 10.0, t_rm = d_rm + 10485760.0;
     const bool pos = d_ac > 0.0 && d_am > 0.0;
+    const double num_c = (d_ac - d_nc) * 10.0, num_m = (d_am - d_nm) * 10.0;  // minus the spec's nz * 10
+    const double ic10 = 10.0 / d_ac, im10 = 10.0 / d_am;
+    const bool zc = d_ac == 0.0, zm = d_am == 0.0;
 #pragma unroll 4
     for (int j = 0; j < nj; ++j) {
       const double icpu = s_dreq[0][j], imem = s_dreq[1][j];
-      const bool fit = (icpu < t_ic && imem < t_im) || (icpu < t_rc && imem < t_rm);
+      const bool fit = ((icpu < t_ic) & (imem < t_im)) | ((icpu < t_rc) & (imem < t_rm));
       const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
       SCORE score = 0;
       if (C.nodeorder) {  // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term
-        const double rc = s_dreq[2][j] + d_nc, rm = s_dreq[3][j] + d_nm;
-        const int lr = (lr_score_f64(rc, d_ac, inv_c) + lr_score_f64(rm, d_am, inv_m)) >> 1;
+        const int lc = zc ? 0 : lr_score_f64(num_c - s_dreq[2][j], d_ac, inv_c);
+        const int lm = zm ? 0 : lr_score_f64(num_m - s_dreq[3][j], d_am, inv_m);
+        const double rc = s_dnz[0][j] + d_nc, rm = s_dnz[1][j] + d_nm;
         // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
-        score = (SCORE)lr * (SCORE)C.w_lr + (SCORE)bra_score_f64(rc, d_ac, rm, d_am, inv_c, inv_m, pos) * (SCORE)C.w_bra;
+        score = s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, d_ac, rm, d_am, ic10, im10, pos)];
       }
       // uniform row bases: the stores take a scalar base and the lane's offset
       uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
@@ -1991,11 +2006,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       KB_SEL_PH(4);
       if constexpr (PROPOSE && CAND) {
         // the node-sharded fed engine's placer: the proposal stays in sh.ord[0..s_count) for the caller's exchange
-        // and merge; with fewer picks than tasks, sh.fin counts every one of them (the local no-fit histogram
-        // applies them all)
-        const int Kp = sh.s_count;
-        if (tid < Kp && Kp < (int)T) atomicAdd(&sh.fin[sel_slot(sh.ord[tid])], 1);
-        __syncthreads();
+        // and merge (shard_place)
         break;
       } else if constexpr (PROPOSE) {
         // the rank's proposal: its best picks in order with their global nodes and commit kinds; when it runs
@@ -3081,29 +3092,15 @@ __device__ __forceinline__ Row row_after(const kb_spec& sp, const Row& r0, int c
 // placer's LDS: every node's key is the sweep's (keys, read from memory) unless its row changed since, on one of
 // the three commit lists; those are re-keyed. bits (LDS, n bits) marks them, so a node listed twice counts once
 // and the streamed pass skips it. Ends after a barrier with the histogram in sh.hist.
-// sset (the node-sharded placer, before its commits): the selected nodes with sh.fin > 0 are keyed at their level
-// after those picks from their segment-start rows first (traj_key64), the rest as above.
 __device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                                 const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
-                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2,
-                                bool sset = false) {
+                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int n = N.n, nw = (n + 31) >> 5;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = tid; i < nw; i += kSelThreads) bits[i] = 0u;
   if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
   __syncthreads();
-  if (sset) {
-    if (tid < sh.n_sel && sh.fin[tid] > 0) {
-      const int w = sh.node[tid];
-      const uint64_t k = traj_key64(N, P, C, sp, sci, P.sc_req + (size_t)spec * N.S, sh.row[tid], sh.stat[tid], w,
-                                    sh.fin[tid], sh.A[tid]);
-      atomicOr(&bits[w >> 5], 1u << (w & 31));
-      if (!(k & kFeasible))
-        for (uint32_t m = (uint32_t)k; m; m &= m - 1) atomicAdd(&sh.hist[__builtin_ctz(m)], 1u);
-    }
-    __syncthreads();
-  }
   for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
     const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : l2[i - n0 - n1]);
     const uint32_t b = 1u << (w & 31);
@@ -3165,6 +3162,8 @@ __device__ __forceinline__ int shard_gt(const uint32_t* ghi, const uint32_t* glo
   return lo;
 }
 constexpr int kShardNoFitR = KB_NUM_REASONS;
+constexpr int kShardHistOff = 3 * kShardSegMax + 4;  // the no-fit round's words in a record
+static_assert(kShardHistOff + kShardNoFitR <= kShardRecW, "inbox record layout");
 // gathered proposals in the placer's candidate space (free between sel_run and the next job's B rows)
 struct ShardGather {
   uint32_t hi[kShardMaxWorld][128], lo[kShardMaxWorld][128];
@@ -3187,15 +3186,13 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
                            int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int T = t_count, W = SP.world;
+  __syncthreads();  // sel_run's no-fit exit writes sh.s_count = 0 from one thread with no barrier after it
   const int kp = sh.s_count;
   stop = KB_STOP_DONE;  // (sel_run's local no-fit outcome is not the job's)
   fail_task = -1;
   panic = 0;
   stopped = 0;
   ShardGather& G = *(ShardGather*)cand;
-  // this rank's rows after all its picks, when it has fewer than T of them (a global no-fit needs every rank's)
-  if (kp < T)
-    fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, keys, l0, n0, l1, n1, nullptr, 0, true);
   if (tid == 0) {
     G.fail = 0;
     G.diverged = 0;
@@ -3205,7 +3202,7 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
   const uint64_t th = (uint64_t)tag << 32;
   const uint32_t hdr0 = (uint32_t)spec, hdr1 = (uint32_t)T;
   const uint32_t hdr2 = (uint32_t)ready0 * 65599u + (uint32_t)minav * 31u + (uint32_t)gang;
-  const int L = 3 * T + 4 + kShardNoFitR;
+  const int L = 3 * T + 4;  // (a global no-fit's histograms follow in a second round at kShardHistOff)
   // record word i of this rank, and where a record word goes in the gathered arrays
   const auto word = [&](int i) -> uint32_t {
     if (i < 3 * T) {
@@ -3218,8 +3215,7 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
       return (uint32_t)(sh.node[s] + N.base) | ((uint32_t)(j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE) << 30);
     }
     if (i == 3 * T) return (uint32_t)kp;
-    if (i < 3 * T + 4) return i == 3 * T + 1 ? hdr0 : (i == 3 * T + 2 ? hdr1 : hdr2);
-    return kp < T ? sh.hist[i - 3 * T - 4] : 0u;
+    return i == 3 * T + 1 ? hdr0 : (i == 3 * T + 2 ? hdr1 : hdr2);
   };
   const auto gput = [&](int w, int i, uint32_t v) {
     if (i < 3 * T) {
@@ -3229,17 +3225,15 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
       else G.nk[w][e] = (int32_t)v;
     } else if (i == 3 * T) {
       G.kp[w] = (int32_t)v;
-    } else if (i < 3 * T + 4) {
-      G.hdr[w][i - 3 * T - 1] = v;
     } else {
-      G.hist[w][i - 3 * T - 4] = v;
+      G.hdr[w][i - 3 * T - 1] = v;
     }
   };
   // ---- write: this rank's record into every other rank's inbox (its own goes straight to LDS) ----
   for (int idx = tid; idx < W * L; idx += kSelThreads) {
     const int w = idx / L, i = idx - w * L;
     const uint32_t v = word(i);
-    if (w == SP.rank) gput(w, i, v);
+    if (w == SP.rank && !SP.self_inbox) gput(w, i, v);
     else
       __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3251,7 +3245,7 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
     uint64_t* own = SP.inbox[SP.rank];
     for (int idx = tid; idx < W * L && !late; idx += kSelThreads) {
       const int w = idx / L, i = idx - w * L;
-      if (w == SP.rank) continue;
+      if (w == SP.rank && !SP.self_inbox) continue;
       const uint64_t* p = shard_word(own, SP.epoch, r, w, i);
       uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       while ((uint32_t)(x >> 32) != tag) {
@@ -3368,7 +3362,45 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
   } else if (kind == KB_STOP_READY) {
     stop = KB_STOP_READY;
     stopped = 1;
-  } else if (kind == KB_STOP_NO_FIT) {  // FitErrors over every rank's rows
+  } else if (kind == KB_STOP_NO_FIT) {
+    // FitErrors over every rank's rows (allocate.go:150-153): each rank's histogram of its rows with the job's
+    // commits applied (as the one-GPU engine computes it: the sweep's keys, the rows the last two jobs and this one
+    // wrote back re-keyed), then a second round of the exchange (17 tagged words per rank) and the sum
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores and the sweep's keys: fresh loads
+    __syncthreads();
+    fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, keys, l0, n0, l1, n1, commit_out, sh.n_commit);
+    if (tid < W * kShardNoFitR) {
+      const int w = tid / kShardNoFitR, b = tid - w * kShardNoFitR;
+      if (w == SP.rank && !SP.self_inbox) {
+        G.hist[w][b] = sh.hist[b];
+      } else {
+        __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, kShardHistOff + b), th | sh.hist[b],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (tid < W * kShardNoFitR) {
+      const int w = tid / kShardNoFitR, b = tid - w * kShardNoFitR;
+      if (w != SP.rank || SP.self_inbox) {
+        const uint64_t* p = shard_word(SP.inbox[SP.rank], SP.epoch, r, w, kShardHistOff + b);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        while ((uint32_t)(x >> 32) != tag) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            G.fail = 1;
+            hjs->t_recv = ((uint64_t)w << 56) | ((uint64_t)(kShardHistOff + b) << 40) | 1ull;
+            hjs->t_done = ((uint64_t)(uint32_t)(x >> 32) << 32) | tag;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        G.hist[w][b] = (uint32_t)x;
+      }
+    }
+    __syncthreads();
+    if (G.fail) return 1;
     if (tid < KB_NUM_REASONS) {
       uint32_t h = 0;
       for (int w = 0; w < W; ++w) h += G.hist[w][tid];

@@ -1471,6 +1471,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     SP.rank = c->shard.rank;
     SP.world = c->shard.world;
     SP.epoch = ++c->shard_epoch;
+    SP.self_inbox = getenv("KB_SHARD_SELF_INBOX") != nullptr;
     c->stats.fed_sharded++;
   }
   // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
