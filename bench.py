@@ -437,17 +437,32 @@ def eval_side(device):
         us = st["kernel_ms"][k] * 1e3 / max(1, st["launches"][k])
         pairs = len(ids) * EVAL_NODES
         alg = pairs * EVAL_OUT_BYTES + EVAL_NODES * 76
-        out = {"kernel": "eval_kernel", "bound": "hbm", "specs": len(ids), "nodes": EVAL_NODES,
+        # (a batch of plain specs, as here, runs eval_plain_kernel: DESIGN.md §4)
+        kname = "eval_plain_kernel" if snap_plain(snap, ids) else "eval_kernel"
+        out = {"kernel": kname, "bound": "hbm", "specs": len(ids), "nodes": EVAL_NODES,
                "avg_launch_us": round(us, 3), "algorithmic_bytes_per_launch": alg,
                "achieved": round(alg / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None, "measured_frac": None}
-        tr = pmc_traffic("eval_kernel", "C2")  # the C2 PMC pass carries this side measurement
+        tr = pmc_traffic(kname, "C2")  # the C2 PMC pass carries this side measurement
         if tr is not None:
             out["traffic"], out["traffic_source"] = tr["bytes_per_launch"], tr["source"]
             out["measured_frac"] = round(tr["bytes_per_launch"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         return out
     except Exception as e:
         return {"error": repr(e)[:300]}
+
+
+def snap_plain(snap, ids):
+    """Every spec of the batch is plain (kb_ctx::spec_plain in kbgpu_host.cpp)."""
+    from scheduler_amd import export as E
+    a = snap.spec_arr[np.asarray(ids)]
+    bad = (E.SPEC_HAS_SELECTOR | E.SPEC_HAS_REQUIRED | E.SPEC_INIT_HAS_MAP | E.SPEC_NA_ERROR | E.SPEC_POD_AFFINITY |
+           E.SPEC_IPA_ERROR)
+    lim = 1 << 49
+    ok = (((a["flags"] & bad) == 0) & (a["pref_term_cnt"] == 0) & (a["port_cnt"] == 0) & (a["aff_class"] < 0) &
+          (a["init_cpu"] >= 0) & (a["init_cpu"] < lim) & (a["init_mem"] >= 0) & (a["init_mem"] < lim) &
+          (a["nz_cpu"] >= 0) & (a["nz_cpu"] < lim) & (a["nz_mem"] >= 0) & (a["nz_mem"] < lim))
+    return bool(ok.all()) and snap.tolerates.shape[1] == 1 and bool(snap.tolerates[:, 0].all())
 
 
 def spawn_ranks(n):
