@@ -47,7 +47,7 @@ def _cases():
     return dict(_clusters(), backfill=backfill_cluster())
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, peer=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -65,7 +65,7 @@ def _rank_main(rank, world, port, q):
             snap = E.Snapshot(cl)
             ctx = runtime.Context(0)
             try:
-                ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+                ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
                 res[name] = _run(name, snap, ctx)
             finally:
                 ctx.close()
@@ -82,8 +82,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("exchange", ["host", "peer"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_one_gpu(world):
+def test_sharded_equals_one_gpu(world, exchange, monkeypatch):
+    """Parity clusters (too small for the sharded engine: every job through the launch path) on 2 and 3 ranks.
+    peer: kb_set_shard_peer contexts, whose non-engine cycles go one job at a time over the host-staged exchange."""
+    if exchange == "peer":
+        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")
     import torch.multiprocessing as mp
     ref = {}
     for name, cl in _cases().items():
@@ -95,7 +100,7 @@ def test_sharded_equals_one_gpu(world):
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctxm.Process(target=_rank_main, args=(r, world, port, q, exchange == "peer")) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -368,7 +373,7 @@ def _aff_cases():
     return dict(affinity_clusters())
 
 
-def _aff_rank_main(rank, world, port, q):
+def _aff_rank_main(rank, world, port, q, peer=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -386,7 +391,7 @@ def _aff_rank_main(rank, world, port, q):
             snap = E.Snapshot(cl)
             ctx = runtime.Context(0)
             try:
-                ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather)
+                ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
                 ctx.upload(snap)
                 r = runtime.result_dict(snap, ctx.allocate(snap))
                 res[name] = {k: r[k] for k in ("events", "binds", "fit_errors")}
@@ -399,8 +404,8 @@ def _aff_rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_affinity_matches_oracle(world):
+@pytest.mark.parametrize("world,exchange", [(2, "host"), (3, "host"), (2, "peer")])
+def test_sharded_affinity_matches_oracle(world, exchange, monkeypatch):
     """Replicated count tables and histograms, one whole-cluster IPA min / max per run (or per task), every
     commit applied on every rank: the oracle's events, binds and FitErrors on every affinity cluster (C4 shapes,
     the edge clusters, the self-affinity clusters whose specs run one task per segment or as cap-1 runs)."""
@@ -410,7 +415,9 @@ def test_sharded_affinity_matches_oracle(world):
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_aff_rank_main, args=(r, world, port, q)) for r in range(world)]
+    if exchange == "peer":  # (ranks sharing the GPU: plain engine launches)
+        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")
+    procs = [ctxm.Process(target=_aff_rank_main, args=(r, world, port, q, exchange == "peer")) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
