@@ -3148,6 +3148,13 @@ __device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N
 __device__ __forceinline__ uint64_t* shard_word(uint64_t* inbox, uint32_t epoch, int r, int w, int i) {
   return inbox + ((((size_t)(epoch & 1u) * kJobSlots + r) * kShardMaxWorld + w) * kShardRecW + i);
 }
+// SP.inbox[w] by selects: a dynamic index into the by-value kernel argument would copy it to scratch
+__device__ __forceinline__ uint64_t* shard_inbox(const ShardPeers& SP, int w) {
+  uint64_t* p = SP.inbox[0];
+#pragma unroll
+  for (int k = 1; k < kShardMaxWorld; ++k) p = w == k ? SP.inbox[k] : p;
+  return p;
+}
 __device__ __forceinline__ uint32_t shard_tag(uint32_t epoch, uint32_t m) {
   return ((epoch & 0xfffu) << 20) | ((m + 1) & 0xfffffu);
 }
@@ -3178,12 +3185,14 @@ static_assert(sizeof(ShardGather) <= 8 * kCandCap, "the gathered proposals fit t
 // After sel_run<PROPOSE, QN, CAND> (sh.ord[0..s_count): this rank's proposal): the local no-fit histogram when the
 // rank ran out of picks, the exchange, the global first-T picks, the stop rules, and the commits on this rank's
 // rows. Returns 0, 1 (a peer's proposal did not arrive within idle_ticks) or 2 (the ranks issued different jobs).
-__device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const ShardPeers& SP, uint32_t xn,
-                           const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp, int spec,
-                           const uint64_t* stat, const uint32_t* keys, const int32_t* l0, int n0, const int32_t* l1,
-                           int n1, int t_begin, int t_count, int ready0, int minav, int gang, int idx_bits,
-                           int32_t* hout, JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
-                           int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped) {
+// (inlined: as a call it made the engine pass its by-value kernel arguments through scratch)
+__device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const ShardPeers& SP,
+                                          uint32_t xn, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
+                                          const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
+                                          const int32_t* l0, int n0, const int32_t* l1, int n1, int t_begin,
+                                          int t_count, int ready0, int minav, int gang, int idx_bits, int32_t* hout,
+                                          JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
+                                          int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int T = t_count, W = SP.world;
   __syncthreads();  // sel_run's no-fit exit writes sh.s_count = 0 from one thread with no barrier after it
@@ -3235,14 +3244,14 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
     const uint32_t v = word(i);
     if (w == SP.rank && !SP.self_inbox) gput(w, i, v);
     else
-      __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
+      __hip_atomic_store(shard_word(shard_inbox(SP, w), SP.epoch, r, SP.rank, i), th | v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // ---- read: every other rank's record from this rank's inbox ----
   {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool late = false;
-    uint64_t* own = SP.inbox[SP.rank];
+    uint64_t* own = shard_inbox(SP, SP.rank);
     for (int idx = tid; idx < W * L && !late; idx += kSelThreads) {
       const int w = idx / L, i = idx - w * L;
       if (w == SP.rank && !SP.self_inbox) continue;
@@ -3376,14 +3385,14 @@ __device__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const S
       if (w == SP.rank && !SP.self_inbox) {
         G.hist[w][b] = sh.hist[b];
       } else {
-        __hip_atomic_store(shard_word(SP.inbox[w], SP.epoch, r, SP.rank, kShardHistOff + b), th | sh.hist[b],
+        __hip_atomic_store(shard_word(shard_inbox(SP, w), SP.epoch, r, SP.rank, kShardHistOff + b), th | sh.hist[b],
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     if (tid < W * kShardNoFitR) {
       const int w = tid / kShardNoFitR, b = tid - w * kShardNoFitR;
       if (w != SP.rank || SP.self_inbox) {
-        const uint64_t* p = shard_word(SP.inbox[SP.rank], SP.epoch, r, w, kShardHistOff + b);
+        const uint64_t* p = shard_word(shard_inbox(SP, SP.rank), SP.epoch, r, w, kShardHistOff + b);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         while ((uint32_t)(x >> 32) != tag) {
