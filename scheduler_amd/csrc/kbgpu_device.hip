@@ -843,14 +843,14 @@ __device__ __forceinline__ int bra_score_f64(double rc, double ac, double rm, do
 }
 template <class SCORE>
 __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
-                                                         int t, uint32_t* reasons, SCORE* scores) {
+                                                         int t, int spb, uint32_t* reasons, SCORE* scores) {
   __shared__ int64_t s_req[4][kEvalPlainSpecs];  // init cpu, init mem, non-zero cpu, non-zero mem
   __shared__ double s_dreq[4][kEvalPlainSpecs];  // init cpu, init mem as doubles; non-zero cpu, mem x 10 (exact)
   __shared__ double s_dnz[2][kEvalPlainSpecs];   // non-zero cpu, mem as doubles
-  __shared__ uint32_t s_be[kEvalPlainSpecs];
-  __shared__ SCORE s_tab[11 * 11];  // lr * w_lr + bra * w_bra for lr, bra in 0..10
-  const int j0 = blockIdx.y * kEvalPlainSpecs;
-  const int nj = t - j0 < kEvalPlainSpecs ? t - j0 : kEvalPlainSpecs;
+  __shared__ uint32_t s_bem[kEvalPlainSpecs];    // BestEffort: all ones
+  __shared__ SCORE s_tab[11 * 11];  // lr * w_lr + bra * w_bra for lr, bra in 0..10 (all 0 without nodeorder)
+  const int j0 = blockIdx.y * spb;
+  const int nj = t - j0 < spb ? t - j0 : spb;
   if ((int)threadIdx.x < nj) {
     const kb_spec sp = P.specs[spec_ids[j0 + threadIdx.x]];
     s_req[0][threadIdx.x] = sp.init_cpu;
@@ -863,11 +863,11 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     s_dreq[3][threadIdx.x] = (double)sp.nz_mem * 10.0;
     s_dnz[0][threadIdx.x] = (double)sp.nz_cpu;
     s_dnz[1][threadIdx.x] = (double)sp.nz_mem;
-    s_be[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? 1u : 0u;
+    s_bem[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? ~0u : 0u;
   }
   if (threadIdx.x >= 128 && threadIdx.x < 128 + 121) {
     const int q = (int)threadIdx.x - 128;
-    s_tab[q] = (SCORE)(q / 11) * (SCORE)C.w_lr + (SCORE)(q % 11) * (SCORE)C.w_bra;
+    s_tab[q] = C.nodeorder ? (SCORE)(q / 11) * (SCORE)C.w_lr + (SCORE)(q % 11) * (SCORE)C.w_bra : (SCORE)0;
   }
   __syncthreads();
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -899,27 +899,53 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     // LessEqual's tolerance folded into the node's side once: r - avail < tol <=> r < avail + tol (exact here)
     const double t_ic = d_ic + 10.0, t_im = d_im + 10485760.0, t_rc = d_rc + 10.0, t_rm = d_rm + 10485760.0;
     const bool pos = d_ac > 0.0 && d_am > 0.0;
-    const double num_c = (d_ac - d_nc) * 10.0, num_m = (d_am - d_nm) * 10.0;  // minus the spec's nz * 10
-    const double ic10 = 10.0 / d_ac, im10 = 10.0 / d_am;
+    // LeastRequested's operands with the zero-capacity case folded in: numerator -1 (minus the spec's nz * 10, so
+    // always negative: score 0), capacity and reciprocal 1
     const bool zc = d_ac == 0.0, zm = d_am == 0.0;
+    const double num_c = zc ? -1.0 : (d_ac - d_nc) * 10.0, num_m = zm ? -1.0 : (d_am - d_nm) * 10.0;
+    const double cap_c = zc ? 1.0 : d_ac, cap_m = zm ? 1.0 : d_am;
+    const double lc_inv = zc ? 1.0 : inv_c, lm_inv = zm ? 1.0 : inv_m;
+    // Balanced's estimate on positive capacities only (elsewhere every spec takes the fallback)
+    const double ic10 = pos ? 10.0 / d_ac : 0.0, im10 = pos ? 10.0 / d_am : 0.0;
+    // The loop body is branch-free, so the unrolled iterations' LDS reads and f64 chains interleave. Balanced's
+    // IEEE-division fallback (f within 1e-9 of an integer, or a capacity <= 0) is deferred: the spec's bit in fb,
+    // and the score is rewritten after the loop (the same thread's later store to the same word)
+    uint32_t fb = 0;
 #pragma unroll 4
     for (int j = 0; j < nj; ++j) {
-      const double icpu = s_dreq[0][j], imem = s_dreq[1][j];
+      const double icpu = s_dreq[0][j], imem = s_dreq[1][j], nzc10 = s_dreq[2][j], nzm10 = s_dreq[3][j];
+      const double nzc = s_dnz[0][j], nzm = s_dnz[1][j];
+      const uint32_t bem = s_bem[j];
       const bool fit = ((icpu < t_ic) & (imem < t_im)) | ((icpu < t_rc) & (imem < t_rm));
-      const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
-      SCORE score = 0;
-      if (C.nodeorder) {  // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term
-        const int lc = zc ? 0 : lr_score_f64(num_c - s_dreq[2][j], d_ac, inv_c);
-        const int lm = zm ? 0 : lr_score_f64(num_m - s_dreq[3][j], d_am, inv_m);
-        const double rc = s_dnz[0][j] + d_nc, rm = s_dnz[1][j] + d_nm;
-        // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
-        score = s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, d_ac, rm, d_am, ic10, im10, pos)];
-      }
+      const uint32_t fm = 0u - (uint32_t)fit;
+      const uint32_t rs = (((post_be & bem) | (after & ~bem)) & fm) | ((1u << KB_R_RESOURCE_FIT) & ~fm);
+      // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term (the table is 0 without nodeorder)
+      const int lc = lr_score_f64(num_c - nzc10, cap_c, lc_inv);
+      const int lm = lr_score_f64(num_m - nzm10, cap_m, lm_inv);
+      const double rc = nzc + d_nc, rm = nzm + d_nm;
+      const bool over = (rc >= d_ac) | (rm >= d_am);
+      const double f = 10.0 - fabs(fma(rc, ic10, -(rm * im10)));  // in [0, 10]
+      const double fr = f - floor(f);
+      const bool po = pos & over;
+      const bool est = pos & !over & (fr > 1e-9) & (fr < 1.0 - 1e-9);
+      fb |= (uint32_t)(!est & !po) << j;
+      // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
+      const SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
       // uniform row bases: the stores take a scalar base and the lane's offset
       uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
       SCORE* srow = scores + (size_t)(j0 + j) * stride;
       rrow[n] = rs;
       srow[n] = score;
+    }
+    if (!C.nodeorder) fb = 0;
+    while (fb) {  // the deferred Balanced fallbacks
+      const int j = __builtin_ctz(fb);
+      fb &= fb - 1;
+      const int lc = lr_score_f64(num_c - s_dreq[2][j], cap_c, lc_inv);
+      const int lm = lr_score_f64(num_m - s_dreq[3][j], cap_m, lm_inv);
+      const double rc = s_dnz[0][j] + d_nc, rm = s_dnz[1][j] + d_nm;
+      scores[(size_t)(j0 + j) * stride + n] =
+          s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, d_ac, rm, d_am, 0.0, 0.0, false)];
     }
     return;
   }
@@ -927,7 +953,7 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     const int64_t icpu = s_req[0][j], imem = s_req[1][j];
     const bool fit = (le_tol(icpu, r.idle_cpu, 10) && le_tol(imem, r.idle_mem, 10ll * 1024 * 1024)) ||
                      (le_tol(icpu, r.rel_cpu, 10) && le_tol(imem, r.rel_mem, 10ll * 1024 * 1024));
-    const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_be[j] ? post_be : after);
+    const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_bem[j] ? post_be : after);
     int64_t score = 0;
     if (C.nodeorder) {
       const int64_t rc = s_req[2][j] + r.nz_cpu, rm = s_req[3][j] + r.nz_mem;
@@ -5504,12 +5530,39 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                      J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
+// eval_plain_kernel's specs per block: the grid sized to one resident round of at most 8 waves per SIMD (the
+// kernel's occupancy; 256 CUs x 4 SIMDs), so no SIMD runs a second, partial round and every SIMD holds as many
+// waves as fit to hide the f64 chains' latency. KB_EVAL_SPB overrides (measurement).
+static int eval_plain_spb(int n, int t) {
+  static const int env = [] {
+    const char* e = getenv("KB_EVAL_SPB");
+    return e ? atoi(e) : 0;
+  }();
+  int spb;
+  if (env > 0) {
+    spb = env;
+  } else {
+    static const int cus = [] {
+      int dev = 0, c = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+      return c;
+    }();
+    const int xblocks = (n + 255) / 256;
+    const int yblocks = (cus * 4 * 8) / (xblocks * 4);  // blocks of 4 waves in one round, per column
+    spb = yblocks > 0 ? (t + yblocks - 1) / yblocks : kEvalPlainSpecs;
+    if (spb < 8) spb = 8;
+  }
+  return spb < 1 ? 1 : (spb > kEvalPlainSpecs ? kEvalPlainSpecs : spb);
+}
 template <class SCORE>
 static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                           uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, void* stream) {
   if (plain) {
-    dim3 grid((N.n + 255) / 256, (t + kEvalPlainSpecs - 1) / kEvalPlainSpecs);
-    hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+    const int spb = eval_plain_spb(N.n, t);
+    dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
+    hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, spb,
                        reasons, scores);
     return;
   }
