@@ -126,13 +126,18 @@ def test_eval_plain_matches_oracle():
     assert np.array_equal(r32, reasons) and np.array_equal(s32.astype(np.int64), scores)
 
 
-@pytest.mark.parametrize("name", ["plain-edge", "C2-2000", "C1-parity"])
-def test_eval_plain_equals_general(name, monkeypatch):
-    """The row-only kernel returns the general eval_kernel's arrays (KB_NO_EVAL_PLAIN) on plain batches."""
+@pytest.mark.parametrize("name,cfg", [("plain-edge", None), ("C2-2000", None), ("C1-parity", None),
+                                      ("plain-edge", {"nodeorder_enabled": 0}),
+                                      ("plain-edge", {"predicates_enabled": 0})])
+def test_eval_plain_equals_general(name, cfg, monkeypatch):
+    """The row-only kernel returns the general eval_kernel's arrays (KB_NO_EVAL_PLAIN) on plain batches, also with
+    the nodeorder or predicates plugin off (the score table all 0; no post reasons)."""
     cl = {"plain-edge": plain_edge_cluster, "C2-2000": lambda: synth.c2(n_nodes=2000, n_jobs=64, tasks_per_job=1,
                                                                         seed=9),
           "C1-parity": lambda: synth.c1(n_nodes=120, n_jobs=24, tasks_per_job=25, seed=1)}[name]()
     snap = E.Snapshot(cl)
+    if cfg:
+        snap.config.update(cfg)
     ids = [int(s) for s in np.nonzero(_plain_spec(snap))[0]]
     assert ids
     out = []
