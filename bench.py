@@ -3,23 +3,23 @@
 metric : pods placed/sec (+ p50 allocate-cycle ms) at 10k nodes x 100k pods (BASELINE.json configs[1], "C2")
 step   : one allocateAction.Execute (actions/allocate/allocate.go:42-193) over the C2 session snapshot:
          re-open the session from the snapshot already resident in HBM (kb_restore_nodes, device-to-device),
-         then kb_allocate (host ordering plugins + per-job device sweep/argmax/commit). The snapshot is
+         then kb_allocate (host ordering plugins + the device's sweep / argmax / commit per job). The snapshot is
          uploaded once before the timed region; value = pods placed / second over the timed steps.
 
-Multi-GPU (N > 1, one process per GPU): every rank schedules its own independent C2 cluster (a partition of the
-fleet with its own seed; no collective on the data path: torch.distributed only for the barriers and the
-max-over-ranks time) -- `value` = all ranks' pods / the max-over-ranks time, scaling "weak", the same per-GPU
-workload as the N = 1 line. One allocate cycle is a sequential chain of jobs, so GPUs add throughput by serving
-partitions. Beside it, "sharded": BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M pods
-whose node table is split across the N ranks: every rank's resident engine proposes its first T picks per job and
-writes them into every rank's inbox over xGMI (kb_set_shard_peer: device memory mapped across the GPUs), then
-merges them on the device -- no host round trip or collective launch per job. `--mode shard` makes that the line.
+Multi-GPU (N > 1, one process per GPU): the SAME workload as N = 1 -- ONE C2 cluster (10k nodes x 100k pods) whose
+node table is split into N contiguous blocks, one per rank (`scaling: "strong"`): every rank's resident engine
+proposes its first T picks per job, writes them into every rank's inbox over xGMI (kb_set_shard_peer: device
+memory mapped across the GPUs) and merges all proposals on the device -- no host round trip or collective launch
+per job. `shard_exchange_us_per_job` is the engines' own stamp of the inbox wait per job. Beside the line:
+"replicas" (every rank its own C2 cluster, no collective: weak scaling) and "sharded_C5" (BASELINE.json
+configs[4]: 50k nodes x 1M pods split N ways). `--mode replicas` makes the replicas the line.
 `python bench.py --gpus N` without torchrun's environment starts the N ranks itself (before any GPU call).
-One GPU also runs C5 whole: `--config C5` (the split fed engine with range selectors).
 
-Extra JSON fields: roofline (dominant kernel, HIP events on the library's stream during the timed region),
-eval_roofline (the fit/score sweep kb_eval at 256 specs x 50k nodes: the HBM-bound kernel), and cpu_baseline
-(the oracle's C++ restatement of the reference algorithm on a bounded sample).
+Extra JSON fields: roofline (the dominant kernel: the resident fed engine on C1/C2/C3/C5, the class loop on C4;
+SURVEY.md §8 d3's bytes per (task, node) over its HIP-event duration, and the cycle's measured HBM bytes from the
+committed rocprofv3 PMC pass), sweep_roofline (the per-job level-0 sweep, measured in a separate cycle), the
+session open, eval_roofline (kb_eval at 256 specs x 50k nodes) and cpu_baseline (the oracle's C++ restatement of
+the reference algorithm on a bounded sample).
 """
 from __future__ import annotations
 
@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="BASELINE.json configuration (default: C2, the headline metric's; C5 node-sharded at N>1)")
+                    help="BASELINE.json configuration (default: C2, the headline metric's, at every N)")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--tasks-per-job", type=int, default=None)
@@ -70,15 +70,20 @@ def main():
     ap.add_argument("--path", default="select", choices=["select", "engine", "trajectory", "rekey"],
                     help="device path for the runs (scheduler_amd.runtime.PATHS)")
     ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "shard"],
-                    help="N>1: shard = ONE cluster, node table split across the ranks, one RCCL all-gather per run "
-                         "segment; replicas = every rank schedules its own cluster (no collective). auto = shard "
-                         "(C5) as the line, plus a short replicas measurement beside it")
-    ap.add_argument("--side-steps", type=int, default=5, help="cycles of the side measurement (auto, N>1)")
+                    help="N>1: shard (auto) = ONE cluster of the configuration, its node table split across the ranks; "
+                         "replicas = every rank schedules its own cluster (no collective)")
+    ap.add_argument("--side-steps", type=int, default=5, help="cycles of each side measurement (N>1)")
+    ap.add_argument("--no-side", action="store_true", help="N>1: no replicas / sharded-C5 side measurements")
     ap.add_argument("--no-eval", action="store_true", help="skip the kb_eval roofline measurement (N=1)")
     ap.add_argument("--timing-every", type=int, default=8,
-                    help="HIP events around the launches of every Nth job call of the timed region")
+                    help="per-job launch paths: HIP events around the launches of every Nth job call of the timed "
+                         "region (fed-engine cycles time the engine's one launch per cycle only)")
+    ap.add_argument("--opt", default="",
+                    help="context options (runtime.make_opts: no_fed, fed_plain_launch, ...), for the profiler's "
+                         "passes and the shared-GPU rehearsal; the default is the production path")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="N>1 rehearsal: every rank on GPU 0 (gloo group; engines launched plainly)")
     args = ap.parse_args()
-    args.mode_auto = args.mode == "auto"
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)  # torchrun's environment is missing: start the ranks (no GPU touched yet)
@@ -86,54 +91,49 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
-    mode = args.mode if args.mode != "auto" else "replicas"
-    args.mode = mode
-    args.config = args.config or ("C5" if mode == "shard" and world > 1 else "C2")
+    args.mode = "shard" if args.mode == "auto" else args.mode
+    args.config = args.config or "C2"
     cfg = CONFIGS[args.config]
     args.nodes = args.nodes or cfg["nodes"]
     args.jobs = args.jobs or cfg["jobs"]
     args.tasks_per_job = args.tasks_per_job or cfg["tasks"]
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # KB_BENCH_SAME_GPU=1: rehearse N ranks on one GPU (gloo process group; with KB_FED_PLAIN_LAUNCH=1, see
-    # scripts/rehearse_multi.sh)
-    same_gpu = os.environ.get("KB_BENCH_SAME_GPU") == "1"
-    device = 0 if same_gpu else local_rank
+    # --same-gpu: rehearse N ranks on one GPU (gloo process group; plain engine launches: cooperative launches from
+    # several processes take turns on one card; scripts/rehearse_multi.sh)
+    from scheduler_amd import runtime as _rt
+    args.options = _rt.parse_options(args.opt)
+    if args.same_gpu and world > 1:
+        args.options.setdefault("fed_plain_launch", True)
+    device = 0 if args.same_gpu else local_rank
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist_mod
         torch.cuda.set_device(device)
-        dist_mod.init_process_group("nccl" if torch.cuda.is_available() and not same_gpu else "gloo")
+        dist_mod.init_process_group("nccl" if torch.cuda.is_available() and not args.same_gpu else "gloo")
         dist = dist_mod
 
-    from scheduler_amd import export, runtime, synth
+    from scheduler_amd import runtime, synth
 
     shard = args.mode == "shard" and world > 1
     # replicas: each rank an independent cluster partition (different seed per rank); shard: one cluster
     seed = synth.SEED + (0 if shard else rank)
-    cl = None
-    walk_ms = None
-    e0 = time.perf_counter()
-    if args.config in ARRAY_CONFIGS:  # the numpy session builder (equal to the exporter: test_export.py)
-        snap = synth.c2_snapshot(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=seed)
-        export_kind = "synth.c2_snapshot (numpy arrays)"
-    else:
-        from scheduler_amd import columns
-        cl = synth.CONFIGS[args.config](n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job,
-                                        seed=seed)
-        w0 = time.perf_counter()
-        cols = columns.columns_of(cl)  # stands in for the Go shim's walk over ssn.Nodes / ssn.Jobs
-        walk_ms = (time.perf_counter() - w0) * 1e3
-        e0 = time.perf_counter()
-        snap = columns.build(cols)
-        export_kind = ("columns.build (vectorised over the session's columns; equal to export.Snapshot array by "
-                       "array: tests/test_columns.py)")
-    export_ms = (time.perf_counter() - e0) * 1e3
-    ctx = runtime.Context(device, timing=not args.no_timing, timing_every=args.timing_every, path=args.path)
-    if shard:
-        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+    snap, sess = session_snapshot(args, seed)
+
+    def make_ctx(every):
+        c = runtime.Context(device, timing=not args.no_timing, timing_every=every, path=args.path,
+                            options=args.options)
+        if shard:
+            c.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+        return c
+
+    # fed-engine cycles: the engine's one launch per cycle is timed (per-job sweep events would add barrier packets
+    # on the sweep queue and host calls to every job); per-job launch paths: every Nth job's launches
+    ctx = make_ctx(1 << 30)
+    u0 = time.perf_counter()
     ctx.upload(snap)
+    sess["upload_ms"] = round((time.perf_counter() - u0) * 1e3, 3)
 
     def step():
         ctx.restore()
@@ -147,6 +147,12 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.warmup and not ctx.stats()["fed_cycles"] and not args.no_timing and not shard:
+        ctx.close()  # per-job launch paths: time every Nth job's launches
+        ctx = make_ctx(args.timing_every)
+        ctx.upload(snap)
+        for _ in range(args.warmup):
+            step()
     ctx.stats(reset=True)
     barrier()
     t0 = time.perf_counter()
@@ -159,6 +165,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    # where a step's host time goes (after the timed region): the session re-open and the kb_allocate call
+    host = host_split(ctx, snap, out)
     # SURVEY.md §8 d1 also asks for the cycle WITH the snapshot upload: time re-uploads of the same snapshot
     # (kb_set_config + kb_upload_nodes + kb_upload_specs [+ affinity tables]; host arrays -> HBM), after the
     # timed region so they do not disturb it
@@ -168,6 +176,9 @@ def main():
             u0 = time.perf_counter()
             ctx.upload(snap)
             up.append((time.perf_counter() - u0) * 1e3)
+        sess["upload_ms"] = round(statistics.median(up), 3)
+    sess["total_ms"] = round(sess["build_ms"] + sess["upload_ms"], 3)
+    ctx.close()
 
     total_placed = placed
     if dist is not None:
@@ -179,29 +190,32 @@ def main():
             p = torch.tensor([placed], dtype=torch.float64, device=tensor_device(dist, device))
             dist.all_reduce(p, op=dist.ReduceOp.SUM)
             total_placed = int(p.item())
-    side = None
-    if world > 1 and mode == "shard":
-        side = {"replicas": replicas_side(args, dist, rank, world, device)}
-    elif world > 1 and args.mode_auto:
-        side = {"sharded": shard_side(args, dist, rank, world, device)}
-    ev = None
+    side = {}
+    if world == 1 and rank == 0 and not args.no_timing:
+        side["sweep_roofline"] = sweep_side(args, cfg, snap, device)
+    if world > 1 and not args.no_side:
+        if shard:
+            side["replicas"] = replicas_side(args, dist, rank, world, device)
+            side["sharded_C5"] = shard_side(args, dist, rank, world, device)
+        else:
+            side["sharded"] = shard_side(args, dist, rank, world, device, config=args.config)
     if world == 1 and rank == 0 and not args.no_eval:
-        ev = eval_side(device)
+        side["eval_roofline"] = eval_side(device)
 
     roofline = roofline_of(st, args, cfg)
-    engine = engine_of(st, args) if st["launches"][runtime.KERNELS.index("fed_engine_kernel")] else None
+    engine = engine_of(st) if st["launches"][runtime.KERNELS.index("fed_engine_kernel")] else None
 
     workload = cfg["workload"]
     if (args.nodes, args.jobs, args.tasks_per_job) != (cfg["nodes"], cfg["jobs"], cfg["tasks"]):
         workload = f"{args.config} shape at {args.nodes} nodes x {args.jobs * args.tasks_per_job} pods"
-    result = None
+    if shard:
+        workload += f", node table split into {world} blocks (one per rank)"
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            if cl is None:  # the oracle runs on the cluster objects of the same workload
-                cl = synth.CONFIGS.get(args.config, synth.c2)(n_nodes=args.nodes, n_jobs=args.jobs,
-                                                            tasks_per_job=args.tasks_per_job, seed=seed)
+            cl = synth.CONFIGS.get(args.config, synth.c2)(n_nodes=args.nodes, n_jobs=args.jobs,
+                                                        tasks_per_job=args.tasks_per_job, seed=seed)
             cpu = cpu_baseline(cl, args.cpu_sample_tasks, args.config)
         result = {
             "metric": "pods placed/sec + p50 allocate-cycle ms at 10k nodes x 100k pods",
@@ -209,20 +223,14 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "p50_cycle_ms": round(statistics.median(times), 3),
             **({"upload_ms": round(statistics.median(up), 3),
                 "p50_cycle_with_upload_ms": round(statistics.median(times) + statistics.median(up), 3)} if up else {}),
-            # session open: building the exported snapshot from the cluster objects (the Go shim's
-            # exportSnapshot twin) + its upload; the reference's counterpart is cache.Snapshot + OnSessionOpen
-            "session_open": {"export_ms": round(export_ms, 1), "export": export_kind,
-                             "upload_ms": round(statistics.median(up), 3) if up else None,
-                             **({"shim_walk_ms": round(walk_ms, 1),
-                                 "shim_walk": "columns.columns_of: the per-pod walk into columns, in Python here "
-                                              "(the Go shim's work; not part of the export)"}
-                                if walk_ms is not None else {})},
+            "session_open": sess,
             "higher_is_better": True, "scaling": "strong" if shard else "weak", "vs_baseline": None,
             "dtype": "int64", "data": f"synthetic (seeded {args.config} generator, SURVEY.md §8 d2)",
             "config": {"workload": workload,
                        "nodes": args.nodes, "pods": args.jobs * args.tasks_per_job, "jobs": args.jobs,
                        "pods_placed_per_cycle": placed // max(1, args.steps),
                        "parallelism": f"node_shard{world}" if shard else f"replicas{world}"},
+            "host_ms_per_step": host,
             "device_ms_per_step": round(st["device_ms"] / args.steps, 3),
             **({"diag_place_phases": diag_summary(st["diag"], placed, "fed_engine_kernel" if engine is not None
                                                   else roofline["kernel"])}
@@ -231,83 +239,163 @@ def main():
             "roofline": roofline,
             **({"engine": engine} if engine is not None else {}),
             "cpu_baseline": cpu,
-            **({"shard_exchange_us_per_segment": exchange_us(st),
-                "shard_segments_per_step": st["launches"][runtime.KERNELS.index("shard_exchange")] / args.steps}
-               if shard else {}),
-            **(side if side is not None else {}),
-            **({"eval_roofline": ev} if ev is not None else {}),
+            **(shard_fields(st, args) if shard else {}),
+            **side,
         }
         print(json.dumps(result), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
+def session_snapshot(args, seed):
+    """The session snapshot of the configuration and its open cost: C2 / C5 from the numpy
+    builder; C1 / C3 / C4 from the generator's columns (synth.COLUMNS: per node and per job, no per-pod objects --
+    the Go shim's columnar walk) through columns.build. build_ms = the snapshot build; the upload
+    is added once the context exists."""
+    from scheduler_amd import synth
+    if args.config in ARRAY_CONFIGS:  # the numpy session builder (equal to the exporter: test_export.py)
+        e0 = time.perf_counter()
+        snap = synth.c2_snapshot(n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job, seed=seed)
+        return snap, {"build_ms": round((time.perf_counter() - e0) * 1e3, 1),
+                      "build": "synth.c2_snapshot (numpy arrays, equal to export.Snapshot: tests/test_export.py)"}
+    from scheduler_amd import columns
+    cols = synth.COLUMNS[args.config](n_nodes=args.nodes, n_jobs=args.jobs, tasks_per_job=args.tasks_per_job,
+                                      seed=seed)
+    e0 = time.perf_counter()
+    snap = columns.build(cols)
+    return snap, {"build_ms": round((time.perf_counter() - e0) * 1e3, 1),
+                  "build": "columns.build over the session's columns (vectorised per pod; equal to export.Snapshot "
+                           "array by array: tests/test_columns.py); the columns come straight from the generator "
+                           "(synth.COLUMNS, no per-pod walk)"}
+
+
+def host_split(ctx, snap, out):
+    """One more step after the timed region, split: kb_restore_nodes (the session re-open) and the kb_allocate call
+    (its own elapsed time, and the Python binding around it)."""
+    r0 = time.perf_counter()
+    ctx.restore()
+    r1 = time.perf_counter()
+    o = ctx.allocate(snap)
+    r2 = time.perf_counter()
+    return {"restore": round((r1 - r0) * 1e3, 3), "allocate_call": round((r2 - r1) * 1e3, 3),
+            "kb_allocate": round(float(o["elapsed_ms"]), 3)}
+
+
 SWEEP_OUT_BYTES = 12  # the level-0 sweep's output per node: 4 B key + 8 B static cache
+# kernels of the allocate cycle whose PMC bytes make up the cycle's traffic (not the eval side measurement, not the
+# upload / restore copies)
+CYCLE_KERNELS = ("sel_sweep_kernel", "sel_place_kernel", "fed_engine_kernel", "fed_cmd_sweep_kernel", "cls_sweep_kernel",
+                 "cls_place_kernel", "aff_commit_kernel", "aff_place_kernel", "aff_reg_kernel", "ipa_minmax_kernel",
+                 "traj_sweep_kernel", "traj_place_kernel", "sweep_keys_kernel", "place_loop_kernel",
+                 "shard_propose_kernel", "shard_commit_kernel")
 
 
-def roofline_of(st, args, cfg, streaming=False):
-    """The roofline of the cycle's HBM-streaming kernel. Fed-engine cycles: the per-job level-0 sweep
-    (sel_sweep_kernel on the sweep stream: every node's row read and its key written once per job -- the hot
-    path's fit/score evaluation of every (job spec, node) pair); the resident engine itself is a latency-bound
-    chain and is reported beside it ("engine"). Other cycles: the kernel with the most event time. achieved =
-    algorithmic bytes per launch (the row bytes of each (task, node) evaluation the launch makes,
-    plus the sweep's output) / the launch's average HIP-event duration on the stream it runs on; traffic = the
-    same kernel's measured HBM bytes per launch from this configuration's committed rocprofv3 PMC pass."""
+def roofline_of(st, args, cfg):
+    """The roofline of the cycle's dominant kernel: the resident fed engine where it ran (one launch per cycle, the
+    whole placement chain), else the kernel with the most HIP-event time (C4: the class loop, cls_place_kernel).
+    achieved = SURVEY.md §8 d3's algorithmic bytes -- the row bytes of every (task, node) evaluation the launch
+    stands for (76 B C1/C2/C5, 124 B C3, 88 B C4) -- over the launch's average HIP-event duration on the stream it
+    runs on. The kernels read far fewer bytes than that (the selection reads each node's row once per job, not once
+    per task): traffic = the HBM bytes the cycle moved per launch of the kernel, from this configuration's committed
+    rocprofv3 PMC pass (every cycle kernel's FETCH_SIZE x 2 + WRITE_SIZE per dispatch x its dispatches per cycle;
+    MI355X_MICROARCH.md's gfx950 correction), and measured_frac = traffic / duration / peak."""
     from scheduler_amd import runtime
     K = runtime.KERNELS
     fed = st["launches"][K.index("fed_engine_kernel")] > 0
-    if fed or (streaming and st["launches"][K.index("sel_sweep_kernel")]):  # streaming: node-sharded cycles
-        k = K.index("sel_sweep_kernel")
+    if fed:
+        k = K.index("fed_engine_kernel")
     else:
-        kern_ms = [0.0 if K[i] in ("shard_exchange", "fed_engine_kernel") else v for i, v in enumerate(st["kernel_ms"])]
+        kern_ms = [0.0 if K[i] in ("shard_exchange",) else v for i, v in enumerate(st["kernel_ms"])]
         k = int(np.argmax(kern_ms)) if any(kern_ms) else 0
     launches = max(1, st["launches"][k])
     avg_ms = st["kernel_ms"][k] / launches
-    per_eval = cfg["row_bytes"] + (SWEEP_OUT_BYTES if K[k] == "sel_sweep_kernel" else 0)
-    bytes_per_launch = st["pairs"][k] * per_eval / launches
+    bytes_per_launch = st["pairs"][k] * cfg["row_bytes"] / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     out = {"bound": "hbm", "kernel": K[k], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "traffic_source": None,
            "avg_launch_us": round(avg_ms * 1e3, 3), "timed_launches": st["launches"][k],
-           "timing": (f"HIP events on the sweep stream around every {args.timing_every}th job's sweep launch in the "
-                      f"timed region" if K[k] == "sel_sweep_kernel" else
-                      f"HIP events on the library stream around every launch of every {args.timing_every}th job "
-                      f"call in the timed region"),
+           "timing": ("HIP events on the library stream around the engine's one launch per cycle, every cycle of the "
+                      "timed region" if fed else
+                      f"HIP events on the library stream around every launch of every {args.timing_every}th job call "
+                      f"in the timed region"),
            "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
-           "algorithmic_bytes_note": (f"{cfg['row_bytes']} B row read + {SWEEP_OUT_BYTES} B key/static cache written "
-                                      f"per node, every node once per job" if K[k] == "sel_sweep_kernel" else
-                                      f"{cfg['row_bytes']} B row per (task, node) evaluation (SURVEY.md §8 d3)"),
+           "algorithmic_bytes_note": (f"SURVEY.md §8 d3: {cfg['row_bytes']} B of node row per (task, node) "
+                                      f"evaluation x the (task, node) pairs the launch decides "
+                                      f"({st['pairs'][k] / launches:.4g}); the kernel itself reads each row once per "
+                                      f"job at most (see traffic)"),
            "avg_us_per_launch": {K[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
                                  for i in range(len(K)) if st["launches"][i]},
            "measured_frac": None}
     full = (args.nodes, args.jobs, args.tasks_per_job) == (cfg["nodes"], cfg["jobs"], cfg["tasks"])
-    tr = pmc_traffic(K[k], args.config) if full else None
+    tr = pmc_cycle_traffic(args.config, K[k]) if full and args.gpus == 1 else None
     if tr is not None:
         out["traffic"] = tr["bytes_per_launch"]
-        out["traffic_source"] = tr["source"] + f": {K[k]} " + (
-            "(the same kernel and launch size; counters taken on the per-job launch path, KB_NO_FED=1, because "
-            "counter collection serialises dispatches and the resident engine waits on the sweeps)" if fed else
-            "(this kernel, this configuration)")
+        out["traffic_source"] = tr["source"]
+        out["cycle_traffic_bytes"] = tr["cycle_bytes"]
         if avg_ms > 0:
             out["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
     return out
 
 
-def engine_of(st, args):
-    """The resident fed engine (one launch per allocate cycle): a latency-bound chain of dependent LDS round
-    trips per job inside one placer workgroup fed by selector workgroups -- not an HBM roofline kernel. Its
-    launch spans the cycle; the per-job time and the committed KB_DIAG phase split (busy vs waiting) are what
-    bound it."""
+def engine_of(st):
+    """The resident fed engine (one launch per allocate cycle): its per-job time and the shader clock over its
+    launches (kb_stats fed_clock_ticks / fed_real_ticks: s_memtime against the 100 MHz s_memrealtime)."""
     from scheduler_amd import runtime
     K = runtime.KERNELS
     k = K.index("fed_engine_kernel")
     launches = max(1, st["launches"][k])
     us = st["kernel_ms"][k] * 1e3 / launches
     jobs = st["job_calls"] / launches
+    clk = 100.0 * st["fed_clock_ticks"] / st["fed_real_ticks"] if st["fed_real_ticks"] else None
     return {"kernel": "fed_engine_kernel", "bound": "latency (per-job dependent chain in one workgroup)",
             "avg_launch_us": round(us, 3), "launches": st["launches"][k], "jobs_per_launch": round(jobs, 1),
-            "us_per_job": round(us / max(1.0, jobs), 3)}
+            "us_per_job": round(us / max(1.0, jobs), 3), "clock_mhz": round(clk, 1) if clk else None}
+
+
+def shard_fields(st, args):
+    """Node-sharded line: the engines' own stamp of the exchange (the placer's wait from writing its record into
+    the peers' inboxes to holding every peer's record) per job, and the launch-path exchanges if any."""
+    from scheduler_amd import runtime
+    out = {"sharded_engine_cycles_per_step": st["fed_sharded"] / args.steps,
+           "shard_exchange_us_per_job": (round(st["shard_wait_ticks"] / 100.0 / st["shard_xchg"], 3)
+                                         if st["shard_xchg"] else None),
+           "shard_exchanges_per_step": st["shard_xchg"] / args.steps}
+    k = runtime.KERNELS.index("shard_exchange")
+    if st["launches"][k]:
+        out["launch_path_exchange_us_per_segment"] = round(st["kernel_ms"][k] * 1e3 / st["launches"][k], 2)
+    return out
+
+
+def sweep_side(args, cfg, snap, device):
+    """The per-job level-0 sweep on its own (sel_sweep_kernel: every node's row read and its 32-bit key and static
+    cache written once per job), from one more cycle with HIP events around every job's sweep (kept out of the
+    timed region: the events add barrier packets to the sweep queue). Algorithmic bytes n x (row + 12 B)."""
+    from scheduler_amd import runtime
+    try:
+        ctx = runtime.Context(device, timing=True, timing_every=1, path=args.path, options=args.options)
+        ctx.upload(snap)
+        ctx.allocate(snap)
+        ctx.restore()
+        ctx.stats(reset=True)
+        ctx.allocate(snap)
+        st = ctx.stats()
+        ctx.close()
+        K = runtime.KERNELS
+        k = K.index("sel_sweep_kernel")
+        if not st["launches"][k]:
+            return None
+        avg_ms = st["kernel_ms"][k] / st["launches"][k]
+        alg = st["pairs"][k] / st["launches"][k] * (cfg["row_bytes"] + SWEEP_OUT_BYTES)
+        out = {"kernel": "sel_sweep_kernel", "avg_launch_us": round(avg_ms * 1e3, 3), "launches": st["launches"][k],
+               "algorithmic_bytes_per_launch": round(alg, 1), "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 2),
+               "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "traffic": None, "measured_frac": None}
+        tr = pmc_traffic("sel_sweep_kernel", args.config)
+        if tr is not None:
+            out["traffic"], out["traffic_source"] = tr["bytes_per_launch"], tr["source"]
+            out["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        return out
+    except Exception as e:  # the side measurement never takes the main line down
+        return {"error": repr(e)[:300]}
 
 
 def tensor_device(dist, device):
@@ -330,21 +418,15 @@ def shard_exchange(dist, rank, device):
     return {"allgather": allgather, "peer": True}
 
 
-def exchange_us(st):
-    from scheduler_amd import runtime
-    k = runtime.KERNELS.index("shard_exchange")
-    return round(st["kernel_ms"][k] * 1e3 / st["launches"][k], 2) if st["launches"][k] else None
-
-
 def replicas_side(args, dist, rank, world, device):
     """Beside the sharded line: every rank schedules its own independent C2 cluster (different seed per rank,
-    no collective), `side_steps` cycles; pods/s over all ranks at the max-over-ranks time."""
+    no collective), `side_steps` cycles; pods/s over all ranks at the max-over-ranks time (weak scaling)."""
     import torch
     from scheduler_amd import runtime, synth
     try:
         c = CONFIGS["C2"]
         snap = synth.c2_snapshot(n_nodes=c["nodes"], n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED + rank)
-        ctx = runtime.Context(device)
+        ctx = runtime.Context(device, options=args.options)
         ctx.upload(snap)
         ctx.allocate(snap)  # warm-up cycle
         dist.barrier()
@@ -368,18 +450,17 @@ def replicas_side(args, dist, rank, world, device):
         return {"error": repr(e)[:300]}
 
 
-def shard_side(args, dist, rank, world, device):
-    """Beside the replicas line (N > 1): BASELINE.json configs[4], C5 -- ONE cluster of 50k C2-shaped nodes x 1M
-    pods whose node table is split across the N ranks (contiguous blocks; per job every rank's engine proposes,
-    writes its proposal into every rank's inbox over xGMI and merges all of them; every rank commits its own rows).
-    `side_steps` cycles after one warm-up; pods/s at the max-over-ranks time."""
+def shard_side(args, dist, rank, world, device, config="C5"):
+    """Beside the line (N > 1): a node-sharded cycle of `config` -- by default BASELINE.json configs[4], C5: ONE
+    cluster of 50k C2-shaped nodes x 1M pods whose node table is split across the N ranks (contiguous blocks; per
+    job every rank's engine proposes, writes its proposal into every rank's inbox over xGMI and merges all of them;
+    every rank commits its own rows). `side_steps` cycles after one warm-up; pods/s at the max-over-ranks time."""
     import torch
     from scheduler_amd import runtime, synth
     try:
-        c = CONFIGS["C5"]
-        nodes = c["nodes"]
-        snap = synth.c2_snapshot(n_nodes=nodes, n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED)
-        ctx = runtime.Context(device, timing=True, timing_every=args.timing_every)
+        c = CONFIGS[config]
+        snap = synth.c2_snapshot(n_nodes=c["nodes"], n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED)
+        ctx = runtime.Context(device, timing=True, timing_every=1 << 30, options=args.options)
         ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
         ctx.upload(snap)
         ctx.allocate(snap)  # warm-up cycle
@@ -398,15 +479,14 @@ def shard_side(args, dist, rank, world, device):
         st = ctx.stats()
         ctx.close()
         a = argparse.Namespace(**vars(args))
-        a.config, a.nodes, a.jobs, a.tasks_per_job = "C5", nodes, c["jobs"], c["tasks"]
+        a.config, a.nodes, a.jobs, a.tasks_per_job, a.steps = config, c["nodes"], c["jobs"], c["tasks"], args.side_steps
         elapsed = float(el.item())
-        out = {"workload": c["workload"], "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
+        out = {"workload": c["workload"] + f", node table split into {world} blocks",
+               "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
                "steps": args.side_steps, "scaling": "strong", "ms_per_step": round(elapsed / args.side_steps * 1e3, 3),
-               "sharded_engine_cycles": st["fed_sharded"], "roofline": roofline_of(st, a, c, streaming=True)}
+               "roofline": roofline_of(st, a, c), **shard_fields(st, a)}
         if st["launches"][runtime.KERNELS.index("fed_engine_kernel")]:
-            out["engine"] = engine_of(st, a)
-        else:  # (a cycle the engine does not serve: the per-job launch path with the host-staged exchange)
-            out["exchange_us_per_segment"] = exchange_us(st)
+            out["engine"] = engine_of(st)
         return out
     except Exception as e:  # the side measurement never takes the main line down
         return {"error": repr(e)[:300]}
@@ -478,13 +558,16 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
+def _prof_summaries(config):
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_prof_summary.json")), reverse=True)
+
+
 def pmc_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass of this configuration
     (profiles/*_<config>_prof_summary.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or
     None when none is committed."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_prof_summary.json")), reverse=True)
-    for f in files:
+    for f in _prof_summaries(config):
         try:
             with open(f) as fh:
                 e = json.load(fh)["kernels"].get(kernel, {})
@@ -492,6 +575,36 @@ def pmc_traffic(kernel, config):
             continue
         if "hbm_bytes_per_launch" in e:
             return {"bytes_per_launch": e["hbm_bytes_per_launch"], "source": os.path.relpath(f, ROOT)}
+    return None
+
+
+def pmc_cycle_traffic(config, kernel):
+    """The allocate cycle's measured HBM bytes from the newest committed PMC pass of this configuration that counts
+    dispatches (scripts/prof_summary.py: every cycle kernel's bytes per dispatch x its dispatches, over the pass's
+    cycles), expressed per launch of `kernel`: the whole cycle for the fed engine (one launch per cycle), else
+    `kernel`'s own bytes per launch. The fed engine's pass runs the per-job launch path (option no_fed: counter
+    collection serialises dispatches, and the resident engine waits on sweeps of another stream), whose kernels
+    read and write what the engine's jobs do."""
+    for f in _prof_summaries(config):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        ks, cycles = d.get("kernels", {}), d.get("pmc_cycles")
+        if not cycles or not any("pmc_dispatches" in e for e in ks.values()):
+            continue
+        cyc = sum(e["hbm_bytes_per_launch"] * e["pmc_dispatches"] for k, e in ks.items()
+                  if k in CYCLE_KERNELS and "hbm_bytes_per_launch" in e and "pmc_dispatches" in e) / cycles
+        src = os.path.relpath(f, ROOT)
+        if kernel == "fed_engine_kernel":
+            return {"bytes_per_launch": round(cyc, 1), "cycle_bytes": round(cyc, 1),
+                    "source": f"{src}: the cycle's kernels (per-job launch path, option no_fed), bytes per dispatch x "
+                              f"dispatches per cycle, summed = one engine launch"}
+        e = ks.get(kernel, {})
+        if "hbm_bytes_per_launch" in e:
+            return {"bytes_per_launch": e["hbm_bytes_per_launch"], "cycle_bytes": round(cyc, 1),
+                    "source": f"{src}: {kernel}'s own bytes per launch"}
     return None
 
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 12
+#define KBGPU_ABI_VERSION 13
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -212,8 +212,14 @@ typedef struct kb_config {
 
 typedef struct kb_opts {
   int32_t device;        /* HIP device ordinal */
-  uint32_t flags;
+  uint32_t flags;        /* KB_OPT_* */
   uint32_t timing_every; /* KB_OPT_TIMING: time the launches of every Nth kb_place_job call (0 or 1: all) */
+  int32_t fed_idle_ms;   /* the fed engine's idle exit (0: 1 s; tests shorten it) */
+  int32_t eval_spb;      /* eval_plain_kernel's specs per block (0: sized from the device's CU count) */
+  int32_t test_stall_ms; /* tests: with test_stall_job >= 0, a host stall of this long before that job */
+  int64_t test_stall_job;/* tests: -1 off */
+  uint32_t shard_epoch0; /* tests: the node-sharded engine's first cycle epoch (0; the inbox tags' wrap) */
+  uint32_t pad;
 } kb_opts;
 
 typedef struct kb_ctx kb_ctx;
@@ -389,6 +395,19 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_OPT_NO_TRAJECTORY (1u << 1) /* no trajectory loop: the per-commit re-key loop (testing the device paths) */
 #define KB_OPT_NO_SELECT (1u << 2)     /* no top-T selection path: the trajectory loop (testing the device paths) */
 #define KB_OPT_ENGINE (1u << 3)        /* serve selection-path jobs from the persistent placement engine */
+/* Path selection and measurement switches (ABI 13: kb_opts fields, never the environment). The default (0) is the
+ * production path; the rest exist so the tests can drive every device path and the profiler can run. */
+#define KB_OPT_NO_FED (1u << 4)             /* a place kernel per job instead of the resident fed engine */
+#define KB_OPT_NO_FED_SPLIT (1u << 5)       /* the one-workgroup fed engine (no selector workgroups) */
+#define KB_OPT_NO_PIPELINE (1u << 6)        /* the serial driver: no speculative job issue */
+#define KB_OPT_NO_AFF_REG (1u << 7)         /* self-dependent affinity runs on the global-memory loop */
+#define KB_OPT_NO_CAP1 (1u << 8)            /* cap-1 affinity specs on the re-sweep loops */
+#define KB_OPT_NO_CLS (1u << 9)             /* class-loop affinity specs on the re-sweep loops */
+#define KB_OPT_NO_EVAL_PLAIN (1u << 10)     /* kb_eval's general kernel on plain batches too */
+#define KB_OPT_FED_SHARED_QUEUES (1u << 11) /* the sweep stream without its own hardware queue (the hazard test) */
+#define KB_OPT_FED_PLAIN_LAUNCH (1u << 12)  /* the engine as a plain launch (ranks sharing one GPU; rocprofv3) */
+#define KB_OPT_SHARD_SELF_INBOX (1u << 13)  /* a rank's own record through its inbox too (exchange tests) */
+#define KB_OPT_FED_DIAG (1u << 14)          /* KB_DIAG builds: print the selector's phase stamps at kb_fed_end */
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -420,6 +439,12 @@ typedef struct kb_stats {
   uint64_t cls_runs;                  /* runs taken by the class loop (KB_KERNEL_CLS_PLACE) */
   uint64_t fed_sharded;               /* of the fed cycles, node-sharded ones (kb_set_shard_peer: the device
                                          exchange between the ranks' engines) */
+  uint64_t shard_rezero;              /* inbox re-zeroings at the tags' epoch wrap (every 4096 sharded cycles) */
+  uint64_t shard_xchg;                /* node-sharded engine: exchanges (jobs that ran) */
+  uint64_t shard_wait_ticks;          /* node-sharded engine: s_memrealtime ticks (100 MHz) this rank's placer spent
+                                         between writing its record and holding every peer's */
+  uint64_t fed_clock_ticks, fed_real_ticks; /* split fed engine: s_memtime (shader clock) and s_memrealtime (100 MHz)
+                                         ticks of the placer's launches, so clock MHz = 100 * clock / real */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

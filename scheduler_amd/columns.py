@@ -85,23 +85,62 @@ def template_key(p: M.Pod):
                  [(c.req, c.ports) for c in p.init], sorted(p.node_selector.items()), p.tolerations, p.affinity))
 
 
-def columns_of(cl: M.Cluster) -> Columns:
-    """A model.Cluster as columns (per pod and per node: the Go shim's walk, for tests)."""
-    n = len(cl.nodes)
-    res_names = sorted({k for nd in cl.nodes for k in nd.alloc})
-    alloc = {k: np.array([nd.alloc.get(k, 0) for nd in cl.nodes], np.int64) for k in res_names}
-    has = {k: np.array([k in nd.alloc for nd in cl.nodes], bool) for k in res_names if E.is_scalar_resource_name(k)}
+def _node_columns(nodes) -> dict:
+    """The node half of Columns from per-node objects."""
+    n = len(nodes)
+    res_names = sorted({k for nd in nodes for k in nd.alloc})
+    alloc = {k: np.array([nd.alloc.get(k, 0) for nd in nodes], np.int64) for k in res_names}
+    has = {k: np.array([k in nd.alloc for nd in nodes], bool) for k in res_names if E.is_scalar_resource_name(k)}
     labels = {}
-    for k in sorted({k for nd in cl.nodes for k in nd.labels}):
+    for k in sorted({k for nd in nodes for k in nd.labels}):
         vals, ids = {}, np.full(n, -1, np.int32)
-        for i, nd in enumerate(cl.nodes):
+        for i, nd in enumerate(nodes):
             if k in nd.labels:
                 ids[i] = vals.setdefault(nd.labels[k], len(vals))
         labels[k] = (ids, list(vals))
     tsets, tix = {}, np.zeros(n, np.int32)
-    for i, nd in enumerate(cl.nodes):
+    for i, nd in enumerate(nodes):
         tix[i] = tsets.setdefault(repr(nd.taints), (len(tsets), nd.taints))[0]
     taint_sets = [t for _, t in sorted(tsets.values(), key=lambda x: x[0])]
+    return dict(node_name=[nd.name for nd in nodes], node_alloc=alloc, node_alloc_has=has, node_labels=labels,
+                node_taint=tix, taint_sets=taint_sets, node_flags=np.array([node_flags(nd) for nd in nodes], np.uint32))
+
+
+def columns_of_blocks(nodes, blocks, pod_groups, queues, tiers) -> Columns:
+    """Columns from per-node objects and pod blocks, without per-pod objects: a block is (template pod, uids,
+    node indices or None) -- pods that share one template (the first pod of the block: its spec, status and group),
+    in pod order. Templates are deduplicated by template_key in block order, as columns_of does per pod, so
+    build(columns_of_blocks(...)) equals build(columns_of(cluster)) for the cluster those pods make up."""
+    nc = _node_columns(nodes)
+    pg_ix = {(g.ns, g.name): i for i, g in enumerate(pod_groups)}
+    tpls, tpl_ix = [], {}
+    parts = {"tpl": [], "group": [], "node": [], "status": [], "ctime": [], "uid": []}
+    for tp, uids, where in blocks:
+        k = template_key(tp)
+        t = tpl_ix.get(k)
+        if t is None:
+            t = tpl_ix[k] = len(tpls)
+            tpls.append(tp)
+        m = len(uids)
+        g = -1
+        if tp.group:
+            g = pg_ix.get((tp.ns, tp.group), -1) if (tp.ns, tp.group) in pg_ix else -3
+        parts["tpl"].append(np.full(m, t, np.int32))
+        parts["group"].append(np.full(m, g, np.int32))
+        parts["node"].append(np.full(m, -1, np.int32) if where is None else np.asarray(where, np.int32))
+        parts["status"].append(np.full(m, E.task_status(tp), np.int32))
+        parts["ctime"].append(np.full(m, tp.ctime, np.int64))
+        parts["uid"].append(np.asarray(uids))
+    cat = {k: (np.concatenate(v) if v else np.zeros(0)) for k, v in parts.items()}
+    return Columns(**nc, templates=tpls, pod_tpl=cat["tpl"].astype(np.int32), pod_group=cat["group"].astype(np.int32),
+                   pod_node=cat["node"].astype(np.int32), pod_status=cat["status"].astype(np.int32),
+                   pod_ctime=cat["ctime"].astype(np.int64), pod_uid=cat["uid"], pod_groups=list(pod_groups),
+                   queues=list(queues), tiers=tiers)
+
+
+def columns_of(cl: M.Cluster) -> Columns:
+    """A model.Cluster as columns (per pod and per node: the Go shim's walk, for tests)."""
+    nc = _node_columns(cl.nodes)
     name_ix = {nd.name: i for i, nd in enumerate(cl.nodes)}
     pg_ix = {(g.ns, g.name): i for i, g in enumerate(cl.pod_groups)}
     tpls, tpl_ix = [], {}
@@ -121,12 +160,24 @@ def columns_of(cl: M.Cluster) -> Columns:
             pod_node[i] = name_ix.get(p.node, POD_NODE_UNKNOWN)
         pod_status[i] = E.task_status(p)
         pod_ctime[i] = p.ctime
-    return Columns(node_name=[nd.name for nd in cl.nodes], node_alloc=alloc, node_alloc_has=has, node_labels=labels,
-                   node_taint=tix, taint_sets=taint_sets,
-                   node_flags=np.array([node_flags(nd) for nd in cl.nodes], np.uint32), templates=tpls,
-                   pod_tpl=pod_tpl, pod_group=pod_group, pod_node=pod_node, pod_status=pod_status, pod_ctime=pod_ctime,
+    return Columns(**nc, templates=tpls, pod_tpl=pod_tpl, pod_group=pod_group, pod_node=pod_node, pod_status=pod_status, pod_ctime=pod_ctime,
                    pod_uid=np.array([p.uid for p in cl.pods]), pod_groups=list(cl.pod_groups),
                    queues=list(cl.queues), tiers=cl.tiers)
+
+
+def isum(idx, v, n):
+    """Per-bin sums of int64 values, exact: np.bincount accumulates its weights in float64, exact only while every
+    partial sum stays below 2^53 (export.Snapshot sums in exact ints); past that, np.add.at in int64."""
+    if not len(idx):
+        return np.zeros(n, np.int64)
+    if v is None:
+        return np.bincount(idx, minlength=n).astype(np.int64)
+    v = np.asarray(v, np.int64)
+    if int(np.abs(v).sum(dtype=np.float64)) < (1 << 52):
+        return np.bincount(idx, weights=v, minlength=n).astype(np.int64)
+    out = np.zeros(n, np.int64)
+    np.add.at(out, idx, v)
+    return out
 
 
 class ColumnarSnapshot:
@@ -196,9 +247,7 @@ class ColumnarSnapshot:
         z = np.zeros(N, np.int64)
         a_cpu = c.node_alloc.get(M.CPU, z)
         a_mem = c.node_alloc.get(M.MEMORY, z)
-        w = lambda v, m=None: np.bincount(on if m is None else on[m], weights=None if v is None else
-                                          (v if m is None else v[m]), minlength=N).astype(np.int64) \
-            if len(on) else np.zeros(N, np.int64)
+        w = lambda v, m=None: isum(on if m is None else on[m], None if v is None else (v if m is None else v[m]), N)
         cpu, mem = self.t_cpu[tp], self.t_mem[tp]
         idle_cpu = a_cpu - w(cpu, ~pip_m)
         idle_mem = a_mem - w(mem, ~pip_m)
@@ -256,8 +305,8 @@ class ColumnarSnapshot:
         self.cols_base = {
             "idle_cpu": idle_cpu[kept], "idle_mem": idle_mem[kept], "rel_cpu": rel_cpu[kept], "rel_mem": rel_mem[kept],
             "alloc_cpu": a_cpu[kept].astype(np.int64), "alloc_mem": a_mem[kept].astype(np.int64),
-            "nz_cpu": np.bincount(pos[ok], weights=self.t_nzc[tp][ok], minlength=n).astype(np.int64),
-            "nz_mem": np.bincount(pos[ok], weights=self.t_nzm[tp][ok], minlength=n).astype(np.int64),
+            "nz_cpu": isum(pos[ok], self.t_nzc[tp][ok], n),
+            "nz_mem": isum(pos[ok], self.t_nzm[tp][ok], n),
             "pod_count": np.bincount(pos[ok], minlength=n).astype(np.int32),
             "max_pods": c.node_alloc.get(M.PODS, z)[kept].astype(np.int32),
             "flags": (c.node_flags[kept] | np.where(a_has[kept], E.NODE_IDLE_HAS_MAP, 0) |

@@ -617,7 +617,7 @@ struct Driver {
     pk.resize(max_pending);
     // Pipelined: job k+1 is launched (guarded) before job k's result is read, so the device runs the jobs
     // back to back while the host does the bookkeeping. Otherwise one kb_place_job per job.
-    bool pipe = kb_job_pipeline_ok(ctx) && getenv("KB_NO_PIPELINE") == nullptr;
+    bool pipe = kb_job_pipeline_ok(ctx) && ctx->use_pipeline;
     if (pipe)
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
     // every job one selection run of an eligible spec: the fed engine serves the whole cycle

@@ -95,6 +95,7 @@ struct kb_ctx {
   void* inbox = nullptr;
   void* peer_inbox[kbgpu::kShardMaxWorld] = {};
   uint32_t shard_epoch = 0;
+  uint32_t shard_epoch0 = 0;  // kb_opts.shard_epoch0 (tests)
   bool traj_full = false;  // trajectory buffers (kTrajMaxJ + 1 levels): chunk maxima fit the place loop
   bool sel_ok = false;     // the node count fits the selection kernel's LDS plan (level-0 keys buffer)
   char* d_job = nullptr;     // device JobState (chains the runs of one job)
@@ -139,24 +140,31 @@ struct kb_ctx {
   // fed engine (kb_fed_begin / kb_fed_end): one resident selection workgroup per allocate cycle, fed by the
   // sweep kernels through a kJobSlots-entry device ring; fed_count[r]: blocks counted into fed_ctr[r] so far
   bool fed = false;
-  bool use_fed = true;  // KB_NO_FED unset
-  bool use_eval_plain = true;  // KB_NO_EVAL_PLAIN unset
+  bool use_fed = true;         // !KB_OPT_NO_FED
+  bool use_eval_plain = true;  // !KB_OPT_NO_EVAL_PLAIN
   void* fed_ring = nullptr;
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;
   void* fed_xchg = nullptr;   // split engine exchange (fed_xchg_bytes)
-  bool use_fed_split = true;  // KB_NO_FED_SPLIT unset
+  bool use_fed_split = true;  // !KB_OPT_NO_FED_SPLIT
+  bool fed_split_now = false;  // the running fed cycle is on the split engine (its FedXchg counters)
   // The resident engine waits for sweeps issued on stream_b: they must never queue behind it on one hardware queue.
   // The engine is a cooperative launch (the device's own cooperative queue, every workgroup co-resident) and
   // stream_b a CU-masked stream (a hardware queue of its own, never shared with other streams of the process).
-  // KB_FED_SHARED_QUEUES=1 (tests): plain launch and plain stream, the hazard these remove; KB_FED_PLAIN_LAUNCH=1:
+  // KB_OPT_FED_SHARED_QUEUES (tests): plain launch and plain stream, the hazard these remove; KB_OPT_FED_PLAIN_LAUNCH:
   // plain launch only (the dedicated sweep stream alone already separates the two).
   bool fed_dedicated = true;
   bool fed_coop = true;
-  // tests only (KB_TEST_STALL_JOB / KB_TEST_STALL_MS, read once at kb_create): kb_allocate's driver sleeps before
+  // tests only (kb_opts.test_stall_job / test_stall_ms): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;
   int test_stall_ms = 1500;
+  bool use_pipeline = true;    // !KB_OPT_NO_PIPELINE
+  bool shard_self_inbox = false;  // KB_OPT_SHARD_SELF_INBOX
+  bool fed_diag = false;       // KB_OPT_FED_DIAG
+  uint64_t fed_idle = 100000000ull;  // the engine's idle exit in s_memrealtime ticks (100 MHz): 1 s
+  int eval_spb = 0;            // kb_opts.eval_spb (0: from cus)
+  int cus = 256;               // compute units of the context's device
   uint32_t fed_count[kbgpu::kJobSlots] = {};
   int fed_r = 0;
   uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)

@@ -149,10 +149,13 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 // plain: every spec of the batch is plain (kb_ctx::spec_plain): the row-only kernel (eval_plain_kernel)
+// cus: the device's compute units (the plain kernel's grid is one resident round); spb > 0 overrides its specs
+// per block (measurement)
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, void* stream);
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, int cus, int spb, void* stream);
 void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, void* stream);
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, int cus, int spb,
+                   void* stream);
 int place_loop_lds_bytes(int n);
 // trajectory path
 constexpr int kTrajMaxJ = 64;
@@ -243,7 +246,7 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 // one job ahead (fed_split_ok(n)); nullptr: one workgroup.
 constexpr int kFedSplitMaxTasks = 100;  // one selection segment (kbgpu_device.hip kSegMax)
 size_t fed_xchg_bytes();
-bool fed_split_ok(int n);
+bool fed_split_ok(int n, bool sharded);
 // selector workgroups of the split engine for n nodes (1: one holds every key; up to 4 node ranges past that;
 // 0: beyond the engine)
 int fed_nsel(int n);
@@ -252,6 +255,7 @@ int fed_nsel(int n);
 // them from its own inbox. Inbox: [2 cycle halves][kJobSlots][kShardMaxWorld][kShardRecW] tagged 64-bit words
 // (tag = epoch << 20 | job + 1 in the high half, so every word validates itself and needs no store order).
 constexpr int kShardMaxWorld = 16;
+constexpr int kShardEpochBits = 12;  // of the cycle epoch in an inbox word's tag (the host re-zeroes at the wrap)
 constexpr int kShardRecW = 3 * kShardSegMax + 24;  // 3 words per pick + kp + 3 header words + the histogram
 static_assert(3 * kShardSegMax + 4 + KB_NUM_REASONS <= kShardRecW, "inbox record layout");
 struct ShardPeers {

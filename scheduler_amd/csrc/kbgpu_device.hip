@@ -2857,7 +2857,8 @@ struct FedXchg {
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
   uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
-  uint64_t sdiag[16];  // KB_DIAG builds: the selector's phase cycles, [8..] the placer's merge (KB_FED_DIAG)
+  uint64_t sdiag[16];  // KB_DIAG builds: [0..6] the selector's phases, [8..11] the placer's merge; [12..15] the placer's
+                       // counters for kb_stats (every build: exchange wait / count, clock / realtime ticks)
 };
 
 // Thread 0: spin (sleeping) until *w reaches want, at most idle_ticks of s_memrealtime. ACQ: with an
@@ -3182,6 +3183,7 @@ __device__ __forceinline__ uint64_t* shard_inbox(const ShardPeers& SP, int w) {
   return p;
 }
 __device__ __forceinline__ uint32_t shard_tag(uint32_t epoch, uint32_t m) {
+  static_assert(kShardEpochBits == 12, "tag layout: 12 epoch bits, 20 exchange bits");
   return ((epoch & 0xfffu) << 20) | ((m + 1) & 0xfffffu);
 }
 // entries of rank h's proposal list (descending, high / low words in LDS) above v
@@ -3218,7 +3220,8 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
                                           const int32_t* l0, int n0, const int32_t* l1, int n1, int t_begin,
                                           int t_count, int ready0, int minav, int gang, int idx_bits, int32_t* hout,
                                           JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
-                                          int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped) {
+                                          int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped,
+                                          uint64_t& wait_acc) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int T = t_count, W = SP.world;
   __syncthreads();  // sel_run's no-fit exit writes sh.s_count = 0 from one thread with no barrier after it
@@ -3274,8 +3277,9 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // ---- read: every other rank's record from this rank's inbox ----
+  const uint64_t t_read0 = __builtin_amdgcn_s_memrealtime();
   {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t0 = t_read0;
     bool late = false;
     uint64_t* own = shard_inbox(SP, SP.rank);
     for (int idx = tid; idx < W * L && !late; idx += kSelThreads) {
@@ -3305,6 +3309,7 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     if (late) G.fail = 1;  // (benign race: every writer stores 1)
   }
   __syncthreads();
+  wait_acc += __builtin_amdgcn_s_memrealtime() - t_read0;  // (thread 0's count is the one reported)
   if (G.fail) return 1;
   if (tid < W && (G.hdr[tid][0] != hdr0 || G.hdr[tid][1] != hdr1 || G.hdr[tid][2] != hdr2 || G.kp[tid] > T))
     G.diverged = 1;
@@ -3454,13 +3459,17 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
 // SPLIT: grid 1 + nsel, workgroup 0 the placer and 1.. the selectors (fed_selector) of nsel node ranges; every
 // job of the cycle one segment (the host checks). Otherwise one workgroup with every node's key in LDS.
 // SHARD (split only): the node-sharded engine -- the placer proposes, exchanges and merges (shard_place).
-template <int QN, bool SPLIT, bool SHARD = false>
+// MSEL: the most selector workgroups the instance serves (1, or kFedMaxSel range selectors past one workgroup's key
+// plan): a one-selector instance carries no range merge code and no per-range registers.
+template <int QN, bool SPLIT, bool SHARD = false, int MSEL = 1>
 __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, DevSpecs P, DevCfg C, int idx_bits,
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
-                                                                 int32_t* exit_flag, FedXchg* X, int nsel,
+                                                                 int32_t* exit_flag, FedXchg* X, int nsel_arg,
                                                                  ShardPeers SP) {
   static_assert(!SHARD || SPLIT, "the node-sharded engine is the split engine");
+  static_assert(MSEL == 1 || (SPLIT && MSEL <= kFedMaxSel), "range selectors belong to the split engine");
+  const int nsel = MSEL == 1 ? 1 : nsel_arg;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   __shared__ FedCmd cm;
@@ -3468,7 +3477,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   __shared__ int32_t bprev[128];  // split: the previous job's selected set, slot order
   __shared__ uint32_t bkey[128];  //   its keys for this job
   __shared__ int32_t s_feas;
-  __shared__ int32_t s_na[kFedMaxSel];  // split: the selectors' candidate counts for this job
+  __shared__ int32_t s_na[MSEL];  // split: the selectors' candidate counts for this job
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -3497,9 +3506,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   int rp = 0;
   // split, thread 0: the next job's command words and selector 0's head, then the other selectors' heads, loaded
   // at this job's end
-  uint64_t pre[16 + kFedMaxSel];
+  uint64_t pre[16 + MSEL];
 #pragma unroll
-  for (int q = 0; q < 16 + kFedMaxSel; ++q) pre[q] = 0;
+  for (int q = 0; q < 16 + MSEL; ++q) pre[q] = 0;
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -3510,6 +3519,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
   uint32_t m = 0;
   uint32_t xn = 0;  // SHARD: exchanges so far (the jobs that ran)
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0_launch = __builtin_amdgcn_s_memrealtime();
+  uint64_t shard_wait = 0;  // SHARD: realtime ticks from this rank's record written to every peer's record read
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
       if (tid == 0) {
@@ -3532,7 +3543,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           c = (int32_t)(uint32_t)h;
           s_na[0] = c;
 #pragma unroll
-          for (int k = 1; k < kFedMaxSel; ++k) {  // the other selectors' lists of this job (unrolled: pre in VGPRs)
+          for (int k = 1; k < MSEL; ++k) {  // the other selectors' lists of this job (unrolled: pre in VGPRs)
             if (k >= nsel || c < 0) continue;
             uint64_t hk = pre[16 + k];
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -3640,12 +3651,12 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       // previous set's rows in the candidate space, else (up to 4 * 128 + 128 rows) in the key space, which a
       // split placer does not otherwise use
       uint32_t* akey = k32;
-      Row* crow = nsel == 1 ? brow + 128 : (Row*)(k32 + kFedMaxSel * 128);
-      uint64_t* cst = (uint64_t*)(crow + (nsel == 1 ? 256 : 128 * (kFedMaxSel + 1)));
-      int32_t* cnd = (int32_t*)(cst + 128 * (kFedMaxSel + 1));
+      Row* crow = MSEL == 1 ? brow + 128 : (Row*)(k32 + MSEL * 128);
+      uint64_t* cst = (uint64_t*)(crow + (MSEL == 1 ? 256 : 128 * (MSEL + 1)));
+      int32_t* cnd = (int32_t*)(cst + 128 * (MSEL + 1));
       int na = 0, list = -1, idx = 0;
 #pragma unroll
-      for (int k = 0; k < kFedMaxSel; ++k) {
+      for (int k = 0; k < MSEL; ++k) {
         const int c = k < nsel ? s_na[k] : 0;
         if (tid >= na && tid < na + c) list = k, idx = tid - na;
         na += c;
@@ -3703,25 +3714,25 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         key = tid < na ? akey[list * 128 + idx] : bkey[tid - na];
         // entries above the key in every list (its own list included: there that is its index), all searches
         // at once: branch-free halving steps over lists of at most 128 (padding past a list's length unread)
-        int c[kFedMaxSel + 1];
+        int c[MSEL + 1];
 #pragma unroll
-        for (int k = 0; k <= kFedMaxSel; ++k) c[k] = 0;
-        int len[kFedMaxSel + 1];
+        for (int k = 0; k <= MSEL; ++k) c[k] = 0;
+        int len[MSEL + 1];
 #pragma unroll
-        for (int k = 0; k <= kFedMaxSel; ++k) len[k] = k < kFedMaxSel ? (k < nsel ? s_na[k] : 0) : nb;
+        for (int k = 0; k <= MSEL; ++k) len[k] = k < MSEL ? (k < nsel ? s_na[k] : 0) : nb;
 #pragma unroll
         for (int step = 64; step >= 1; step >>= 1) {
 #pragma unroll
-          for (int k = 0; k <= kFedMaxSel; ++k) {
-            if (k < kFedMaxSel && k >= nsel) continue;  // (uniform) lists past the selectors
-            const uint32_t* l = k < kFedMaxSel ? akey + k * 128 : sh.emin;
+          for (int k = 0; k <= MSEL; ++k) {
+            if (k < MSEL && k >= nsel) continue;  // (uniform) lists past the selectors
+            const uint32_t* l = k < MSEL ? akey + k * 128 : sh.emin;
             const int p = c[k] + step;
             if (p <= len[k] && l[p - 1] > key) c[k] = p;
           }
         }
         pos = 0;
 #pragma unroll
-        for (int k = 0; k <= kFedMaxSel; ++k) pos += c[k];
+        for (int k = 0; k <= MSEL; ++k) pos += c[k];
       }
       // the T best feasible (A is all feasible; infeasible keys rank below every feasible one), slots in node
       // order: the winners' tie rule on equal score fields takes lower slots first, which must be lower nodes
@@ -3800,7 +3811,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                                  prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr,
                                  prev_slot[1] >= 0 ? prev_ncommit[1] : 0, cm.t_begin, cm.t_count, cm.ready0, minav,
                                  gang, idx_bits, S.hout[slot], js, hjs, S.commits[slot], idle_ticks, stop, fail_task,
-                                 placed, ready, panic, stopped);
+                                 placed, ready, panic, stopped, shard_wait);
       if (rc != 0) {  // a peer never answered (every rank's engine leaves), or the ranks issued different jobs
         if (tid == 0) {
           atomicMax(exit_flag, 1);
@@ -3826,7 +3837,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         brow[tid] = row_after(sp, sh.row[tid], sh.fin[tid], sh.A[tid]);
       }
       nbprev = ns;
-      if (sh.need_hist && nsel > 1) {  // no fit, the table past one key plan: the histogram streamed (below)
+      if (sh.need_hist && MSEL > 1 && nsel > 1) {  // no fit, the table past one key plan: the histogram streamed (below)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
         __syncthreads();
         const int32_t* l0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
@@ -3881,7 +3892,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
       for (int q = 0; q < 16; ++q) pre[q] = x_load64(&X->s_cmd[rn][q]);
 #pragma unroll
-      for (int k = 0; k < kFedMaxSel; ++k) pre[16 + k] = k < nsel ? x_load64(&X->s_head[rn][k]) : 0;
+      for (int k = 0; k < MSEL; ++k) pre[16 + k] = k < nsel ? x_load64(&X->s_head[rn][k]) : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a barrier alone waits for LDS only)
     __syncthreads();
@@ -3906,6 +3917,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   if (SPLIT && tid == 0)
     for (int k = 0; k < 4; ++k) X->sdiag[8 + k] = mg[k];
 #endif
+  if (SPLIT && tid == 0) {  // for the host's stats: the exchange's cost (kb_stats.shard_wait_ticks / shard_xchg) and
+                           // the shader clock over the launch (fed_clock_ticks / fed_real_ticks)
+    X->sdiag[12] = shard_wait;
+    X->sdiag[13] = xn;
+    X->sdiag[14] = __builtin_amdgcn_s_memtime() - clk0;
+    X->sdiag[15] = __builtin_amdgcn_s_memrealtime() - rt0_launch;
+  }
 }
 
 int fed_lds_bytes(int n) {
@@ -3937,8 +3955,11 @@ int fed_nsel(int n) {
     if (fed_sel_chunk(n, k) <= kFedSelNodes) return k;
   return 0;
 }
-// the placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096
-bool fed_split_ok(int n) { return fed_nsel(n) > 0 && n > 4 * kSelThreads; }
+// The placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096.
+// Unsharded tables of one key group stay on the one-workgroup engine; a node-sharded rank's block (the sharded engine
+// is the split one) may be of any size: its instance then holds two key groups (n_pad = 4096, so the placer's
+// candidate keys and nodes still fit its key array).
+bool fed_split_ok(int n, bool sharded) { return fed_nsel(n) > 0 && (sharded ? n > 0 : n > 4 * kSelThreads); }
 
 size_t shard_inbox_bytes() { return (size_t)2 * kJobSlots * kShardMaxWorld * kShardRecW * sizeof(uint64_t); }
 
@@ -3957,8 +3978,9 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   }
   // past one workgroup's key plan: nsel range selectors of kFedSelQ key groups each (split engine only)
   int nsel = xchg ? fed_nsel(N.n) : 1;
-  const int qn = nsel > 1 ? kFedSelQ : sel_qn(N.n);
-  const int bytes = nsel > 1 ? 4 * (4 * kSelThreads * kFedSelQ) + 8 * kCandCap : fed_lds_bytes(N.n);
+  int qn = nsel > 1 ? kFedSelQ : sel_qn(N.n);
+  if (xchg && qn == 1) qn = 2;  // a sharded rank's block of one key group: the split instance of two (fed_split_ok)
+  const int bytes = qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : fed_lds_bytes(N.n);
   const FedCmd* ring_c = (const FedCmd*)ring;
   FedXchg* X = (FedXchg*)xchg;
   ShardPeers SP = shard;
@@ -3966,7 +3988,6 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                   (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP};
   const bool sharded = SP.world > 0;
   if (sharded && !xchg) return (int)hipErrorInvalidValue;  // the node-sharded engine is the split engine
-  // (no split instance for one key group: fed_split_ok needs n > 4 * kSelThreads)
   const void* f = nullptr;
   bool split = false;
 #define KB_FED_QN(Q)                                                                                         \
@@ -3974,6 +3995,9 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
     split = xchg && Q != 1;                                                                                 \
     f = split ? (sharded ? (const void*)fed_engine_kernel<Q, Q != 1, Q != 1> : (const void*)fed_engine_kernel<Q, Q != 1>) \
               : (const void*)fed_engine_kernel<Q, false>;                                                  \
+    if (Q == kFedSelQ && split && nsel > 1)  /* range selectors: the instance with the lists' merge */       \
+      f = sharded ? (const void*)fed_engine_kernel<kFedSelQ, true, true, kFedMaxSel>                          \
+                  : (const void*)fed_engine_kernel<kFedSelQ, true, false, kFedMaxSel>;                      \
     break;
   switch (qn) {
     KB_FED_QN(1)
@@ -4801,6 +4825,7 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // ---------------------------------------------------------------------------
 // 4 waves: the task loop's wave gets the whole VGPR file of its SIMD (1024 threads cap it at 128 and spill)
 constexpr int kClsThreads = 256;
+constexpr int kClsPM = 4;  // a class phase's members per lane (classes of at most 256 nodes)
 static_assert(kClsMaxK <= 16 * 64 && kClsMaxK % kClsThreads == 0, "classes per lane: at most 16");
 
 // wave-uniform signed max / min on DPP (ordering-preserving bias to unsigned); |v| < 2^62
@@ -5083,39 +5108,53 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
   // A winner keeps its score for several pods (LR / BRA move in steps): most commits read a register.
   int hot = -1, hot_c = 0, hot_A = 0, hot_n = 0, hot_lim = 0, p_node = -1, p_A = 0;
   uint64_t hk = 0, pk = 0;
-  const auto flush_hot = [&]() {  // lane 0: the hot node's commits as row deltas (NodeInfo.AddTask)
+  // c commits of the spec on node v, the first ac of them Allocates, as row deltas (NodeInfo.AddTask); any lane
+  const auto flush_node = [&](int v, int c, int64_t ac) {
+    const int64_t pc = c - ac;
+    // read before the atomics: a load issued after them would wait for them too (in-order vmcnt)
+    const uint32_t fl = sp.req_sc_mask ? N.flags[v] : 0u;
+    if (ac) {
+      atomicAdd((unsigned long long*)&N.idle_cpu[v], (unsigned long long)(-ac * sp.req_cpu));
+      atomicAdd((unsigned long long*)&N.idle_mem[v], (unsigned long long)(-ac * sp.req_mem));
+    }
+    if (pc) {
+      atomicAdd((unsigned long long*)&N.rel_cpu[v], (unsigned long long)(-pc * sp.req_cpu));
+      atomicAdd((unsigned long long*)&N.rel_mem[v], (unsigned long long)(-pc * sp.req_mem));
+    }
+    atomicAdd(&N.pod_count[v], c);
+    atomicAdd((unsigned long long*)&N.nz_cpu[v], (unsigned long long)((int64_t)c * sp.nz_cpu));
+    atomicAdd((unsigned long long*)&N.nz_mem[v], (unsigned long long)((int64_t)c * sp.nz_mem));
+    uint64_t m = sp.req_sc_mask;
+    while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
+      const int q = __builtin_ctzll(m);
+      m &= m - 1;
+      if (ac && (fl & KB_NODE_IDLE_HAS_MAP))
+        atomicAdd((unsigned long long*)&N.idle_sc[(size_t)q * n + v], (unsigned long long)(-ac * scr[q]));
+      if (pc && (fl & KB_NODE_REL_HAS_MAP))
+        atomicAdd((unsigned long long*)&N.rel_sc[(size_t)q * n + v], (unsigned long long)(-pc * scr[q]));
+    }
+    for (uint32_t i = 0; i < sp.port_cnt; ++i) {
+      const kb_port q = P.ports[sp.port_off + i];
+      atomicOr((unsigned long long*)&N.port_used[(size_t)q.slot * n + v], 1ull << q.ip);
+    }
+  };
+  const auto flush_hot = [&]() {  // lane 0: the hot node's commits
     if (hot < 0 || hot_c == 0) return;
     if (lane == 0) {
-      const int64_t ac = hot_c < hot_A ? hot_c : hot_A, pc = hot_c - ac;
-      // read before the atomics: a load issued after them would wait for them too (in-order vmcnt)
-      const uint32_t fl = sp.req_sc_mask ? N.flags[hot] : 0u;
-      if (ac) {
-        atomicAdd((unsigned long long*)&N.idle_cpu[hot], (unsigned long long)(-ac * sp.req_cpu));
-        atomicAdd((unsigned long long*)&N.idle_mem[hot], (unsigned long long)(-ac * sp.req_mem));
-      }
-      if (pc) {
-        atomicAdd((unsigned long long*)&N.rel_cpu[hot], (unsigned long long)(-pc * sp.req_cpu));
-        atomicAdd((unsigned long long*)&N.rel_mem[hot], (unsigned long long)(-pc * sp.req_mem));
-      }
-      atomicAdd(&N.pod_count[hot], hot_c);
-      atomicAdd((unsigned long long*)&N.nz_cpu[hot], (unsigned long long)((int64_t)hot_c * sp.nz_cpu));
-      atomicAdd((unsigned long long*)&N.nz_mem[hot], (unsigned long long)((int64_t)hot_c * sp.nz_mem));
-      uint64_t m = sp.req_sc_mask;
-      while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
-        const int q = __builtin_ctzll(m);
-        m &= m - 1;
-        if (ac && (fl & KB_NODE_IDLE_HAS_MAP))
-          atomicAdd((unsigned long long*)&N.idle_sc[(size_t)q * n + hot], (unsigned long long)(-ac * scr[q]));
-        if (pc && (fl & KB_NODE_REL_HAS_MAP))
-          atomicAdd((unsigned long long*)&N.rel_sc[(size_t)q * n + hot], (unsigned long long)(-pc * scr[q]));
-      }
-      for (uint32_t i = 0; i < sp.port_cnt; ++i) {
-        const kb_port q = P.ports[sp.port_off + i];
-        atomicOr((unsigned long long*)&N.port_used[(size_t)q.slot * n + hot], 1ull << q.ip);
-      }
+      flush_node(hot, hot_c, hot_c < hot_A ? hot_c : hot_A);
       lv16[hot] = (uint16_t)(hot_n + hot_c);
     }
   };
+  // Class phases (exact batching of the per-task argmax). When a commit can only raise its own class's count
+  // (every own increment > 0 and on the class slot, the min at 0, InterPodAffinity weight >= 0), the winner's
+  // class R only gains -- its count grows, and its score with it (ipa_score is monotone in the count; the max
+  // follows R's count or stays) -- while every other class only loses (its count is fixed, the max can only
+  // grow). So from a task whose winner is in R, as long as R's best base key plus R's score at the phase's start
+  // beats S, the best other class's key at the start, the argmax is R's best node: the picks are R's members in
+  // base-key order (each member's keys after 1..kClsL commits are the sweep's levels), with no landscape and
+  // no class rescan per task. The phase ends at the first pick that is not provably R's (then the per-task
+  // path decides, exactly), at a member past the sweep's levels, or at a stop rule.
+  const bool phase_ok = (!ipa || (wsign == 1 && only_f && c_wpa >= 0)) && KQ <= 4;
   AFF_STAMP(0);
   int64_t mn = 0, mx = 0;
   bool mm_ok = false;  // mn / mx hold the current min / max
@@ -5214,6 +5253,172 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     const uint64_t who = __ballot(mine >= 0);
     const int cw = __builtin_amdgcn_readlane(mine, (int)__builtin_ctzll(who));
     AFF_STAMP(1);
+    if (phase_ok && (!ipa || mn == 0) && coff[cw + 1] - coff[cw] <= 64u * kClsPM) {
+      const uint32_t m0 = coff[cw], m1 = coff[cw + 1];
+      uint64_t s2 = 0;  // S: the best other class (keys are distinct: they carry the node)
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) s2 = kq[q] != best ? umax64(s2, kq[q]) : s2;
+      s2 = wave_max_dpp(s2);
+      int64_t cR = 0, incR = 0;  // R's count and the spec's increment of it per commit
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        if (q == (cw >> 6)) {
+          const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)cq[q], cw & 63);
+          const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)cq[q] >> 32), cw & 63);
+          cR = (int64_t)(((uint64_t)hi << 32) | lo);
+        }
+#pragma unroll
+      for (int e = 0; e < kClsE; ++e) {
+        if (!e_has[e]) continue;
+        int32_t d = -1;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+          if (q == (cw >> 6)) d = (int32_t)__builtin_amdgcn_readlane((uint32_t)cd[e][q], cw & 63);
+        if (d >= 0) incR += e_w[e];
+      }
+      const int64_t lift = ipa ? (int64_t)ipa_score(cR, mn, mx) * c_wpa : 0;  // R's score term at the start
+      flush_hot();
+      wave_sync_lds();
+      hot = -1, hot_c = 0, p_node = -1;
+      // R's members, kClsPM per lane: node, current key, commits so far in this run, Allocates before full, and
+      // the sweep's keys after 1..kClsL commits (the levels still ahead; all loads in flight at once)
+      int nd[kClsPM], lev[kClsPM], am[kClsPM], cc[kClsPM];
+      uint64_t key[kClsPM], L[kClsPM][kClsL];
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
+        const uint32_t ix = m0 + (uint32_t)(j * 64 + lane);
+        nd[j] = ix < m1 ? (int)mem[ix] : -1;
+        cc[j] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
+        key[j] = nd[j] >= 0 ? bk[nd[j]] : 0;
+        lev[j] = nd[j] >= 0 ? (int)lv16[nd[j]] : kClsL;
+      }
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
+        am[j] = nd[j] >= 0 ? amax[nd[j]] : 0;
+#pragma unroll
+        for (int l = 0; l < kClsL; ++l) L[j][l] = nd[j] >= 0 && l >= lev[j] ? lvl[(size_t)l * n + nd[j]] : 0;
+      }
+      const uint64_t liftk = (uint64_t)lift << 24;
+      // a member past the sweep's levels: its next 64 keys across the lanes (lane l: the key after rel0 + l + 1
+      // commits on its row as HBM holds it -- the commits before the phase, flushed at its start), dh_A the
+      // Allocates before Idle stops fitting on that row, as the per-task path's deep keys
+      int dh = -1, dh_rel0 = 0, dh_A = 0;
+      uint64_t dhk = 0;
+      bool fenced = false;
+      int took = 0;
+      for (;;) {
+        uint64_t b = 0;
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j) b = umax64(b, key[j]);
+        b = wave_max_dpp(b);
+        if (!(b & kFeasible) || b + liftk <= s2) break;  // not provably R's: the per-task path decides
+        if ((int64_t)((b >> 24) & ((1ull << 39) - 1)) - kScoreBias + lift <= -1) break;  // (the panic: per task)
+        int jw = -1;
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j) jw = key[j] == b ? j : jw;
+        const int wl = (int)__builtin_ctzll(__ballot(jw >= 0));
+        int ml = 0, ma = 0, mc = 0;
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j)
+          if (j == jw) ml = lev[j], ma = am[j], mc = cc[j];
+        const int lw = __builtin_amdgcn_readlane(ml, wl);
+        const int wn = (int)(kIdxMask - (uint32_t)(b & kIdxMask));
+        int kind;
+        uint64_t dnk = 0;
+        if (lw < kClsL) {
+          kind = lw < __builtin_amdgcn_readlane(ma, wl) ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+        } else {  // past the sweep's levels: keys from its row (rel: this phase's commits on it so far)
+          const int rel = __builtin_amdgcn_readlane(mc, wl);
+          if (wn != dh || rel - dh_rel0 >= 64) {
+            if (!fenced) {  // the row deltas flushed at the phase's start (atomics): visible to the loads below
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+              fenced = true;
+            }
+            Row r;
+            r.flags = N.flags[wn];
+            r.max_pods = N.max_pods[wn];
+            r.alloc_cpu = N.alloc_cpu[wn];
+            r.alloc_mem = N.alloc_mem[wn];
+            r.pod_count = __hip_atomic_load(&N.pod_count[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.idle_cpu = __hip_atomic_load(&N.idle_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.idle_mem = __hip_atomic_load(&N.idle_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.rel_cpu = __hip_atomic_load(&N.rel_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.rel_mem = __hip_atomic_load(&N.rel_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.nz_cpu = __hip_atomic_load(&N.nz_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r.nz_mem = __hip_atomic_load(&N.nz_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dh_A = cls_allocs_deep(N, sp, sci, scr, r, wn);
+            const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[wn], wn, rel + lane + 1, dh_A);
+            dhk = (k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)wn)) : k;
+            dh = wn, dh_rel0 = rel;
+          }
+          dnk = hk_at(dhk, rel - dh_rel0);
+          kind = rel < dh_A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+        }
+        if (lane == wl) {
+#pragma unroll
+          for (int j = 0; j < kClsPM; ++j)
+            if (j == jw) {
+              uint64_t nk = dnk;
+#pragma unroll
+              for (int l = 0; l < kClsL; ++l) nk = l == lev[j] ? L[j][l] : nk;
+              key[j] = nk;
+              ++lev[j];
+              ++cc[j];
+            }
+        }
+        if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
+        cR += incR;
+        mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
+        ++took;
+        ++placed;
+        ++pb_n;
+        if (kind == KB_PLACE_ALLOCATE) ++ready;
+        if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+          stop = KB_STOP_READY;
+          stopped = 1;
+          break;
+        }
+        if (pb_n == pb_cap) {
+          wave_sync_lds();
+          for (int k = lane; k < pb_n; k += 64) {
+            const uint32_t e = pbs[k];
+            hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+            hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+          }
+          wave_sync_lds();
+          pb_base += pb_n;
+          pb_n = 0;
+        }
+        if (t + took == t_count) break;
+      }
+      // the members' commits: keys, levels and row deltas back; R's best and count
+      uint64_t nb = 0;
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
+        nb = umax64(nb, key[j]);
+        if (cc[j] > 0) {
+          const int l0 = lev[j] - cc[j];
+          const int ac = am[j] > l0 ? (am[j] - l0 < cc[j] ? am[j] - l0 : cc[j]) : 0;
+          flush_node(nd[j], cc[j], ac);
+          lv16[nd[j]] = (uint16_t)lev[j];
+          bk[nd[j]] = key[j];
+        }
+      }
+      nb = wave_max_dpp(nb);
+      if (lane == 0) cbest[cw] = nb;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        if (q == (cw >> 6) && lane == (cw & 63)) cq[q] = cR;
+      wave_sync_lds();
+      if (took > 0) {
+        if (stopped) break;
+        t += took - 1;
+        continue;
+      }
+    }
     // commit: Session.Allocate / Pipeline on the winner's row (allocate.go:159-182). A new hot node (or the
     // hot one past its keys) first.
     if (w != hot || hot_c == hot_lim) {
@@ -5480,7 +5685,8 @@ int configure_kernels() {
 #define KB_FED_F(Q) \
   (const void*)fed_engine_kernel<Q, false>, (const void*)fed_engine_kernel<Q, true>, (const void*)fed_engine_kernel<Q, true, true>
   for (const void* f : {KB_FED_F(0), (const void*)fed_engine_kernel<1, false>, KB_FED_F(2), KB_FED_F(3), KB_FED_F(4), KB_FED_F(5), KB_FED_F(6),
-                        KB_FED_F(8), KB_FED_F(10)}) {
+                        KB_FED_F(8), KB_FED_F(10), (const void*)fed_engine_kernel<kFedSelQ, true, false, kFedMaxSel>,
+                        (const void*)fed_engine_kernel<kFedSelQ, true, true, kFedMaxSel>}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFedDynLimit);
     if (e != hipSuccess) return (int)e;
   }
@@ -5531,26 +5737,15 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 }
 
 // eval_plain_kernel's specs per block: the grid sized to one resident round of at most 8 waves per SIMD (the
-// kernel's occupancy; 256 CUs x 4 SIMDs), so no SIMD runs a second, partial round and every SIMD holds as many
-// waves as fit to hide the f64 chains' latency. KB_EVAL_SPB overrides (measurement).
-static int eval_plain_spb(int n, int t) {
-  static const int env = [] {
-    const char* e = getenv("KB_EVAL_SPB");
-    return e ? atoi(e) : 0;
-  }();
+// kernel's occupancy; cus CUs x 4 SIMDs), so no SIMD runs a second, partial round and every SIMD holds as many
+// waves as fit to hide the f64 chains' latency. spb_opt > 0 overrides (kb_opts.eval_spb: measurement).
+static int eval_plain_spb(int n, int t, int cus, int spb_opt) {
   int spb;
-  if (env > 0) {
-    spb = env;
+  if (spb_opt > 0) {
+    spb = spb_opt;
   } else {
-    static const int cus = [] {
-      int dev = 0, c = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-        c = 256;
-      return c;
-    }();
     const int xblocks = (n + 255) / 256;
-    const int yblocks = (cus * 4 * 8) / (xblocks * 4);  // blocks of 4 waves in one round, per column
+    const int yblocks = ((cus > 0 ? cus : 256) * 4 * 8) / (xblocks * 4);  // blocks of 4 waves in one round, per column
     spb = yblocks > 0 ? (t + yblocks - 1) / yblocks : kEvalPlainSpecs;
     if (spb < 8) spb = 8;
   }
@@ -5558,9 +5753,10 @@ static int eval_plain_spb(int n, int t) {
 }
 template <class SCORE>
 static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                          uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, void* stream) {
+                          uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, int cus, int spb_opt,
+                          void* stream) {
   if (plain) {
-    const int spb = eval_plain_spb(N.n, t);
+    const int spb = eval_plain_spb(N.n, t, cus, spb_opt);
     dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
     hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, spb,
                        reasons, scores);
@@ -5575,12 +5771,13 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                        reasons, scores, mm);
 }
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, void* stream) {
-  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, stream);
+                 uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, int cus, int spb, void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, cus, spb, stream);
 }
 void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
-                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, void* stream) {
-  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, stream);
+                   uint32_t* reasons, int32_t* scores, const int64_t* mm, bool plain, int cus, int spb,
+                   void* stream) {
+  launch_eval_t(N, P, C, spec_ids, t, reasons, scores, mm, plain, cus, spb, stream);
 }
 
 // kb_apply: one thread per row delta of a commit made outside the device -- NodeInfo.AddTask / RemoveTask

@@ -231,16 +231,25 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->device = opts ? opts->device : 0;
   c->timing = opts && (opts->flags & KB_OPT_TIMING);
   c->timing_every = opts && opts->timing_every > 1 ? opts->timing_every : 1;
-  c->use_aff_reg = getenv("KB_NO_AFF_REG") == nullptr;  // testing: force the global-memory affinity loop
-  c->use_cap1 = getenv("KB_NO_CAP1") == nullptr;        // testing: cap-1 specs on the re-sweep loops
-  c->use_cls = getenv("KB_NO_CLS") == nullptr;          // testing: class-loop specs on the re-sweep loops
-  c->use_fed = getenv("KB_NO_FED") == nullptr;          // testing: a place kernel per job instead
-  c->use_eval_plain = getenv("KB_NO_EVAL_PLAIN") == nullptr;  // testing: kb_eval's general kernel on plain specs
-  c->use_fed_split = getenv("KB_NO_FED_SPLIT") == nullptr;  // testing: the one-workgroup fed engine
-  c->fed_dedicated = getenv("KB_FED_SHARED_QUEUES") == nullptr;  // testing: the shared-queue hazard
-  c->fed_coop = c->fed_dedicated && getenv("KB_FED_PLAIN_LAUNCH") == nullptr;
-  if (const char* e = getenv("KB_TEST_STALL_JOB")) c->test_stall_job = atoll(e);
-  if (const char* e = getenv("KB_TEST_STALL_MS")) c->test_stall_ms = atoi(e);
+  const uint32_t fl = opts ? opts->flags : 0u;
+  c->use_aff_reg = !(fl & KB_OPT_NO_AFF_REG);
+  c->use_cap1 = !(fl & KB_OPT_NO_CAP1);
+  c->use_cls = !(fl & KB_OPT_NO_CLS);
+  c->use_fed = !(fl & KB_OPT_NO_FED);
+  c->use_eval_plain = !(fl & KB_OPT_NO_EVAL_PLAIN);
+  c->use_fed_split = !(fl & KB_OPT_NO_FED_SPLIT);
+  c->use_pipeline = !(fl & KB_OPT_NO_PIPELINE);
+  c->fed_dedicated = !(fl & KB_OPT_FED_SHARED_QUEUES);
+  c->fed_coop = c->fed_dedicated && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
+  c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
+  c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
+  if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
+  if (opts && opts->eval_spb > 0) c->eval_spb = opts->eval_spb;
+  if (opts) c->shard_epoch0 = opts->shard_epoch0;
+  if (opts && opts->test_stall_job >= 0) {
+    c->test_stall_job = opts->test_stall_job;
+    if (opts->test_stall_ms > 0) c->test_stall_ms = opts->test_stall_ms;
+  }
   c->timing_now = c->timing;
   c->use_traj = !(opts && (opts->flags & KB_OPT_NO_TRAJECTORY));
   c->use_sel = !(opts && (opts->flags & KB_OPT_NO_SELECT));
@@ -260,6 +269,11 @@ kb_ctx* kb_create(const kb_opts* opts) {
     c->err = "hipStreamCreate (engine) failed";
     c->broken = true;
     return c;
+  }
+  {  // grids sized per device (eval_plain_kernel's resident round)
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cu > 0)
+      c->cus = cu;
   }
   if (int e = kbgpu::configure_kernels()) {
     c->err = std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString((hipError_t)e);
@@ -913,7 +927,29 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
     c->peer_inbox[w] = p;
   }
   c->peer = true;
-  c->shard_epoch = 0;
+  c->shard_epoch = c->shard_epoch0;
+  return KB_OK;
+}
+
+// The inbox words carry kShardEpochBits of the cycle epoch (shard_tag): a word a cycle left behind -- a longer
+// record, a no-fit histogram written only on NO_FIT -- would read as current again 2^kShardEpochBits cycles later in
+// the same cycle half. So at every epoch that is a multiple of the wrap every rank zeroes its own inbox between two
+// host barriers (the all-gather callback): the first passes once every rank's previous cycle has ended (no peer
+// writes in flight), the second once every inbox is clean (no rank starts the cycle before).
+static int shard_inbox_rezero(kb_ctx* c) {
+  const int W = c->shard.world;
+  std::vector<uint32_t> tok((size_t)W + 1, 0u);
+  tok[0] = c->shard_epoch + 1;
+  if (int rc = c->ag_fn(c->ag_user, tok.data(), tok.data() + 1, sizeof(uint32_t)))
+    return fail(c, KB_E_HIP, "all-gather callback failed (%d) before the inbox re-zeroing", rc);
+  for (int w = 0; w < W; ++w)
+    if (tok[1 + w] != tok[0])
+      return fail(c, KB_E_STATE, "node-sharded engine: rank %d is at epoch %u, this rank at %u", w, tok[1 + w], tok[0]);
+  HIP_OK(c, hipMemset(c->inbox, 0, shard_inbox_bytes()));
+  HIP_OK(c, hipDeviceSynchronize());
+  if (int rc = c->ag_fn(c->ag_user, tok.data(), tok.data() + 1, sizeof(uint32_t)))
+    return fail(c, KB_E_HIP, "all-gather callback failed (%d) after the inbox re-zeroing", rc);
+  c->stats.shard_rezero++;
   return KB_OK;
 }
 
@@ -1398,7 +1434,7 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
   if ((c->sharded && !c->peer) || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
-  if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n))) return 0;  // the sharded engine is the split one
+  if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n, c->sharded))) return 0;  // the sharded engine is the split one
   const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
   if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
   if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
@@ -1407,20 +1443,13 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
   return c->use_fed ? 1 : 0;
 }
 
-// 1 s of s_memrealtime (100 MHz) without a command: the engine exits (KB_FED_IDLE_MS: tests shorten it)
-static uint64_t fed_idle_ticks() {
-  const char* e = getenv("KB_FED_IDLE_MS");
-  const long ms = e ? atol(e) : 0;
-  return ms > 0 ? (uint64_t)ms * 100000ull : 100000000ull;
-}
-
 int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return 0;
-  if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n) &&
+  if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) &&
                       max_job_tasks <= (uint32_t)kFedSplitMaxTasks))
     return 0;
   const int ns = fed_nsel(c->N.n);
-  return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
+  return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
 }
 
 int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
@@ -1438,6 +1467,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     for (int s = 0; s < kJobSlots; ++s) c->fed_count[s] = 0;
   }
   HIP_OK(c, hipMemsetAsync(c->fed_exit, 0, sizeof(int32_t), c->stream));
+  c->fed_split_now = false;
   FedSlotPtrs sp;
   for (int s = 0; s < kJobSlots; ++s) {
     sp.keys[s] = c->sel_keys[s];
@@ -1457,11 +1487,12 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     c->timing_now = tn;
   }
   void* xchg = nullptr;
-  if (c->use_fed_split && fed_split_ok(c->N.n) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
+  if (c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
     if (!c->fed_xchg) HIP_OK(c, hipMalloc(&c->fed_xchg, fed_xchg_bytes()));
     HIP_OK(c, hipMemsetAsync(c->fed_xchg, 0, fed_xchg_bytes(), c->stream));  // job numbers restart per cycle
     xchg = c->fed_xchg;
     c->stats.fed_split++;
+    c->fed_split_now = true;
   }
   c->stats.fed_cycles++;
   ShardPeers SP{};
@@ -1470,12 +1501,14 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     for (int w = 0; w < c->shard.world; ++w) SP.inbox[w] = (uint64_t*)c->peer_inbox[w];
     SP.rank = c->shard.rank;
     SP.world = c->shard.world;
+    if (((c->shard_epoch + 1) & ((1u << kShardEpochBits) - 1)) == 0)
+      if (int rc = shard_inbox_rezero(c)) return rc;
     SP.epoch = ++c->shard_epoch;
-    SP.self_inbox = getenv("KB_SHARD_SELF_INBOX") != nullptr;
+    SP.self_inbox = c->shard_self_inbox ? 1 : 0;
     c->stats.fed_sharded++;
   }
   // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
-  const uint64_t idle = c->sharded ? 10 * fed_idle_ticks() : fed_idle_ticks();
+  const uint64_t idle = c->sharded ? 10 * c->fed_idle : c->fed_idle;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
                                           c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP));
   HIP_OK(c, hipGetLastError());
@@ -1516,7 +1549,7 @@ int kb_fed_end(kb_ctx* c) {
   const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit
   if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
   if (c->timing) c->ev_collect(true);
-  if (getenv("KB_FED_DIAG") && c->fed_xchg && c->stats.fed_split) {  // KB_DIAG builds: the selector's phases
+  if (c->fed_diag && c->fed_xchg && c->stats.fed_split) {  // KB_DIAG builds: the selector's phases
     uint64_t d[16] = {};
     if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - sizeof(d), sizeof(d), hipMemcpyDeviceToHost) ==
         hipSuccess && d[6]) {
@@ -1525,6 +1558,16 @@ int kb_fed_end(kb_ctx* c) {
       fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_set_exclude=%.0f "
               "wait_done_patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
               (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6], (double)d[5] / d[6]);
+    }
+  }
+  if (c->fed_xchg && c->fed_split_now) {  // the placer's counters (FedXchg::sdiag[12..15])
+    uint64_t d[4] = {};
+    if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - 4 * sizeof(uint64_t), sizeof(d),
+                  hipMemcpyDeviceToHost) == hipSuccess) {
+      c->stats.shard_wait_ticks += d[0];
+      c->stats.shard_xchg += d[1];
+      c->stats.fed_clock_ticks += d[2];
+      c->stats.fed_real_ticks += d[3];
     }
   }
   // an idle exit after every job was served (a host stall before this call) loses nothing
@@ -1707,10 +1750,11 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
     }
     c->ev_begin(&ea);
     if constexpr (sizeof(SCORE) == 8)
-      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain, c->stream);
+      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain, c->cus,
+                  c->eval_spb, c->stream);
     else
       launch_eval32(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain,
-                    c->stream);
+                    c->cus, c->eval_spb, c->stream);
     c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
     if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
     if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))

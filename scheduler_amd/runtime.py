@@ -89,7 +89,9 @@ def shard_range(n_total: int, rank: int, world: int):
 
 
 class kb_opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("timing_every", C.c_uint32)]
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("timing_every", C.c_uint32), ("fed_idle_ms", C.c_int32),
+                ("eval_spb", C.c_int32), ("test_stall_ms", C.c_int32), ("test_stall_job", C.c_int64),
+                ("shard_epoch0", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class kb_job_req(C.Structure):
@@ -123,13 +125,20 @@ class kb_stats(C.Structure):
                 ("job_calls", C.c_uint64), ("device_ms", C.c_double), ("diag", C.c_uint64 * 8),
                 ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64),
                 ("cap1_runs", C.c_uint64), ("cls_runs", C.c_uint64),
-                ("fed_sharded", C.c_uint64)]
+                ("fed_sharded", C.c_uint64), ("shard_rezero", C.c_uint64), ("shard_xchg", C.c_uint64),
+                ("shard_wait_ticks", C.c_uint64), ("fed_clock_ticks", C.c_uint64), ("fed_real_ticks", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
 KB_OPT_NO_TRAJECTORY = 2
 KB_OPT_NO_SELECT = 4
 KB_OPT_ENGINE = 8
+# path selection / measurement switches (kb_opts.flags, include/kbgpu.h KB_OPT_*): the default is the production
+# path; tests and the profiler name the others through Context(options=...)
+OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6, "no_aff_reg": 1 << 7,
+                "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
+                "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14}
+OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
            "shard_propose_kernel", "shard_exchange", "shard_commit_kernel", "fed_engine_kernel", "cls_place_kernel")
@@ -141,7 +150,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 12  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 13  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -203,15 +212,46 @@ def _ptr(a):
     return a.ctypes.data_as(P) if a is not None and a.size else None
 
 
-class Context:
-    """One device-resident session snapshot (kb_ctx)."""
+def make_opts(device: int = 0, timing: bool = False, path: str = "select", timing_every: int = 1,
+              options: dict | None = None) -> kb_opts:
+    """kb_opts for kb_create. `options`: names of OPTION_FLAGS (true: set) and OPTION_VALUES (ints); an unknown
+    name raises (a misspelt switch must not silently leave the production path on)."""
+    options = dict(options or {})
+    flags = (KB_OPT_TIMING if timing else 0) | PATHS[path]
+    vals = {"fed_idle_ms": 0, "eval_spb": 0, "test_stall_job": -1, "test_stall_ms": 0, "shard_epoch0": 0}
+    for k, v in options.items():
+        if k in OPTION_FLAGS:
+            flags |= OPTION_FLAGS[k] if v else 0
+        elif k in vals:
+            vals[k] = int(v)
+        else:
+            raise KbError(KB_E_INVALID, f"unknown context option {k!r}")
+    return kb_opts(device, flags, timing_every, vals["fed_idle_ms"], vals["eval_spb"], vals["test_stall_ms"],
+                   vals["test_stall_job"], vals["shard_epoch0"], 0)
 
-    def __init__(self, device: int = 0, timing: bool = False, path: str = "select", timing_every: int = 1):
+
+def parse_options(text: str | None) -> dict:
+    """`name,name=value,...` (bench.py / scripts --opt) -> a Context options dict."""
+    out = {}
+    for part in (text or "").split(","):
+        part = part.strip()
+        if not part or part == "none":
+            continue
+        k, _, v = part.partition("=")
+        out[k.strip()] = int(v) if v else True
+    return out
+
+
+class Context:
+    """One device-resident session snapshot (kb_ctx). `options`: make_opts's switches (tests, profiling)."""
+
+    def __init__(self, device: int = 0, timing: bool = False, path: str = "select", timing_every: int = 1,
+                 options: dict | None = None):
         self.lib = load_library()
         self._keep = []
         self.overlay_reason = {}
         self.overlay_fail = {}
-        opts = kb_opts(device, (KB_OPT_TIMING if timing else 0) | PATHS[path], timing_every)
+        opts = make_opts(device, timing, path, timing_every, options)
         self.ctx = self.lib.kb_create(C.byref(opts))
         if not self.ctx:
             raise KbError(KB_E_HIP, "kb_create failed")
@@ -351,7 +391,9 @@ class Context:
                 "job_calls": st.job_calls, "device_ms": st.device_ms, "diag": list(st.diag),
                 "fed_abandon": st.fed_abandon, "fed_cycles": st.fed_cycles, "fed_split": st.fed_split,
                 "cap1_runs": st.cap1_runs, "cls_runs": st.cls_runs,
-                "fed_sharded": st.fed_sharded}
+                "fed_sharded": st.fed_sharded, "shard_rezero": st.shard_rezero, "shard_xchg": st.shard_xchg,
+                "shard_wait_ticks": st.shard_wait_ticks, "fed_clock_ticks": st.fed_clock_ticks,
+                "fed_real_ticks": st.fed_real_ticks}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))
@@ -615,11 +657,12 @@ def host_reason_strings(snap: E.Snapshot, out: dict, job: int, task: int) -> dic
     return hist
 
 
-def allocate(cluster, device: int = 0, path: str = "select", stats_out: dict | None = None) -> dict:
+def allocate(cluster, device: int = 0, path: str = "select", stats_out: dict | None = None,
+             options: dict | None = None) -> dict:
     """One allocate cycle of `cluster` on the GPU; returns binds / events / fit errors like the oracle
-    (stats_out: filled with the context's kb_get_stats counters)."""
+    (stats_out: filled with the context's kb_get_stats counters; options: Context's)."""
     snap = E.Snapshot(cluster)
-    ctx = Context(device, path=path)
+    ctx = Context(device, path=path, options=options)
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)
@@ -630,11 +673,11 @@ def allocate(cluster, device: int = 0, path: str = "select", stats_out: dict | N
         ctx.close()
 
 
-def allocate_backfill(cluster, device: int = 0, path: str = "select") -> dict:
+def allocate_backfill(cluster, device: int = 0, path: str = "select", options: dict | None = None) -> dict:
     """The default action list, allocate then backfill (util.go:32), on the GPU. Returns what allocate() does
     plus "backfill_fit_errors" in the oracle's format."""
     snap = E.Snapshot(cluster)
-    ctx = Context(device, path=path)
+    ctx = Context(device, path=path, options=options)
     try:
         ctx.upload(snap)
         out = ctx.backfill(snap, ctx.allocate(snap))

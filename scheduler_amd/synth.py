@@ -11,6 +11,8 @@ same shapes. There is no network: all data is synthetic.
 """
 from __future__ import annotations
 
+import dataclasses
+
 import numpy as np
 
 from . import model as M
@@ -19,28 +21,61 @@ GI = 1024 ** 3
 SEED = 20250217
 
 
-def _queue_pg(cluster, n_jobs, min_member, queue="default", prefix="job", ns="ns"):
-    cluster.queues.append(M.Queue(name=queue, weight=1))
+class Parts:
+    """A generated cluster before its pods exist: nodes, pod groups, queues and pod blocks. A block is (template pod,
+    pod names, node indices or None): the pods of one job share everything but their name / uid (ns-name) and node,
+    so the cluster (per-pod objects, expand()) and its columns (columns(): numpy per pod, objects per node and per
+    job) come from the same draws."""
+
+    def __init__(self):
+        self.nodes, self.pod_groups, self.queues, self.blocks = [], [], [], []
+
+    def cluster(self) -> M.Cluster:
+        cl = M.Cluster(nodes=self.nodes, pod_groups=self.pod_groups, queues=self.queues)
+        for tp, names, where in self.blocks:
+            for i, nm in enumerate(names):
+                cl.pods.append(dataclasses.replace(
+                    tp, name=nm, uid=f"{tp.ns}-{nm}", node="" if where is None else self.nodes[int(where[i])].name,
+                    labels=dict(tp.labels), containers=[M.Container(req=dict(c.req)) for c in tp.containers],
+                    tolerations=[dict(x) for x in tp.tolerations], node_selector=dict(tp.node_selector)))
+        return cl
+
+    def columns(self):
+        from . import columns as CL
+        blocks = [(tp, [f"{tp.ns}-{nm}" for nm in names], where) for tp, names, where in self.blocks]
+        return CL.columns_of_blocks(self.nodes, blocks, self.pod_groups, self.queues, M.Cluster().tiers)
+
+
+def _block(parts, ns, names, group, req, node_ix=None, **kw):
+    tp = M.Pod(ns=ns, name=names[0], uid=f"{ns}-{names[0]}", group=group, containers=[M.Container(req=dict(req))],
+               node="" if node_ix is None else parts.nodes[int(node_ix[0])].name, **kw)
+    parts.blocks.append((tp, names, node_ix))
+
+
+def _queue_pg_parts(parts, n_jobs, min_member, queue="default", prefix="job", ns="ns"):
+    parts.queues.append(M.Queue(name=queue, weight=1))
     for j in range(n_jobs):
-        cluster.pod_groups.append(M.PodGroup(ns=ns, name=f"{prefix}{j:05d}", queue=queue, min_member=min_member))
+        parts.pod_groups.append(M.PodGroup(ns=ns, name=f"{prefix}{j:05d}", queue=queue, min_member=min_member))
 
 
-def c1(n_nodes=1000, n_jobs=100, tasks_per_job=50, seed=SEED) -> M.Cluster:
+def c1_parts(n_nodes=1000, n_jobs=100, tasks_per_job=50, seed=SEED) -> Parts:
     """C1: 1k nodes {32 cores, 128Gi, 110 pods, hostname/zone/rack labels}; jobs of 50 identical tasks."""
     rng = np.random.default_rng(seed)
-    cl = M.Cluster()
+    pt = Parts()
     for i in range(n_nodes):
-        cl.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: 32000, M.MEMORY: 128 * GI, M.PODS: 110},
+        pt.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: 32000, M.MEMORY: 128 * GI, M.PODS: 110},
                                labels={"kubernetes.io/hostname": f"node-{i:05d}", "zone": f"z{i % 10}",
                                        "rack": f"r{i % 100}"}))
-    _queue_pg(cl, n_jobs, tasks_per_job)
+    _queue_pg_parts(pt, n_jobs, tasks_per_job)
     cpus, mems = [500, 1000, 2000], [1 * GI, 2 * GI, 4 * GI]
     for j in range(n_jobs):
         req = {M.CPU: int(rng.choice(cpus)), M.MEMORY: int(rng.choice(mems))}
-        for t in range(tasks_per_job):
-            cl.pods.append(M.Pod(ns="ns", name=f"job{j:05d}-{t:04d}", uid=f"ns-job{j:05d}-{t:04d}",
-                                 group=f"job{j:05d}", containers=[M.Container(req=dict(req))]))
-    return cl
+        _block(pt, "ns", [f"job{j:05d}-{t:04d}" for t in range(tasks_per_job)], f"job{j:05d}", req)
+    return pt
+
+
+def c1(n_nodes=1000, n_jobs=100, tasks_per_job=50, seed=SEED) -> M.Cluster:
+    return c1_parts(n_nodes, n_jobs, tasks_per_job, seed).cluster()
 
 
 def c2(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, fill=None) -> M.Cluster:
@@ -54,25 +89,23 @@ def c2(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, fill=None) -> M
     if fill is not None:
         need = float((cpus * tasks_per_job).sum())
         cpu_cap = max(4000, int(need / fill / n_nodes) // 1000 * 1000)
-    cl = M.Cluster()
+    pt = Parts()
     for i in range(n_nodes):
-        cl.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: cpu_cap, M.MEMORY: mem_cap, M.PODS: 110}))
-    _queue_pg(cl, n_jobs, tasks_per_job)
+        pt.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: cpu_cap, M.MEMORY: mem_cap, M.PODS: 110}))
+    _queue_pg_parts(pt, n_jobs, tasks_per_job)
     for j in range(n_jobs):
-        req = {M.CPU: int(cpus[j]), M.MEMORY: int(mems[j])}
-        for t in range(tasks_per_job):
-            cl.pods.append(M.Pod(ns="ns", name=f"job{j:05d}-{t:04d}", uid=f"ns-job{j:05d}-{t:04d}",
-                                 group=f"job{j:05d}", containers=[M.Container(req=dict(req))]))
-    return cl
+        _block(pt, "ns", [f"job{j:05d}-{t:04d}" for t in range(tasks_per_job)], f"job{j:05d}",
+               {M.CPU: int(cpus[j]), M.MEMORY: int(mems[j])})
+    return pt.cluster()
 
 
-def c3(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_racks=400) -> M.Cluster:
+def c3_parts(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_racks=400) -> Parts:
     """C3: 4 node classes; 25% GPU nodes (nvidia.com/gpu=8, taint gpu=true:NoSchedule); 5% maint:NoExecute.
     Jobs: 20% request GPUs and tolerate gpu; 30% required zone affinity; 30% preferred terms; 10% nodeSelector."""
     rng = np.random.default_rng(seed)
     classes = [(16000, 64 * GI, "small"), (32000, 128 * GI, "medium"), (64000, 256 * GI, "large"),
                (96000, 512 * GI, "xlarge")]
-    cl = M.Cluster()
+    pt = Parts()
     for i in range(n_nodes):
         cpu, mem, typ = classes[int(rng.integers(0, 4))]
         alloc = {M.CPU: cpu, M.MEMORY: mem, M.PODS: 110}
@@ -83,10 +116,10 @@ def c3(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_r
         if rng.random() < 0.05:
             taints.append({"key": "maint", "value": "", "effect": "NoExecute"})
         zone = f"zone-{int(rng.integers(0, n_zones)):02d}"
-        cl.nodes.append(M.Node(name=f"node-{i:05d}", alloc=alloc, taints=taints,
+        pt.nodes.append(M.Node(name=f"node-{i:05d}", alloc=alloc, taints=taints,
                                labels={"zone": zone, "rack": f"rack-{int(rng.integers(0, n_racks)):03d}",
                                        "node-type": typ, "kubernetes.io/hostname": f"node-{i:05d}"}))
-    _queue_pg(cl, n_jobs, tasks_per_job)
+    _queue_pg_parts(pt, n_jobs, tasks_per_job)
     for j in range(n_jobs):
         req = {M.CPU: int(rng.integers(1, 17)) * 250, M.MEMORY: int(rng.integers(1, 17)) * (GI // 2)}
         tol, sel, aff = [], {}, None
@@ -108,16 +141,17 @@ def c3(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_r
             aff = {"nodeAffinity": {"preferred": prefs}}
         elif r2 < 0.7:
             sel = {"node-type": classes[int(rng.integers(0, 4))][2]}
-        for t in range(tasks_per_job):
-            cl.pods.append(M.Pod(ns="ns", name=f"job{j:05d}-{t:04d}", uid=f"ns-job{j:05d}-{t:04d}",
-                                 group=f"job{j:05d}", containers=[M.Container(req=dict(req))],
-                                 tolerations=[dict(x) for x in tol], node_selector=dict(sel),
-                                 affinity=None if aff is None else aff))
-    return cl
+        _block(pt, "ns", [f"job{j:05d}-{t:04d}" for t in range(tasks_per_job)], f"job{j:05d}", req,
+               tolerations=[dict(x) for x in tol], node_selector=dict(sel), affinity=aff)
+    return pt
 
 
-def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_racks=100, n_pre=None,
-       pre_job_size=100) -> M.Cluster:
+def c3(n_nodes=20000, n_jobs=2000, tasks_per_job=100, seed=SEED, n_zones=20, n_racks=400) -> M.Cluster:
+    return c3_parts(n_nodes, n_jobs, tasks_per_job, seed, n_zones, n_racks).cluster()
+
+
+def c4_parts(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_racks=100, n_pre=None,
+             pre_job_size=100) -> Parts:
     """C4: nodes {64 cores, 256Gi, 110 pods} in n_zones zones x n_racks racks (contiguous), plus n_pre
     running pods (default n_nodes) in running gang jobs labelled job=<name>, app=svc|web. Services (app=svc)
     run only in the first 30% of the zones; the first service also carries required anti-affinity
@@ -127,22 +161,22 @@ def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_r
     10% of the jobs are noisy=true."""
     rng = np.random.default_rng(seed)
     n_pre = n_nodes if n_pre is None else n_pre
-    cl = M.Cluster()
+    pt = Parts()
     racks_per_zone = max(1, n_racks // n_zones)
     for i in range(n_nodes):
         rack = i * n_racks // n_nodes
-        cl.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: 64000, M.MEMORY: 256 * GI, M.PODS: 110},
+        pt.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: 64000, M.MEMORY: 256 * GI, M.PODS: 110},
                                labels={"kubernetes.io/hostname": f"node-{i:05d}",
                                        "zone": f"z{min(n_zones - 1, rack // racks_per_zone)}",
                                        "rack": f"r{rack}"}))
-    cl.queues.append(M.Queue(name="default", weight=1))
+    pt.queues.append(M.Queue(name="default", weight=1))
     # running jobs (lister pods)
     n_pre_jobs = max(1, n_pre // pre_job_size)
     svc_nodes = max(1, int(n_nodes * 0.3))
     for j in range(n_pre_jobs):
         name = f"pre{j:04d}"
         svc = j % 5 == 0
-        cl.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=pre_job_size,
+        pt.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=pre_job_size,
                                         phase="Running"))
         aff = None
         if j == 0:
@@ -150,17 +184,13 @@ def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_r
             aff = {"podAntiAffinity": {
                 "required": [dict(noisy, topologyKey="kubernetes.io/hostname")],
                 "preferred": [{"weight": 10, "podAffinityTerm": dict(noisy, topologyKey="zone")}]}}
-        for t in range(pre_job_size):
-            node = int(rng.integers(0, svc_nodes if svc else n_nodes))
-            cl.pods.append(M.Pod(ns="ns", name=f"{name}-{t:04d}", uid=f"ns-{name}-{t:04d}", group=name,
-                                 node=f"node-{node:05d}", phase="Running",
-                                 labels={"job": name, "app": "svc" if svc else "web"},
-                                 containers=[M.Container(req={M.CPU: 1000, M.MEMORY: 2 * GI})],
-                                 affinity=aff))
+        where = np.array([int(rng.integers(0, svc_nodes if svc else n_nodes)) for _ in range(pre_job_size)], np.int64)
+        _block(pt, "ns", [f"{name}-{t:04d}" for t in range(pre_job_size)], name, {M.CPU: 1000, M.MEMORY: 2 * GI},
+               node_ix=where, phase="Running", labels={"job": name, "app": "svc" if svc else "web"}, affinity=aff)
     # pending jobs
     for j in range(n_jobs):
         name = f"job{j:05d}"
-        cl.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=tasks_per_job))
+        pt.pod_groups.append(M.PodGroup(ns="ns", name=name, queue="default", min_member=tasks_per_job))
         req = {M.CPU: int(rng.integers(1, 9)) * 250, M.MEMORY: int(rng.integers(1, 9)) * (GI // 2)}
         labels = {"job": name}
         if rng.random() < 0.1:
@@ -175,14 +205,31 @@ def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_r
         elif kind < 0.8:
             aff = {"podAffinity": {"required": [{"labelSelector": {"matchLabels": {"app": "svc"}},
                                                  "topologyKey": "zone"}]}}
-        for t in range(tasks_per_job):
-            cl.pods.append(M.Pod(ns="ns", name=f"{name}-{t:04d}", uid=f"ns-{name}-{t:04d}", group=name,
-                                 labels=dict(labels), containers=[M.Container(req=dict(req))],
-                                 affinity=None if aff is None else aff))
-    return cl
+        _block(pt, "ns", [f"{name}-{t:04d}" for t in range(tasks_per_job)], name, req, labels=dict(labels),
+               affinity=aff)
+    return pt
+
+
+def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_racks=100, n_pre=None,
+       pre_job_size=100) -> M.Cluster:
+    return c4_parts(n_nodes, n_jobs, tasks_per_job, seed, n_zones, n_racks, n_pre, pre_job_size).cluster()
+
+
+def c1_columns(**kw):
+    """synth.c1's columns straight from the generator's draws (no per-pod objects: columns.columns_of_blocks)."""
+    return c1_parts(**kw).columns()
+
+
+def c3_columns(**kw):
+    return c3_parts(**kw).columns()
+
+
+def c4_columns(**kw):
+    return c4_parts(**kw).columns()
 
 
 CONFIGS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4}
+COLUMNS = {"C1": c1_columns, "C3": c3_columns, "C4": c4_columns}
 
 
 class ArraySnapshot:

@@ -1,16 +1,17 @@
 #!/bin/bash
 # SQ counters of kb_eval's eval_kernel (scripts/eval_probe.py: 256 specs x 50k nodes), one pass per group
 # (rocprofv3 takes at most 8 SQ counters per pass): instructions per wave by kind and where the waves wait.
+# The profiled process is the measuring one (eval_probe.py starts no other program) at the launcher's own grid.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc_eval}
 mkdir -p $OUT
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/trace -o run --output-format csv -- python3 scripts/eval_probe.py 5 > $OUT/trace.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH -d $PWD/$OUT/p1 -o run --output-format csv -- python3 scripts/eval_probe.py 2 > $OUT/p1.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_TRANS_F32 -d $PWD/$OUT/p2 -o run --output-format csv -- python3 scripts/eval_probe.py 2 > $OUT/p2.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $PWD/$OUT/p3 -o run --output-format csv -- python3 scripts/eval_probe.py 2 > $OUT/p3.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $PWD/$OUT/p4 -o run --output-format csv -- python3 scripts/eval_probe.py 2 > $OUT/p4.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/trace -o run --output-format csv -- python3 scripts/eval_probe.py --batches 5 > $OUT/trace.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH -d $PWD/$OUT/p1 -o run --output-format csv -- python3 scripts/eval_probe.py --batches 1 --per 2 > $OUT/p1.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_TRANS_F32 -d $PWD/$OUT/p2 -o run --output-format csv -- python3 scripts/eval_probe.py --batches 1 --per 2 > $OUT/p2.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $PWD/$OUT/p3 -o run --output-format csv -- python3 scripts/eval_probe.py --batches 1 --per 2 > $OUT/p3.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $PWD/$OUT/p4 -o run --output-format csv -- python3 scripts/eval_probe.py --batches 1 --per 2 > $OUT/p4.log 2>&1 || exit $?
 python3 - "$OUT" <<'PY'
 import csv, glob, json, os, sys
 out = sys.argv[1]

@@ -1,6 +1,10 @@
 """Summarise rocprofv3 output for profiles/: kernel-trace stats and PMC (FETCH_SIZE / WRITE_SIZE) per launch.
 
-usage: python3 scripts/prof_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json>
+usage: python3 scripts/prof_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json> [pmc_cycles]
+
+pmc_cycles: the allocate cycles the PMC passes ran (bench.py --steps 1 --warmup 0 --no-timing: the step and the
+host-split cycle after it = 2); with it, each kernel's PMC dispatch count makes the cycle's measured traffic
+(bench.py pmc_cycle_traffic: bytes per dispatch x dispatches / cycles, summed over the cycle's kernels).
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced read (MI355X_MICROARCH.md, HBM section), so `hbm_read_bytes` doubles it; WRITE_SIZE is taken
@@ -49,14 +53,16 @@ def counters(d, counter):
 
 def main():
     trace, fetch, write, out = sys.argv[1:5]
+    cycles = int(sys.argv[5]) if len(sys.argv) > 5 else None
     ks = kernel_stats(trace)
     fs = counters(fetch, "FETCH_SIZE")
     ws = counters(write, "WRITE_SIZE")
-    res = {"kernels": {}}
+    res = {"kernels": {}, **({"pmc_cycles": cycles} if cycles else {})}
     for k in sorted(set(ks) | set(fs) | set(ws)):
         e = dict(ks.get(k, {}))
         if k in fs:
             e["fetch_size_kib_per_launch"] = round(fs[k]["avg_kib"], 2)
+            e["pmc_dispatches"] = fs[k]["dispatches"]
             e["hbm_read_bytes_per_launch"] = round(2 * fs[k]["avg_kib"] * 1024, 1)
         if k in ws:
             e["write_size_kib_per_launch"] = round(ws[k]["avg_kib"], 2)

@@ -4,12 +4,11 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-export KB_BENCH_SAME_GPU=1
-# ranks sharing the card: plain engine launches (cooperative launches from several processes take turns on it)
-export KB_FED_PLAIN_LAUNCH=1
+# --same-gpu: every rank on GPU 0, plain engine launches (cooperative launches from several processes take turns on
+# the card)
 run() {  # run <name> <args...>: `bench.py --gpus 2` spawns its two ranks itself (as the driver's N=2 line)
   local name=$1; shift
-  timeout -k 10 500 python bench.py --gpus 2 "$@" > gpurun_out/$name.log 2>&1
+  timeout -k 10 500 python bench.py --gpus 2 --same-gpu "$@" > gpurun_out/$name.log 2>&1
   local rc=$?; echo "=== $name rc=$rc"; grep '^{' gpurun_out/$name.log | head -c 1500; echo
   return $rc
 }

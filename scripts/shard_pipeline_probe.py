@@ -3,7 +3,8 @@
           inboxes and merges on the device, one launch per cycle plus one sweep per job;
   rccl -- the pipelined launch path (sweep, proposal, ncclAllGather, merge + commit per job);
   none -- the unsharded fed engine on the same box, for comparison.
-Usage: python3 scripts/shard_pipeline_probe.py [peer|rccl ...]   (KB_NO_PIPELINE=1: the serial driver)"""
+Usage: python3 scripts/shard_pipeline_probe.py [--opt no_pipeline,...] [peer|rccl ...]   (no_pipeline: the serial
+driver)"""
 import json
 import os
 import sys
@@ -13,8 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scheduler_amd import runtime, synth  # noqa: E402
 
 
-def probe(kind, snap):
-    ctx = runtime.Context(0, timing=True)
+def probe(kind, snap, opts):
+    ctx = runtime.Context(0, timing=True, options=opts)
     if kind == "peer":
         ctx.set_shard(0, 1, snap.n_nodes, allgather=lambda b: b, peer=True)
     elif kind == "rccl":
@@ -32,7 +33,7 @@ def probe(kind, snap):
     k = runtime.KERNELS
     per = {k[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 2) for i in range(len(k)) if st["launches"][i]}
     jobs = st["job_calls"] / 3
-    print(json.dumps({"exchange": kind, "pipeline": os.environ.get("KB_NO_PIPELINE") is None,
+    print(json.dumps({"exchange": kind, "pipeline": not opts.get("no_pipeline"),
                       "cycle_ms": round(min(ts) * 1e3, 2), "us_per_job": round(min(ts) * 1e6 / jobs, 2),
                       "pods_per_s": round(int(out["n_events"]) / min(ts), 1), "sharded_engine_cycles":
                       st["fed_sharded"], "us_per_launch": per}), flush=True)
@@ -41,8 +42,12 @@ def probe(kind, snap):
 
 def main():
     snap = synth.c2_snapshot(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=synth.SEED)
-    for kind in sys.argv[1:] or ["none", "peer", "rccl"]:
-        probe(kind, snap)
+    args = sys.argv[1:]
+    opts = {}
+    if args[:1] == ["--opt"]:
+        opts, args = runtime.parse_options(args[1]), args[2:]
+    for kind in args or ["none", "peer", "rccl"]:
+        probe(kind, snap, opts)
 
 
 if __name__ == "__main__":

@@ -85,3 +85,30 @@ def test_columnar_snapshot_allocates_like_the_exporter(name, cluster):
     for f in ("task_node", "task_status", "job_fail_task", "job_reason_hist"):
         assert np.array_equal(a[f], b[f]), f
     assert np.array_equal(a["event_task"][:k], b["event_task"][:k])
+
+
+GEN_COLUMNS = [
+    ("C1", dict(n_nodes=150, n_jobs=12, tasks_per_job=9, seed=5)),
+    ("C3", dict(n_nodes=400, n_jobs=30, tasks_per_job=12, seed=9, n_zones=5, n_racks=40)),
+    ("C4", dict(n_nodes=300, n_jobs=30, tasks_per_job=10, n_zones=5, n_racks=25, n_pre=300, pre_job_size=20, seed=23)),
+]
+
+
+@pytest.mark.parametrize("name,kw", GEN_COLUMNS, ids=[g[0] for g in GEN_COLUMNS])
+def test_generator_columns_equal_the_walk(name, kw):
+    """synth.c1/c3/c4_columns build the bench configurations' columns from the generator's draws, per node and per
+    job (bench.py's session open for C1 / C3 / C4: no per-pod walk): the snapshot equals the exporter's on the same
+    cluster, array by array."""
+    gen = {"C1": synth.c1, "C3": synth.c3, "C4": synth.c4}[name]
+    ref = E.Snapshot(gen(**kw))
+    got = COL.build(synth.COLUMNS[name](**kw))
+    assert_same_snapshot(ref, got)
+
+
+def test_isum_exact_past_float53():
+    """Per-node sums of int64 requests stay exact where float64 bincount would round."""
+    idx = np.array([0, 0, 1, 0])
+    v = np.array([(1 << 53) + 1, 2, 5, -3], np.int64)
+    assert COL.isum(idx, v, 2).tolist() == [(1 << 53), 5]
+    assert COL.isum(np.array([1, 1]), np.array([3, 4], np.int64), 3).tolist() == [0, 7, 0]
+    assert COL.isum(np.zeros(0, np.int64), None, 2).tolist() == [0, 0]

@@ -27,9 +27,8 @@ pytestmark = pytest.mark.gpu
 def _child(q, shared):
     """One fresh process: torch's HIP runtime first (as in bench.py's ranks), then the library's."""
     try:
-        if shared:
-            os.environ["KB_FED_SHARED_QUEUES"] = "1"
-        os.environ["KB_FED_IDLE_MS"] = "300"  # a stall shows as an abandon within the test's time
+        # a stall shows as an abandon within the test's time; shared: the sweep stream without its own queue
+        options = {"fed_idle_ms": 300, "fed_shared_queues": shared}
         import torch
         import torch.distributed as dist
         with socket.socket() as sk:
@@ -50,7 +49,7 @@ def _child(q, shared):
         snap = E.Snapshot(cl)
         res, raw = [], []
         for extra in range(8):
-            ctx = runtime.Context(0)
+            ctx = runtime.Context(0, options=options)
             try:
                 for _ in range(extra):  # between the library's main stream and its sweep stream
                     s = ctypes.c_void_p()
@@ -91,7 +90,7 @@ def test_fed_engine_progress_beside_other_streams():
 
 def test_shared_queues_hazard_is_real():
     """The same process layout with the engine launched plainly and the sweep stream from the shared pool
-    (KB_FED_SHARED_QUEUES=1): the hazard is observable -- some layouts stall the engine into its idle exit --
+    (option fed_shared_queues): the hazard is observable -- some layouts stall the engine into its idle exit --
     and the cycle still ends with the oracle's placements on the launch path (correct, 300 ms slower)."""
     ref = pyoracle.allocate(synth.c2(n_nodes=3000, n_jobs=40, tasks_per_job=40, seed=51), workers=8)
     res = _run(shared=True)

@@ -129,8 +129,8 @@ def test_eval_plain_matches_oracle():
 @pytest.mark.parametrize("name,cfg", [("plain-edge", None), ("C2-2000", None), ("C1-parity", None),
                                       ("plain-edge", {"nodeorder_enabled": 0}),
                                       ("plain-edge", {"predicates_enabled": 0})])
-def test_eval_plain_equals_general(name, cfg, monkeypatch):
-    """The row-only kernel returns the general eval_kernel's arrays (KB_NO_EVAL_PLAIN) on plain batches, also with
+def test_eval_plain_equals_general(name, cfg):
+    """The row-only kernel returns the general eval_kernel's arrays (option no_eval_plain) on plain batches, also with
     the nodeorder or predicates plugin off (the score table all 0; no post reasons)."""
     cl = {"plain-edge": plain_edge_cluster, "C2-2000": lambda: synth.c2(n_nodes=2000, n_jobs=64, tasks_per_job=1,
                                                                         seed=9),
@@ -141,10 +141,8 @@ def test_eval_plain_equals_general(name, cfg, monkeypatch):
     ids = [int(s) for s in np.nonzero(_plain_spec(snap))[0]]
     assert ids
     out = []
-    for env in (None, "1"):
-        if env:
-            monkeypatch.setenv("KB_NO_EVAL_PLAIN", env)
-        ctx = runtime.Context(0)
+    for general in (False, True):
+        ctx = runtime.Context(0, options={"no_eval_plain": general})
         try:
             ctx.upload(snap)
             out.append(ctx.eval(ids) + ctx.eval32(ids))
@@ -309,38 +307,33 @@ PIPE_CLUSTERS = CLUSTERS + [
 
 @pytest.mark.parametrize("mode", ["fed", "launch", "serial"])
 @pytest.mark.parametrize("name,cluster", PIPE_CLUSTERS, ids=[c[0] for c in PIPE_CLUSTERS])
-def test_driver_pipeline_parity(name, cluster, mode, monkeypatch):
+def test_driver_pipeline_parity(name, cluster, mode):
     """kb_allocate's driver issues job k+1 before job k's result is read, guarded on job k's predicted
     outcome (a failed guard turns job k+1 into no-ops and the driver re-issues the real next job), with
     job k+1's level-0 sweep overlapping job k. fed: one resident selection workgroup fed by the sweeps
     (cycles whose jobs are single selection runs); launch: a place kernel per job; serial: one
     kb_place_job round trip per job. All match the oracle."""
-    if mode == "launch":
-        monkeypatch.setenv("KB_NO_FED", "1")
-    elif mode == "serial":
-        monkeypatch.setenv("KB_NO_PIPELINE", "1")
+    opts = {"launch": {"no_fed": True}, "serial": {"no_pipeline": True}}.get(mode, {})
     ref = pyoracle.allocate(cluster)
-    got = runtime.allocate(cluster)
+    got = runtime.allocate(cluster, options=opts)
     _compare(ref, got)
 
 
-AFF_VARIANTS = {"default": {}, "aff-reg": {"KB_NO_CAP1": "1", "KB_NO_CLS": "1"},
-                "aff-global": {"KB_NO_CAP1": "1", "KB_NO_CLS": "1", "KB_NO_AFF_REG": "1"}}
+AFF_VARIANTS = {"default": {}, "aff-reg": {"no_cap1": True, "no_cls": True},
+                "aff-global": {"no_cap1": True, "no_cls": True, "no_aff_reg": True}}
 
 
 @pytest.mark.parametrize("variant", sorted(AFF_VARIANTS))
 @pytest.mark.parametrize("name,cluster", affinity_clusters(), ids=[c[0] for c in affinity_clusters()])
-def test_affinity_loop_variants(name, cluster, variant, monkeypatch):
+def test_affinity_loop_variants(name, cluster, variant):
     """Specs whose own commits move their inter-pod affinity inputs. default: cap-1 specs (required
     anti-affinity to their own pods over hostname) as selection runs and histogram-only specs on the class
     loop (cls_place_kernel), the rest on the register-resident loop; aff-reg: every such spec on the
     register-resident loop (aff_reg_kernel); aff-global: the global-memory loop (aff_place_kernel). All
     match the oracle."""
-    for k, v in AFF_VARIANTS[variant].items():
-        monkeypatch.setenv(k, v)
     ref = pyoracle.allocate(cluster)
     ctx_stats = {}
-    got = runtime.allocate(cluster, stats_out=ctx_stats)
+    got = runtime.allocate(cluster, stats_out=ctx_stats, options=AFF_VARIANTS[variant])
     _compare(ref, got)
     if name.startswith("self-aff") or name == "C4-parity":
         # the clusters built for them do reach the new paths (or, with them off, none of them)
@@ -348,17 +341,14 @@ def test_affinity_loop_variants(name, cluster, variant, monkeypatch):
         assert (ctx_stats["cap1_runs"] > 0) == on and (ctx_stats["cls_runs"] > 0) == on, ctx_stats
 
 
-def test_fed_engine_survives_a_host_stall(monkeypatch):
+def test_fed_engine_survives_a_host_stall():
     """The resident engine exits after its idle bound without a command. A host stall longer than that in
     the middle of a cycle (a GC pause, descheduling) must not fail the cycle: the job the host waits for, and
     the rest of the cycle, finish on the launch path with the oracle's placements."""
-    monkeypatch.setenv("KB_FED_IDLE_MS", "40")
-    monkeypatch.setenv("KB_TEST_STALL_JOB", "3")
-    monkeypatch.setenv("KB_TEST_STALL_MS", "400")
     cl = synth.c2(n_nodes=300, n_jobs=20, tasks_per_job=20, seed=9)
     ref = pyoracle.allocate(cl)
     snap = E.Snapshot(cl)
-    ctx = runtime.Context(0)
+    ctx = runtime.Context(0, options={"fed_idle_ms": 40, "test_stall_job": 3, "test_stall_ms": 400})
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)
@@ -382,16 +372,14 @@ SPLIT_CLUSTERS = [
 
 @pytest.mark.parametrize("split", [True, False], ids=["split", "one-workgroup"])
 @pytest.mark.parametrize("name,cluster", SPLIT_CLUSTERS, ids=[c[0] for c in SPLIT_CLUSTERS])
-def test_fed_split_engine_parity(name, cluster, split, monkeypatch):
+def test_fed_split_engine_parity(name, cluster, split):
     """The split fed engine (n > 2048, every job one segment): a second workgroup selects each job's
     candidate nodes one job ahead, leaving out the nodes the job before may commit to, which the placer
     re-keys and merges in. Same placements, statuses and FitErrors as the oracle, and as the one-workgroup
-    engine (KB_NO_FED_SPLIT)."""
-    if not split:
-        monkeypatch.setenv("KB_NO_FED_SPLIT", "1")
+    engine (option no_fed_split)."""
     ref = pyoracle.allocate(cluster)
     snap = E.Snapshot(cluster)
-    ctx = runtime.Context(0)
+    ctx = runtime.Context(0, options={"no_fed_split": not split})
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)

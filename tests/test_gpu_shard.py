@@ -21,6 +21,11 @@ pytestmark = pytest.mark.gpu
 NAMES = ["C1-parity", "C2-parity", "C2-fill0.9", "C3-parity", "C2-nogang", "edge-mixed"]
 
 
+# ranks sharing one GPU: plain engine launches (cooperative launches from several processes take turns on the card,
+# DESIGN.md §5; one process per GPU, as deployed, keeps the cooperative launch)
+SHARED_GPU = {"fed_plain_launch": True}
+
+
 def _clusters():
     return {name: cl for name, cl in parity_clusters() if name in NAMES}
 
@@ -63,7 +68,7 @@ def _rank_main(rank, world, port, q, peer=False):
     try:
         for name, cl in _cases().items():
             snap = E.Snapshot(cl)
-            ctx = runtime.Context(0)
+            ctx = runtime.Context(0, options=SHARED_GPU if peer else None)
             try:
                 ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
                 res[name] = _run(name, snap, ctx)
@@ -84,11 +89,9 @@ def _free_port():
 
 @pytest.mark.parametrize("exchange", ["host", "peer"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_one_gpu(world, exchange, monkeypatch):
+def test_sharded_equals_one_gpu(world, exchange):
     """Parity clusters (too small for the sharded engine: every job through the launch path) on 2 and 3 ranks.
     peer: kb_set_shard_peer contexts, whose non-engine cycles go one job at a time over the host-staged exchange."""
-    if exchange == "peer":
-        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")
     import torch.multiprocessing as mp
     ref = {}
     for name, cl in _cases().items():
@@ -306,7 +309,7 @@ def _c5_full_rank(rank, world, port, q, peer=False):
         return b"".join(bytes(o.tolist()) for o in outs)
     try:
         snap = synth.c2_snapshot(n_nodes=50000, n_jobs=10000, tasks_per_job=100, seed=synth.SEED)
-        ctx = runtime.Context(0)
+        ctx = runtime.Context(0, options=SHARED_GPU if peer else None)
         try:
             ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
             ctx.upload(snap)
@@ -328,7 +331,7 @@ def _c5_full_rank(rank, world, port, q, peer=False):
 
 
 @pytest.mark.parametrize("exchange", ["host", "peer"])
-def test_c5_full_eight_ranks_match_oracle_digest(exchange, monkeypatch):
+def test_c5_full_eight_ranks_match_oracle_digest(exchange):
     """BASELINE.json configs[4] at its stated size and split: 50k nodes x 1M pods, the node table sharded 8 ways
     (8 ranks sharing the GPU). host: one host-staged all-gather over gloo per run segment; peer: the node-sharded
     fed engine (kb_set_shard_peer), every job's proposals exchanged between the ranks' resident engines through
@@ -336,8 +339,6 @@ def test_c5_full_eight_ranks_match_oracle_digest(exchange, monkeypatch):
     placements, 7,373 s of oracle time)."""
     import json
     import torch.multiprocessing as mp
-    if exchange == "peer":  # ranks sharing one GPU: plain launches (cooperative ones from several processes
-        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")  # take turns on the card, DESIGN.md §5)
     golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     with open(os.path.join(golden, "digest-C5.json")) as f:
         meta = json.load(f)
@@ -389,7 +390,7 @@ def _aff_rank_main(rank, world, port, q, peer=False):
     try:
         for name, cl in _aff_cases().items():
             snap = E.Snapshot(cl)
-            ctx = runtime.Context(0)
+            ctx = runtime.Context(0, options=SHARED_GPU if peer else None)
             try:
                 ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=peer)
                 ctx.upload(snap)
@@ -405,7 +406,7 @@ def _aff_rank_main(rank, world, port, q, peer=False):
 
 
 @pytest.mark.parametrize("world,exchange", [(2, "host"), (3, "host"), (2, "peer")])
-def test_sharded_affinity_matches_oracle(world, exchange, monkeypatch):
+def test_sharded_affinity_matches_oracle(world, exchange):
     """Replicated count tables and histograms, one whole-cluster IPA min / max per run (or per task), every
     commit applied on every rank: the oracle's events, binds and FitErrors on every affinity cluster (C4 shapes,
     the edge clusters, the self-affinity clusters whose specs run one task per segment or as cap-1 runs)."""
@@ -415,8 +416,6 @@ def test_sharded_affinity_matches_oracle(world, exchange, monkeypatch):
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    if exchange == "peer":  # (ranks sharing the GPU: plain engine launches)
-        monkeypatch.setenv("KB_FED_PLAIN_LAUNCH", "1")
     procs = [ctxm.Process(target=_aff_rank_main, args=(r, world, port, q, exchange == "peer")) for r in range(world)]
     for p in procs:
         p.start()

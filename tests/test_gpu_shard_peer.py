@@ -18,8 +18,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _cases(world):
-    """Fed-eligible cycles (one <= 100-task run per job) with every rank's block over the split engine's 2048 nodes:
-    full gangs, half gangs whose jobs are popped again, a cycle that runs out of room (NO_FIT), BestEffort-free."""
+    """Fed-eligible cycles (one <= 100-task run per job): full gangs, half gangs whose jobs are popped again, a cycle
+    that runs out of room (NO_FIT), blocks of fewer nodes than one key group."""
     n = 2100 * world + 300
     half = synth.c2_snapshot(n_nodes=n, n_jobs=90, tasks_per_job=40, seed=23)
     half.s_job_min = np.full_like(half.s_job_min, 20)  # ready at half the job: popped again for the rest
@@ -27,6 +27,9 @@ def _cases(world):
         "c2-gang": synth.c2_snapshot(n_nodes=n, n_jobs=120, tasks_per_job=60, seed=21),
         "c2-nofit": synth.c2_snapshot(n_nodes=n, n_jobs=60, tasks_per_job=100, seed=22, fill=2.5),
         "c2-halfgang": half,
+        # every rank's block under one key group (2048 nodes): the sharded engine's two-group instance (8 ranks
+        # split C2's 10k nodes into 1,250-node blocks)
+        "c2-small": synth.c2_snapshot(n_nodes=1200 * world + 100, n_jobs=50, tasks_per_job=50, seed=24),
     }
 
 
@@ -43,8 +46,8 @@ def _reference(snap, cycles):
         ctx.close()
 
 
-def _sharded(snap, rank, world, allgather, cycles, barrier=None):
-    ctx = runtime.Context(0)
+def _sharded(snap, rank, world, allgather, cycles, barrier=None, options=None):
+    ctx = runtime.Context(0, options=options)
     try:
         ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
         ctx.upload(snap)
@@ -71,13 +74,13 @@ def test_peer_engine_one_rank():
         assert got == ref, name
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, cycles=2, options=None, names=None):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
     # ranks sharing one GPU: plain engine launches (cooperative launches from several processes take turns on the
     # card -- 10 ms per job here; one process per GPU, as deployed, keeps the cooperative launch)
-    os.environ["KB_FED_PLAIN_LAUNCH"] = "1"
+    options = dict(options or {}, fed_plain_launch=True)
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def allgather(b):
@@ -89,9 +92,11 @@ def _rank_main(rank, world, port, q):
     res = {}
     try:
         for name, snap in _cases(world).items():
+            if names is not None and name not in names:
+                continue
             print(f"rank {rank}/{world}: {name}", flush=True)
-            got, st = _sharded(snap, rank, world, allgather, 2, barrier=dist.barrier)
-            res[name] = (got, st["fed_sharded"], st["fed_abandon"])
+            got, st = _sharded(snap, rank, world, allgather, cycles, barrier=dist.barrier, options=options)
+            res[name] = (got, st["fed_sharded"], st["fed_abandon"], st["shard_rezero"])
         q.put((rank, res, None))
     except Exception as e:  # report, do not hang the parent
         q.put((rank, None, repr(e)))
@@ -128,6 +133,48 @@ def test_peer_engine_ranks_equal_one_gpu(world):
             p.join(timeout=60)
     for r in range(world):
         for name in ref:
-            out, n_sharded, n_abandon = got[r][name]
+            out, n_sharded, n_abandon, _ = got[r][name]
             assert n_sharded == 2 and n_abandon == 0, (world, r, name)
             assert out == ref[name], (world, r, name)
+
+
+EPOCH_WRAP = 1 << 12  # kShardEpochBits of the cycle epoch in an inbox word's tag (kbgpu_device.h)
+
+
+def test_peer_engine_one_rank_epoch_wrap():
+    """The inbox tags keep 12 bits of the cycle epoch, so every 4096 cycles the ranks re-zero their inboxes between
+    two host barriers (a word an earlier cycle left -- a no-fit histogram, a longer record -- must never read as
+    current). One rank started just below the wrap: four cycles across it, every one a NO_FIT cycle, equal to one
+    unsharded GPU, with exactly one re-zeroing."""
+    snap = _cases(1)["c2-nofit"]
+    ref = _reference(snap, 4)
+    got, st = _sharded(snap, 0, 1, lambda b: b, 4, options={"shard_epoch0": EPOCH_WRAP - 2})
+    assert st["fed_sharded"] == 4 and st["fed_abandon"] == 0 and st["shard_rezero"] == 1, st
+    assert got == ref
+
+
+def test_peer_engine_two_ranks_epoch_wrap():
+    """Two ranks across the epoch wrap (the re-zeroing's two barriers run through the all-gather callback)."""
+    import torch.multiprocessing as mp
+    world, cycles = 2, 4
+    ref = {name: _reference(snap, cycles) for name, snap in _cases(world).items() if name == "c2-nofit"}
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_rank_main, args=(r, world, port, q, cycles, {"shard_epoch0": EPOCH_WRAP - 2},
+                                                   ["c2-nofit"])) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, f"rank {rank}: {err}"
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        out, n_sharded, n_abandon, n_rezero = got[r]["c2-nofit"]
+        assert n_sharded == cycles and n_abandon == 0 and n_rezero == 1, (r, n_sharded, n_abandon, n_rezero)
+        assert out == ref["c2-nofit"], r
