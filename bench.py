@@ -614,8 +614,8 @@ DIAG_PHASES = {
                          "nofit_hist"],
     "fed_engine_kernel": ["key_load_patch", "node_select", "node_setup", "e_sequences", "winners_order",
                           "commit_publish_nofit", "wait_for_command"],
-    "cls_place_kernel": ["prologue_rest", "minmax_keys_argmax", "commit", "rescan_counts", "prologue_loads",
-                         "stop_flush", "hot_switches_x1000"],
+    "cls_place_kernel": ["prologue", "per_task_path", "phase_setup", "phase_rounds", "phase_picks",
+                         "phase_deep_keys_writeback", "counts_picks_1e6rounds_1e12deep"],
     "aff_place_kernel": ["prologue", "live_loads_minmax", "keys_argmax", "commit", "table_incr_fence", "stop_flush",
                          "nofit_hist"],
 }
@@ -625,7 +625,7 @@ def diag_summary(d, tasks, kernel):
     """Per-task shader cycles of each place-kernel phase (KB_DIAG builds) and the implied clock."""
     names = DIAG_PHASES.get(kernel, [f"phase{i}" for i in range(7)])
     clock_mhz = d[7] and (sum(d[:7]) / (d[7] / 100.0))
-    return {"cycles_per_task": {n: round(d[i] / max(1, tasks), 1) for i, n in enumerate(names)},
+    return {"cycles_per_task": {n: round(d[i] / max(1, tasks), 1) for i, n in enumerate(names)}, "totals": list(d),
             "fill_cycles_total": d[6],
             "clock_mhz": round(clock_mhz, 1) if clock_mhz else None}
 

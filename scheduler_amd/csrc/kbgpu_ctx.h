@@ -165,6 +165,7 @@ struct kb_ctx {
   uint64_t fed_idle = 100000000ull;  // the engine's idle exit in s_memrealtime ticks (100 MHz): 1 s
   int eval_spb = 0;            // kb_opts.eval_spb (0: from cus)
   int cus = 256;               // compute units of the context's device
+  int eval_bpc32 = 2, eval_bpc64 = 2;  // eval_plain_kernel's resident blocks per CU (kb_eval32 / kb_eval instance)
   uint32_t fed_count[kbgpu::kJobSlots] = {};
   int fed_r = 0;
   uint64_t fed_tasks = 0;  // tasks the engine placed or tried this session (timing pairs)

@@ -149,8 +149,9 @@ void launch_place_loop(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                        uint64_t* keys, const uint64_t* cmax, const uint64_t* stat, JobState* js, int first,
                        int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 // plain: every spec of the batch is plain (kb_ctx::spec_plain): the row-only kernel (eval_plain_kernel)
-// cus: the device's compute units (the plain kernel's grid is one resident round); spb > 0 overrides its specs
-// per block (measurement)
+// cus: the device's compute units | the plain kernel instance's resident blocks per CU << 16 (its grid is one
+// resident round); spb > 0 overrides its specs per block (measurement)
+int eval_plain_blocks_per_cu(bool i32);
 void launch_eval(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                  uint32_t* reasons, int64_t* scores, const int64_t* mm, bool plain, int cus, int spb, void* stream);
 void launch_eval32(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,

@@ -931,11 +931,17 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       fb |= (uint32_t)(!est & !po) << j;
       // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
       const SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
-      // uniform row bases: the stores take a scalar base and the lane's offset
+      // uniform row bases: the stores take a scalar base and the lane's offset; non-temporal (the output is
+      // streamed once, never read back by this kernel: no point keeping it in the caches)
       uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
       SCORE* srow = scores + (size_t)(j0 + j) * stride;
+#ifndef KB_EVAL_TEMPORAL
+      __builtin_nontemporal_store(rs, rrow + n);
+      __builtin_nontemporal_store(score, srow + n);
+#else  // (A/B builds: the plain stores)
       rrow[n] = rs;
       srow[n] = score;
+#endif
     }
     if (!C.nodeorder) fb = 0;
     while (fb) {  // the deferred Balanced fallbacks
@@ -4825,7 +4831,8 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // ---------------------------------------------------------------------------
 // 4 waves: the task loop's wave gets the whole VGPR file of its SIMD (1024 threads cap it at 128 and spill)
 constexpr int kClsThreads = 256;
-constexpr int kClsPM = 4;  // a class phase's members per lane (classes of at most 256 nodes)
+constexpr int kClsPM = 2;  // a class phase's members per lane (classes of at most 128 nodes)
+constexpr int kClsStaticLds = 6144;  // the kernel's static LDS (the phase's level queues, 4 KB) and slack
 static_assert(kClsMaxK <= 16 * 64 && kClsMaxK % kClsThreads == 0, "classes per lane: at most 16");
 
 // wave-uniform signed max / min on DPP (ordering-preserving bias to unsigned); |v| < 2^62
@@ -4844,7 +4851,7 @@ static size_t cls_lds_bytes(int n, int K, int pb_cap) {
 }
 
 bool cls_fits(int n, int K) {
-  return n > 0 && n < 65536 && K >= 1 && K <= kClsMaxK && cls_lds_bytes(n, K, 256) + 2048 <= (size_t)kLdsLimit;
+  return n > 0 && n < 65536 && K >= 1 && K <= kClsMaxK && cls_lds_bytes(n, K, 256) + kClsStaticLds <= (size_t)kLdsLimit;
 }
 
 // Chip-wide prologue of a class-loop run, grid (nodes, 1 + kClsL): level 0 -> the base key (allocate's
@@ -4888,6 +4895,23 @@ __device__ __forceinline__ uint64_t hk_at(uint64_t hk, int j) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// A node's row as HBM holds it mid-run (the run's deltas flushed as atomics; the caller fenced after them).
+__device__ __forceinline__ Row cls_row_now(const DevNodes& N, int w) {
+  Row r;
+  r.flags = N.flags[w];
+  r.max_pods = N.max_pods[w];
+  r.alloc_cpu = N.alloc_cpu[w];
+  r.alloc_mem = N.alloc_mem[w];
+  r.pod_count = __hip_atomic_load(&N.pod_count[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.idle_cpu = __hip_atomic_load(&N.idle_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.idle_mem = __hip_atomic_load(&N.idle_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.rel_cpu = __hip_atomic_load(&N.rel_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.rel_mem = __hip_atomic_load(&N.rel_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.nz_cpu = __hip_atomic_load(&N.nz_cpu[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.nz_mem = __hip_atomic_load(&N.nz_mem[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+
 // The class loop's deep-node path (rare: a node past the sweep's levels).
 __device__ __forceinline__ int cls_allocs_deep(const DevNodes& N, const kb_spec& sp, const int64_t* sci,
                                             const int64_t* scr, const Row& r, int n) {
@@ -4920,7 +4944,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
   uint32_t* pbs = cur + K;
   uint16_t* mem = (uint16_t*)(pbs + pb_cap);
   uint16_t* lv16 = mem + n;  // commits of this run per node
-  __shared__ uint32_t wsum[kClsThreads / 64];
+  __shared__ uint32_t s_phq[64 * kClsPM * kClsL];  // a class phase: member p's 32-bit keys of its next levels
   if ((!first && js->stopped) || guard_fails(g)) {
     if (threadIdx.x == 0) {
       if (first) js->n_placed = -1;  // a skipped speculative job (see sel_place_kernel)
@@ -5277,13 +5301,34 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         if (d >= 0) incR += e_w[e];
       }
       const int64_t lift = ipa ? (int64_t)ipa_score(cR, mn, mx) * c_wpa : 0;  // R's score term at the start
+      // A member may be picked here when its biased base score is at least thr: its key plus R's score beats S
+      // by the score alone (ties with S go to the per-task path), and its score plus R's is not the panic.
+      // The phase's keys are 32-bit: (biased score - thr + 1) << 8 | (255 - position in R's node-ordered list),
+      // 1 below thr (never picked), 0 infeasible -- exact order among the pickable keys.
+      int64_t thr = (int64_t)kScoreBias - lift;
+      if (s2 & kFeasible) {
+        const int64_t t2 = (int64_t)((s2 >> 24) & ((1ull << 39) - 1)) - lift + 1;
+        thr = t2 > thr ? t2 : thr;
+      }
+      bool enc_bad = false;
+      const auto enc = [&](uint64_t k, uint32_t tie) -> uint32_t {
+        if (!(k & kFeasible)) return 0u;
+        const int64_t d = (int64_t)((k >> 24) & ((1ull << 39) - 1)) - thr + 1;
+        if (d <= 0) return 1u;
+        if (d >= (1ll << 23)) {
+          enc_bad = true;
+          return 1u;
+        }
+        return ((uint32_t)d << 8) | tie;
+      };
       flush_hot();
       wave_sync_lds();
       hot = -1, hot_c = 0, p_node = -1;
-      // R's members, kClsPM per lane: node, current key, commits so far in this run, Allocates before full, and
-      // the sweep's keys after 1..kClsL commits (the levels still ahead; all loads in flight at once)
-      int nd[kClsPM], lev[kClsPM], am[kClsPM], cc[kClsPM];
-      uint64_t key[kClsPM], L[kClsPM][kClsL];
+      // R's members, kClsPM per lane (position p = j * 64 + lane): node, 32-bit key, commits so far in this run,
+      // Allocates before full (the sweep's), and the queue of its next keys from the sweep's levels
+      int nd[kClsPM], lev[kClsPM], am[kClsPM], cc[kClsPM], qn[kClsPM];
+      uint32_t k32[kClsPM];
+      uint64_t key0[kClsPM];
 #pragma unroll
       for (int j = 0; j < kClsPM; ++j) {
         const uint32_t ix = m0 + (uint32_t)(j * 64 + lane);
@@ -5292,120 +5337,188 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       }
 #pragma unroll
       for (int j = 0; j < kClsPM; ++j) {
-        key[j] = nd[j] >= 0 ? bk[nd[j]] : 0;
+        key0[j] = nd[j] >= 0 ? bk[nd[j]] : 0;
         lev[j] = nd[j] >= 0 ? (int)lv16[nd[j]] : kClsL;
       }
+      uint64_t Lk[kClsPM][kClsL];
 #pragma unroll
       for (int j = 0; j < kClsPM; ++j) {
         am[j] = nd[j] >= 0 ? amax[nd[j]] : 0;
 #pragma unroll
-        for (int l = 0; l < kClsL; ++l) L[j][l] = nd[j] >= 0 && l >= lev[j] ? lvl[(size_t)l * n + nd[j]] : 0;
+        for (int i = 0; i < kClsL; ++i)
+          Lk[j][i] = nd[j] >= 0 && lev[j] + i < kClsL ? lvl[(size_t)(lev[j] + i) * n + nd[j]] : 0;
       }
-      const uint64_t liftk = (uint64_t)lift << 24;
-      // a member past the sweep's levels: its next 64 keys across the lanes (lane l: the key after rel0 + l + 1
-      // commits on its row as HBM holds it -- the commits before the phase, flushed at its start), dh_A the
-      // Allocates before Idle stops fitting on that row, as the per-task path's deep keys
-      int dh = -1, dh_rel0 = 0, dh_A = 0;
-      uint64_t dhk = 0;
-      bool fenced = false;
-      int took = 0;
-      for (;;) {
-        uint64_t b = 0;
-#pragma unroll
-        for (int j = 0; j < kClsPM; ++j) b = umax64(b, key[j]);
-        b = wave_max_dpp(b);
-        if (!(b & kFeasible) || b + liftk <= s2) break;  // not provably R's: the per-task path decides
-        if ((int64_t)((b >> 24) & ((1ull << 39) - 1)) - kScoreBias + lift <= -1) break;  // (the panic: per task)
-        int jw = -1;
-#pragma unroll
-        for (int j = 0; j < kClsPM; ++j) jw = key[j] == b ? j : jw;
-        const int wl = (int)__builtin_ctzll(__ballot(jw >= 0));
-        int ml = 0, ma = 0, mc = 0;
-#pragma unroll
-        for (int j = 0; j < kClsPM; ++j)
-          if (j == jw) ml = lev[j], ma = am[j], mc = cc[j];
-        const int lw = __builtin_amdgcn_readlane(ml, wl);
-        const int wn = (int)(kIdxMask - (uint32_t)(b & kIdxMask));
-        int kind;
-        uint64_t dnk = 0;
-        if (lw < kClsL) {
-          kind = lw < __builtin_amdgcn_readlane(ma, wl) ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
-        } else {  // past the sweep's levels: keys from its row (rel: this phase's commits on it so far)
-          const int rel = __builtin_amdgcn_readlane(mc, wl);
-          if (wn != dh || rel - dh_rel0 >= 64) {
-            if (!fenced) {  // the row deltas flushed at the phase's start (atomics): visible to the loads below
-              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-              fenced = true;
-            }
-            Row r;
-            r.flags = N.flags[wn];
-            r.max_pods = N.max_pods[wn];
-            r.alloc_cpu = N.alloc_cpu[wn];
-            r.alloc_mem = N.alloc_mem[wn];
-            r.pod_count = __hip_atomic_load(&N.pod_count[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.idle_cpu = __hip_atomic_load(&N.idle_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.idle_mem = __hip_atomic_load(&N.idle_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.rel_cpu = __hip_atomic_load(&N.rel_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.rel_mem = __hip_atomic_load(&N.rel_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.nz_cpu = __hip_atomic_load(&N.nz_cpu[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r.nz_mem = __hip_atomic_load(&N.nz_mem[wn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            dh_A = cls_allocs_deep(N, sp, sci, scr, r, wn);
-            const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[wn], wn, rel + lane + 1, dh_A);
-            dhk = (k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)wn)) : k;
-            dh = wn, dh_rel0 = rel;
-          }
-          dnk = hk_at(dhk, rel - dh_rel0);
-          kind = rel < dh_A ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
-        }
-        if (lane == wl) {
-#pragma unroll
-          for (int j = 0; j < kClsPM; ++j)
-            if (j == jw) {
-              uint64_t nk = dnk;
-#pragma unroll
-              for (int l = 0; l < kClsL; ++l) nk = l == lev[j] ? L[j][l] : nk;
-              key[j] = nk;
-              ++lev[j];
-              ++cc[j];
-            }
-        }
-        if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
-        cR += incR;
-        mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
-        ++took;
-        ++placed;
-        ++pb_n;
-        if (kind == KB_PLACE_ALLOCATE) ++ready;
-        if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
-          stop = KB_STOP_READY;
-          stopped = 1;
-          break;
-        }
-        if (pb_n == pb_cap) {
-          wave_sync_lds();
-          for (int k = lane; k < pb_n; k += 64) {
-            const uint32_t e = pbs[k];
-            hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-            hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
-          }
-          wave_sync_lds();
-          pb_base += pb_n;
-          pb_n = 0;
-        }
-        if (t + took == t_count) break;
-      }
-      // the members' commits: keys, levels and row deltas back; R's best and count
-      uint64_t nb = 0;
 #pragma unroll
       for (int j = 0; j < kClsPM; ++j) {
-        nb = umax64(nb, key[j]);
+        const int pj = j * 64 + lane;
+        const uint32_t tie = 255u - (uint32_t)pj;
+        k32[j] = enc(key0[j], tie);
+        qn[j] = kClsL - lev[j];  // queue entries: entry i = the key after lev + i + 1 commits
+#pragma unroll
+        for (int i = 0; i < kClsL; ++i)
+          if (i < qn[j]) s_phq[pj * kClsL + i] = enc(Lk[j][i], tie);
+      }
+      wave_sync_lds();
+      // a member past the sweep's levels: its next 64 keys across the lanes (lane l: the key after rel0 + l + 1 of
+      // this phase's commits on its row as HBM holds it -- the commits before the phase, flushed at its start), as
+      // the per-task path's deep keys
+      int dh = -1, dh_rel0 = 0;
+      uint32_t dk32 = 0;
+      bool fenced = false;
+      int took = 0;
+      bool done = false;
+#ifdef KB_DIAG_AFF
+      uint64_t why = 4;  // the phase's end: 1 below the bound, 2 a deep key out of range, 3 a stop / the run's end
+      uint64_t n_rounds = 0, n_deep = 0;
+#endif
+      AFF_STAMP(2);
+      // Each round: one wave reduction finds the winner and the runner-up; the winner then takes picks as long as
+      // its next key stays above the runner-up's (a node keeps its score for several pods: LR / BRA move in steps),
+      // each pick scalar work on its queue, read once into a register across the lanes.
+      while (!done && !__ballot(enc_bad)) {
+        uint32_t m = k32[0];
+#pragma unroll
+        for (int j = 1; j < kClsPM; ++j) m = k32[j] > m ? k32[j] : m;
+        m = wave_max_u32(m);
+        if (m < 256u) {  // not provably R's (or infeasible): the per-task path decides
+#ifdef KB_DIAG_AFF
+          why = 1;
+#endif
+          break;
+        }
+        int jw = -1;
+        uint64_t hit = 0;
+        uint32_t r2 = 0;
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j) {
+          const uint64_t h = __ballot(k32[j] == m);
+          if (jw < 0 && h) jw = j, hit = h;
+          r2 = k32[j] != m && k32[j] > r2 ? k32[j] : r2;
+        }
+        const uint32_t m2 = wave_max_u32(r2);  // the runner-up (keys are distinct)
+        const int wl = (int)__builtin_ctzll(hit);
+        const int p = jw * 64 + wl;  // the winner's position in R
+        int ml = 0, ma = 0, mq = 0, mc = 0, mn_ = 0;
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j)
+          if (j == jw) ml = lev[j], ma = am[j], mq = qn[j], mc = cc[j], mn_ = nd[j];
+        const int lw = __builtin_amdgcn_readlane(ml, wl);   // its commits in this run so far
+        const int aw = __builtin_amdgcn_readlane(ma, wl);   // Allocates before Idle stops fitting (run start)
+        const int qw = __builtin_amdgcn_readlane(mq, wl);   // its queue entries
+        const int cw0 = __builtin_amdgcn_readlane(mc, wl);  // its commits in this phase so far
+        const int wn = __builtin_amdgcn_readlane(mn_, wl);
+        // lane i: queue entry cw0 + i (the key after cw0 + i + 1 phase commits)
+        const uint32_t hq = cw0 + lane < qw && lane < kClsL ? s_phq[p * kClsL + cw0 + lane] : 0u;
+        int c = 0;
+        uint32_t nk = m;
+#ifdef KB_DIAG_AFF
+        ++n_rounds;
+#endif
+        AFF_STAMP(3);
+        for (;;) {
+          // the pick: Session.Allocate while InitResreq fits Idle, then Pipeline (the run-start A: the closed form)
+          const int kind = lw + c < aw ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+          if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
+          cR += incR;
+          mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
+          ++c;
+          ++took;
+          ++placed;
+          ++pb_n;
+          if (kind == KB_PLACE_ALLOCATE) ++ready;
+          if (pb_n == pb_cap) {
+            wave_sync_lds();
+            for (int k = lane; k < pb_n; k += 64) {
+              const uint32_t e = pbs[k];
+              hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+              hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+            }
+            wave_sync_lds();
+            pb_base += pb_n;
+            pb_n = 0;
+          }
+          // its next key: after rel phase commits -- queue entry rel - 1 (lane c - 1 of hq), or past the sweep's
+          // levels from its row
+          const int rel = cw0 + c;
+          bool stop_now = false;
+          if (rel - 1 < qw) {
+            nk = (uint32_t)__builtin_amdgcn_readlane((int)hq, c - 1);
+          } else {
+            if (wn != dh || rel - 1 - dh_rel0 >= 64) {
+              AFF_STAMP(4);
+#ifdef KB_DIAG_AFF
+              ++n_deep;
+#endif
+              if (!fenced) {  // the row deltas flushed at the phase's start (atomics): visible to the loads below
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+                fenced = true;
+              }
+              const Row r = cls_row_now(N, wn);
+              const int dA = cls_allocs_deep(N, sp, sci, scr, r, wn);
+              const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[wn], wn, rel + lane, dA);
+              dk32 = enc((k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)wn)) : k, 255u - (uint32_t)p);
+              dh = wn, dh_rel0 = rel - 1;
+              AFF_STAMP(5);
+              if (__ballot(enc_bad)) {  // (a deep key out of the 32-bit range: the per-task path from here)
+#ifdef KB_DIAG_AFF
+                why = 2;
+#endif
+                stop_now = true;
+              }
+            }
+            nk = stop_now ? 1u : (uint32_t)__builtin_amdgcn_readlane((int)dk32, rel - 1 - dh_rel0);
+          }
+          if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+            stop = KB_STOP_READY;
+            stopped = 1;
+            stop_now = true;
+          }
+          if (t + took == t_count) stop_now = true;
+          if (!stop_now && nk > m2 && nk >= 256u) continue;  // it still beats every other member
+          // the winner's state back into its lane's registers
+          if (lane == wl) {
+#pragma unroll
+            for (int j = 0; j < kClsPM; ++j)
+              if (j == jw) k32[j] = nk, lev[j] += c, cc[j] += c;
+          }
+          done = stop_now;
+          break;
+        }
+      }
+      AFF_STAMP(4);
+#ifdef KB_DIAG_AFF
+      if (why == 4 && took > 0) why = 3;
+#endif
+      // the members' commits: row deltas, levels and 64-bit keys back (the sweep's level key, or past its levels
+      // the row's, after the deltas), then R's best and count
+      bool deep_any = false;
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
         if (cc[j] > 0) {
           const int l0 = lev[j] - cc[j];
           const int ac = am[j] > l0 ? (am[j] - l0 < cc[j] ? am[j] - l0 : cc[j]) : 0;
           flush_node(nd[j], cc[j], ac);
           lv16[nd[j]] = (uint16_t)lev[j];
-          bk[nd[j]] = key[j];
+          deep_any = deep_any || lev[j] > kClsL;
         }
+      }
+      if (__ballot(deep_any)) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // the deltas just flushed
+      uint64_t nb = 0;
+#pragma unroll
+      for (int j = 0; j < kClsPM; ++j) {
+        uint64_t k = key0[j];
+        if (cc[j] > 0) {
+          if (lev[j] <= kClsL) {
+            k = lvl[(size_t)(lev[j] - 1) * n + nd[j]];
+          } else {
+            const Row r = cls_row_now(N, nd[j]);
+            const uint64_t kk = cls_key_deep(N, P, C, sp, sci, scr, r, stat[nd[j]], nd[j], 0,
+                                             cls_allocs_deep(N, sp, sci, scr, r, nd[j]));
+            k = (kk & kFeasible) ? (kk | (uint64_t)(kIdxMask - (uint32_t)nd[j])) : kk;
+          }
+          bk[nd[j]] = k;
+        }
+        nb = umax64(nb, k);
       }
       nb = wave_max_dpp(nb);
       if (lane == 0) cbest[cw] = nb;
@@ -5413,6 +5526,11 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       for (int q = 0; q < KQ; ++q)
         if (q == (cw >> 6) && lane == (cw & 63)) cq[q] = cR;
       wave_sync_lds();
+      AFF_STAMP(5);
+#ifdef KB_DIAG_AFF
+      // counts: picks + 1e6 per round (a reduction and its winner's stretch) + 1e12 per deep-key computation
+      dg[6] += (uint64_t)took + 1000000ull * n_rounds + 1000000000000ull * n_deep;
+#endif
       if (took > 0) {
         if (stopped) break;
         t += took - 1;
@@ -5475,7 +5593,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       pbs[pb_n] = (uint32_t)w | ((uint32_t)kind << 30);
     }
     wave_sync_lds();
-    AFF_STAMP(2);
+    AFF_STAMP(1);
     if (moved) {  // the winner's key fell: its class's best again
       const uint32_t m0 = coff[cw], m1 = coff[cw + 1];
       uint64_t b = 0;
@@ -5542,7 +5660,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       }
     }
     wave_sync_lds();
-    AFF_STAMP(3);
+    AFF_STAMP(1);
     ++placed;
     ++pb_n;
     if (kind == KB_PLACE_ALLOCATE) ++ready;
@@ -5561,7 +5679,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       pb_base += pb_n;
       pb_n = 0;
     }
-    AFF_STAMP(5);
+    AFF_STAMP(1);
   }
   flush_hot();
   for (int k = lane; k < pb_n; k += 64) {
@@ -5585,7 +5703,7 @@ void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                      C, spec, bk, stat, lvl, amax, first ? (const JobState*)nullptr : js, g);
   int pb_cap = aff_pb_cap(t_count);
   const size_t fixed = cls_lds_bytes(N.n, K, 0);
-  const size_t cap_max = ((size_t)kLdsLimit - 2048 - fixed) / 4;
+  const size_t cap_max = ((size_t)kLdsLimit - kClsStaticLds - fixed) / 4;
   if ((size_t)pb_cap > cap_max) pb_cap = (int)cap_max;
   const size_t bytes = cls_lds_bytes(N.n, K, pb_cap);
 #define KB_CLS_Q(Q)                                                                                              \
@@ -5669,7 +5787,7 @@ int configure_kernels() {
     for (const void* f : {(const void*)cls_place_kernel<1>, (const void*)cls_place_kernel<2>,
                           (const void*)cls_place_kernel<4>, (const void*)cls_place_kernel<8>,
                           (const void*)cls_place_kernel<16>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - 2048);
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsLimit - kClsStaticLds);
       if (e != hipSuccess) return (int)e;
     }
   }
@@ -5736,16 +5854,24 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
                      J, idx_bits, traj, cmax32, amax, stat, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, seq);
 }
 
-// eval_plain_kernel's specs per block: the grid sized to one resident round of at most 8 waves per SIMD (the
-// kernel's occupancy; cus CUs x 4 SIMDs), so no SIMD runs a second, partial round and every SIMD holds as many
-// waves as fit to hide the f64 chains' latency. spb_opt > 0 overrides (kb_opts.eval_spb: measurement).
-static int eval_plain_spb(int n, int t, int cus, int spb_opt) {
+// eval_plain_kernel's resident blocks per CU (its occupancy: the instance's registers decide it), per instance
+int eval_plain_blocks_per_cu(bool i32) {
+  int nb = 0;
+  const hipError_t e = i32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int32_t>, 256, 0)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int64_t>, 256, 0);
+  return e == hipSuccess && nb > 0 ? nb : 2;
+}
+
+// eval_plain_kernel's specs per block: the grid sized to one resident round (cus CUs x bpc resident blocks of 4
+// waves: the kernel's occupancy), so no SIMD runs a second, partial round and every SIMD holds as many waves as fit
+// to hide the f64 chains' latency. spb_opt > 0 overrides (kb_opts.eval_spb: measurement).
+static int eval_plain_spb(int n, int t, int cus, int bpc, int spb_opt) {
   int spb;
   if (spb_opt > 0) {
     spb = spb_opt;
   } else {
     const int xblocks = (n + 255) / 256;
-    const int yblocks = ((cus > 0 ? cus : 256) * 4 * 8) / (xblocks * 4);  // blocks of 4 waves in one round, per column
+    const int yblocks = ((cus > 0 ? cus : 256) * (bpc > 0 ? bpc : 2)) / xblocks;  // blocks in one round, per column
     spb = yblocks > 0 ? (t + yblocks - 1) / yblocks : kEvalPlainSpecs;
     if (spb < 8) spb = 8;
   }
@@ -5756,7 +5882,7 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                           uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, int cus, int spb_opt,
                           void* stream) {
   if (plain) {
-    const int spb = eval_plain_spb(N.n, t, cus, spb_opt);
+    const int spb = eval_plain_spb(N.n, t, cus & 0xffff, cus >> 16, spb_opt);
     dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
     hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, spb,
                        reasons, scores);

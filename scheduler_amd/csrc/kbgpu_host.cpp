@@ -275,6 +275,8 @@ kb_ctx* kb_create(const kb_opts* opts) {
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cu > 0)
       c->cus = cu;
   }
+  c->eval_bpc32 = kbgpu::eval_plain_blocks_per_cu(true);
+  c->eval_bpc64 = kbgpu::eval_plain_blocks_per_cu(false);
   if (int e = kbgpu::configure_kernels()) {
     c->err = std::string("hipFuncSetAttribute(dynamic LDS): ") + hipGetErrorString((hipError_t)e);
     c->broken = true;
@@ -1750,11 +1752,11 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
     }
     c->ev_begin(&ea);
     if constexpr (sizeof(SCORE) == 8)
-      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain, c->cus,
-                  c->eval_spb, c->stream);
+      launch_eval(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain,
+                  c->cus | c->eval_bpc64 << 16, c->eval_spb, c->stream);
     else
       launch_eval32(c->N, c->P, c->cfg, d_ids, (int)cnt, d_r, d_s, c->aff_ok ? c->mm_eval : nullptr, plain,
-                    c->cus, c->eval_spb, c->stream);
+                    c->cus | c->eval_bpc32 << 16, c->eval_spb, c->stream);
     c->ev_end(ea, KB_KERNEL_EVAL, (uint64_t)cnt * n);
     if (hipGetLastError() != hipSuccess) rc = KB_E_HIP;
     if (reasons && hipMemcpyAsync(reasons + (size_t)b * n, d_r, cnt * n * 4, hipMemcpyDeviceToHost, c->stream))
