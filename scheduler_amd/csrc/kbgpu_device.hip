@@ -5004,6 +5004,26 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
   }
   for (int j = tid; j < n; j += kClsThreads) lv16[j] = 0;
   __syncthreads();
+  // per class (kClsCT per thread, the rest after): each histogram's domain (class-uniform: read at the first
+  // member) and the count -- their loads issued before the base keys' gather below, so the latencies overlap
+  constexpr int kClsCT = 2;
+  int32_t cdd[kClsCT][kClsE];
+  int64_t cc0[kClsCT];
+#pragma unroll
+  for (int u = 0; u < kClsCT; ++u) {
+    const int c = tid + u * kClsThreads;
+    const bool any = c < K && coff[c + 1] > coff[c];
+    const int i0 = any ? mem[coff[c]] : 0;
+#pragma unroll
+    for (int e = 0; e < kClsE; ++e) cdd[u][e] = any && e < ne ? A.topo_dom[(size_t)e_slot[e] * n + i0] : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kClsCT; ++u) {
+    cc0[u] = 0;
+#pragma unroll
+    for (int e = 0; e < kClsE; ++e)
+      if (cdd[u][e] >= 0) cc0[u] += ld_cnt<false>(&A.h[e_off[e] + cdd[u][e]]);
+  }
   // base keys into LDS and each class's best: every thread a contiguous stretch of the member list, a
   // running max per class, flushed at class boundaries (atomics only where stretches share a class)
   {
@@ -5017,7 +5037,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     }
     int c = lo;
     uint64_t run = 0;
-    constexpr int kB = 16;
+    constexpr int kB = 48;  // 10k nodes: one round of gathers per thread
     for (int jb = j0; jb < j1; jb += kB) {
       uint64_t kk[kB];
       int nd[kB];
@@ -5042,8 +5062,17 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     if (run) atomicMax((unsigned long long*)&cbest[c], (unsigned long long)run);
   }
   __syncthreads();
-  // per class: each histogram's domain (class-uniform: read at the first member) and the count
-  for (int c = tid; c < K; c += kClsThreads) {
+#pragma unroll
+  for (int u = 0; u < kClsCT; ++u) {
+    const int c = tid + u * kClsThreads;
+    if (c < K) {
+#pragma unroll
+      for (int e = 0; e < kClsE; ++e) cdom[e * K + c] = cdd[u][e];
+      cnt[c] = cc0[u];
+    }
+  }
+  // the classes past kClsCT per thread: the same, after
+  for (int c = tid + kClsCT * kClsThreads; c < K; c += kClsThreads) {
     int64_t c0 = 0;
     const bool any = coff[c + 1] > coff[c];
     const int i0 = any ? mem[coff[c]] : 0;
@@ -5415,75 +5444,96 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         ++n_rounds;
 #endif
         AFF_STAMP(3);
-        for (;;) {
-          // the pick: Session.Allocate while InitResreq fits Idle, then Pipeline (the run-start A: the closed form)
-          const int kind = lw + c < aw ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
-          if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
-          cR += incR;
-          mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
-          ++c;
-          ++took;
-          ++placed;
-          ++pb_n;
-          if (kind == KB_PLACE_ALLOCATE) ++ready;
-          if (pb_n == pb_cap) {
-            wave_sync_lds();
-            for (int k = lane; k < pb_n; k += 64) {
-              const uint32_t e = pbs[k];
-              hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-              hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+        bool stop_now = false;
+        for (;;) {  // the winner's stretch (its deep keys computed between the inner loop's passes)
+          bool need_deep = false;
+          for (;;) {
+            // the pick: Session.Allocate while InitResreq fits Idle, then Pipeline (the run-start A: the closed form)
+            const int kind = lw + c < aw ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+            if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
+            cR += incR;
+            mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
+            ++c;
+            ++took;
+            ++placed;
+            ++pb_n;
+            if (kind == KB_PLACE_ALLOCATE) ++ready;
+            if (pb_n == pb_cap) {
+              wave_sync_lds();
+              for (int k = lane; k < pb_n; k += 64) {
+                const uint32_t e = pbs[k];
+                hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+                hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+              }
+              wave_sync_lds();
+              pb_base += pb_n;
+              pb_n = 0;
             }
-            wave_sync_lds();
-            pb_base += pb_n;
-            pb_n = 0;
+            // its next key: after rel phase commits -- queue entry rel - 1 (lane c - 1 of hq), else the deep keys
+            const int rel = cw0 + c;
+            if (rel - 1 < qw) {
+              nk = (uint32_t)__builtin_amdgcn_readlane((int)hq, c - 1);
+            } else if (wn == dh && rel - 1 - dh_rel0 < 64) {
+              nk = (uint32_t)__builtin_amdgcn_readlane((int)dk32, rel - 1 - dh_rel0);
+            } else {
+              need_deep = true;
+              break;
+            }
+            if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+              stop = KB_STOP_READY;
+              stopped = 1;
+              stop_now = true;
+            }
+            if (t + took == t_count) stop_now = true;
+            if (!stop_now && nk > m2 && nk >= 256u) continue;  // it still beats every other member
+            break;
           }
-          // its next key: after rel phase commits -- queue entry rel - 1 (lane c - 1 of hq), or past the sweep's
-          // levels from its row
+          if (!need_deep) break;
+          // past the sweep's levels: its next 64 keys from its row (lane l: the key after rel + l phase commits)
+          AFF_STAMP(4);
+#ifdef KB_DIAG_AFF
+          ++n_deep;
+#endif
           const int rel = cw0 + c;
-          bool stop_now = false;
-          if (rel - 1 < qw) {
-            nk = (uint32_t)__builtin_amdgcn_readlane((int)hq, c - 1);
-          } else {
-            if (wn != dh || rel - 1 - dh_rel0 >= 64) {
-              AFF_STAMP(4);
-#ifdef KB_DIAG_AFF
-              ++n_deep;
-#endif
-              if (!fenced) {  // the row deltas flushed at the phase's start (atomics): visible to the loads below
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-                fenced = true;
-              }
-              const Row r = cls_row_now(N, wn);
-              const int dA = cls_allocs_deep(N, sp, sci, scr, r, wn);
-              const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[wn], wn, rel + lane, dA);
-              dk32 = enc((k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)wn)) : k, 255u - (uint32_t)p);
-              dh = wn, dh_rel0 = rel - 1;
-              AFF_STAMP(5);
-              if (__ballot(enc_bad)) {  // (a deep key out of the 32-bit range: the per-task path from here)
-#ifdef KB_DIAG_AFF
-                why = 2;
-#endif
-                stop_now = true;
-              }
-            }
-            nk = stop_now ? 1u : (uint32_t)__builtin_amdgcn_readlane((int)dk32, rel - 1 - dh_rel0);
+          if (!fenced) {  // the row deltas flushed at the phase's start (atomics): visible to the loads below
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            fenced = true;
           }
-          if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+          // (an opaque copy of the node: its row addresses are formed here, not hoisted into every round's
+          // preamble, where the compiler had spilled them)
+          int wq = wn;
+          asm volatile("" : "+s"(wq));
+          const Row r = cls_row_now(N, wq);
+          const int dA = cls_allocs_deep(N, sp, sci, scr, r, wq);
+          const uint64_t k = cls_key_deep(N, P, C, sp, sci, scr, r, stat[wq], wq, rel + lane, dA);
+          dk32 = enc((k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)wq)) : k, 255u - (uint32_t)p);
+          dh = wn, dh_rel0 = rel - 1;
+          AFF_STAMP(5);
+          if (__ballot(enc_bad)) {  // (a deep key out of the 32-bit range: the per-task path from here)
+#ifdef KB_DIAG_AFF
+            why = 2;
+#endif
+            stop_now = true;
+            nk = 1u;
+          } else {
+            nk = (uint32_t)__builtin_amdgcn_readlane((int)dk32, 0);
+          }
+          if (!gang || ready >= minav) {  // (the pick's stop rules, as in the inner loop)
             stop = KB_STOP_READY;
             stopped = 1;
             stop_now = true;
           }
           if (t + took == t_count) stop_now = true;
-          if (!stop_now && nk > m2 && nk >= 256u) continue;  // it still beats every other member
-          // the winner's state back into its lane's registers
-          if (lane == wl) {
-#pragma unroll
-            for (int j = 0; j < kClsPM; ++j)
-              if (j == jw) k32[j] = nk, lev[j] += c, cc[j] += c;
-          }
-          done = stop_now;
+          if (!stop_now && nk > m2 && nk >= 256u) continue;
           break;
         }
+        // the winner's state back into its lane's registers
+        if (lane == wl) {
+#pragma unroll
+          for (int j = 0; j < kClsPM; ++j)
+            if (j == jw) k32[j] = nk, lev[j] += c, cc[j] += c;
+        }
+        done = stop_now;
       }
       AFF_STAMP(4);
 #ifdef KB_DIAG_AFF

@@ -208,6 +208,12 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+SESSION_ARRAYS = ("s_task_job", "s_task_spec", "s_task_status", "s_task_priority", "s_task_ctime", "s_task_uid_rank",
+                  "s_task_resreq", "s_task_resreq_mask", "s_job_queue", "s_job_priority", "s_job_min", "s_job_ctime",
+                  "s_job_uid_rank", "s_job_pg_pending", "s_queue_weight", "s_queue_ctime", "s_queue_uid_rank",
+                  "s_total", "s_tiers")
+
+
 def _ptr(a):
     return a.ctypes.data_as(P) if a is not None and a.size else None
 
@@ -449,22 +455,13 @@ class Context:
     def allocate(self, snap: E.Snapshot):
         """kb_allocate: allocateAction.Execute over the uploaded snapshot."""
         nt, nj = len(snap.session_tasks), len(snap.jobs)
-        arrs = dict(
-            task_job=snap.s_task_job, task_spec=snap.s_task_spec, task_status=snap.s_task_status,
-            task_priority=snap.s_task_priority, task_ctime=snap.s_task_ctime, task_uid_rank=snap.s_task_uid_rank,
-            task_resreq=np.ascontiguousarray(snap.s_task_resreq), task_resreq_mask=snap.s_task_resreq_mask,
-            job_queue=snap.s_job_queue, job_priority=snap.s_job_priority, job_min_available=snap.s_job_min,
-            job_ctime=snap.s_job_ctime, job_uid_rank=snap.s_job_uid_rank, job_pg_pending=snap.s_job_pg_pending,
-            queue_weight=snap.s_queue_weight, queue_ctime=snap.s_queue_ctime, queue_uid_rank=snap.s_queue_uid_rank,
-            total_alloc=snap.s_total, tier_plugins=snap.s_tiers)
-        ssn = kb_session(
-            len(snap.acc_scalars), nt, *[_ptr(arrs[k]) for k in ("task_job", "task_spec", "task_status",
-                                                               "task_priority", "task_ctime", "task_uid_rank",
-                                                               "task_resreq", "task_resreq_mask")],
-            nj, *[_ptr(arrs[k]) for k in ("job_queue", "job_priority", "job_min_available", "job_ctime",
-                                         "job_uid_rank", "job_pg_pending")],
-            len(snap.queues), *[_ptr(arrs[k]) for k in ("queue_weight", "queue_ctime", "queue_uid_rank")],
-            _ptr(arrs["total_alloc"]), snap.s_total_mask, len(snap.s_tiers), _ptr(arrs["tier_plugins"]))
+        key = (id(snap),) + tuple(id(getattr(snap, a)) for a in SESSION_ARRAYS)
+        cached = getattr(self, "_ssn_cache", None)
+        if cached is not None and cached[0] == key:  # the session arrays' struct, built once per snapshot and arrays
+            ssn = cached[1]
+        else:
+            ssn = self._session_struct(snap, nt, nj)
+            self._ssn_cache = (key, ssn, self._ssn_keep)
         out = {"task_node": np.zeros(max(nt, 1), np.int32), "task_status": np.zeros(max(nt, 1), np.int32),
                "job_fail_task": np.zeros(max(nj, 1), np.int32),
                "job_reason_hist": np.zeros((max(nj, 1), KB_NUM_REASONS), np.uint32),
@@ -484,6 +481,27 @@ class Context:
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
         return out
+
+    def _session_struct(self, snap, nt, nj):
+        """kb_session over the snapshot's session arrays (kept alive with the struct in self._ssn_cache)."""
+        arrs = dict(
+            task_job=snap.s_task_job, task_spec=snap.s_task_spec, task_status=snap.s_task_status,
+            task_priority=snap.s_task_priority, task_ctime=snap.s_task_ctime, task_uid_rank=snap.s_task_uid_rank,
+            task_resreq=np.ascontiguousarray(snap.s_task_resreq), task_resreq_mask=snap.s_task_resreq_mask,
+            job_queue=snap.s_job_queue, job_priority=snap.s_job_priority, job_min_available=snap.s_job_min,
+            job_ctime=snap.s_job_ctime, job_uid_rank=snap.s_job_uid_rank, job_pg_pending=snap.s_job_pg_pending,
+            queue_weight=snap.s_queue_weight, queue_ctime=snap.s_queue_ctime, queue_uid_rank=snap.s_queue_uid_rank,
+            total_alloc=snap.s_total, tier_plugins=snap.s_tiers)
+        ssn = kb_session(
+            len(snap.acc_scalars), nt, *[_ptr(arrs[k]) for k in ("task_job", "task_spec", "task_status",
+                                                               "task_priority", "task_ctime", "task_uid_rank",
+                                                               "task_resreq", "task_resreq_mask")],
+            nj, *[_ptr(arrs[k]) for k in ("job_queue", "job_priority", "job_min_available", "job_ctime",
+                                         "job_uid_rank", "job_pg_pending")],
+            len(snap.queues), *[_ptr(arrs[k]) for k in ("queue_weight", "queue_ctime", "queue_uid_rank")],
+            _ptr(arrs["total_alloc"]), snap.s_total_mask, len(snap.s_tiers), _ptr(arrs["tier_plugins"]))
+        self._ssn_keep = (snap, arrs)  # (the struct points into these)
+        return ssn
 
     def backfill(self, snap: E.Snapshot, out: dict) -> dict:
         """backfillAction.Execute (actions/backfill/backfill.go:40-90) on the session kb_allocate left in `out`.

@@ -31,7 +31,10 @@ KIND = {"allocate": 1, "pipeline": 2}
 
 
 # C5-head: the first placements of a 300-job C5-shaped cluster (the sharded 3-rank test compares a prefix)
-HEADS = {"C5-head": (dict(n_nodes=50000, n_jobs=300, tasks_per_job=100), 3000)}
+HEADS = {"C5-head": (dict(n_nodes=50000, n_jobs=300, tasks_per_job=100), 3000),
+         # past the resident engine's node ceiling on one GPU (4 range selectors x 20,480 nodes): 100k C2-shaped
+         # nodes, the whole cycle of 30 jobs (test_gpu_big.py runs it on the per-commit re-key path)
+         "X100k-head": (dict(n_nodes=100000, n_jobs=30, tasks_per_job=100), 3000)}
 # BASELINE.json configs[4] at full size: the C2 shape at 50k nodes x 1M pods (10k jobs)
 SHAPES = {"C5": dict(n_nodes=50000, n_jobs=10000, tasks_per_job=100)}
 

@@ -102,3 +102,32 @@ def test_c5_one_gpu_matches_oracle_prefix():
     assert np.array_equal(out["task_node"][et].astype(np.int32), want["event_node"])
     kinds = np.where(out["task_status"][et] == E.ST["Pipelined"], 2, 1).astype(np.int8)
     assert np.array_equal(kinds, want["event_kind"])
+
+
+def test_100k_nodes_one_gpu_matches_oracle_head():
+    """Past the resident engine's node ceiling on one GPU (four range selectors of 20,480 nodes): 100k C2-shaped
+    nodes x 30 jobs of 100 tasks. The cycle runs on the per-job launch path with 64-bit keys and a re-key per commit
+    (sweep_keys_kernel + place_loop_kernel); all 3,000 placements are the oracle's (tests/golden/digest-X100k-head)."""
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(golden, "digest-X100k-head.json")) as f:
+        meta = json.load(f)
+    want = np.load(os.path.join(golden, "digest-X100k-head.npz"), allow_pickle=False)
+    snap = synth.c2_snapshot(n_nodes=100000, n_jobs=30, tasks_per_job=100, seed=synth.SEED)
+    ctx = runtime.Context(0, timing=True)
+    try:
+        ctx.upload(snap)
+        out = ctx.allocate(snap)
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    assert st["fed_cycles"] == 0, st  # (beyond the engine: the launch path)
+    k = meta["max_tasks"]
+    assert int(out["n_events"]) == meta["events"] == k
+    et = out["event_task"][:k].astype(np.int32)
+    assert np.array_equal(et, want["event_task"])
+    assert np.array_equal(out["task_node"][et].astype(np.int32), want["event_node"])
+    kinds = np.where(out["task_status"][et] == E.ST["Pipelined"], 2, 1).astype(np.int8)
+    assert np.array_equal(kinds, want["event_kind"])
+    K = runtime.KERNELS
+    print({K[i]: (st["launches"][i], round(st["kernel_ms"][i], 2)) for i in range(len(K)) if st["launches"][i]},
+          "cycle ms", round(out["elapsed_ms"], 1), flush=True)
