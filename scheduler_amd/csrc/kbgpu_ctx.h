@@ -176,6 +176,9 @@ struct kb_ctx {
   int32_t fed_exit_code = 0;   // the engine's exit flag when it left early (wait_seq)
   uint64_t n_fed_abandon = 0;  // cycles finished on the launch path after the engine idled out
   char* h_eval = nullptr;
+  void *eval_ids = nullptr, *eval_r = nullptr, *eval_s = nullptr;  // kb_eval's device buffers (persistent)
+  size_t eval_cap = 0;        // pairs the output buffers hold
+  uint32_t eval_ids_cap = 0;
 
   double device_ms = 0;  // wall time inside kb_place_job
 

@@ -312,6 +312,9 @@ void kb_destroy(kb_ctx* c) {
   if (c->fed_exit) (void)hipFree(c->fed_exit);
   if (c->fed_xchg) (void)hipFree(c->fed_xchg);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
+  (void)hipFree(c->eval_ids);
+  (void)hipFree(c->eval_r);
+  (void)hipFree(c->eval_s);
   if (c->h_cmd) (void)hipHostFree(c->h_cmd);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
   if (c->d_rec) (void)hipFree(c->d_rec);
@@ -1726,9 +1729,23 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
   uint32_t* d_r;
   SCORE* d_s;
   const uint32_t tc = std::min(t, chunk);
-  HIP_OK(c, hipMalloc(&d_ids, std::max<uint32_t>(tc, 1) * 4));
-  HIP_OK(c, hipMalloc(&d_r, std::max<size_t>(tc * n, 1) * 4));
-  HIP_OK(c, hipMalloc(&d_s, std::max<size_t>(tc * n, 1) * sizeof(SCORE)));
+  // the output buffers persist in the context (grown, never shrunk): no allocation per call, and one placement of
+  // the pages for the context's life
+  const size_t need = std::max<size_t>(tc * n, 1);
+  if (c->eval_cap < need || c->eval_ids_cap < std::max<uint32_t>(tc, 1)) {
+    (void)hipFree(c->eval_ids);
+    (void)hipFree(c->eval_r);
+    (void)hipFree(c->eval_s);
+    c->eval_ids = nullptr, c->eval_r = nullptr, c->eval_s = nullptr, c->eval_cap = 0, c->eval_ids_cap = 0;
+    HIP_OK(c, hipMalloc(&c->eval_ids, std::max<uint32_t>(tc, 1) * 4));
+    HIP_OK(c, hipMalloc(&c->eval_r, need * 4));
+    HIP_OK(c, hipMalloc(&c->eval_s, need * 8));  // (room for 64-bit scores)
+    c->eval_cap = need;
+    c->eval_ids_cap = std::max<uint32_t>(tc, 1);
+  }
+  d_ids = (int32_t*)c->eval_ids;
+  d_r = (uint32_t*)c->eval_r;
+  d_s = (SCORE*)c->eval_s;
   int rc = KB_OK;
   for (uint32_t b = 0; b < t && rc == KB_OK; b += chunk) {
     const uint32_t cnt = std::min(chunk, t - b);
@@ -1767,9 +1784,6 @@ static int eval_impl(kb_ctx* c, const int32_t* spec_ids, uint32_t t, uint32_t* r
     if (hipStreamSynchronize(c->stream) != hipSuccess) rc = KB_E_HIP;
   }
   if (c->timing) c->ev_collect(true);
-  (void)hipFree(d_ids);
-  (void)hipFree(d_r);
-  (void)hipFree(d_s);
   if (rc) return fail(c, rc, "kb_eval: HIP failure");
   return KB_OK;
 }
