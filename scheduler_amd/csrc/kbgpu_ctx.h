@@ -34,6 +34,7 @@ struct kb_ctx {
   uint32_t aff_n_tables = 0, aff_n_h = 0;  // kb_apply_affinity's bounds
   uint64_t* cls_lvl = nullptr;  // [kClsLevels][n] class loop scratch: keys after 1..kClsLevels commits
   int32_t* cls_amax = nullptr;  // [n] class loop scratch: Allocates before Idle stops fitting
+  uint64_t* cls_cbest = nullptr;  // [kClsMaxK] class loop: each class's best base key (sweep -> place kernel; 0 between)
   // per topology slot that is some spec's class slot: its classes as member lists (offsets [K + 1], node ids
   // by class [n]; device copies in aff_mem), else null
   std::vector<uint32_t*> cls_coff;

@@ -179,7 +179,7 @@ void launch_aff_reg(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int s
                     int32_t* hout, JobState* hjs, uint32_t seq, void* stream);
 // The class loop for specs whose own commits move only their histograms (kbgpu_host.cpp
 // classify_self_dynamic): F = the finest moving slot, K = its domain count + 1. cls_fits: the LDS plan
-// holds n nodes and K classes. The run's global table updates are left to launch_aff_commit.
+// holds n nodes and K classes. The kernel applies the run's global table updates itself.
 bool cls_fits(int n, int K);
 // Scratch: bk / stat [n], lvl [kClsLevels][n], amax [n] (the chip-wide prologue's base keys, static cache,
 // keys after 1..kClsLevels commits, Allocates before Idle stops fitting). coff [K + 1] / mem [n]: slot F's
@@ -187,8 +187,8 @@ bool cls_fits(int n, int K);
 constexpr int kClsLevels = 8;
 void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int F, int K, int t_begin,
                       int t_count, uint64_t* bk, uint64_t* stat, uint64_t* lvl, int32_t* amax, const uint32_t* coff,
-                      const uint16_t* mem, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout,
-                      JobState* hjs, uint32_t seq, SpecGuard g, void* stream);
+                      const uint16_t* mem, uint64_t* cbest, JobState* js, int first, int ready0, int minav0,
+                      int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g, void* stream);
 
 // A fed-engine job command (launch_sel_sweep's `fed` / launch_fed_cmd).
 struct FedCmdArgs {
@@ -215,7 +215,9 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
                       SpecGuard g = SpecGuard{nullptr, 0, 0, 0}, int32_t* commit_out = nullptr,
                       const int32_t* patch = nullptr, const JobState* patch_js = nullptr,
-                      const uint32_t* wait_ctr = nullptr, uint32_t wait_target = 0);
+                      const uint32_t* wait_ctr = nullptr, uint32_t wait_target = 0, int aff_pl = 0);
+// aff_pl: the kernel applies the run's affinity table commits itself (needs sel_aff_pl_fits)
+bool sel_aff_pl_fits(int n, int t_count);
 
 // Placement engine (kbgpu_device.hip): the selection path as one persistent workgroup serving the
 // commands posted to `cmd` from sequence number seq0 on; exits on KB_ENG_EXIT or after idle_ticks

@@ -1801,7 +1801,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
                                         ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS,
-                                        FedPub pub = FedPub{}) {
+                                        FedPub pub = FedPub{}, uint32_t* pl = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2118,9 +2118,9 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         const int at = t_begin + done_tasks + tid;
         hout[2 * at] = sh.node[s] + N.base;
         hout[2 * at + 1] = j < sh.A[s] ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+        if (pl != nullptr) pl[at - t_begin] = (uint32_t)sh.node[s] | (j < sh.A[s] ? 1u << 31 : 0u);
       }
       __syncthreads();
-      // the touched nodes' keys matter only to a later segment or to the no-fit histogram
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram; commit_out
       // lists the rows for the next job, whose level-0 sweep ran before these stores (kb_job_issue)
       const bool rekey = !CAND && (kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count));
@@ -2216,7 +2216,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int t_begin, int t_count, int idx_bits, const uint32_t* keys32,
     const uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout, JobState* hjs,
     uint32_t seq, SpecGuard g, int32_t* commit_out, const int32_t* patch, const JobState* patch_js,
-    const uint32_t* wait_ctr, uint32_t wait_target) {
+    const uint32_t* wait_ctr, uint32_t wait_target, int pl_off) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   __shared__ SelShared sh;
   if ((!first && js->stopped) || guard_fails(g)) {
@@ -2297,8 +2297,11 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   __syncthreads();
   KB_SEL_PH(0);
 
-  sel_run<false, QN>(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed, stop, fail_task,
-          panic, stopped, hout, js, hjs, rp, nullptr, commit_out SEL_DIAG_ARGS);
+  // pl_off > 0: the run's placements also into LDS (node | allocate << 31), for its affinity table commits below
+  uint32_t* pl = pl_off > 0 ? lds32 + pl_off / 4 : nullptr;
+  sel_run<false, QN>(sh, k32, cand, N, P, C, sp, spec, t_begin, t_count, idx_bits, stat, ready, minav, gang, placed,
+                     stop, fail_task, panic, stopped, hout, js, hjs, rp, nullptr, commit_out SEL_DIAG_ARGS, FedPub{},
+                     pl);
 #ifdef KB_DIAG
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
@@ -2312,6 +2315,11 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
   }
+  // an affinity spec's commits into the global tables, after the whole run (a cap-1 run's closed form and its
+  // later segments' keys read the tables as of the run's start); the next kernel on the stream sees them
+  if (pl != nullptr)
+    for (int k = tid; k < sh.lo.placed - t_begin; k += kSelThreads)
+      apply_commit_tables(P.A, sp, (int)(pl[k] & 0x7fffffffu), (int)(pl[k] >> 31), 1);
 }
 
 // ===========================================================================
@@ -2767,14 +2775,16 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
                       int idx_bits, const uint32_t* keys32, const uint64_t* stat, JobState* js, int first, int ready0,
                       int minav0, int gang0, int32_t* hout, JobState* hjs, uint32_t seq, void* stream,
                       SpecGuard g, int32_t* commit_out, const int32_t* patch, const JobState* patch_js,
-                      const uint32_t* wait_ctr, uint32_t wait_target) {
+                      const uint32_t* wait_ctr, uint32_t wait_target, int aff_pl) {
   const int qn = sel_qn(N.n);
-  const int bytes = qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : sel_lds_bytes(N.n);
+  const int base = qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : sel_lds_bytes(N.n);
+  const int pl_off = aff_pl && base + 4 * t_count <= kSelDynLimit ? base : 0;  // (caller: sel_aff_pl_fits)
+  const int bytes = base + (pl_off ? 4 * t_count : 0);
 #define KB_SEL_QN(Q)                                                                                                \
   case Q:                                                                                                          \
     hipLaunchKernelGGL(sel_place_kernel<Q>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C, spec,  \
                        t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs, seq, \
-                       g, commit_out, patch, patch_js, wait_ctr, wait_target);                                     \
+                       g, commit_out, patch, patch_js, wait_ctr, wait_target, pl_off);                             \
     break;
   switch (qn) {
     KB_SEL_QN(1)
@@ -2788,9 +2798,15 @@ void launch_sel_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
     default:
       hipLaunchKernelGGL(sel_place_kernel<0>, dim3(1), dim3(kSelThreads), bytes, (hipStream_t)stream, N, P, C, spec,
                          t_begin, t_count, idx_bits, keys32, stat, js, first, ready0, minav0, gang0, hout, hjs, seq,
-                         g, commit_out, patch, patch_js, wait_ctr, wait_target);
+                         g, commit_out, patch, patch_js, wait_ctr, wait_target, pl_off);
   }
 #undef KB_SEL_QN
+}
+
+bool sel_aff_pl_fits(int n, int t_count) {
+  const int qn = sel_qn(n);
+  const int base = qn > 0 ? 4 * (4 * kSelThreads * qn) + 8 * kCandCap : sel_lds_bytes(n);
+  return base + 4 * t_count <= kSelDynLimit;
 }
 
 
@@ -4827,7 +4843,7 @@ void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 // classes in the committed node's domains (nodeorder.go:161-172 AddPod). Per task: one wave, a few lane
 // ops per class and per member of the winner's class, no block barriers; aff_reg_kernel re-keys every node.
 // Prologue on the whole block: base keys, class member lists (CSR) and class state in LDS. The run's
-// global table updates come after it (aff_commit_kernel, from the placements).
+// global table updates come at its end, from the placements.
 // ---------------------------------------------------------------------------
 // 4 waves: the task loop's wave gets the whole VGPR file of its SIMD (1024 threads cap it at 128 and spill)
 constexpr int kClsThreads = 256;
@@ -4860,29 +4876,50 @@ bool cls_fits(int n, int K) {
 // level j >= 1 -> the key after j commits of the spec (traj_key64's closed form: the first A Allocate, the
 // rest Pipeline). A node failing a static check at level 0 never commits, so levels >= 1 leave them out.
 constexpr int kClsL = kClsLevels;
-__global__ __launch_bounds__(256) void cls_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, uint64_t* bk,
-                                                        uint64_t* stat, uint64_t* lvl, int32_t* amax,
-                                                        const JobState* js, SpecGuard g) {
+__global__ __launch_bounds__(256) void cls_sweep_kernel(DevNodes N, DevSpecs P, DevCfg C, int spec, int F, int K,
+                                                        uint64_t* bk, uint64_t* stat, uint64_t* lvl, int32_t* amax,
+                                                        uint64_t* cbest, const JobState* js, SpecGuard g) {
   if ((js != nullptr && js->stopped) || guard_fails(g)) return;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int j = blockIdx.y;
-  if (i >= N.n) return;
+  const bool in = i < N.n;
+  if (j != 0 && !in) return;
   const DevAff& A = P.A;
   const kb_spec sp = P.specs[spec];
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   const int64_t* scr = P.sc_req + (size_t)spec * N.S;
-  const Row r = load_row(N, i);
-  const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
   if (j == 0) {
-    const kb_aff_spec as = A.specs[sp.aff_class];
-    const int32_t ov = ov_row(P, spec);
-    uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
-    if (!rs && C.predicates) rs = aff_reasons<false>(A, as, i);
-    if (!rs && ov >= 0 && P.ov_fail[(size_t)ov * N.n + i]) rs = kHostError;
-    bk[i] = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
-    stat[i] = st;
-    amax[i] = allocs_before_full(N, sp, sci, scr, r, i);
+    // level 0: the base key, and each class's best base key (class = the node's F-domain, K - 1 without one)
+    // as one atomic max per class present in the wave (the place kernel reads cbest and zeroes it again)
+    uint64_t key = 0;
+    int c = -1;
+    if (in) {
+      const Row r = load_row(N, i);
+      const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
+      const kb_aff_spec as = A.specs[sp.aff_class];
+      const int32_t ov = ov_row(P, spec);
+      uint32_t rs = row_reasons(N, P, C, sp, sci, r, st, i);
+      if (!rs && C.predicates) rs = aff_reasons<false>(A, as, i);
+      if (!rs && ov >= 0 && P.ov_fail[(size_t)ov * N.n + i]) rs = kHostError;
+      key = make_key(rs, rs ? 0 : row_score(C, sp, r, st), i);
+      bk[i] = key;
+      stat[i] = st;
+      amax[i] = allocs_before_full(N, sp, sci, scr, r, i);
+      const int32_t d = A.topo_dom[(size_t)F * N.n + i];
+      c = d >= 0 ? d : K - 1;
+    }
+    uint64_t todo = __ballot(c >= 0);
+    while (todo) {  // wave-uniform: one class per pass (members are contiguous in a class slot's usual layout)
+      const int cl = __builtin_amdgcn_readlane(c, __builtin_ctzll(todo));
+      const bool mine = c == cl;
+      const uint64_t m = wave_max_u64(mine ? key : 0);
+      if (mine && (threadIdx.x & 63) == __builtin_ctzll(todo) && m)
+        atomicMax((unsigned long long*)&cbest[cl], (unsigned long long)m);
+      todo &= ~__ballot(mine);
+    }
   } else {
+    const Row r = load_row(N, i);
+    const uint64_t st = static_eval<false>(N, P, C, sp, spec, r.flags, i, nullptr);
     const uint64_t k = traj_key64(N, P, C, sp, sci, scr, r, st, i, j, allocs_before_full(N, sp, sci, scr, r, i));
     lvl[(size_t)(j - 1) * N.n + i] = (k & kFeasible) ? (k | (uint64_t)(kIdxMask - (uint32_t)i)) : k;
   }
@@ -4927,7 +4964,7 @@ template <int KQ>
 __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     DevNodes N, DevSpecs P, DevCfg C, int spec, int F, int K, int t_begin, int t_count, const uint64_t* bkg,
     const uint64_t* stat, const uint64_t* lvl, const int32_t* amax, const uint32_t* coff_g, const uint16_t* mem_g,
-    JobState* js, int first,
+    uint64_t* cbest_g, JobState* js, int first,
     int ready0, int minav0,
     int gang0, int32_t* hout, JobState* hjs, int pb_cap, uint32_t seq, SpecGuard g) {
   // dynamic LDS: bk u64[n] base keys | cbest u64[K] class best base key | cnt i64[K] class counts |
@@ -4951,6 +4988,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       js->stopped = 1;
       js->n_commit = 0;
     }
+    for (int c = threadIdx.x; c < K; c += kClsThreads) cbest_g[c] = 0;  // (its sweep skipped too: already 0)
     signal_skip(hjs, seq);
     return;
   }
@@ -4976,23 +5014,34 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       e_slot[e] = h.slot, e_off[e] = (int32_t)h.h_off;
     }
   }
-  // the class member lists (static per topology slot: built at kb_upload_affinity) into LDS
+  // the class member lists (static per topology slot: built at kb_upload_affinity), the base keys and each
+  // class's best (both from the sweep) into LDS; every load of a thread in flight at once, 16 bytes each
   for (int c = tid; c <= K; c += kClsThreads) coff[c] = coff_g[c];
-  for (int c = tid; c < K; c += kClsThreads) cbest[c] = 0;
-  {  // the member list in 16-byte loads, all of a thread's in flight at once (mem_g is padded to 8 entries)
+  for (int c = tid; c < K; c += kClsThreads) {
+    cbest[c] = cbest_g[c];
+    cbest_g[c] = 0;  // for the next run's sweep
+  }
+  {
     const uint4* mg = (const uint4*)mem_g;
-    const int nv = (n + 7) / 8;
-    constexpr int kV = 8;
-    for (int v0 = 0; v0 < nv; v0 += kV * kClsThreads) {
-      uint4 x[kV];
+    const uint4* kg = (const uint4*)bkg;
+    const int nv = (n + 7) / 8;  // mem_g is padded to 8 entries
+    const int nk = n / 2;        // key pairs (an odd n's last key below)
+    constexpr int kV = 4;
+    for (int v0 = 0; v0 < 4 * nv; v0 += kV * 4 * kClsThreads) {  // (4 nv >= nk)
+      uint4 x[kV], y[4 * kV];
 #pragma unroll
       for (int q = 0; q < kV; ++q) {
-        const int v = v0 + q * kClsThreads + tid;
+        const int v = v0 / 4 + q * kClsThreads + tid;
         x[q] = v < nv ? mg[v] : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
-      for (int q = 0; q < kV; ++q) {
+      for (int q = 0; q < 4 * kV; ++q) {
         const int v = v0 + q * kClsThreads + tid;
+        y[q] = v < nk ? kg[v] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < kV; ++q) {
+        const int v = v0 / 4 + q * kClsThreads + tid;
         if (v < nv) {
           const uint32_t w4[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
 #pragma unroll
@@ -5000,12 +5049,18 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
             if (8 * v + h < n) mem[8 * v + h] = (uint16_t)(w4[h >> 1] >> (16 * (h & 1)));
         }
       }
+#pragma unroll
+      for (int q = 0; q < 4 * kV; ++q) {
+        const int v = v0 + q * kClsThreads + tid;
+        if (v < nk) ((uint4*)bk)[v] = y[q];
+      }
     }
+    if ((n & 1) && tid == 0) bk[n - 1] = bkg[n - 1];
   }
   for (int j = tid; j < n; j += kClsThreads) lv16[j] = 0;
   __syncthreads();
-  // per class (kClsCT per thread, the rest after): each histogram's domain (class-uniform: read at the first
-  // member) and the count -- their loads issued before the base keys' gather below, so the latencies overlap
+  // per class (kClsCT per thread in flight together, the rest after): each histogram's domain (class-uniform:
+  // read at the first member) and the count
   constexpr int kClsCT = 2;
   int32_t cdd[kClsCT][kClsE];
   int64_t cc0[kClsCT];
@@ -5024,44 +5079,6 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
     for (int e = 0; e < kClsE; ++e)
       if (cdd[u][e] >= 0) cc0[u] += ld_cnt<false>(&A.h[e_off[e] + cdd[u][e]]);
   }
-  // base keys into LDS and each class's best: every thread a contiguous stretch of the member list, a
-  // running max per class, flushed at class boundaries (atomics only where stretches share a class)
-  {
-    const int ch = (n + kClsThreads - 1) / kClsThreads;
-    const int j0 = tid * ch < n ? tid * ch : n, j1 = j0 + ch < n ? j0 + ch : n;
-    int lo = 0, hi = K;  // the class of position j0: the last c with coff[c] <= j0
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if ((int)coff[mid] <= j0) lo = mid;
-      else hi = mid;
-    }
-    int c = lo;
-    uint64_t run = 0;
-    constexpr int kB = 48;  // 10k nodes: one round of gathers per thread
-    for (int jb = j0; jb < j1; jb += kB) {
-      uint64_t kk[kB];
-      int nd[kB];
-#pragma unroll
-      for (int q = 0; q < kB; ++q) nd[q] = jb + q < j1 ? mem[jb + q] : 0;
-#pragma unroll
-      for (int q = 0; q < kB; ++q) kk[q] = jb + q < j1 ? bkg[nd[q]] : 0;
-#pragma unroll
-      for (int q = 0; q < kB; ++q) {
-        const int j = jb + q;
-        if (j < j1) {
-          while (j >= (int)coff[c + 1]) {
-            if (run) atomicMax((unsigned long long*)&cbest[c], (unsigned long long)run);
-            run = 0;
-            ++c;
-          }
-          bk[nd[q]] = kk[q];
-          run = umax64(run, kk[q]);
-        }
-      }
-    }
-    if (run) atomicMax((unsigned long long*)&cbest[c], (unsigned long long)run);
-  }
-  __syncthreads();
 #pragma unroll
   for (int u = 0; u < kClsCT; ++u) {
     const int c = tid + u * kClsThreads;
@@ -5742,15 +5759,26 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #endif
   __threadfence_system();
   __builtin_amdgcn_wave_barrier();
+  // the run's commits into the global tables, now that no key of this run reads them: from pbs when the run
+  // never wrapped it, else back from the host buffer (the fence above made every lane's stores visible)
+  const int run_n = pb_base + pb_n - t_begin;
+  if (run_n <= pb_cap)
+    for (int k = lane; k < run_n; k += 64) {
+      const uint32_t e = pbs[k];
+      apply_commit_tables(P.A, sp, (int)(e & 0x3fffffffu), (int)(e >> 30) == KB_PLACE_ALLOCATE ? 1 : 0, 1);
+    }
+  else
+    for (int p = t_begin + lane; p < pb_base + pb_n; p += 64)
+      apply_commit_tables(P.A, sp, hout[2 * p], hout[2 * p + 1] == KB_PLACE_ALLOCATE ? 1 : 0, 1);
   if (lane == 0) publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, seq);
 }
 
 void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int F, int K, int t_begin,
                       int t_count, uint64_t* bk, uint64_t* stat, uint64_t* lvl, int32_t* amax, const uint32_t* coff,
-                      const uint16_t* mem, JobState* js, int first, int ready0, int minav0, int gang0, int32_t* hout,
-                      JobState* hjs, uint32_t seq, SpecGuard g, void* stream) {
+                      const uint16_t* mem, uint64_t* cbest, JobState* js, int first, int ready0, int minav0,
+                      int gang0, int32_t* hout, JobState* hjs, uint32_t seq, SpecGuard g, void* stream) {
   hipLaunchKernelGGL(cls_sweep_kernel, dim3((N.n + 255) / 256, 1 + kClsL), dim3(256), 0, (hipStream_t)stream, N, P,
-                     C, spec, bk, stat, lvl, amax, first ? (const JobState*)nullptr : js, g);
+                     C, spec, F, K, bk, stat, lvl, amax, cbest, first ? (const JobState*)nullptr : js, g);
   int pb_cap = aff_pb_cap(t_count);
   const size_t fixed = cls_lds_bytes(N.n, K, 0);
   const size_t cap_max = ((size_t)kLdsLimit - kClsStaticLds - fixed) / 4;
@@ -5758,9 +5786,8 @@ void launch_cls_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   const size_t bytes = cls_lds_bytes(N.n, K, pb_cap);
 #define KB_CLS_Q(Q)                                                                                              \
   hipLaunchKernelGGL(cls_place_kernel<Q>, dim3(1), dim3(kClsThreads), bytes, (hipStream_t)stream, N, P, C, spec, F, \
-                     K, \
-                     t_begin, t_count, bk, stat, lvl, amax, coff, mem, js, first, ready0, minav0, gang0, hout, hjs, pb_cap, \
-                     seq, g)
+                     K, t_begin, t_count, bk, stat, lvl, amax, coff, mem, cbest, js, first, ready0, minav0, gang0, hout, \
+                     hjs, pb_cap, seq, g)
   const int q = (K + 63) / 64;
   if (q <= 1) KB_CLS_Q(1);
   else if (q <= 2) KB_CLS_Q(2);

@@ -414,6 +414,10 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, n * sizeof(int32_t)));
   c->work_mem.push_back(p);
   c->cls_amax = (int32_t*)p;
+  HIP_OK(c, hipMalloc(&p, kClsMaxK * sizeof(uint64_t)));
+  c->work_mem.push_back(p);
+  c->cls_cbest = (uint64_t*)p;
+  HIP_OK(c, hipMemset(p, 0, kClsMaxK * sizeof(uint64_t)));
   c->idx_bits = 1;  // key index field: global node indices when sharded
   const unsigned long long n_keys = c->sharded ? c->shard.n_total : n;
   while ((1ull << c->idx_bits) < n_keys) ++c->idx_bits;
@@ -1250,6 +1254,8 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     const bool sel = !dyn && sel_fits;
     const bool traj = !sel && !dyn && c->use_traj && key32 && c->traj_full && traj_lds_bytes(c->N.n, run, &pbc) > 0;
     const bool cls = dyn && cls_run_ok(c, spec);
+    // the selection kernel applies the run's affinity table commits itself when its placements fit LDS
+    const bool sel_pl = sel && aff && c->spec_incr[spec] && sel_aff_pl_fits(c->N.n, (int)run);
     if (first && g.prev && !sel && !cls)
       return fail(c, KB_E_INVALID, "guarded job takes neither the selection path nor the class loop");
     const SpecGuard gr = first ? g : SpecGuard{nullptr, 0, 0, 0};
@@ -1262,8 +1268,9 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
       const int cls_F = c->cls_slot(spec);
       c->ev_begin(&ea);
       launch_cls_place(c->N, c->P, c->cfg, spec, cls_F, (int)c->aff_slot_D[cls_F] + 1, (int)t, run, c->keys, c->stat,
-                       c->cls_lvl, c->cls_amax, c->cls_coff[cls_F], c->cls_mem[cls_F], js, first, job->ready_num,
-                       job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr, c->stream);
+                       c->cls_lvl, c->cls_amax, c->cls_coff[cls_F], c->cls_mem[cls_F], c->cls_cbest, js, first,
+                       job->ready_num, job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, gr,
+                       c->stream);
       c->ev_end(ea, KB_KERNEL_CLS_PLACE, 0);
       c->stats.cls_runs++;
     } else if (dyn) {
@@ -1302,7 +1309,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                        job->min_available, job->gang_ready, hout_dev, hjs_dev, ++c->seq, c->stream, gr,
                        one_run ? c->commits[si] : nullptr, ov ? c->commits[si ^ 1] : nullptr,
                        ov ? (const JobState*)c->slot[si ^ 1].d : nullptr, ov ? c->sweep_ctr + si : nullptr,
-                       c->sweep_target[si]);
+                       c->sweep_target[si], sel_pl ? 1 : 0);
       c->ev_end(ea, KB_KERNEL_SEL_PLACE, 0);
       listed = one_run;
     } else if (traj) {
@@ -1326,7 +1333,9 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                         c->stream);
       c->ev_end(ea, KB_KERNEL_PLACE, 0);  // pairs filled in from the placements below
     }
-    if (aff && (!dyn || cls) && c->spec_incr[spec])  // this run's commits update the affinity tables
+    // this run's commits update the affinity tables (the class loop and the per-task loops apply them themselves,
+    // and so does the selection kernel when sel_pl)
+    if (aff && !dyn && !sel_pl && c->spec_incr[spec])
       launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, 0, c->stream);
     t = e;
   }

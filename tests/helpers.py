@@ -121,6 +121,14 @@ def plain_edge_cluster(seed=7):
         if i == 11:
             nd.conditions.append({"type": "MemoryPressure", "status": "True"})
             nd.conditions.append({"type": "DiskPressure", "status": "True"})
+    # zero-capacity nodes (the score kernels' capacity-0 branches) and nodes already full on one resource (a
+    # non-zero request at or above the allocatable)
+    for i, alloc in ((13, {m.CPU: 0}), (15, {m.MEMORY: 0}), (17, {m.CPU: 0, m.MEMORY: 0})):  # (odd: no pods)
+        cl.nodes[i].alloc.update(alloc)
+    for i, res in ((19, m.CPU), (21, m.MEMORY)):
+        nd = cl.nodes[i]
+        cl.pods.append(m.Pod(ns="sys", name=f"full{i}", uid=f"sys-full{i}", node=nd.name, phase="Running",
+                             containers=[m.Container(req={res: nd.alloc[res]})]))
     keep = []
     for p in cl.pods:
         plain = not (p.node_selector or p.tolerations or p.affinity or
