@@ -5418,6 +5418,103 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
       uint64_t n_rounds = 0, n_deep = 0;
 #endif
       AFF_STAMP(2);
+      // The merge first in bulk: the picks of a greedy merge of the members' key sequences come out in descending
+      // order of each entry's prefix minimum along its member's sequence (the effective key; entries of different
+      // members never tie: the low byte is the position), one wave maximum per pick over the members' effective
+      // heads. It stops before taking a member's last known entry (the key after it would be a deep key) and at
+      // the bound, a stop rule or the run's end; the rounds below go on from its state (same greedy order).
+      if (!__ballot(enc_bad)) {
+        uint32_t ef[kClsPM][kClsL + 1];  // member j's effective keys from its next pick on (0: none / unknown)
+        uint32_t info[kClsPM];           // node | next pick an Allocate << 30 | next entry is the last known << 31
+        int ptr[kClsPM];
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j) {
+          const uint32_t tie = 255u - (uint32_t)(j * 64 + lane);
+          ef[j][0] = k32[j];
+#pragma unroll
+          for (int i = 0; i < kClsL; ++i)
+            ef[j][i + 1] = i < qn[j] ? umin32(ef[j][i], enc(Lk[j][i], tie)) : 0u;
+          ptr[j] = 0;
+          info[j] = (uint32_t)(nd[j] & 0x3fffffff) | (lev[j] < am[j] ? 1u << 30 : 0u) | (qn[j] <= 0 ? 1u << 31 : 0u);
+        }
+        const int t_left = __builtin_amdgcn_readfirstlane(t_count - t);
+        for (;;) {
+          took = __builtin_amdgcn_readfirstlane(took);
+          placed = __builtin_amdgcn_readfirstlane(placed);
+          pb_n = __builtin_amdgcn_readfirstlane(pb_n);
+          ready = __builtin_amdgcn_readfirstlane(ready);
+          uint32_t h = ef[0][0];
+#pragma unroll
+          for (int j = 1; j < kClsPM; ++j) h = umax32(h, ef[j][0]);
+          const uint32_t m = wave_max32_dpp(h);
+          if (m < 256u) break;  // (the rounds end the phase there too)
+          int jw = kClsPM - 1;
+          uint64_t hit = 0;
+#pragma unroll
+          for (int j = kClsPM - 1; j >= 0; --j) {
+            const uint64_t b = __ballot(ef[j][0] == m);
+            if (b) jw = j, hit = b;
+          }
+          const int wl = (int)__builtin_ctzll(hit);
+          uint32_t isel = info[0];
+#pragma unroll
+          for (int j = 1; j < kClsPM; ++j) isel = j == jw ? info[j] : isel;
+          const uint32_t wi = (uint32_t)__builtin_amdgcn_readlane((int)isel, wl);
+          if (wi >> 31) break;  // its last known entry: the rounds take it (and its deep keys)
+          const int kind = (wi >> 30) & 1u ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
+          pbs[pb_n] = (wi & 0x3fffffffu) | ((uint32_t)kind << 30);  // (every lane the same word)
+          cR += incR;
+          mx = cR > mx ? cR : mx;
+          ++took;
+          ++placed;
+          ++pb_n;
+          ready += kind == KB_PLACE_ALLOCATE ? 1 : 0;
+          if (pb_n == pb_cap) {
+            wave_sync_lds();
+            for (int k0 = 0; k0 < pb_n; k0 += 64) {
+              const int k = k0 + lane;
+              if (k < pb_n) {
+                const uint32_t e = pbs[k];
+                hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+                hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+              }
+            }
+            wave_sync_lds();
+            pb_base += pb_n;
+            pb_n = 0;
+          }
+          // the winner's lane advances: its effective keys shift by one, its pick count and info follow
+          const bool me = lane == wl;
+#pragma unroll
+          for (int j = 0; j < kClsPM; ++j)
+            if (j == jw) {
+#pragma unroll
+              for (int i = 0; i < kClsL; ++i) ef[j][i] = me ? ef[j][i + 1] : ef[j][i];
+              ef[j][kClsL] = me ? 0u : ef[j][kClsL];
+              ptr[j] += me ? 1 : 0;
+              info[j] = (uint32_t)(nd[j] & 0x3fffffff) | (lev[j] + ptr[j] < am[j] ? 1u << 30 : 0u) |
+                        (ptr[j] >= qn[j] ? 1u << 31 : 0u);
+            }
+          const bool rdy = !gang || ready >= minav;  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+          stop = rdy ? KB_STOP_READY : stop;
+          stopped = rdy ? 1 : stopped;
+          if (rdy || took == t_left) {
+            done = true;
+            break;
+          }
+        }
+        // the members' state for the rounds: commits in this phase, in this run, and the actual next key
+#pragma unroll
+        for (int j = 0; j < kClsPM; ++j)
+          if (ptr[j] > 0) {
+            cc[j] += ptr[j];
+            lev[j] += ptr[j];
+            k32[j] = s_phq[(j * 64 + lane) * kClsL + ptr[j] - 1];
+          }
+#ifdef KB_DIAG_AFF
+        if (done) why = 3;
+#endif
+      }
       // Each round: one wave reduction finds the winner and the runner-up; the winner then takes picks as long as
       // its next key stays above the runner-up's (a node keeps its score for several pods: LR / BRA move in steps),
       // each pick scalar work on its queue, read once into a register across the lanes.
@@ -5465,22 +5562,34 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
         for (;;) {  // the winner's stretch (its deep keys computed between the inner loop's passes)
           bool need_deep = false;
           for (;;) {
+            // (wave-uniform loop state, stated as such, and one exit test: the loop branches on scalars)
+            c = __builtin_amdgcn_readfirstlane(c);
+            took = __builtin_amdgcn_readfirstlane(took);
+            placed = __builtin_amdgcn_readfirstlane(placed);
+            pb_n = __builtin_amdgcn_readfirstlane(pb_n);
+            ready = __builtin_amdgcn_readfirstlane(ready);
+            dh = __builtin_amdgcn_readfirstlane(dh);
+            dh_rel0 = __builtin_amdgcn_readfirstlane(dh_rel0);
+            const int t_left = __builtin_amdgcn_readfirstlane(t_count - t);
             // the pick: Session.Allocate while InitResreq fits Idle, then Pipeline (the run-start A: the closed form)
             const int kind = lw + c < aw ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
-            if (lane == 0) pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);
+            pbs[pb_n] = (uint32_t)wn | ((uint32_t)kind << 30);  // (every lane the same word)
             cR += incR;
             mx = cR > mx ? cR : mx;  // (phase_ok: the min stays 0, the max follows R or stays)
             ++c;
             ++took;
             ++placed;
             ++pb_n;
-            if (kind == KB_PLACE_ALLOCATE) ++ready;
+            ready += kind == KB_PLACE_ALLOCATE ? 1 : 0;
             if (pb_n == pb_cap) {
               wave_sync_lds();
-              for (int k = lane; k < pb_n; k += 64) {
-                const uint32_t e = pbs[k];
-                hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-                hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+              for (int k0 = 0; k0 < pb_n; k0 += 64) {
+                const int k = k0 + lane;
+                if (k < pb_n) {
+                  const uint32_t e = pbs[k];
+                  hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+                  hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+                }
               }
               wave_sync_lds();
               pb_base += pb_n;
@@ -5488,23 +5597,20 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
             }
             // its next key: after rel phase commits -- queue entry rel - 1 (lane c - 1 of hq), else the deep keys
             const int rel = cw0 + c;
-            if (rel - 1 < qw) {
-              nk = (uint32_t)__builtin_amdgcn_readlane((int)hq, c - 1);
-            } else if (wn == dh && rel - 1 - dh_rel0 < 64) {
-              nk = (uint32_t)__builtin_amdgcn_readlane((int)dk32, rel - 1 - dh_rel0);
-            } else {
-              need_deep = true;
-              break;
-            }
-            if (!gang || ready >= minav) {  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
-              stop = KB_STOP_READY;
-              stopped = 1;
-              stop_now = true;
-            }
-            if (t + took == t_count) stop_now = true;
-            if (!stop_now && nk > m2 && nk >= 256u) continue;  // it still beats every other member
-            break;
+            const int iq = rel - 1, id = rel - 1 - dh_rel0;
+            const uint32_t nq = (uint32_t)__builtin_amdgcn_readlane((int)hq, (c - 1) & 63);
+            const uint32_t nd = (uint32_t)__builtin_amdgcn_readlane((int)dk32, id & 63);
+            const bool inq = iq < qw;
+            need_deep = !inq && !(wn == dh && id < 64);
+            nk = inq ? nq : nd;
+            const bool rdy = !gang || ready >= minav;  // ssn.JobReady(job) (allocate.go:184-187; gang.go:122-125)
+            stop = rdy ? KB_STOP_READY : stop;
+            stopped = rdy ? 1 : stopped;
+            stop_now = rdy || took == t_left;
+            // it still beats every other member: the next pick is its own
+            if (need_deep || stop_now || nk <= m2 || nk < 256u) break;
           }
+          AFF_STAMP(4);
           if (!need_deep) break;
           // past the sweep's levels: its next 64 keys from its row (lane l: the key after rel + l phase commits)
           AFF_STAMP(4);
