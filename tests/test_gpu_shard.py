@@ -65,6 +65,7 @@ def _rank_main(rank, world, port, q, peer=False):
         return b"".join(bytes(o.tolist()) for o in outs)
 
     res = {}
+    name = None
     try:
         for name, cl in _cases().items():
             snap = E.Snapshot(cl)
@@ -76,7 +77,7 @@ def _rank_main(rank, world, port, q, peer=False):
                 ctx.close()
         q.put((rank, res, None))
     except Exception as e:  # report, do not hang the parent
-        q.put((rank, None, repr(e)))
+        q.put((rank, None, f"{name}: {e!r}"))
     finally:
         dist.destroy_process_group()
 
@@ -106,13 +107,15 @@ def test_sharded_equals_one_gpu(world, exchange):
     procs = [ctxm.Process(target=_rank_main, args=(r, world, port, q, exchange == "peer")) for r in range(world)]
     for p in procs:
         p.start()
-    got = {}
-    for _ in range(world):
+    got, errs = {}, []
+    for _ in range(world):  # every rank's outcome before judging (a stalled peer shows in the others' errors)
         rank, res, err = q.get(timeout=240)
-        assert err is None, f"rank {rank}: {err}"
+        if err is not None:
+            errs.append(f"rank {rank}: {err}")
         got[rank] = res
     for p in procs:
         p.join(timeout=60)
+    assert not errs, "\n".join(errs)
     for r in range(world):
         for name in ref:
             assert got[r][name] == ref[name], (world, r, name)
