@@ -496,6 +496,9 @@ EVAL_SPECS, EVAL_NODES = 256, 50000
 EVAL_OUT_BYTES = 8  # kb_eval32: u32 reason mask + i32 score per (spec, node)
 
 
+EVAL_WARMUP, EVAL_TIMED = 200, 20
+
+
 def eval_side(device):
     """The fit/score sweep on its own (kb_eval): reasons + scores of EVAL_SPECS specs x
     EVAL_NODES nodes (a C2-shaped table, one spec per job), through kb_eval32. HIP events around the kernel;
@@ -507,9 +510,13 @@ def eval_side(device):
         ctx = runtime.Context(device, timing=True)
         ctx.upload(snap)
         ids = (np.arange(EVAL_SPECS) % len(snap.spec_arr)).astype(np.int32)  # (equal requests share a spec)
-        ctx.eval32(ids)  # warm-up
+        # warm-up long enough for the card's power management to leave the idle memory / clock state the allocate
+        # cycles left it in (a few launches after the cycles ran 47 us against 33-36 us in a process that ran
+        # kb_eval only: DESIGN.md §4), then the timed launches
+        for _ in range(EVAL_WARMUP):
+            ctx.eval32(ids)
         ctx.stats(reset=True)
-        for _ in range(5):
+        for _ in range(EVAL_TIMED):
             ctx.eval32(ids)
         st = ctx.stats()
         ctx.close()
