@@ -5465,7 +5465,9 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #pragma unroll
           for (int j = 1; j < kClsPM; ++j) isel = j == jw ? info[j] : isel;
           const uint32_t wi = (uint32_t)__builtin_amdgcn_readlane((int)isel, wl);
-          if (wi >> 31) break;  // its last known entry: the rounds take it (and its deep keys)
+          // its last known entry: the rounds take it (and its deep keys); a full placement buffer: the rounds
+          // flush it (no flush code here, so the loop keeps its few scalars in registers)
+          if ((wi >> 31) || pb_n == pb_cap) break;
           const int kind = (wi >> 30) & 1u ? KB_PLACE_ALLOCATE : KB_PLACE_PIPELINE;
           pbs[pb_n] = (wi & 0x3fffffffu) | ((uint32_t)kind << 30);  // (every lane the same word)
           cR += incR;
@@ -5474,20 +5476,6 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
           ++placed;
           ++pb_n;
           ready += kind == KB_PLACE_ALLOCATE ? 1 : 0;
-          if (pb_n == pb_cap) {
-            wave_sync_lds();
-            for (int k0 = 0; k0 < pb_n; k0 += 64) {
-              const int k = k0 + lane;
-              if (k < pb_n) {
-                const uint32_t e = pbs[k];
-                hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
-                hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
-              }
-            }
-            wave_sync_lds();
-            pb_base += pb_n;
-            pb_n = 0;
-          }
           // the winner's lane advances: its effective keys shift by one, its pick count and info follow
           const bool me = lane == wl;
 #pragma unroll
@@ -5516,6 +5504,20 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
             lev[j] += ptr[j];
             k32[j] = s_phq[(j * 64 + lane) * kClsL + ptr[j] - 1];
           }
+        if (pb_n == pb_cap) {  // (the rounds write pbs[pb_n] before they test for a full buffer)
+          wave_sync_lds();
+          for (int k0 = 0; k0 < pb_n; k0 += 64) {
+            const int k = k0 + lane;
+            if (k < pb_n) {
+              const uint32_t e = pbs[k];
+              hout[2 * (pb_base + k)] = (int32_t)(e & 0x3fffffffu);
+              hout[2 * (pb_base + k) + 1] = (int32_t)(e >> 30);
+            }
+          }
+          wave_sync_lds();
+          pb_base += pb_n;
+          pb_n = 0;
+        }
 #ifdef KB_DIAG_AFF
         if (done) why = 3;
 #endif

@@ -452,8 +452,10 @@ class Context:
         k = res.n_placed
         return nodes[:k].copy(), kinds[:k].copy(), res
 
-    def allocate(self, snap: E.Snapshot):
-        """kb_allocate: allocateAction.Execute over the uploaded snapshot."""
+    def allocate(self, snap: E.Snapshot, out: dict | None = None):
+        """kb_allocate: allocateAction.Execute over the uploaded snapshot. `out`: the result dict of an earlier
+        call on a session of the same size, whose arrays this cycle overwrites (a serving loop's reused result
+        buffers: no fresh pages per cycle); by default new arrays."""
         nt, nj = len(snap.session_tasks), len(snap.jobs)
         key = (id(snap),) + tuple(id(getattr(snap, a)) for a in SESSION_ARRAYS)
         cached = getattr(self, "_ssn_cache", None)
@@ -462,10 +464,14 @@ class Context:
         else:
             ssn = self._session_struct(snap, nt, nj)
             self._ssn_cache = (key, ssn, self._ssn_keep)
-        out = {"task_node": np.zeros(max(nt, 1), np.int32), "task_status": np.zeros(max(nt, 1), np.int32),
-               "job_fail_task": np.zeros(max(nj, 1), np.int32),
-               "job_reason_hist": np.zeros((max(nj, 1), KB_NUM_REASONS), np.uint32),
-               "event_task": np.zeros(max(nt, 1), np.int32)}
+        if out is not None and len(out["task_node"]) == max(nt, 1) and len(out["job_fail_task"]) == max(nj, 1):
+            out = {k: out[k] for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist", "event_task")}
+            out["event_task"][:] = 0  # (kb_allocate writes the first n_events entries)
+        else:
+            out = {"task_node": np.zeros(max(nt, 1), np.int32), "task_status": np.zeros(max(nt, 1), np.int32),
+                   "job_fail_task": np.zeros(max(nj, 1), np.int32),
+                   "job_reason_hist": np.zeros((max(nj, 1), KB_NUM_REASONS), np.uint32),
+                   "event_task": np.zeros(max(nt, 1), np.int32)}
         res = kb_cycle_result(*[_ptr(out[k]) for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist",
                                                        "event_task")], 0, 0, 0.0, 0.0)
         self._hook()

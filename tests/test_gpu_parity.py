@@ -450,3 +450,21 @@ def test_eval_scores_random_ratios():
         ctx.close()
     for i, s in enumerate(spec_ids):
         assert list(scores[i]) == ref["tasks"][i]["score"], s
+
+
+def test_allocate_reused_result_buffers():
+    """Context.allocate(snap, out=previous): the same arrays as a fresh call, cycle after cycle (restore between)."""
+    snap = E.Snapshot(synth.c2(n_nodes=200, n_jobs=40, tasks_per_job=30, seed=2, fill=0.9))
+    ctx = runtime.Context(0)
+    try:
+        ctx.upload(snap)
+        fresh = ctx.allocate(snap)
+        prev = None
+        for _ in range(3):
+            ctx.restore()
+            prev = ctx.allocate(snap, out=prev)
+            for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist", "event_task"):
+                assert np.array_equal(prev[k], fresh[k]), k
+            assert prev["n_events"] == fresh["n_events"]
+    finally:
+        ctx.close()
