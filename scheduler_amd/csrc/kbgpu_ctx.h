@@ -53,6 +53,8 @@ struct kb_ctx {
   uint32_t* cmax32 = nullptr;  // [ceil(n/64)]
   uint32_t* amax = nullptr;    // [n] allocations before Idle stops fitting
   int idx_bits = 0;
+  std::vector<std::vector<uint32_t>> aff_rd, aff_wr;  // per spec: affinity inputs its sweep reads / its commits write
+  int prev_run_spec = -1;                              // the listed previous job's spec (aff_sweep_indep)
   std::vector<char> spec_traj_ok;  // per spec: score range fits the 32-bit key
   std::vector<int64_t> spec_pref_weight;
   std::vector<char> spec_ipa_err;   // per spec: KB_SPEC_IPA_ERROR (the batch score errors: 64-bit keys)

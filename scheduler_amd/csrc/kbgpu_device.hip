@@ -2306,7 +2306,15 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   if (tid == 0) publish_diag(hjs, dg, __builtin_amdgcn_s_memrealtime() - rt0);
 #endif
   if (tid == 0) sh.lo = LoopOut{stop, fail_task, placed, ready, minav, gang, panic, stopped, 0, 0, 0, 0};
-  // every wave's host-buffer and row stores are complete before the barrier; one lane then releases
+  // an affinity spec's commits into the global tables, after the whole run (a cap-1 run's closed form and its
+  // later segments' keys read the tables as of the run's start) and before the publish: once the host has read
+  // this job, its tables are final (a later job's sweep may start on the other stream then)
+  if (pl != nullptr) {
+    __syncthreads();
+    for (int k = tid; k < sh.lo.placed - t_begin; k += kSelThreads)
+      apply_commit_tables(P.A, sp, (int)(pl[k] & 0x7fffffffu), (int)(pl[k] >> 31), 1);
+  }
+  // every wave's host-buffer, row and table stores are complete before the barrier; one lane then releases
   // at system scope and publishes (the host spins on the sequence number)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2315,11 +2323,6 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
     publish_state(js, hjs, sh.lo.stopped, sh.lo.stop, sh.lo.fail_task, sh.lo.placed, sh.lo.ready, sh.lo.minav,
                   sh.lo.gang, sh.lo.panic, seq);
   }
-  // an affinity spec's commits into the global tables, after the whole run (a cap-1 run's closed form and its
-  // later segments' keys read the tables as of the run's start); the next kernel on the stream sees them
-  if (pl != nullptr)
-    for (int k = tid; k < sh.lo.placed - t_begin; k += kSelThreads)
-      apply_commit_tables(P.A, sp, (int)(pl[k] & 0x7fffffffu), (int)(pl[k] >> 31), 1);
 }
 
 // ===========================================================================

@@ -577,10 +577,23 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   c->spec_incr.assign(a->m, 0);
   c->spec_aff_reg.assign(a->m, 0);
   c->spec_aff_err.assign(a->m, 0);
+  c->aff_rd.assign(a->m, {});
+  c->aff_wr.assign(a->m, {});
   for (uint32_t s = 0; s < a->m; ++s) {
     const int32_t ac = specs[s].aff_class;
     if (ac < -1 || ac >= (int32_t)a->m) return fail(c, KB_E_INVALID, "spec %u aff_class %d", s, ac);
     if (ac >= 0) {
+      // what a sweep of this spec reads (check tables, its histograms) and what its commits write (lister tables,
+      // histogram increments): histograms as h_off | 1 << 31
+      const kb_aff_spec& x = a->specs[ac];
+      auto& rd = c->aff_rd[s];
+      auto& wr = c->aff_wr[s];
+      for (uint32_t i = 0; i < x.check_cnt; ++i) rd.push_back((uint32_t)a->checks[x.check_off + i].table);
+      for (uint32_t i = 0; i < x.hist_cnt; ++i) rd.push_back(a->hists[x.hist_off + i].h_off | 1u << 31);
+      for (uint32_t i = 0; i < x.lister_cnt; ++i) wr.push_back((uint32_t)a->lister[x.lister_off + i]);
+      for (uint32_t i = 0; i < x.incr_cnt; ++i) wr.push_back(a->incr[x.incr_off + i].h_off | 1u << 31);
+      std::sort(rd.begin(), rd.end());
+      std::sort(wr.begin(), wr.end());
       for (uint32_t i = 0; i < a->specs[ac].check_cnt; ++i)
         if (a->checks[a->specs[ac].check_off + i].kind == KB_AFF_ERROR) c->spec_aff_err[s] = 1;
       c->spec_dyn[s] = (a->specs[ac].flags & KB_AFF_SELF_DYNAMIC) != 0;
@@ -1218,6 +1231,21 @@ static uint32_t slots_cap(const kb_ctx* c) {
   return cap;
 }
 
+// The commits of a run of spec a leave every input of a sweep of spec b as it was (the affinity tables b's checks
+// and histograms read are not among those a's commits write), so b's sweep may overlap a's place kernel.
+static bool aff_sweep_indep(const kb_ctx* c, int a, int b) {
+  if (a < 0 || b < 0 || (size_t)a >= c->aff_wr.size() || (size_t)b >= c->aff_rd.size()) return a < 0;
+  const auto& w = c->aff_wr[a];
+  const auto& r = c->aff_rd[b];
+  size_t i = 0, j = 0;
+  while (i < w.size() && j < r.size()) {
+    if (w[i] == r[j]) return false;
+    if (w[i] < r[j]) ++i;
+    else ++j;
+  }
+  return true;
+}
+
 // A self-dependent spec the class loop takes (classify_self_dynamic; its LDS plan fits).
 static bool cls_run_ok(const kb_ctx* c, int spec) {
   const int F = c->cls_slot(spec);
@@ -1237,6 +1265,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
   memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
   int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
   bool listed = false;
+  int run_spec = -1;
   uint32_t t = 0;
   while (t < job->n_tasks) {
     uint32_t e = t + 1;
@@ -1287,14 +1316,18 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
       if (aff && c->spec_dyn[spec]) c->stats.cap1_runs++;
       uint32_t* kt = c->sel_keys[si];
       uint64_t* st = c->sel_stat[si];
-      // A job that is one run without inter-pod terms lists the rows it commits. When the previous job
-      // (the other slot) did, this run's level-0 sweep goes to stream_b right after the job before that
-      // one, overlapping the previous job's place kernel, and the place kernel re-keys that job's rows.
-      const bool one_run = !aff && t == 0 && e == job->n_tasks;
-      const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1);
+      // A job that is one run (without InterPodAffinity histograms -- their normalisation is a pass of its own
+      // before the sweep -- and applying its own table commits before it publishes) lists the rows it commits. When the previous job (the other slot) did, and its
+      // commits leave this spec's affinity inputs alone (aff_sweep_indep: the tables its checks and histograms
+      // read), this run's level-0 sweep goes to stream_b right after the job before that one, overlapping the
+      // previous job's place kernel, and the place kernel re-keys that job's rows.
+      const bool one_run = !(aff && (c->spec_hist[spec] || (c->spec_incr[spec] && !sel_pl))) && t == 0 &&
+                           e == job->n_tasks;
+      const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1) &&
+                      (!aff || aff_sweep_indep(c, c->prev_run_spec, spec));
       if (ov) {
         c->ev_begin(&ea, c->stream_b);
-        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, false, c->stream_b,
+        launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, aff, c->stream_b,
                          SpecGuard{nullptr, 0, 0, 0}, c->sweep_ctr + si);
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
         c->sweep_target[si] += (uint32_t)((c->N.n + 63) / 64);
@@ -1312,6 +1345,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
                        c->sweep_target[si], sel_pl ? 1 : 0);
       c->ev_end(ea, KB_KERNEL_SEL_PLACE, 0);
       listed = one_run;
+      run_spec = spec;
     } else if (traj) {
       const int J = std::min(run, kTrajDefaultJ);
       c->ev_begin(&ea);
@@ -1341,6 +1375,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
   }
   HIP_OK(c, hipGetLastError());
   c->prev_listed = listed;
+  c->prev_run_spec = listed ? run_spec : -1;
   c->prev_slot = si;
   S.seq = c->seq;
   S.ev_e = c->pending.size();

@@ -12,6 +12,6 @@ step() {
   echo "=== $name rc=$rc"; tail -n 2 "gpurun_out/${TAG}_$name.log" | cut -c1-400
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step tests 600 python -u -m pytest -m gpu -v -s -rf -p no:cacheprovider --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_digest.py -k "reused or variants or affinity or C4 or C2"
+step tests 600 python -u -m pytest -m gpu -v -s -rf -p no:cacheprovider --timeout 240 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_digest.py -k "reused or variants or affinity or C4 or C2 or pipeline or e2e"
 step bench_C2 300 python bench.py --steps 20 --warmup 2 --no-eval --no-cpu-baseline
 step bench_C4 300 python bench.py --config C4 --steps 5 --warmup 1 --no-cpu-baseline --no-eval
