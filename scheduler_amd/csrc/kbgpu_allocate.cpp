@@ -394,7 +394,17 @@ struct Driver {
   double loop_ms = 0;  // KB_HOST_TRACE: time in the job loop of run()
   GoHeap<int> qheap;
   std::vector<GoHeap<int>> jheaps;
-  std::vector<std::vector<int>> job_pending;
+  // each job's Pending tasks in task order, as one CSR array (job j: pend[pend_off[j] .. pend_off[j + 1]))
+  std::vector<int> pend;
+  std::vector<uint32_t> pend_off;
+  struct Span {
+    const int* b;
+    const int* e;
+    const int* begin() const { return b; }
+    const int* end() const { return e; }
+    size_t size() const { return (size_t)(e - b); }
+  };
+  Span job_pending(int j) const { return Span{pend.data() + pend_off[j], pend.data() + pend_off[j + 1]}; }
   std::vector<int32_t> specs, pn, pk;
   std::vector<uint32_t> node_reasons;  // NO_FIT hook
   int hook_rc = KB_OK;
@@ -404,8 +414,8 @@ struct Driver {
   void build_pending(int j) {  // allocate.go:114-129 (BestEffort tasks skipped)
     JobS& js = jobs[j];
     if (js.pending_built) return;
-    js.pending.reserve(job_pending[j].size());
-    for (int t : job_pending[j])
+    js.pending.reserve(job_pending(j).size());
+    for (int t : job_pending(j))
       if (!task_res_empty(t)) js.pending.push_back(t);
     std::sort(js.pending.begin(), js.pending.end(), [this](int a, int b) { return task_less(a, b); });
     js.pending_built = true;
@@ -592,6 +602,7 @@ struct Driver {
   }
 
   int run() {
+    const auto r0 = std::chrono::steady_clock::now();
     qheap.less = [this](const int& a, const int& b) { return queue_less(a, b); };
     sq.less = qheap.less;
     jheaps.assign(s.n_queues, GoHeap<int>());
@@ -600,11 +611,20 @@ struct Driver {
     std::vector<int> jorder(s.n_jobs);
     for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
     std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
-    job_pending.assign(s.n_jobs, {});
-    uint32_t max_pending = 1;
+    pend_off.assign(s.n_jobs + 1, 0);
     for (uint32_t t = 0; t < s.n_tasks; ++t)
-      if (task_status[t] == KB_ST_PENDING) job_pending[s.task_job[t]].push_back((int)t);
-    for (uint32_t j = 0; j < s.n_jobs; ++j) max_pending = std::max<uint32_t>(max_pending, job_pending[j].size());
+      if (task_status[t] == KB_ST_PENDING) ++pend_off[s.task_job[t] + 1];
+    uint32_t max_pending = 1;
+    for (uint32_t j = 0; j < s.n_jobs; ++j) {
+      max_pending = std::max<uint32_t>(max_pending, pend_off[j + 1]);
+      pend_off[j + 1] += pend_off[j];
+    }
+    pend.resize(pend_off[s.n_jobs]);
+    {
+      std::vector<uint32_t> cur(pend_off.begin(), pend_off.end() - 1);
+      for (uint32_t t = 0; t < s.n_tasks; ++t)
+        if (task_status[t] == KB_ST_PENDING) pend[cur[s.task_job[t]]++] = (int)t;
+    }
     for (int j : jorder) {
       if (s.job_pg_pending[j]) continue;                                              // allocate.go:50-52
       if (has[KB_PLUGIN_GANG] && jobs[j].valid < s.job_min_available[j]) continue;  // JobValid, gang.go:48-69
@@ -625,7 +645,7 @@ struct Driver {
     std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
     for (uint32_t j = 0; fed && j < s.n_jobs; ++j) {
       int sp0 = -1;
-      for (int t : job_pending[j]) {
+      for (int t : job_pending(j)) {
         const int sp = s.task_spec[t];
         if (sp == sp0) continue;
         if (task_res_empty(t)) continue;  // BestEffort: never placed by allocate
@@ -645,8 +665,10 @@ struct Driver {
     // node-sharded with the peer exchange only: the fed engine pipelines; any other cycle's jobs go one at a time
     // through the host-staged exchange
     if (!fed && ctx->sharded && !ctx->comm) pipe = false;
+    const auto r1 = std::chrono::steady_clock::now();
     if (fed)
       if (int rc = kb_fed_begin(ctx, max_pending)) return rc;
+    const auto r2 = std::chrono::steady_clock::now();
     struct FedEnd {  // the engine is stopped on every way out of the loop
       kb_ctx* c;
       bool on;
@@ -776,11 +798,15 @@ struct Driver {
       fprintf(stderr, "kb_host_trace jobs=%llu speculate_issue_us=%.2f finish_wait_us=%.2f apply_next_us=%.2f\n",
               (unsigned long long)n_iter, t_spec / n_iter, t_fin / n_iter, t_apply / n_iter);
     out->n_events = n_events;
+    const auto r3 = std::chrono::steady_clock::now();
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
     if (fed) {
       fed_end.on = false;
       if (int rc = kb_fed_end(ctx)) return rc;
     }
+    if (trace)
+      fprintf(stderr, "kb_host_trace pre_ms=%.3f fed_begin_ms=%.3f post_ms=%.3f\n", us(r0, r1) * 1e-3,
+              us(r1, r2) * 1e-3, us(r3, clk::now()) * 1e-3);
     return KB_OK;
   }
 };
