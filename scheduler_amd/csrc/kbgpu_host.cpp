@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <cstdarg>
@@ -243,6 +244,8 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->fed_coop = c->fed_dedicated && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
   c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
+  c->shard_small = (fl & KB_OPT_SHARD_SMALL_BLOCKS) != 0;
+  c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
   if (opts && opts->eval_spb > 0) c->eval_spb = opts->eval_spb;
   if (opts) c->shard_epoch0 = opts->shard_epoch0;
@@ -916,6 +919,14 @@ int kb_set_shard(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) 
 // The node-sharded fed engine's exchange: this rank's inbox in its GPU's memory (uncached: peers write it over
 // xGMI and the engine polls it), its IPC handle all-gathered through fn, the peers' inboxes opened. fn stays the
 // host-staged exchange of jobs the engine does not run.
+// The next epoch no node-sharded context of this process has used (every rank's contexts advance it alike).
+static std::atomic<uint32_t> g_peer_epoch_next{0};
+static void note_peer_epoch(uint32_t next) {
+  uint32_t cur = g_peer_epoch_next.load();
+  while (next > cur && !g_peer_epoch_next.compare_exchange_weak(cur, next)) {
+  }
+}
+
 int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) {
   if (int rc = kb_set_shard(c, sh, fn, user)) return rc;
   const size_t bytes = shard_inbox_bytes();
@@ -932,11 +943,20 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
     c->peer_inbox[w] = nullptr;
   }
   const int W = sh->world;
-  std::vector<hipIpcMemHandle_t> h((size_t)W + 1);
+  // with the handle, each rank's next unused epoch in this process: the context starts past every rank's, so the
+  // words an earlier context of these processes left in recycled inbox memory never carry a current tag
+  struct PeerHello {
+    hipIpcMemHandle_t h;
+    uint32_t epoch, pad;
+  };
+  std::vector<PeerHello> h((size_t)W + 1);
+  h[0].epoch = g_peer_epoch_next.load();
+  uint32_t start = h[0].epoch;
   if (W > 1) {
-    HIP_OK(c, hipIpcGetMemHandle(&h[0], c->inbox));
-    if (int rc = fn(user, &h[0], &h[1], sizeof(hipIpcMemHandle_t)))
+    HIP_OK(c, hipIpcGetMemHandle(&h[0].h, c->inbox));
+    if (int rc = fn(user, &h[0], &h[1], sizeof(PeerHello)))
       return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the inbox handles", rc);
+    for (int w = 0; w < W; ++w) start = std::max(start, h[1 + w].epoch);
   }
   for (int w = 0; w < W; ++w) {
     if (w == sh->rank) {
@@ -944,12 +964,13 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
       continue;
     }
     void* p = nullptr;
-    const hipError_t e = hipIpcOpenMemHandle(&p, h[1 + w], hipIpcMemLazyEnablePeerAccess);
+    const hipError_t e = hipIpcOpenMemHandle(&p, h[1 + w].h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) return fail(c, KB_E_HIP, "hipIpcOpenMemHandle (rank %d's inbox): %s", w, hipGetErrorString(e));
     c->peer_inbox[w] = p;
   }
   c->peer = true;
-  c->shard_epoch = c->shard_epoch0;
+  c->shard_epoch = c->shard_epoch0 ? c->shard_epoch0 : start;  // (an explicit start: the epoch-wrap tests)
+  note_peer_epoch(c->shard_epoch + 1);
   return KB_OK;
 }
 
@@ -1231,6 +1252,12 @@ static uint32_t slots_cap(const kb_ctx* c) {
   return cap;
 }
 
+// The split (and node-sharded) engine takes this context's table (shard_small_blocks: sharded blocks of any size,
+// for the small-block divergence diagnosis).
+static bool split_ok(const kb_ctx* c) {
+  return fed_split_ok(c->N.n, c->sharded) || (c->sharded && c->shard_small && c->N.n > 0 && fed_nsel(c->N.n) > 0);
+}
+
 // The commits of a run of spec a leave every input of a sweep of spec b as it was (the affinity tables b's checks
 // and histograms read are not among those a's commits write), so b's sweep may overlap a's place kernel.
 static bool aff_sweep_indep(const kb_ctx* c, int a, int b) {
@@ -1396,6 +1423,10 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
   // pipelined, so issue-to-finish walls would count the overlap twice)
   const double wall =
       S.issue_ms + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count();
+  if (c->issue_trace && c->fed)
+    fprintf(stderr, "kb_finish rank=%d seq=%u slot=%d skipped=%d placed=%d stop=%d ready=%d stopped=%d\n",
+            c->sharded ? c->shard.rank : 0, S.seq, si, skipped ? 1 : 0, hs->n_placed, hs->stop, hs->ready_num,
+            hs->stopped);
   if (hs->stall == 2)
     return fail(c, KB_E_STATE, "node-sharded ranks exchanged different segments (their drivers diverged)");
   if (hs->stall)
@@ -1483,7 +1514,7 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
   if ((c->sharded && !c->peer) || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
-  if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n, c->sharded))) return 0;  // the sharded engine is the split one
+  if (c->sharded && !(c->use_fed_split && split_ok(c))) return 0;  // the sharded engine is the split one
   const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
   if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
   if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
@@ -1494,11 +1525,11 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
 
 int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return 0;
-  if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) &&
+  if (c->sharded && !(c->peer && c->use_fed_split && split_ok(c) &&
                       max_job_tasks <= (uint32_t)kFedSplitMaxTasks))
     return 0;
   const int ns = fed_nsel(c->N.n);
-  return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
+  return ns == 1 || (ns > 1 && c->use_fed_split && split_ok(c) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
 }
 
 int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
@@ -1510,6 +1541,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c->slot[kJobSlots - 1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
   if (!c->fed_ring) {
     HIP_OK(c, hipMalloc(&c->fed_ring, fed_ring_bytes()));
+    HIP_OK(c, hipMemset(c->fed_ring, 0, fed_ring_bytes()));  // (recycled memory: no earlier context's commands)
     HIP_OK(c, hipMalloc((void**)&c->fed_ctr, kJobSlots * sizeof(uint32_t)));
     HIP_OK(c, hipMalloc((void**)&c->fed_exit, sizeof(int32_t)));
     HIP_OK(c, hipMemset(c->fed_ctr, 0, kJobSlots * sizeof(uint32_t)));
@@ -1536,7 +1568,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     c->timing_now = tn;
   }
   void* xchg = nullptr;
-  if (c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
+  if (c->use_fed_split && split_ok(c) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
     if (!c->fed_xchg) HIP_OK(c, hipMalloc(&c->fed_xchg, fed_xchg_bytes()));
     HIP_OK(c, hipMemsetAsync(c->fed_xchg, 0, fed_xchg_bytes(), c->stream));  // job numbers restart per cycle
     xchg = c->fed_xchg;
@@ -1553,6 +1585,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     if (((c->shard_epoch + 1) & ((1u << kShardEpochBits) - 1)) == 0)
       if (int rc = shard_inbox_rezero(c)) return rc;
     SP.epoch = ++c->shard_epoch;
+    note_peer_epoch(c->shard_epoch + 1);
     SP.self_inbox = c->shard_self_inbox ? 1 : 0;
     c->stats.fed_sharded++;
   }
@@ -1688,6 +1721,10 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
                  job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
                  pred ? pred->ready : 0, ++c->seq};
+    if (c->issue_trace)
+      fprintf(stderr, "kb_issue rank=%d seq=%u slot=%d spec=%d tasks=%u guard=%d stop=%d placed=%d ready=%d\n",
+              c->sharded ? c->shard.rank : 0, c->seq, slot, job->task_specs[0], job->n_tasks, pred ? 1 : 0,
+              pred ? pred->stop : 0, pred ? pred->placed : 0, pred ? pred->ready : 0);
     S.ev_b = c->pending.size();
     if (int rc = fed_post(c, a, slot, true)) return rc;
     S.ev_e = c->pending.size();
