@@ -31,11 +31,20 @@ def rank_main(rank, world, port, tag, case):
         cases = [n for _ in range(int(os.environ.get("PROBE_REPEAT", "3"))) for n in names + ["backfill"]]
     else:
         cases = [case]
+    if case == "big":  # blocks past kShardEngineMinNodes: C2-shaped clusters, several contexts per process
+        cases = [f"c2big{i}" for i in range(int(os.environ.get("PROBE_REPEAT", "8")))]
     pcs = dict(parity_clusters())
+    from scheduler_amd import synth
+    for i in range(16):
+        pcs[f"c2big{i}"] = None
     bad = 0
     for name in cases:
-        cl = backfill_cluster() if name == "backfill" else pcs[name]
-        snap = E.Snapshot(cl)
+        if name.startswith("c2big"):
+            k = int(name[5:])
+            snap = synth.c2_snapshot(n_nodes=4000 + 300 * k, n_jobs=60, tasks_per_job=40 + k, seed=30 + k,
+                                     fill=0.9 if k % 3 == 2 else None)
+        else:
+            snap = E.Snapshot(backfill_cluster() if name == "backfill" else pcs[name])
         ctx = runtime.Context(0, options={"fed_plain_launch": True, "shard_small_blocks": True})
         try:
             ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
