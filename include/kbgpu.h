@@ -408,7 +408,6 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_OPT_FED_PLAIN_LAUNCH (1u << 12)  /* the engine as a plain launch (ranks sharing one GPU; rocprofv3) */
 #define KB_OPT_SHARD_SELF_INBOX (1u << 13)  /* a rank's own record through its inbox too (exchange tests) */
 #define KB_OPT_FED_DIAG (1u << 14)          /* KB_DIAG builds: print the selector's phase stamps at kb_fed_end */
-#define KB_OPT_SHARD_SMALL_BLOCKS (1u << 15) /* the node-sharded engine on blocks under 1,024 nodes too (diagnosis) */
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2

@@ -165,7 +165,6 @@ struct kb_ctx {
   bool use_pipeline = true;    // !KB_OPT_NO_PIPELINE
   bool shard_self_inbox = false;  // KB_OPT_SHARD_SELF_INBOX
   bool fed_diag = false;       // KB_OPT_FED_DIAG
-  bool shard_small = false;    // KB_OPT_SHARD_SMALL_BLOCKS
   bool issue_trace = false;    // KB_HOST_TRACE: every fed job issue on stderr
   uint64_t fed_idle = 100000000ull;  // the engine's idle exit in s_memrealtime ticks (100 MHz): 1 s
   int eval_spb = 0;            // kb_opts.eval_spb (0: from cus)

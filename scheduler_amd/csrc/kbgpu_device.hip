@@ -3982,14 +3982,9 @@ int fed_nsel(int n) {
 }
 // The placer's candidate keys and nodes (2 x 4 * kSelThreads words) share its key array: n_pad >= 4096.
 // Unsharded tables of one key group stay on the one-workgroup engine; a node-sharded rank's block (the sharded engine
-// is the split one) may be as small as kShardEngineMinNodes: its instance then holds two key groups (n_pad = 4096, so
-// the placer's candidate keys and nodes still fit its key array). Smaller blocks take the launch path: with 8-node
-// blocks on 3 ranks one parity cluster's cycle had the ranks' engines exchange records of different jobs (open,
-// DESIGN.md §8); 1,200-node blocks (test_gpu_shard_peer's c2-small on 3 ranks, C2 on 8 ranks) are covered.
-constexpr int kShardEngineMinNodes = 1024;
-bool fed_split_ok(int n, bool sharded) {
-  return fed_nsel(n) > 0 && (sharded ? n >= kShardEngineMinNodes : n > 4 * kSelThreads);
-}
+// is the split one) may be of any size: its instance then holds two key groups (n_pad = 4096, so the placer's
+// candidate keys and nodes still fit its key array).
+bool fed_split_ok(int n, bool sharded) { return fed_nsel(n) > 0 && (sharded ? n > 0 : n > 4 * kSelThreads); }
 
 size_t shard_inbox_bytes() { return (size_t)2 * kJobSlots * kShardMaxWorld * kShardRecW * sizeof(uint64_t); }
 

@@ -15,6 +15,15 @@
 
 #include "kbgpu_ctx.h"
 
+// hipMemset on device memory runs on the null stream and may return before it is done; the library's kernels run on
+// non-blocking streams, which do not wait for the null stream. So every zeroing waits for itself: a context whose
+// buffers come from memory an earlier context of the process freed must not start a kernel on the old contents
+// (round 4: the fed engine's counters and command ring, recycled, let a node-sharded engine read a stale command).
+static hipError_t memset_sync(void* p, int v, size_t n) {
+  const hipError_t e = hipMemset(p, v, n);
+  return e != hipSuccess ? e : hipStreamSynchronize(nullptr);
+}
+
 using namespace kbgpu;
 
 namespace {
@@ -49,7 +58,7 @@ int upload(kb_ctx* c, std::vector<void*>& owned, T** dst, const T* src, size_t c
     HIP_OK(c, hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
   } else {
     if (count && required) return fail(c, KB_E_INVALID, "missing array of %zu elements", count);
-    HIP_OK(c, hipMemset(p, 0, bytes));
+    HIP_OK(c, memset_sync(p, 0, bytes));
   }
   *dst = (T*)p;
   return KB_OK;
@@ -244,7 +253,6 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->fed_coop = c->fed_dedicated && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
   c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
-  c->shard_small = (fl & KB_OPT_SHARD_SMALL_BLOCKS) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
   if (opts && opts->eval_spb > 0) c->eval_spb = opts->eval_spb;
@@ -420,7 +428,7 @@ int kb_upload_nodes(kb_ctx* c, const kb_nodes* in) {
   HIP_OK(c, hipMalloc(&p, kClsMaxK * sizeof(uint64_t)));
   c->work_mem.push_back(p);
   c->cls_cbest = (uint64_t*)p;
-  HIP_OK(c, hipMemset(p, 0, kClsMaxK * sizeof(uint64_t)));
+  HIP_OK(c, memset_sync(p, 0, kClsMaxK * sizeof(uint64_t)));
   c->idx_bits = 1;  // key index field: global node indices when sharded
   const unsigned long long n_keys = c->sharded ? c->shard.n_total : n;
   while ((1ull << c->idx_bits) < n_keys) ++c->idx_bits;
@@ -892,12 +900,12 @@ static int shard_common(kb_ctx* c, const kb_shard* sh) {
   HIP_OK(c, hipSetDevice(c->device));
   if (!c->d_rec) {
     HIP_OK(c, hipMalloc((void**)&c->d_rec, sizeof(ShardRec)));
-    HIP_OK(c, hipMemset(c->d_rec, 0, sizeof(ShardRec)));
+    HIP_OK(c, memset_sync(c->d_rec, 0, sizeof(ShardRec)));
   }
   if (c->d_rec_all) (void)hipFree(c->d_rec_all);
   c->d_rec_all = nullptr;
   HIP_OK(c, hipMalloc((void**)&c->d_rec_all, sizeof(ShardRec) * (size_t)sh->world));
-  HIP_OK(c, hipMemset(c->d_rec_all, 0, sizeof(ShardRec) * (size_t)sh->world));
+  HIP_OK(c, memset_sync(c->d_rec_all, 0, sizeof(ShardRec) * (size_t)sh->world));
   c->shard = *sh;
   c->sharded = true;
   c->peer = false;  // (kb_set_shard_peer sets it after this)
@@ -936,7 +944,7 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
       HIP_OK(c, hipMalloc(&c->inbox, bytes));
     }
   }
-  HIP_OK(c, hipMemset(c->inbox, 0, bytes));
+  HIP_OK(c, memset_sync(c->inbox, 0, bytes));
   HIP_OK(c, hipDeviceSynchronize());
   for (int w = 0; w < kShardMaxWorld; ++w) {
     if (c->peer_inbox[w] && c->peer_inbox[w] != c->inbox) (void)hipIpcCloseMemHandle(c->peer_inbox[w]);
@@ -988,7 +996,7 @@ static int shard_inbox_rezero(kb_ctx* c) {
   for (int w = 0; w < W; ++w)
     if (tok[1 + w] != tok[0])
       return fail(c, KB_E_STATE, "node-sharded engine: rank %d is at epoch %u, this rank at %u", w, tok[1 + w], tok[0]);
-  HIP_OK(c, hipMemset(c->inbox, 0, shard_inbox_bytes()));
+  HIP_OK(c, memset_sync(c->inbox, 0, shard_inbox_bytes()));
   HIP_OK(c, hipDeviceSynchronize());
   if (int rc = c->ag_fn(c->ag_user, tok.data(), tok.data() + 1, sizeof(uint32_t)))
     return fail(c, KB_E_HIP, "all-gather callback failed (%d) after the inbox re-zeroing", rc);
@@ -1197,7 +1205,7 @@ static int ensure_sel_bufs(kb_ctx* c) {
   }
   if (!c->stream_b) {
     HIP_OK(c, hipMalloc((void**)&c->sweep_ctr, 2 * sizeof(uint32_t)));
-    HIP_OK(c, hipMemset(c->sweep_ctr, 0, 2 * sizeof(uint32_t)));
+    HIP_OK(c, memset_sync(c->sweep_ctr, 0, 2 * sizeof(uint32_t)));
     c->sweep_target[0] = c->sweep_target[1] = 0;
     if (c->fed_dedicated) {  // a hardware queue of its own (kb_ctx::fed_dedicated): a mask of every CU
       hipDeviceProp_t prop;
@@ -1225,7 +1233,7 @@ static int ensure_slots(kb_ctx* c, uint32_t n_tasks, bool all) {
     if (!c->d_jobx[s]) {
       void* p;
       HIP_OK(c, hipMalloc(&p, sizeof(JobState)));
-      HIP_OK(c, hipMemset(p, 0, sizeof(JobState)));
+      HIP_OK(c, memset_sync(p, 0, sizeof(JobState)));
       c->work_mem.push_back(p);
       c->d_jobx[s] = (char*)p;
     }
@@ -1250,12 +1258,6 @@ static uint32_t slots_cap(const kb_ctx* c) {
   uint32_t cap = c->job_cap;
   for (int s = 1; s < kJobSlots; ++s) cap = std::min(cap, c->jobx_cap[s]);
   return cap;
-}
-
-// The split (and node-sharded) engine takes this context's table (shard_small_blocks: sharded blocks of any size,
-// for the small-block divergence diagnosis).
-static bool split_ok(const kb_ctx* c) {
-  return fed_split_ok(c->N.n, c->sharded) || (c->sharded && c->shard_small && c->N.n > 0 && fed_nsel(c->N.n) > 0);
 }
 
 // The commits of a run of spec a leave every input of a sweep of spec b as it was (the affinity tables b's checks
@@ -1514,7 +1516,7 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 int kb_spec_fed_ok(kb_ctx* c, int spec) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
   if ((c->sharded && !c->peer) || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
-  if (c->sharded && !(c->use_fed_split && split_ok(c))) return 0;  // the sharded engine is the split one
+  if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n, c->sharded))) return 0;  // the sharded engine is the split one
   const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
   if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
   if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
@@ -1525,11 +1527,11 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
 
 int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return 0;
-  if (c->sharded && !(c->peer && c->use_fed_split && split_ok(c) &&
+  if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) &&
                       max_job_tasks <= (uint32_t)kFedSplitMaxTasks))
     return 0;
   const int ns = fed_nsel(c->N.n);
-  return ns == 1 || (ns > 1 && c->use_fed_split && split_ok(c) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
+  return ns == 1 || (ns > 1 && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks);
 }
 
 int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
@@ -1541,10 +1543,10 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c->slot[kJobSlots - 1].h || !c->stream_b) return fail(c, KB_E_STATE, "kb_job_reserve first");
   if (!c->fed_ring) {
     HIP_OK(c, hipMalloc(&c->fed_ring, fed_ring_bytes()));
-    HIP_OK(c, hipMemset(c->fed_ring, 0, fed_ring_bytes()));  // (recycled memory: no earlier context's commands)
+    HIP_OK(c, memset_sync(c->fed_ring, 0, fed_ring_bytes()));  // (recycled memory: no earlier context's commands)
     HIP_OK(c, hipMalloc((void**)&c->fed_ctr, kJobSlots * sizeof(uint32_t)));
     HIP_OK(c, hipMalloc((void**)&c->fed_exit, sizeof(int32_t)));
-    HIP_OK(c, hipMemset(c->fed_ctr, 0, kJobSlots * sizeof(uint32_t)));
+    HIP_OK(c, memset_sync(c->fed_ctr, 0, kJobSlots * sizeof(uint32_t)));
     for (int s = 0; s < kJobSlots; ++s) c->fed_count[s] = 0;
   }
   HIP_OK(c, hipMemsetAsync(c->fed_exit, 0, sizeof(int32_t), c->stream));
@@ -1568,7 +1570,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     c->timing_now = tn;
   }
   void* xchg = nullptr;
-  if (c->use_fed_split && split_ok(c) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
+  if (c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
     if (!c->fed_xchg) HIP_OK(c, hipMalloc(&c->fed_xchg, fed_xchg_bytes()));
     HIP_OK(c, hipMemsetAsync(c->fed_xchg, 0, fed_xchg_bytes(), c->stream));  // job numbers restart per cycle
     xchg = c->fed_xchg;
@@ -1691,7 +1693,7 @@ int kb_fed_abandon(kb_ctx* c) {
   }
   HIP_OK(c, hipStreamSynchronize(c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream_b));  // the unserved jobs' sweeps (they only read rows)
-  HIP_OK(c, hipMemset(c->fed_exit, 0, sizeof(int32_t)));
+  HIP_OK(c, memset_sync(c->fed_exit, 0, sizeof(int32_t)));
   for (auto& sl : c->slot) sl.busy = false;
   c->prev_listed = false;
   c->n_fed_abandon++;

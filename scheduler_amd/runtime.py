@@ -137,8 +137,7 @@ KB_OPT_ENGINE = 8
 # path; tests and the profiler name the others through Context(options=...)
 OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6, "no_aff_reg": 1 << 7,
                 "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
-                "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14,
-                "shard_small_blocks": 1 << 15}
+                "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14}
 OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",

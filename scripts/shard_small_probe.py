@@ -1,6 +1,7 @@
-"""Diagnosis of the node-sharded engine on small blocks: the backfill parity cluster's allocate cycle
-on W ranks sharing one GPU, peer exchange, shard_small_blocks on, every fed job issue / finish traced per rank
-(KB_HOST_TRACE) into gpurun_out/<tag>_rank<r>.err. Usage: scripts/shard_small_probe.py <tag> [world] [case]"""
+"""The node-sharded engine across consecutive contexts of one process: allocate cycles on W ranks
+sharing one GPU, peer exchange, every fed job issue / finish traced per rank (KB_HOST_TRACE) into
+gpurun_out/<tag>_rank<r>.err. Cases: one parity cluster, "all" (the sharded parity test's sequence, repeated),
+"fresh" (each context in processes of its own), "big" (C2-shaped clusters of 4k+ nodes). Usage: scripts/shard_small_probe.py <tag> [world] [case]"""
 import os
 import socket
 import sys
@@ -31,7 +32,7 @@ def rank_main(rank, world, port, tag, case):
         cases = [n for _ in range(int(os.environ.get("PROBE_REPEAT", "3"))) for n in names + ["backfill"]]
     else:
         cases = [case]
-    if case == "big":  # blocks past kShardEngineMinNodes: C2-shaped clusters, several contexts per process
+    if case == "big":  # C2-shaped clusters (1.3k+ nodes per rank), several contexts per process
         cases = [f"c2big{i}" for i in range(int(os.environ.get("PROBE_REPEAT", "8")))]
     pcs = dict(parity_clusters())
     from scheduler_amd import synth
@@ -45,7 +46,7 @@ def rank_main(rank, world, port, tag, case):
                                      fill=0.9 if k % 3 == 2 else None)
         else:
             snap = E.Snapshot(backfill_cluster() if name == "backfill" else pcs[name])
-        ctx = runtime.Context(0, options={"fed_plain_launch": True, "shard_small_blocks": True})
+        ctx = runtime.Context(0, options={"fed_plain_launch": True})
         try:
             ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
             ctx.upload(snap)

@@ -91,8 +91,9 @@ def _free_port():
 @pytest.mark.parametrize("exchange", ["host", "peer"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_equals_one_gpu(world, exchange):
-    """Parity clusters (too small for the sharded engine: every job through the launch path) on 2 and 3 ranks.
-    peer: kb_set_shard_peer contexts, whose non-engine cycles go one job at a time over the host-staged exchange."""
+    """Parity clusters on 2 and 3 ranks, one context per cluster in the same processes. host: the launch-path
+    exchange for every job; peer: kb_set_shard_peer contexts -- the node-sharded engine on 8-100-node blocks, and the
+    host-staged exchange for the cycles it does not take."""
     import torch.multiprocessing as mp
     ref = {}
     for name, cl in _cases().items():
