@@ -328,12 +328,17 @@ def roofline_of(st, args, cfg):
                                       f"job at most (see traffic)"),
            "avg_us_per_launch": {K[i]: round(st["kernel_ms"][i] * 1e3 / st["launches"][i], 3)
                                  for i in range(len(K)) if st["launches"][i]},
-           "measured_frac": None}
+           "measured_frac": None,
+           "frac_meaning": ("definitional, not bandwidth: SURVEY.md §8 d3's row bytes of every (task, node) "
+                            "evaluation the launch decides, over its duration; the kernel reads each row at most once "
+                            "per job (the selection's algorithmic saving, DESIGN.md §3), so frac counts avoided work and "
+                            "can exceed 1 (C5). The bandwidth figure is measured_frac (traffic / duration / peak)")}
     full = (args.nodes, args.jobs, args.tasks_per_job) == (cfg["nodes"], cfg["jobs"], cfg["tasks"])
     tr = pmc_cycle_traffic(args.config, K[k]) if full and args.gpus == 1 else None
     if tr is not None:
         out["traffic"] = tr["bytes_per_launch"]
         out["traffic_source"] = tr["source"]
+        out["traffic_is_proxy"] = fed
         out["cycle_traffic_bytes"] = tr["cycle_bytes"]
         if avg_ms > 0:
             out["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
@@ -609,8 +614,10 @@ def pmc_cycle_traffic(config, kernel):
         src = os.path.relpath(f, ROOT)
         if kernel == "fed_engine_kernel":
             return {"bytes_per_launch": round(cyc, 1), "cycle_bytes": round(cyc, 1),
-                    "source": f"{src}: the cycle's kernels (per-job launch path, option no_fed), bytes per dispatch x "
-                              f"dispatches per cycle, summed = one engine launch"}
+                    "source": f"PROXY, not the engine's own counters: {src}: the same cycle on the per-job launch path "
+                              f"(option no_fed; counter collection serialises dispatches, so the resident engine cannot "
+                              f"be fed under it), every cycle kernel's bytes per dispatch x dispatches per cycle, summed "
+                              f"= one engine launch"}
         e = ks.get(kernel, {})
         if "hbm_bytes_per_launch" in e:
             return {"bytes_per_launch": e["hbm_bytes_per_launch"], "cycle_bytes": round(cyc, 1),
@@ -641,22 +648,39 @@ def diag_summary(d, tasks, kernel):
 
 
 def cpu_baseline(cluster, sample_tasks, config):
-    """The oracle (C++ restatement of the reference, ParallelizeUntil-style pool) on the first
-    `sample_tasks` placements of the same workload."""
+    """The oracle (C++ restatement of the reference, ParallelizeUntil-style pool) on the first `sample_tasks`
+    placements of the same workload: 16 workers (the reference's ParallelizeUntil(..., 16, ...)), and beside it the
+    same sample on every core this process may run on ("Also report an all-cores run")."""
     from oracle import pyoracle
-    cores = min(16, os.cpu_count() or 1)
     try:
-        aff = len(os.sched_getaffinity(0))
-        cores = min(cores, aff)
+        avail = len(os.sched_getaffinity(0))
     except AttributeError:
-        pass
-    out = pyoracle.allocate(cluster, workers=cores, max_tasks=sample_tasks)
-    placed = len(out["events"])
-    secs = out["elapsed_ms"] / 1e3
-    return {"value": round(placed / secs, 1) if secs > 0 else None, "unit": "pods/s", "cores": cores,
-            "kind": "port", "sample": f"first {out['attempts']} task placements of the {config} cycle "
-                                      f"({placed} placed in {secs:.2f} s, {cores} worker threads, "
-                                      f"reference-structured full predicate+score sweep per task)"}
+        avail = os.cpu_count() or 1
+    label = "CPU restatement of the reference algorithm (oracle/oracle.cpp), not the Go reference"
+
+    def run(workers):
+        out = pyoracle.allocate(cluster, workers=workers, max_tasks=sample_tasks)
+        placed = len(out["events"])
+        secs = out["elapsed_ms"] / 1e3
+        return out, placed, secs
+
+    cores = min(16, avail)
+    out, placed, secs = run(cores)
+    res = {"value": round(placed / secs, 1) if secs > 0 else None, "unit": "pods/s", "cores": cores,
+           "kind": "port", "label": label,
+           "sample": f"first {out['attempts']} task placements of the {config} cycle "
+                     f"({placed} placed in {secs:.2f} s, {cores} worker threads, "
+                     f"reference-structured full predicate+score sweep per task)",
+           "host": {"nproc_visible": os.cpu_count(), "affinity_cpus": avail}}
+    if avail > cores:
+        out2, placed2, secs2 = run(avail)
+        res["all_cores"] = {"value": round(placed2 / secs2, 1) if secs2 > 0 else None, "unit": "pods/s",
+                            "cores": avail, "sample": f"the same {out2['attempts']} placements on {avail} worker "
+                                                      f"threads ({secs2:.2f} s)"}
+    else:
+        res["all_cores"] = {"value": res["value"], "cores": cores,
+                            "sample": "this process may run on no more than the 16 cores above"}
+    return res
 
 
 if __name__ == "__main__":

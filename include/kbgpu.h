@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 13
+#define KBGPU_ABI_VERSION 14
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -405,9 +405,15 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_OPT_NO_CLS (1u << 9)             /* class-loop affinity specs on the re-sweep loops */
 #define KB_OPT_NO_EVAL_PLAIN (1u << 10)     /* kb_eval's general kernel on plain batches too */
 #define KB_OPT_FED_SHARED_QUEUES (1u << 11) /* the sweep stream without its own hardware queue (the hazard test) */
-#define KB_OPT_FED_PLAIN_LAUNCH (1u << 12)  /* the engine as a plain launch (ranks sharing one GPU; rocprofv3) */
+#define KB_OPT_FED_PLAIN_LAUNCH (1u << 12)  /* (ABI 14: the default; kept so old option sets still parse) */
 #define KB_OPT_SHARD_SELF_INBOX (1u << 13)  /* a rank's own record through its inbox too (exchange tests) */
 #define KB_OPT_FED_DIAG (1u << 14)          /* KB_DIAG builds: print the selector's phase stamps at kb_fed_end */
+/* ABI 14: the resident engine is a plain launch after an explicit residency check (every workgroup of its 2-5
+ * workgroup grid fits the device at once: hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs); this flag restores
+ * round 4's cooperative launch, for A/B measurements only (rocprofv3 7.2 crashes at exit after one). */
+#define KB_OPT_FED_COOP_LAUNCH (1u << 15)
+/* ABI 14, tests only: this rank's kb_set_shard_peer pre-flight words carry a wrong tag (every rank must fail). */
+#define KB_OPT_TEST_PEER_BADTAG (1u << 16)
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -445,6 +451,17 @@ typedef struct kb_stats {
                                          between writing its record and holding every peer's */
   uint64_t fed_clock_ticks, fed_real_ticks; /* split fed engine: s_memtime (shader clock) and s_memrealtime (100 MHz)
                                          ticks of the placer's launches, so clock MHz = 100 * clock / real */
+  /* ABI 14 */
+  uint64_t sweep_overlap;             /* per-job launch path: level-0 sweeps that overlapped the previous job */
+  uint64_t overlap_refused_tables;    /* ... sweeps kept in order because a job still in flight writes tables
+                                         the sweep reads (aff_sweep_indep, or an affinity-table commit queued
+                                         after the publish of the job two back) */
+  uint64_t shard_phase_ticks[6];      /* node-sharded engine, s_memrealtime ticks summed over the exchanges:
+                                         [0] proposal (the rank's merge, e-sequences and winners), [1] writing
+                                         the record into every peer's inbox, [2] waiting for every peer's record,
+                                         [3] the global merge and stop rules, [4] commit + publish, [5] no-fit
+                                         histogram rounds */
+  uint64_t peer_checks;               /* kb_set_shard_peer pre-flight round trips that passed (peers x inboxes) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 
@@ -558,6 +575,13 @@ int kb_set_shard_rccl(kb_ctx* ctx, const kb_shard* shard, const uint8_t id[KB_CO
  * Replaces the per-task argmax all-reduce of SURVEY.md §8 e1 (scheduler_helper.go:147-158 over every rank's
  * nodes); ranks must run the same cycles (a divergence fails with KB_E_STATE). */
 int kb_set_shard_peer(kb_ctx* ctx, const kb_shard* shard, kb_allgather_fn fn, void* user);
+/* ABI 14: before it returns, kb_set_shard_peer checks the path every cycle will take. For every peer on another GPU,
+ * hipDeviceCanAccessPeer (the peer's GPU found by its PCI bus id); then a tagged-word round trip through every opened
+ * inbox: each rank stores a word into every peer's inbox from its GPU (system scope, as the engine's records go),
+ * the ranks meet in fn, each reads the words in its own inbox and answers every peer with a second word, and the
+ * ranks meet again and check the answers. The outcome is all-gathered, so every rank fails alike: KB_E_HIP (no
+ * peer access) or KB_E_STATE (a word missing or wrong), naming the rank pair. kb_stats.peer_checks counts the
+ * words that passed. */
 
 /* ---- layer 2: session (allocate action + ordering plugins on the host) ---- */
 

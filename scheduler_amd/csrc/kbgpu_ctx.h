@@ -116,6 +116,10 @@ struct kb_ctx {
     bool busy = false;
     std::chrono::steady_clock::time_point t_issue;
     double issue_ms = 0;
+    // the spec whose affinity-table commit (aff_commit_kernel) the slot's last job queued after its final place
+    // kernel, -1 none: that commit may still run after the host has read the job (the place kernel publishes
+    // first), so a later sweep that reads those tables must not overlap it (place_issue)
+    int aff_tail_spec = -1;
   };
   JobSlot slot[kbgpu::kJobSlots];
   char* d_jobx[kbgpu::kJobSlots] = {};  // slots 1..: device / pinned host job state (+ placements)
@@ -149,21 +153,22 @@ struct kb_ctx {
   uint32_t* fed_ctr = nullptr;
   int32_t* fed_exit = nullptr;
   void* fed_xchg = nullptr;   // split engine exchange (fed_xchg_bytes)
+  uint64_t* h_fed_ctrs = nullptr;  // pinned: the placer's counters at the end of fed_xchg, copied at kb_fed_end
   bool use_fed_split = true;  // !KB_OPT_NO_FED_SPLIT
   bool fed_split_now = false;  // the running fed cycle is on the split engine (its FedXchg counters)
   // The resident engine waits for sweeps issued on stream_b: they must never queue behind it on one hardware queue.
-  // The engine is a cooperative launch (the device's own cooperative queue, every workgroup co-resident) and
-  // stream_b a CU-masked stream (a hardware queue of its own, never shared with other streams of the process).
-  // KB_OPT_FED_SHARED_QUEUES (tests): plain launch and plain stream, the hazard these remove; KB_OPT_FED_PLAIN_LAUNCH:
-  // plain launch only (the dedicated sweep stream alone already separates the two).
+  // stream_b is a CU-masked stream (a hardware queue of its own, never shared with other streams of the process),
+  // and the engine a plain launch whose every workgroup fits the device at once (launch_fed_engine checks the
+  // occupancy first). KB_OPT_FED_SHARED_QUEUES (tests): a plain stream_b, the hazard the dedicated queue removes.
   bool fed_dedicated = true;
-  bool fed_coop = true;
+  bool fed_coop = false;  // KB_OPT_FED_COOP_LAUNCH (A/B only): the default is a plain launch + residency check
   // tests only (kb_opts.test_stall_job / test_stall_ms): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;
   int test_stall_ms = 1500;
   bool use_pipeline = true;    // !KB_OPT_NO_PIPELINE
   bool shard_self_inbox = false;  // KB_OPT_SHARD_SELF_INBOX
+  bool test_peer_badtag = false;  // KB_OPT_TEST_PEER_BADTAG
   bool fed_diag = false;       // KB_OPT_FED_DIAG
   bool issue_trace = false;    // KB_HOST_TRACE: every fed job issue on stderr
   uint64_t fed_idle = 100000000ull;  // the engine's idle exit in s_memrealtime ticks (100 MHz): 1 s

@@ -268,6 +268,9 @@ struct ShardPeers {
   int32_t self_inbox;               // testing (KB_SHARD_SELF_INBOX=1): the rank's own record through its inbox too
 };
 size_t shard_inbox_bytes();
+// kb_set_shard_peer's pre-flight (n <= 64 words read)
+void launch_peer_put(uint64_t* dst, uint64_t v, void* stream);
+void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream);
 // coop: a cooperative launch (every workgroup co-resident, on the device's cooperative queue); returns the
 // launch's hipError_t. shard.world > 0: the node-sharded engine (split engine only).
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,

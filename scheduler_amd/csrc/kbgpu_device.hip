@@ -2882,6 +2882,7 @@ struct FedXchg {
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
   uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
+  uint64_t sphase[8];  // SHARD: the placer's exchange phases (kb_stats.shard_phase_ticks), ahead of sdiag
   uint64_t sdiag[16];  // KB_DIAG builds: [0..6] the selector's phases, [8..11] the placer's merge; [12..15] the placer's
                        // counters for kb_stats (every build: exchange wait / count, clock / realtime ticks)
 };
@@ -3246,7 +3247,7 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
                                           int t_count, int ready0, int minav, int gang, int idx_bits, int32_t* hout,
                                           JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
                                           int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped,
-                                          uint64_t& wait_acc) {
+                                          uint64_t* ph) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int T = t_count, W = SP.world;
   __syncthreads();  // sel_run's no-fit exit writes sh.s_count = 0 from one thread with no barrier after it
@@ -3293,6 +3294,9 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     }
   };
   // ---- write: this rank's record into every other rank's inbox (its own goes straight to LDS) ----
+  // ph (thread 0's s_memrealtime phase sums, kb_stats.shard_phase_ticks): [1] write, [2] wait, [3] merge + stop
+  // rules, [4] commit, [5] no-fit round
+  const uint64_t t_write0 = __builtin_amdgcn_s_memrealtime();
   for (int idx = tid; idx < W * L; idx += kSelThreads) {
     const int w = idx / L, i = idx - w * L;
     const uint32_t v = word(i);
@@ -3303,6 +3307,7 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
   }
   // ---- read: every other rank's record from this rank's inbox ----
   const uint64_t t_read0 = __builtin_amdgcn_s_memrealtime();
+  ph[1] += t_read0 - t_write0;
   {
     const uint64_t t0 = t_read0;
     bool late = false;
@@ -3334,7 +3339,8 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     if (late) G.fail = 1;  // (benign race: every writer stores 1)
   }
   __syncthreads();
-  wait_acc += __builtin_amdgcn_s_memrealtime() - t_read0;  // (thread 0's count is the one reported)
+  const uint64_t t_merge0 = __builtin_amdgcn_s_memrealtime();
+  ph[2] += t_merge0 - t_read0;  // (thread 0's count is the one reported)
   if (G.fail) return 1;
   if (tid < W && (G.hdr[tid][0] != hdr0 || G.hdr[tid][1] != hdr1 || G.hdr[tid][2] != hdr2 || G.kp[tid] > T))
     G.diverged = 1;
@@ -3403,6 +3409,8 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     }
   }
   __syncthreads();
+  const uint64_t t_commit0 = __builtin_amdgcn_s_memrealtime();
+  ph[3] += t_commit0 - t_merge0;
   const int cut = G.cut, kind = G.kind;
   // placements (every rank writes the whole sequence) and the picks on this rank's rows, per local slot
   if (tid < cut) {
@@ -3420,6 +3428,8 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
   }
   placed = cut;
   ready = ready0 + G.n_alloc;
+  const uint64_t t_hist0 = __builtin_amdgcn_s_memrealtime();
+  ph[4] += t_hist0 - t_commit0;
   if (kind == 3) {
     fail_task = t_begin + cut;
     panic = 1;
@@ -3475,6 +3485,7 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     stop = KB_STOP_NO_FIT;
     fail_task = t_begin + cut;
     stopped = 1;
+    ph[5] += __builtin_amdgcn_s_memrealtime() - t_hist0;
   }
   if (tid == 0) sh.need_hist = 0;
   __syncthreads();
@@ -3545,7 +3556,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint32_t m = 0;
   uint32_t xn = 0;  // SHARD: exchanges so far (the jobs that ran)
   const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0_launch = __builtin_amdgcn_s_memrealtime();
-  uint64_t shard_wait = 0;  // SHARD: realtime ticks from this rank's record written to every peer's record read
+  // SHARD: s_memrealtime ticks per phase of the exchanges (kb_stats.shard_phase_ticks; [2] the wait for every peer's
+  // record after writing this rank's, also kb_stats.shard_wait_ticks)
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t t_job0 = 0;
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
       if (tid == 0) {
@@ -3641,6 +3655,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     dg[5] = pub_prev;
     const uint64_t rt0 = rt_wait0;
 #endif
+    if constexpr (SHARD) t_job0 = __builtin_amdgcn_s_memrealtime();
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
     const int64_t* sci = P.sc_init + (size_t)spec * N.S;
@@ -3830,13 +3845,15 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       sel_run<true, QN, true>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
                               gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
                               S.commits[slot] SEL_DIAG_ARGS, pub);
+      ph[0] += __builtin_amdgcn_s_memrealtime() - t_job0;
       const int rc = shard_place(sh, k32, cand, SP, xn++, N, P, C, sp, spec, stat, S.keys[slot],
                                  prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr,
                                  prev_slot[0] >= 0 ? prev_ncommit[0] : 0,
                                  prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr,
                                  prev_slot[1] >= 0 ? prev_ncommit[1] : 0, cm.t_begin, cm.t_count, cm.ready0, minav,
                                  gang, idx_bits, S.hout[slot], js, hjs, S.commits[slot], idle_ticks, stop, fail_task,
-                                 placed, ready, panic, stopped, shard_wait);
+                                 placed, ready, panic, stopped, ph);
+      t_job0 = __builtin_amdgcn_s_memrealtime();  // (the publish below counts as commit)
       if (rc != 0) {  // a peer never answered (every rank's engine leaves), or the ranks issued different jobs
         if (tid == 0) {
           atomicMax(exit_flag, 1);
@@ -3928,6 +3945,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       // after that release (the job's rows written back): the selector may re-key them
       if (SPLIT) tag_store(&X->p_done[r], m + 1, (uint32_t)ncommit);
     }
+    if constexpr (SHARD) ph[4] += __builtin_amdgcn_s_memrealtime() - t_job0;
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
     prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
     prev_slot[0] = slot, prev_ncommit[0] = ncommit;
@@ -3944,7 +3962,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
   if (SPLIT && tid == 0) {  // for the host's stats: the exchange's cost (kb_stats.shard_wait_ticks / shard_xchg) and
                            // the shader clock over the launch (fed_clock_ticks / fed_real_ticks)
-    X->sdiag[12] = shard_wait;
+    X->sdiag[12] = ph[2];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) X->sphase[k] = ph[k];
     X->sdiag[13] = xn;
     X->sdiag[14] = __builtin_amdgcn_s_memtime() - clk0;
     X->sdiag[15] = __builtin_amdgcn_s_memrealtime() - rt0_launch;
@@ -3987,6 +4007,22 @@ int fed_nsel(int n) {
 bool fed_split_ok(int n, bool sharded) { return fed_nsel(n) > 0 && (sharded ? n > 0 : n > 4 * kSelThreads); }
 
 size_t shard_inbox_bytes() { return (size_t)2 * kJobSlots * kShardMaxWorld * kShardRecW * sizeof(uint64_t); }
+
+// kb_set_shard_peer's pre-flight: one tagged word stored into a peer's inbox from this GPU (system scope, as
+// shard_place writes its records over xGMI), and this rank's inbox words read back the way the engine polls them.
+__global__ void peer_put_kernel(uint64_t* dst, uint64_t v) {
+  if (threadIdx.x == 0) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void peer_get_kernel(const uint64_t* src, int n, uint64_t* out) {
+  const int i = threadIdx.x;
+  if (i < n) out[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void launch_peer_put(uint64_t* dst, uint64_t v, void* stream) {
+  hipLaunchKernelGGL(peer_put_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst, v);
+}
+void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream) {
+  hipLaunchKernelGGL(peer_get_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, src, n, out);
+}
 
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
@@ -4041,6 +4077,16 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   if (sharded && !split) return (int)hipErrorInvalidValue;
   const dim3 grid(split ? 1 + nsel : 1), block(kSelThreads);
   if (coop) return (int)hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)bytes, (hipStream_t)stream);
+  // A plain launch: its workgroups spin on each other, so every one of them must be resident at once. The
+  // dispatcher places them as CUs free up (the sweeps they wait for run on another hardware queue and never wait
+  // for the engine), so it suffices that the whole grid fits the device at this LDS / register footprint -- the
+  // one check a cooperative launch adds (MI355X_MICROARCH.md: same residency for a grid this small).
+  int per_cu = 0, cus = 0, dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kSelThreads, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  if ((long)per_cu * cus < (long)grid.x) return (int)hipErrorCooperativeLaunchTooLarge;
   return (int)hipLaunchKernel(f, grid, block, args, (size_t)bytes, (hipStream_t)stream);
 }
 

@@ -250,8 +250,9 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->use_fed_split = !(fl & KB_OPT_NO_FED_SPLIT);
   c->use_pipeline = !(fl & KB_OPT_NO_PIPELINE);
   c->fed_dedicated = !(fl & KB_OPT_FED_SHARED_QUEUES);
-  c->fed_coop = c->fed_dedicated && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
+  c->fed_coop = c->fed_dedicated && (fl & KB_OPT_FED_COOP_LAUNCH) && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
   c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
+  c->test_peer_badtag = (fl & KB_OPT_TEST_PEER_BADTAG) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
@@ -322,6 +323,7 @@ void kb_destroy(kb_ctx* c) {
   if (c->fed_ctr) (void)hipFree(c->fed_ctr);
   if (c->fed_exit) (void)hipFree(c->fed_exit);
   if (c->fed_xchg) (void)hipFree(c->fed_xchg);
+  if (c->h_fed_ctrs) (void)hipHostFree(c->h_fed_ctrs);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   (void)hipFree(c->eval_ids);
   (void)hipFree(c->eval_r);
@@ -935,6 +937,85 @@ static void note_peer_epoch(uint32_t next) {
   }
 }
 
+// The pre-flight round trip (include/kbgpu.h, kb_set_shard_peer). Inbox words [0, W): rank w's hello; [W, 2W): rank
+// w's answer. A word is 0x5EED << 48 | kind << 40 | (sender << 8 | receiver) << 16 | this setup's nonce, so a word
+// of an earlier setup in recycled memory never reads as current. Ends with every inbox zeroed and the ranks met.
+static int shard_peer_preflight(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user, uint32_t start) {
+  const int W = sh->world, me = sh->rank;
+  uint64_t* own = (uint64_t*)c->inbox;
+  uint64_t* got = nullptr;
+  HIP_OK(c, hipMalloc((void**)&got, 2 * kShardMaxWorld * sizeof(uint64_t)));
+  struct Free {
+    uint64_t* p;
+    ~Free() { (void)hipFree(p); }
+  } free_got{got};
+  const uint16_t nonce = (uint16_t)(0x9e37u * (start + 1u));  // (start: the same on every rank)
+  const auto word = [&](int kind, int from, int to) {
+    return (0x5EEDull << 48) | ((uint64_t)kind << 40) | ((uint64_t)((from << 8) | to) << 16) | nonce;
+  };
+  struct Outcome {
+    int32_t ok, from, to, kind;
+    uint64_t seen;
+  };
+  Outcome mine{1, -1, -1, 0, 0};
+  std::vector<uint64_t> h(2 * (size_t)W);
+  const auto meet = [&](const char* when) -> int {
+    uint32_t tok = 1;
+    std::vector<uint32_t> all((size_t)W);
+    if (int rc = fn(user, &tok, all.data(), sizeof(tok)))
+      return fail(c, KB_E_HIP, "all-gather callback failed (%d) %s", rc, when);
+    return KB_OK;
+  };
+  const auto check = [&](int kind) -> int {  // this rank's inbox words of `kind`: every peer's, with its tag
+    launch_peer_get(own, 2 * W, got, c->stream);
+    HIP_OK(c, hipGetLastError());
+    HIP_OK(c, hipMemcpyAsync(h.data(), got, 2 * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int w = 0; w < W && mine.ok; ++w) {
+      if (w == me) continue;
+      const uint64_t x = h[(size_t)kind * W + w];
+      if (x != word(kind, w, me)) mine = Outcome{0, w, me, kind, x};
+      else c->stats.peer_checks++;
+    }
+    return KB_OK;
+  };
+  // 1. hello: this rank's word into every peer's inbox, over the path the engine's records take
+  for (int w = 0; w < W; ++w)
+    if (w != me)
+      launch_peer_put((uint64_t*)c->peer_inbox[w] + me, word(0, me, w) ^ (c->test_peer_badtag ? 1ull << 47 : 0ull),
+                      c->stream);
+  HIP_OK(c, hipGetLastError());
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (int rc = meet("after the pre-flight hello")) return rc;
+  if (int rc = check(0)) return rc;
+  // 2. answer every peer whose hello arrived intact
+  for (int w = 0; w < W && mine.ok; ++w)
+    if (w != me) launch_peer_put((uint64_t*)c->peer_inbox[w] + W + me, word(1, me, w), c->stream);
+  HIP_OK(c, hipGetLastError());
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (int rc = meet("after the pre-flight answers")) return rc;
+  if (mine.ok)
+    if (int rc = check(1)) return rc;
+  // 3. every rank's outcome, so that all of them fail alike (a rank that saw nothing wrong names the first pair that
+  //    failed elsewhere)
+  std::vector<Outcome> all((size_t)W);
+  if (int rc = fn(user, &mine, all.data(), sizeof(Outcome)))
+    return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the pre-flight outcomes", rc);
+  HIP_OK(c, memset_sync(c->inbox, 0, shard_inbox_bytes()));
+  HIP_OK(c, hipDeviceSynchronize());
+  if (int rc = meet("after the pre-flight")) return rc;  // no rank starts a cycle before every inbox is clean
+  for (int w = 0; w < W; ++w)
+    if (!all[w].ok) {
+      const Outcome& o = all[w];
+      return fail(c, KB_E_STATE,
+                  "node-sharded pre-flight: rank %d read %s from rank %d as %016llx, wanted %016llx (the %s path "
+                  "between these ranks' GPUs does not deliver the engine's words)", o.to,
+                  o.kind ? "the answer" : "the hello", o.from, (unsigned long long)o.seen,
+                  (unsigned long long)word(o.kind, o.from, o.to), o.kind ? "answer" : "hello");
+    }
+  return KB_OK;
+}
+
 int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* user) {
   if (int rc = kb_set_shard(c, sh, fn, user)) return rc;
   const size_t bytes = shard_inbox_bytes();
@@ -956,12 +1037,15 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
   struct PeerHello {
     hipIpcMemHandle_t h;
     uint32_t epoch, pad;
+    char bus[32];  // the rank's GPU (PCI bus id): peers on another GPU are checked for peer access
   };
   std::vector<PeerHello> h((size_t)W + 1);
+  memset(h.data(), 0, h.size() * sizeof(PeerHello));
   h[0].epoch = g_peer_epoch_next.load();
   uint32_t start = h[0].epoch;
   if (W > 1) {
     HIP_OK(c, hipIpcGetMemHandle(&h[0].h, c->inbox));
+    HIP_OK(c, hipDeviceGetPCIBusId(h[0].bus, (int)sizeof(h[0].bus) - 1, c->device));
     if (int rc = fn(user, &h[0], &h[1], sizeof(PeerHello)))
       return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the inbox handles", rc);
     for (int w = 0; w < W; ++w) start = std::max(start, h[1 + w].epoch);
@@ -971,11 +1055,24 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
       c->peer_inbox[w] = c->inbox;
       continue;
     }
+    if (strncmp(h[1 + w].bus, h[0].bus, sizeof(h[0].bus)) != 0) {  // another GPU: the xGMI path must be open
+      int ord = -1, can = 0;
+      if (hipDeviceGetByPCIBusId(&ord, h[1 + w].bus) != hipSuccess || ord < 0) {
+        (void)hipGetLastError();
+        return fail(c, KB_E_HIP, "rank %d's GPU (%s) is not visible to rank %d", w, h[1 + w].bus, sh->rank);
+      }
+      HIP_OK(c, hipDeviceCanAccessPeer(&can, c->device, ord));
+      if (!can)
+        return fail(c, KB_E_HIP, "rank %d (GPU %s) cannot access rank %d's GPU (%s): no peer path", sh->rank,
+                    h[0].bus, w, h[1 + w].bus);
+    }
     void* p = nullptr;
     const hipError_t e = hipIpcOpenMemHandle(&p, h[1 + w].h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) return fail(c, KB_E_HIP, "hipIpcOpenMemHandle (rank %d's inbox): %s", w, hipGetErrorString(e));
     c->peer_inbox[w] = p;
   }
+  if (W > 1)
+    if (int rc = shard_peer_preflight(c, sh, fn, user, start)) return rc;
   c->peer = true;
   c->shard_epoch = c->shard_epoch0 ? c->shard_epoch0 : start;  // (an explicit start: the epoch-wrap tests)
   note_peer_epoch(c->shard_epoch + 1);
@@ -1114,6 +1211,7 @@ static int shard_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
         c->sweep_target[si] += (uint32_t)((c->N.n + 63) / 64);
         c->n_overlap++;
+        c->stats.sweep_overlap++;
       } else {
         c->ev_begin(&ea);
         launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, aff, c->stream, gr);
@@ -1295,6 +1393,9 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
   int32_t* hout_dev = (int32_t*)(S.hdev + sizeof(JobState));
   bool listed = false;
   int run_spec = -1;
+  // the job two back (this slot's last one) may have left an affinity-table commit queued behind its publish
+  const int tail_spec = S.aff_tail_spec;
+  S.aff_tail_spec = -1;
   uint32_t t = 0;
   while (t < job->n_tasks) {
     uint32_t e = t + 1;
@@ -1352,8 +1453,13 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
       // previous job's place kernel, and the place kernel re-keys that job's rows.
       const bool one_run = !(aff && (c->spec_hist[spec] || (c->spec_incr[spec] && !sel_pl))) && t == 0 &&
                            e == job->n_tasks;
-      const bool ov = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1) &&
-                      (!aff || aff_sweep_indep(c, c->prev_run_spec, spec));
+      // With affinity the sweep reads count tables and histograms: neither the previous job's commits (listed, so
+      // applied before it published) nor an aff_commit_kernel the job two back queued after its publish may write
+      // what this sweep reads (the latter runs on `stream`, which the overlapped sweep does not wait for).
+      const bool ov_ok = one_run && c->stream_b && c->prev_listed && c->prev_slot == (si ^ 1);
+      const bool ov = ov_ok && (!aff || (aff_sweep_indep(c, c->prev_run_spec, spec) &&
+                                         aff_sweep_indep(c, tail_spec, spec)));
+      if (ov_ok && !ov) c->stats.overlap_refused_tables++;
       if (ov) {
         c->ev_begin(&ea, c->stream_b);
         launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, nullptr, aff, c->stream_b,
@@ -1361,6 +1467,7 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
         c->ev_end(ea, KB_KERNEL_SEL_SWEEP, (uint64_t)c->N.n, c->stream_b);
         c->sweep_target[si] += (uint32_t)((c->N.n + 63) / 64);
         c->n_overlap++;
+        c->stats.sweep_overlap++;
       } else {
         c->ev_begin(&ea);
         launch_sel_sweep(c->N, c->P, c->cfg, spec, c->idx_bits, kt, st, first ? nullptr : js, aff, c->stream, gr);
@@ -1398,8 +1505,12 @@ static int place_issue(kb_ctx* c, const kb_job_req* job, int si, const SpecGuard
     }
     // this run's commits update the affinity tables (the class loop and the per-task loops apply them themselves,
     // and so does the selection kernel when sel_pl)
-    if (aff && !dyn && !sel_pl && c->spec_incr[spec])
+    if (aff && !dyn && !sel_pl && c->spec_incr[spec]) {
       launch_aff_commit(c->P, spec, (int)t, run, js, hout_dev, 0, c->stream);
+      S.aff_tail_spec = spec;  // (a later run's place kernel, in stream order after it, clears the hazard)
+    } else {
+      S.aff_tail_spec = -1;
+    }
     t = e;
   }
   HIP_OK(c, hipGetLastError());
@@ -1572,6 +1683,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   void* xchg = nullptr;
   if (c->use_fed_split && fed_split_ok(c->N.n, c->sharded) && max_job_tasks <= (uint32_t)kFedSplitMaxTasks) {
     if (!c->fed_xchg) HIP_OK(c, hipMalloc(&c->fed_xchg, fed_xchg_bytes()));
+    if (!c->h_fed_ctrs) HIP_OK(c, hipHostMalloc((void**)&c->h_fed_ctrs, 24 * sizeof(uint64_t), hipHostMallocDefault));
     HIP_OK(c, hipMemsetAsync(c->fed_xchg, 0, fed_xchg_bytes(), c->stream));  // job numbers restart per cycle
     xchg = c->fed_xchg;
     c->stats.fed_split++;
@@ -1630,29 +1742,32 @@ int kb_fed_end(kb_ctx* c) {
     c->ev_end(c->fed_ev, KB_KERNEL_FED_ENGINE, c->fed_tasks * (uint64_t)c->N.n);
     c->fed_ev = nullptr;
   }
+  // the placer's counters (FedXchg::sphase, sdiag): copied behind the engine on its stream into pinned memory, so
+  // reading them adds no device round trip to the cycle
+  const bool ctrs = c->fed_xchg && c->fed_split_now && c->h_fed_ctrs;
+  constexpr size_t kCtrWords = 24;  // sphase[8] + sdiag[16], the end of FedXchg
+  if (ctrs)
+    (void)hipMemcpyAsync(c->h_fed_ctrs, (char*)c->fed_xchg + fed_xchg_bytes() - kCtrWords * sizeof(uint64_t),
+                         kCtrWords * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream);
   const hipError_t e = hipStreamSynchronize(c->stream);  // bounded: EXIT, or the engine's idle exit
   if (rc == KB_OK && e != hipSuccess) rc = fail(c, KB_E_HIP, "fed engine: %s", hipGetErrorString(e));
   if (c->timing) c->ev_collect(true);
-  if (c->fed_diag && c->fed_xchg && c->stats.fed_split) {  // KB_DIAG builds: the selector's phases
-    uint64_t d[16] = {};
-    if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - sizeof(d), sizeof(d), hipMemcpyDeviceToHost) ==
-        hipSuccess && d[6]) {
+  if (ctrs && e == hipSuccess) {
+    const uint64_t* ph = c->h_fed_ctrs;     // sphase
+    const uint64_t* d = c->h_fed_ctrs + 8;  // sdiag
+    if (c->fed_diag && d[6]) {  // KB_DIAG builds: the selector's phases
       fprintf(stderr, "kb_fed_placer_merge cycles/job loads=%.0f b_order=%.0f union_rank=%.0f slots=%.0f\n",
               (double)d[8] / d[6], (double)d[9] / d[6], (double)d[10] / d[6], (double)d[11] / d[6]);
       fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_set_exclude=%.0f "
               "wait_done_patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
               (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6], (double)d[5] / d[6]);
     }
-  }
-  if (c->fed_xchg && c->fed_split_now) {  // the placer's counters (FedXchg::sdiag[12..15])
-    uint64_t d[4] = {};
-    if (hipMemcpy(d, (char*)c->fed_xchg + fed_xchg_bytes() - 4 * sizeof(uint64_t), sizeof(d),
-                  hipMemcpyDeviceToHost) == hipSuccess) {
-      c->stats.shard_wait_ticks += d[0];
-      c->stats.shard_xchg += d[1];
-      c->stats.fed_clock_ticks += d[2];
-      c->stats.fed_real_ticks += d[3];
-    }
+    c->stats.shard_wait_ticks += d[12];
+    c->stats.shard_xchg += d[13];
+    c->stats.fed_clock_ticks += d[14];
+    c->stats.fed_real_ticks += d[15];
+    if (c->sharded)
+      for (int k = 0; k < 6; ++k) c->stats.shard_phase_ticks[k] += ph[k];
   }
   // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;

@@ -126,7 +126,9 @@ class kb_stats(C.Structure):
                 ("fed_abandon", C.c_uint64), ("fed_cycles", C.c_uint64), ("fed_split", C.c_uint64),
                 ("cap1_runs", C.c_uint64), ("cls_runs", C.c_uint64),
                 ("fed_sharded", C.c_uint64), ("shard_rezero", C.c_uint64), ("shard_xchg", C.c_uint64),
-                ("shard_wait_ticks", C.c_uint64), ("fed_clock_ticks", C.c_uint64), ("fed_real_ticks", C.c_uint64)]
+                ("shard_wait_ticks", C.c_uint64), ("fed_clock_ticks", C.c_uint64), ("fed_real_ticks", C.c_uint64),
+                ("sweep_overlap", C.c_uint64), ("overlap_refused_tables", C.c_uint64),
+                ("shard_phase_ticks", C.c_uint64 * 6), ("peer_checks", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -137,7 +139,8 @@ KB_OPT_ENGINE = 8
 # path; tests and the profiler name the others through Context(options=...)
 OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6, "no_aff_reg": 1 << 7,
                 "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
-                "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14}
+                "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14,
+                "fed_coop_launch": 1 << 15, "test_peer_badtag": 1 << 16}
 OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
@@ -150,7 +153,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 13  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 14  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -399,7 +402,9 @@ class Context:
                 "cap1_runs": st.cap1_runs, "cls_runs": st.cls_runs,
                 "fed_sharded": st.fed_sharded, "shard_rezero": st.shard_rezero, "shard_xchg": st.shard_xchg,
                 "shard_wait_ticks": st.shard_wait_ticks, "fed_clock_ticks": st.fed_clock_ticks,
-                "fed_real_ticks": st.fed_real_ticks}
+                "fed_real_ticks": st.fed_real_ticks, "sweep_overlap": st.sweep_overlap,
+                "overlap_refused_tables": st.overlap_refused_tables,
+                "shard_phase_ticks": list(st.shard_phase_ticks), "peer_checks": st.peer_checks}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

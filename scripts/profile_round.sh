@@ -16,11 +16,9 @@ CONFIGS=${*:-C1 C2 C3 C4 C5}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-# rocprofv3 (ROCm 7.2) segfaults in its exit handlers after a cooperative launch: under the profiler the engine
-# takes a plain launch (same kernel, same grid; the CU-masked sweep stream still keeps the sweeps off its queue)
-# PLAIN=none: the engine's cooperative launch under the profiler too (rocprofv3 crashed at exit after one in
-# round 3; the default keeps the plain launch of the same kernel and grid)
-PLAIN=${PLAIN:-fed_plain_launch}
+# ABI 14: the engine is a plain launch in production too (rocprofv3 7.2 segfaulted at exit after the cooperative
+# launch rounds 1-4 used), so the profiled cycle is the production cycle. PLAIN=fed_coop_launch: the old launch.
+PLAIN=${PLAIN:-none}
 run() {  # run <name> <timeout> <cmd...>: stop the script on a crash / timeout
   local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1

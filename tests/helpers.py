@@ -400,3 +400,55 @@ def digest_arrays(event_task, event_node, event_kind, job_fail):
     for a in (event_task, event_node, event_kind, job_fail):
         h.update(np.ascontiguousarray(a).tobytes())
     return h.hexdigest()
+
+
+def overlap_cluster(kind, n_nodes=48, seed=3):
+    """Affinity jobs shaped for the launch path's overlapped level-0 sweep (kbgpu_host.cpp place_issue): job k+1's
+    sweep runs on the second stream beside job k's place kernel unless a job still in flight writes an affinity
+    table the sweep reads.
+    disjoint: every job has required affinity to a running app=svc pod over zone and nothing reads the jobs' own
+              labels: no job writes a table, so the sweeps overlap.
+    shared:   'web' jobs (label role=web, no terms of their own) alternate with 'guard' jobs (required
+              anti-affinity to role=web over rack): each web job's commits write the table the next guard job's
+              sweep reads, so that sweep stays in order.
+    tail:     a 'heavy' job (role=web, a preferred node-affinity weight past the 32-bit key: the 64-bit re-key loop,
+              whose table commit is a separate kernel queued after its publish), then a plain job (listed), then a
+              guard job reading the heavy job's table: the guard's sweep must wait for that commit (the job two back).
+    """
+    import random
+    rng = random.Random(seed)
+    cl = m.Cluster(tiers=m.default_tiers())
+    for i in range(n_nodes):
+        cl.nodes.append(m.Node(name=f"n{i:02d}", alloc={m.CPU: 8000, m.MEMORY: 32 * GI, m.PODS: 30},
+                               labels={"kubernetes.io/hostname": f"n{i:02d}", "zone": f"z{i % 4}",
+                                       "rack": f"r{i % 12}", "tier": "a" if i % 2 else "b"}))
+    cl.queues.append(m.Queue(name="q", weight=1))
+    cl.pod_groups.append(m.PodGroup(ns="ns", name="run", queue="q", min_member=1, phase="Running"))
+    for t in range(3):
+        cl.pods.append(m.Pod(ns="ns", name=f"svc-{t}", uid=f"ns-svc-{t}", group="run", node=f"n{rng.randrange(n_nodes):02d}",
+                             phase="Running", labels={"app": "svc"},
+                             containers=[m.Container(req={m.CPU: 500, m.MEMORY: GI})]))
+    svc = {"podAffinity": {"required": [{"labelSelector": {"matchLabels": {"app": "svc"}}, "topologyKey": "zone"}]}}
+    guard = {"podAntiAffinity": {"required": [{"labelSelector": {"matchLabels": {"role": "web"}},
+                                              "topologyKey": "rack"}]}}
+    heavy = {"nodeAffinity": {"preferred": [{"weight": 1 << 24, "preference": {"matchExpressions": [
+        {"key": "tier", "operator": "In", "values": ["a"]}]}}]}}
+    if kind == "disjoint":
+        jobs = [(f"j{j:02d}", {"job": f"j{j:02d}"}, svc, 4 + j % 3) for j in range(10)]
+    elif kind == "shared":
+        jobs = []
+        for j in range(5):
+            jobs.append((f"j{2 * j:02d}-web", {"role": "web"}, None, 3))
+            jobs.append((f"j{2 * j + 1:02d}-guard", {"job": f"g{j}"}, guard, 2))
+    else:
+        jobs = []
+        for j in range(3):
+            jobs.append((f"j{3 * j:02d}-heavy", {"role": "web"}, heavy, 3))
+            jobs.append((f"j{3 * j + 1:02d}-plain", {"job": f"p{j}"}, None, 4))
+            jobs.append((f"j{3 * j + 2:02d}-guard", {"job": f"g{j}"}, guard, 2))
+    for name, labels, aff, n in jobs:
+        cl.pod_groups.append(m.PodGroup(ns="ns", name=name, queue="q", min_member=n))
+        for t in range(n):
+            cl.pods.append(m.Pod(ns="ns", name=f"{name}-{t}", uid=f"ns-{name}-{t}", group=name, labels=dict(labels),
+                                 affinity=aff, containers=[m.Container(req={m.CPU: 1000, m.MEMORY: 2 * GI})]))
+    return cl

@@ -2,9 +2,9 @@
 
 The engine (one launch per allocate cycle) waits for per-job sweep kernels issued on a second stream. If that
 stream shared a hardware queue with the engine's, a sweep would queue behind the engine and the engine would
-wait out its idle bound (1 s) before the cycle finished on the launch path. The library launches the engine
-cooperatively (the device's cooperative queue) and creates the sweep stream with a CU mask (a hardware queue
-of its own), so neither can happen whatever other streams the process holds: here a torch process group with
+wait out its idle bound (1 s) before the cycle finished on the launch path. The library creates the sweep stream
+with a CU mask (a hardware queue of its own; the engine is a plain launch on the library's main stream after a
+residency check, ABI 14), so that cannot happen whatever other streams the process holds: here a torch process group with
 its communicator streams, torch's stream pool, and 0..7 raw HIP streams created between the library's own
 streams. Every cycle must finish on the engine (fed_abandon == 0) with the oracle's placements
 (allocate.go:95-192: one cycle must not stall).
@@ -89,7 +89,7 @@ def test_fed_engine_progress_beside_other_streams():
 
 
 def test_shared_queues_hazard_is_real():
-    """The same process layout with the engine launched plainly and the sweep stream from the shared pool
+    """The same process layout with the sweep stream from the shared pool
     (option fed_shared_queues): the hazard is observable -- some layouts stall the engine into its idle exit --
     and the cycle still ends with the oracle's placements on the launch path (correct, 300 ms slower)."""
     ref = pyoracle.allocate(synth.c2(n_nodes=3000, n_jobs=40, tasks_per_job=40, seed=51), workers=8)

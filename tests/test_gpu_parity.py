@@ -468,3 +468,23 @@ def test_allocate_reused_result_buffers():
             assert prev["n_events"] == fresh["n_events"]
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("kind", ["disjoint", "shared", "tail"])
+def test_affinity_sweep_overlap(kind):
+    """The launch path overlaps job k+1's level-0 sweep with job k's place kernel (second stream) only when no job
+    still in flight writes an affinity table that sweep reads: the previous job's own commits (aff_sweep_indep),
+    and a table commit the job two back queued after its publish (the 64-bit re-key loop's aff_commit_kernel),
+    which the host may have read past before that kernel ran. disjoint: the sweeps overlap; shared / tail: they
+    stay in order. Oracle parity in every case."""
+    from helpers import overlap_cluster
+    cl = overlap_cluster(kind)
+    ref = pyoracle.allocate(cl)
+    st = {}
+    got = runtime.allocate(cl, stats_out=st)
+    _compare(ref, got)
+    assert st["fed_cycles"] == 0, st  # (affinity jobs: the per-job launch path)
+    if kind == "disjoint":
+        assert st["sweep_overlap"] > 0 and st["overlap_refused_tables"] == 0, st
+    else:
+        assert st["overlap_refused_tables"] > 0, st

@@ -23,7 +23,7 @@ NAMES = ["C1-parity", "C2-parity", "C2-fill0.9", "C3-parity", "C2-nogang", "edge
 
 # ranks sharing one GPU: plain engine launches (cooperative launches from several processes take turns on the card,
 # DESIGN.md §5; one process per GPU, as deployed, keeps the cooperative launch)
-SHARED_GPU = {"fed_plain_launch": True}
+SHARED_GPU = {}  # (ranks sharing one GPU: since ABI 14 every engine launch is plain, the default)
 
 
 def _clusters():

@@ -78,9 +78,8 @@ def _rank_main(rank, world, port, q, cycles=2, options=None, names=None):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
-    # ranks sharing one GPU: plain engine launches (cooperative launches from several processes take turns on the
-    # card -- 10 ms per job here; one process per GPU, as deployed, keeps the cooperative launch)
-    options = dict(options or {}, fed_plain_launch=True)
+    # (the engine is a plain launch since ABI 14; fed_plain_launch stays accepted)
+    options = dict(options or {})
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def allgather(b):
@@ -96,7 +95,7 @@ def _rank_main(rank, world, port, q, cycles=2, options=None, names=None):
                 continue
             print(f"rank {rank}/{world}: {name}", flush=True)
             got, st = _sharded(snap, rank, world, allgather, cycles, barrier=dist.barrier, options=options)
-            res[name] = (got, st["fed_sharded"], st["fed_abandon"], st["shard_rezero"])
+            res[name] = (got, st["fed_sharded"], st["fed_abandon"], st["shard_rezero"], st["peer_checks"])
         q.put((rank, res, None))
     except Exception as e:  # report, do not hang the parent
         q.put((rank, None, repr(e)))
@@ -133,8 +132,10 @@ def test_peer_engine_ranks_equal_one_gpu(world):
             p.join(timeout=60)
     for r in range(world):
         for name in ref:
-            out, n_sharded, n_abandon, _ = got[r][name]
+            out, n_sharded, n_abandon, _, n_checks = got[r][name]
             assert n_sharded == 2 and n_abandon == 0, (world, r, name)
+            # the pre-flight: a hello and an answer from every peer arrived intact
+            assert n_checks == 2 * (world - 1), (world, r, name, n_checks)
             assert out == ref[name], (world, r, name)
 
 
@@ -175,6 +176,58 @@ def test_peer_engine_two_ranks_epoch_wrap():
         for p in procs:
             p.join(timeout=60)
     for r in range(world):
-        out, n_sharded, n_abandon, n_rezero = got[r]["c2-nofit"]
+        out, n_sharded, n_abandon, n_rezero, _ = got[r]["c2-nofit"]
         assert n_sharded == cycles and n_abandon == 0 and n_rezero == 1, (r, n_sharded, n_abandon, n_rezero)
         assert out == ref["c2-nofit"], r
+
+
+def _badtag_main(rank, world, port, q, bad_rank):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+    try:
+        ctx = runtime.Context(0, options={"test_peer_badtag": rank == bad_rank})
+        try:
+            ctx.set_shard(rank, world, 4000, allgather=allgather, peer=True)
+            q.put((rank, None))
+        except runtime.KbError as e:
+            q.put((rank, (e.code, str(e))))
+        finally:
+            ctx.close()
+    except Exception as e:
+        q.put((rank, (-1, repr(e))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_preflight_fails_loudly(world):
+    """kb_set_shard_peer's pre-flight round trip: when one rank's words arrive wrong (forced here: rank 1 stores a
+    bad tag), EVERY rank's kb_set_shard_peer fails with KB_E_STATE naming the rank pair -- before any cycle, instead
+    of a 10 s engine timeout in the first one."""
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_badtag_main, args=(r, world, port, q, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            rank, err = q.get(timeout=120)
+            got[rank] = err
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert got[r] is not None, f"rank {r} passed the pre-flight"
+        code, msg = got[r]
+        assert code == runtime.KB_E_STATE and "pre-flight" in msg and "from rank 1" in msg, (r, msg)
