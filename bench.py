@@ -50,6 +50,11 @@ CONFIGS = {
                workload="C4: 10k nodes x 100k pods, inter-pod (anti)affinity over hostname / zone / rack"),
     "C5": dict(nodes=50000, jobs=10000, tasks=100, row_bytes=76,
                workload="C5: 50k nodes x 1M pods (C2 shape), node table sharded across the GPUs"),
+    # not a BASELINE.json configuration: VERDICT r04's mixed cycle (C2 plus ~2% two-template jobs and ~2% jobs with
+    # inter-pod anti-affinity), to hold against the C2 line per job
+    "C2M": dict(nodes=10000, jobs=1000, tasks=100, row_bytes=80,
+                workload="C2M: C2's 10k nodes x 100k pods with ~2% PS/worker (two-template) jobs and ~2% jobs with "
+                         "required pod anti-affinity over hostname (a mixed cycle)"),
 }
 ARRAY_CONFIGS = ("C2", "C5")  # built by synth.c2_snapshot (numpy) instead of per-pod objects
 
@@ -355,9 +360,12 @@ def engine_of(st):
     us = st["kernel_ms"][k] * 1e3 / launches
     jobs = st["job_calls"] / launches
     clk = 100.0 * st["fed_clock_ticks"] / st["fed_real_ticks"] if st["fed_real_ticks"] else None
+    place = [{"xcc": int(v) >> 32, "se": (int(v) >> 13) & 7, "cu": (int(v) >> 8) & 15} if v else None
+             for v in st.get("fed_wg_place", [0, 0])]
     return {"kernel": "fed_engine_kernel", "bound": "latency (per-job dependent chain in one workgroup)",
             "avg_launch_us": round(us, 3), "launches": st["launches"][k], "jobs_per_launch": round(jobs, 1),
-            "us_per_job": round(us / max(1.0, jobs), 3), "clock_mhz": round(clk, 1) if clk else None}
+            "us_per_job": round(us / max(1.0, jobs), 3), "clock_mhz": round(clk, 1) if clk else None,
+            "placement": {"placer": place[0], "selector": place[1]}}
 
 
 def shard_fields(st, args):

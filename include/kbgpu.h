@@ -461,7 +461,12 @@ typedef struct kb_stats {
                                          the record into every peer's inbox, [2] waiting for every peer's record,
                                          [3] the global merge and stop rules, [4] commit + publish, [5] no-fit
                                          histogram rounds */
-  uint64_t peer_checks;               /* kb_set_shard_peer pre-flight round trips that passed (peers x inboxes) */
+  uint64_t peer_checks;               /* kb_set_shard_peer pre-flight words that passed (2 per peer) */
+  uint64_t fed_wg_place[2];           /* the last split engine launch: where its placer [0] and selector 0 [1] ran,
+                                         XCC id << 32 | HW_ID (CU id bits 11:8, SIMD 5:4, SE 15:13) */
+  uint64_t off_engine_units;          /* kb_allocate units the resident engine does not take (inter-pod affinity,
+                                         host-evaluated reasons, ...), run on the launch path between two engine
+                                         launches of a cycle that otherwise runs on the engine */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

@@ -439,12 +439,52 @@ struct Driver {
     return false;
   }
 
-  kb_job_req make_req(int j) {
-    JobS& js = jobs[j];
-    const size_t nt = js.pending.size() - js.cursor;
-    specs.resize(nt);
-    for (size_t i = 0; i < nt; ++i) specs[i] = s.task_spec[js.pending[js.cursor + i]];
-    return kb_job_req{specs.data(), (uint32_t)nt, js.ready, s.job_min_available[j], gang_ready_on ? 1 : 0};
+  // A unit: what one device call places. On the fed engine, one run of one spec (at most unit_cap tasks: the split
+  // engine's segment); on the launch paths, the rest of the job (they chain a job's runs on the device). A job pop
+  // is one or more units: a unit that places all its tasks without the job becoming ready is followed, in the same
+  // pop, by the job's next unit (allocate.go:135-188 goes on with the next task) with no heap operation between.
+  struct Unit {
+    int q = -1, j = -1;
+    size_t cur = 0;
+    uint32_t len = 0;
+    bool last = true, fed = false;
+    bool operator==(const Unit& o) const {
+      return q == o.q && j == o.j && cur == o.cur && len == o.len && fed == o.fed;
+    }
+  };
+  bool fed_allowed = false;  // the cycle may run units on the resident engine
+  uint32_t unit_cap = 0;     // kb_fed_unit_cap: 0 = any length
+  std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
+  bool spec_fed_ok(int sp) {
+    if (sp < 0) return false;
+    if ((size_t)sp >= spec_fed.size()) spec_fed.resize(sp + 1, -1);
+    if (spec_fed[sp] < 0) spec_fed[sp] = (int8_t)kb_spec_fed_ok(ctx, sp);
+    return spec_fed[sp] != 0;
+  }
+  // the unit job j's pending list has at its cursor (j popped from queue q)
+  Unit unit_at(int q, int j) {
+    const JobS& js = jobs[j];
+    Unit u;
+    u.q = q, u.j = j, u.cur = js.cursor;
+    const size_t n = js.pending.size();
+    const int sp0 = s.task_spec[js.pending[u.cur]];
+    if (fed_allowed && spec_fed_ok(sp0)) {
+      const size_t lim = unit_cap ? std::min(n, u.cur + unit_cap) : n;
+      size_t e = u.cur + 1;
+      while (e < lim && s.task_spec[js.pending[e]] == sp0) ++e;
+      u.len = (uint32_t)(e - u.cur);
+      u.fed = true;
+    } else {
+      u.len = (uint32_t)(n - u.cur);
+    }
+    u.last = u.cur + u.len == n;
+    return u;
+  }
+  kb_job_req make_req(const Unit& u) {
+    const JobS& js = jobs[u.j];
+    specs.resize(u.len);
+    for (uint32_t i = 0; i < u.len; ++i) specs[i] = s.task_spec[js.pending[u.cur + i]];
+    return kb_job_req{specs.data(), u.len, js.ready, s.job_min_available[u.j], gang_ready_on ? 1 : 0};
   }
   int check_specs(int j) const {
     const JobS& js = jobs[j];
@@ -453,8 +493,11 @@ struct Driver {
     return KB_OK;
   }
 
-  // Session.Allocate / Session.Pipeline for the job's placements, then the heap pushes of the loop tail.
-  void apply(int q, int j, const kb_job_result& res) {
+  // Session.Allocate / Session.Pipeline for the unit's placements, then the heap pushes of the loop tail. Returns
+  // true when the pop goes on with the job's next unit (the unit placed all its tasks, the job is not ready, and
+  // it has more pending tasks): no loop tail then.
+  bool apply(const Unit& u, const kb_job_result& res) {
+    const int q = u.q, j = u.j;
     JobS& js = jobs[j];
     for (uint32_t i = 0; i < res.n_placed; ++i) {
       int t = js.pending[js.cursor + i];
@@ -491,16 +534,20 @@ struct Driver {
       }
     } else if (res.stop == KB_STOP_READY) {
       jheaps[q].push(j);
+    } else if (!u.last && res.n_placed == u.len && js.cursor < js.pending.size()) {
+      return true;
     }
     qheap.push(q);
+    return false;
   }
 
   // The place call's outcome when every task it places is Allocated (the stop rules of the place
   // kernels): a gang job stops READY at the task that brings ready to minAvailable, a job without the
   // gang JobReady check after its first task; otherwise every task places and the call ends DONE.
-  void predict(int j, int& stop, int& placed) const {
+  void predict(const Unit& u, int& stop, int& placed) const {
+    const int j = u.j;
     const JobS& js = jobs[j];
-    const int nt = (int)(js.pending.size() - js.cursor);
+    const int nt = (int)u.len;
     if (!gang_ready_on) {
       stop = KB_STOP_READY;
       placed = 1;
@@ -511,19 +558,21 @@ struct Driver {
     placed = std::min(need, nt);
   }
 
-  // Jobs in flight on the device (pipelined driver), oldest first. Entry i > 0 was issued speculatively,
-  // guarded on entry i-1 ending as predicted; `pred` is the entry's own predicted outcome (set by the
-  // replay that issued the entry after it).
+  // Units in flight on the device (pipelined driver), oldest first. Entry i > 0 was issued speculatively, guarded on
+  // entry i-1 ending as predicted; `pred` is the entry's own predicted outcome (set by the replay that issued the
+  // entry after it).
   struct Flight {
-    int q, j, slot;
+    Unit u;
+    int slot;
     kb_job_pred pred;
   };
   std::vector<Flight> fl;
 
-  // Speculation: find the job the loop pops next IF every job in flight ends as predicted, and issue it into
-  // `free_slot` guarded on the last one's prediction. The predictions are applied to the driver state in
-  // order and the loop tail / head replayed on scratch copies of the heaps; then the state is put back.
-  // Returns false (nothing issued) when there is no next job or it cannot be guarded.
+  // Speculation: find the unit the loop runs next IF every unit in flight ends as predicted, and issue it into
+  // `free_slot` guarded on the last one's prediction. The predictions are applied to the driver state in order and
+  // the loop tail / head (or the job's next unit) replayed on scratch copies of the heaps; then the state is put back.
+  // Returns false (nothing issued) when there is no next unit, it cannot be guarded, or it belongs to the other
+  // device mode (mode_fed: the resident engine runs the chain; the chain ends where the mode changes).
   GoHeap<int> sq;
   std::vector<std::pair<int, GoHeap<int>>> sjh;
   struct SavedJob {
@@ -539,7 +588,7 @@ struct Driver {
   };
   std::vector<SavedJob> saved_jobs;
   std::vector<SavedQueue> saved_queues;
-  bool speculate(int free_slot) {
+  bool speculate(int free_slot, bool mode_fed) {
     saved_jobs.clear();
     saved_queues.clear();
     sq.items = qheap.items;
@@ -551,35 +600,38 @@ struct Driver {
       return sjh.back().second;
     };
     bool ok = true;
-    int q2 = -1, j2 = -1;
+    Unit nu;
     for (size_t i = 0; i < fl.size() && ok; ++i) {
       Flight& f = fl[i];
       int stop, placed;
-      predict(f.j, stop, placed);
-      JobS& js = jobs[f.j];
+      predict(f.u, stop, placed);
+      JobS& js = jobs[f.u.j];
       bool seen = false;
-      for (const auto& e : saved_jobs) seen = seen || e.j == f.j;
-      if (!seen) saved_jobs.push_back(SavedJob{f.j, js.ready, js.cursor, js.drf_alloc, js.drf_share});
+      for (const auto& e : saved_jobs) seen = seen || e.j == f.u.j;
+      if (!seen) saved_jobs.push_back(SavedJob{f.u.j, js.ready, js.cursor, js.drf_alloc, js.drf_share});
       seen = false;
-      for (const auto& e : saved_queues) seen = seen || e.q == f.q;
-      if (!seen) saved_queues.push_back(SavedQueue{f.q, queues[f.q].allocated, queues[f.q].share});
+      for (const auto& e : saved_queues) seen = seen || e.q == f.u.q;
+      if (!seen) saved_queues.push_back(SavedQueue{f.u.q, queues[f.u.q].allocated, queues[f.u.q].share});
       const int ready0 = js.ready;
       for (int k = 0; k < placed; ++k) on_allocate_event(js.pending[js.cursor + k]);
       js.ready += placed;
       js.cursor += placed;
-      share_update(f.j);
+      share_update(f.u.j);
       f.pred = kb_job_pred{f.slot, stop, placed, ready0 + placed};
-      // the loop tail of the predicted outcome, then the next loop head
-      if (stop == KB_STOP_READY) jh(f.q).push(f.j);
-      sq.push(f.q);
-      int nq, nj;
-      ok = next_job(sq, jh, nq, nj);
-      if (ok && i + 1 < fl.size()) ok = nq == fl[i + 1].q && nj == fl[i + 1].j;  // issued by the same replay
-      q2 = nq, j2 = nj;
+      if (stop == KB_STOP_DONE && !f.u.last) {  // the pop goes on with the job's next unit
+        nu = unit_at(f.u.q, f.u.j);
+      } else {  // the loop tail of the predicted outcome, then the next loop head
+        if (stop == KB_STOP_READY) jh(f.u.q).push(f.u.j);
+        sq.push(f.u.q);
+        int nq, nj;
+        ok = next_job(sq, jh, nq, nj) && check_specs(nj) == KB_OK;
+        if (ok) nu = unit_at(nq, nj);
+      }
+      if (ok && i + 1 < fl.size()) ok = nu == fl[i + 1].u;  // issued by the same replay
     }
-    ok = ok && check_specs(j2) == KB_OK;
+    ok = ok && nu.fed == mode_fed;
     if (ok) {
-      const kb_job_req req = make_req(j2);
+      const kb_job_req req = make_req(nu);
       ok = kb_job_guardable(ctx, &req) != 0;
       if (ok) {
         const kb_job_pred pred = fl.back().pred;
@@ -597,8 +649,21 @@ struct Driver {
       queues[e.q].allocated = e.allocated;
       queues[e.q].share = e.share;
     }
-    if (ok) fl.push_back(Flight{q2, j2, free_slot, kb_job_pred{}});
+    if (ok) fl.push_back(Flight{nu, free_slot, kb_job_pred{}});
     return ok;
+  }
+
+  // The unit after u (cont: u's job goes on), or the next loop head's. 1: nu set, 0: the cycle is over, < 0: error.
+  int advance(const Unit& u, bool cont, Unit& nu) {
+    if (cont) {
+      nu = unit_at(u.q, u.j);
+      return 1;
+    }
+    int nq, nj;
+    if (!next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj)) return 0;
+    if (check_specs(nj)) return KB_E_INVALID;
+    nu = unit_at(nq, nj);
+    return 1;
   }
 
   int run() {
@@ -635,54 +700,49 @@ struct Driver {
     }
     pn.resize(max_pending);
     pk.resize(max_pending);
-    // Pipelined: job k+1 is launched (guarded) before job k's result is read, so the device runs the jobs
-    // back to back while the host does the bookkeeping. Otherwise one kb_place_job per job.
-    bool pipe = kb_job_pipeline_ok(ctx) && ctx->use_pipeline;
+    // Pipelined: unit k+1 is launched (guarded) before unit k's result is read, so the device runs them back to
+    // back while the host does the bookkeeping. Otherwise one kb_place_job per unit.
+    const bool pipe = kb_job_pipeline_ok(ctx) && ctx->use_pipeline;
     if (pipe)
       if (int rc = kb_job_reserve(ctx, max_pending)) return rc;
-    // every job one selection run of an eligible spec: the fed engine serves the whole cycle
-    bool fed = pipe && kb_fed_cycle_ok(ctx, max_pending);
-    std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
-    for (uint32_t j = 0; fed && j < s.n_jobs; ++j) {
-      int sp0 = -1;
-      for (int t : job_pending(j)) {
-        const int sp = s.task_spec[t];
-        if (sp == sp0) continue;
-        if (task_res_empty(t)) continue;  // BestEffort: never placed by allocate
-        if (sp < 0) {
-          fed = false;
-          break;
+    // The resident fed engine runs every unit whose spec it takes (kb_spec_fed_ok: one selection run, no inter-pod
+    // terms); a unit it does not take (inter-pod affinity, host-evaluated reasons, ...) runs on the launch path
+    // between two engine launches. node-sharded with the peer exchange: the launch path's units go one at a time
+    // through the host-staged exchange.
+    unit_cap = kb_fed_unit_cap(ctx);
+    const uint32_t max_unit = unit_cap ? std::min(max_pending, unit_cap) : max_pending;
+    fed_allowed = pipe && kb_fed_cycle_ok(ctx, max_unit);
+    if (fed_allowed) {  // worth it when most of the cycle's tasks are engine units: every switch costs an engine
+      uint64_t all = 0, eng = 0;  // stop and relaunch (C4: ~20% eligible jobs stay on the launch path)
+      for (uint32_t t = 0; t < s.n_tasks; ++t)
+        if (task_status[t] == KB_ST_PENDING && !task_res_empty(t)) {
+          ++all;
+          eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
         }
-        if ((size_t)sp >= spec_fed.size()) spec_fed.resize(sp + 1, -1);
-        if (spec_fed[sp] < 0) spec_fed[sp] = (int8_t)kb_spec_fed_ok(ctx, sp);
-        if (sp0 >= 0 || !spec_fed[sp]) {  // a second spec in the job, or an ineligible one
-          fed = false;
-          break;
-        }
-        sp0 = sp;
-      }
+      fed_allowed = 2 * eng > all;
     }
-    // node-sharded with the peer exchange only: the fed engine pipelines; any other cycle's jobs go one at a time
-    // through the host-staged exchange
-    if (!fed && ctx->sharded && !ctx->comm) pipe = false;
+    const bool launch_pipe = pipe && !(ctx->sharded && !ctx->comm);
     const auto r1 = std::chrono::steady_clock::now();
-    if (fed)
-      if (int rc = kb_fed_begin(ctx, max_pending)) return rc;
-    const auto r2 = std::chrono::steady_clock::now();
     struct FedEnd {  // the engine is stopped on every way out of the loop
       kb_ctx* c;
-      bool on;
+      bool on = false;
       ~FedEnd() {
         if (on) (void)kb_fed_end(c);
       }
-    } fed_end{ctx, fed};
-    int q, j;
-    bool have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
-    if (have && check_specs(j)) return KB_E_INVALID;
-    // KB_HOST_TRACE=1: per-job host timings on stderr at the end of the cycle (speculative issue, wait in
+    } engine{ctx};
+    double fed_begin_ms = 0;
+    Unit u;
+    int hv;
+    {
+      int q, j;
+      hv = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j) ? 1 : 0;
+      if (hv && check_specs(j)) return KB_E_INVALID;
+      if (hv) u = unit_at(q, j);
+    }
+    // KB_HOST_TRACE=1: per-unit host timings on stderr at the end of the cycle (speculative issue, wait in
     // finish, bookkeeping after it)
     const bool trace = getenv("KB_HOST_TRACE") != nullptr;
-    const int64_t stall_job = ctx->test_stall_job;  // tests (read once at kb_create): a host stall before job k
+    const int64_t stall_job = ctx->test_stall_job;  // tests (read once at kb_create): a host stall before unit k
     const int stall_ms = ctx->test_stall_ms;
     uint64_t n_iter_all = 0;
     const auto loop0 = std::chrono::steady_clock::now();
@@ -692,21 +752,7 @@ struct Driver {
     const auto us = [](clk::time_point a, clk::time_point b) {
       return std::chrono::duration<double, std::micro>(b - a).count();
     };
-    if (!pipe) {  // one kb_place_job per job
-      while (have) {
-        const kb_job_req req = make_req(j);
-        kb_job_result res;
-        if (int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res)) return rc;
-        apply(q, j, res);
-        if (hook_rc) return hook_rc;
-        have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, q, j);
-        if (have && check_specs(j)) return KB_E_INVALID;
-      }
-    }
-    // Pipelined: jobs are issued before the result of the jobs ahead of them is read (the fed engine: two
-    // ahead, kJobSlots slots; the per-job launch path: one ahead, two slots), so the device runs them back to
-    // back while the host does the bookkeeping.
-    int n_slots = fed ? kbgpu::kJobSlots : 2;
+    int n_slots = 2;
     const auto free_slot = [&]() {
       for (int sl = 0; sl < n_slots; ++sl) {
         bool used = false;
@@ -715,82 +761,116 @@ struct Driver {
       }
       return -1;
     };
-    fl.clear();
-    if (have && pipe) {
-      const kb_job_req req = make_req(j);
-      if (int rc = kb_job_issue(ctx, &req, 0, nullptr)) return rc;
-      fl.push_back(Flight{q, j, 0, kb_job_pred{}});
-    }
-    while (!fl.empty()) {
-      const auto c0 = clk::now();
-      for (;;) {  // top up the speculative chain
-        const int fs = (int)fl.size() < n_slots ? free_slot() : -1;
-        if (fs < 0 || !speculate(fs)) break;
+    while (hv > 0) {
+      // the unit's device mode: start the engine for a fed unit, stop it for the others (every unit in flight has
+      // drained: the speculation never crosses a mode change)
+      bool mode = u.fed;
+      if (mode && !engine.on) {
+        const auto b0 = clk::now();
+        if (int rc = kb_fed_begin(ctx, max_unit)) return rc;
+        engine.on = true;
+        fed_begin_ms += us(b0, clk::now()) * 1e-3;
+      } else if (!mode && engine.on) {
+        engine.on = false;
+        if (int rc = kb_fed_end(ctx)) return rc;
       }
-      const auto c1 = clk::now();
-      if (stall_job >= 0 && (int64_t)n_iter_all == stall_job)  // KB_TEST_STALL_JOB: a host stall (GC pause, ...)
-        std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
-      ++n_iter_all;
-      Flight f0 = fl.front();
-      kb_job_result res;
-      int rc = kb_job_finish(ctx, f0.slot, pn.data(), pk.data(), &res, 0);
-      if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this job and the rest of the
-        rc = kb_fed_abandon(ctx);  // cycle run on the launch path (the speculative jobs never ran)
-        fl.assign(1, f0);
-        fl[0].slot = 0;
-        n_slots = 2;
-        if (rc == KB_OK) {
-          const kb_job_req req = make_req(f0.j);
-          rc = kb_job_issue(ctx, &req, 0, nullptr);
+      if (!mode && fed_allowed) ctx->stats.off_engine_units++;
+      if (!mode && !launch_pipe) {  // one kb_place_job per unit
+        const kb_job_req req = make_req(u);
+        kb_job_result res;
+        if (int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res)) return rc;
+        const bool cont = apply(u, res);
+        if (hook_rc) return hook_rc;
+        Unit nu;
+        hv = advance(u, cont, nu);
+        if (hv < 0) return hv;
+        u = nu;
+        continue;
+      }
+      // pipelined (the fed engine: two units ahead, kJobSlots slots; the launch path: one ahead, two slots)
+      n_slots = mode ? kbgpu::kJobSlots : 2;
+      fl.clear();
+      {
+        const kb_job_req req = make_req(u);
+        if (int rc = kb_job_issue(ctx, &req, 0, nullptr)) return rc;
+        fl.push_back(Flight{u, 0, kb_job_pred{}});
+      }
+      while (!fl.empty()) {
+        const auto c0 = clk::now();
+        for (;;) {  // top up the speculative chain
+          const int fs = (int)fl.size() < n_slots ? free_slot() : -1;
+          if (fs < 0 || !speculate(fs, mode)) break;
         }
-        if (rc == KB_OK) rc = kb_job_finish(ctx, 0, pn.data(), pk.data(), &res, 0);
-      }
-      const kb_job_pred& pred = fl.front().pred;
-      const bool chained = fl.size() > 1;
-      const bool match = chained && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
-                         jobs[f0.j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
-                                                            (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
-      if (chained && !match) {  // every later guard fails on the device as well: drain the skipped jobs
-        for (size_t i = 1; i < fl.size(); ++i) {
-          kb_job_result skip;
-          int rc2 = kb_job_finish(ctx, fl[i].slot, nullptr, nullptr, &skip, 1);
-          if (rc2 == kFedIdleExit) {  // it never ran, nor did the ones after it: nothing to drain
-            rc2 = kb_fed_abandon(ctx);
-            n_slots = 2;
+        const auto c1 = clk::now();
+        if (stall_job >= 0 && (int64_t)n_iter_all == stall_job)  // KB_TEST_STALL_JOB: a host stall (GC pause, ...)
+          std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
+        ++n_iter_all;
+        Flight f0 = fl.front();
+        kb_job_result res;
+        int rc = kb_job_finish(ctx, f0.slot, pn.data(), pk.data(), &res, 0);
+        if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this unit and the rest of the chain
+          rc = kb_fed_abandon(ctx);  // run on the launch path (the speculative units never ran)
+          engine.on = false;
+          mode = false;
+          fl.assign(1, f0);
+          fl[0].slot = 0;
+          n_slots = 2;
+          if (rc == KB_OK) {
+            const kb_job_req req = make_req(f0.u);
+            rc = kb_job_issue(ctx, &req, 0, nullptr);
+          }
+          if (rc == KB_OK) rc = kb_job_finish(ctx, 0, pn.data(), pk.data(), &res, 0);
+        }
+        const kb_job_pred& pred = fl.front().pred;
+        const bool chained = fl.size() > 1;
+        const bool match = chained && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
+                           jobs[f0.u.j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
+                                                                (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
+        if (chained && !match) {  // every later guard fails on the device as well: drain the skipped units
+          for (size_t i = 1; i < fl.size(); ++i) {
+            kb_job_result skip;
+            int rc2 = kb_job_finish(ctx, fl[i].slot, nullptr, nullptr, &skip, 1);
+            if (rc2 == kFedIdleExit) {  // it never ran, nor did the ones after it: nothing to drain
+              rc2 = kb_fed_abandon(ctx);
+              engine.on = false;
+              mode = false;
+              n_slots = 2;
+              if (rc == KB_OK) rc = rc2;
+              break;
+            }
             if (rc == KB_OK) rc = rc2;
-            break;
           }
-          if (rc == KB_OK) rc = rc2;
+          fl.resize(1);
         }
-        fl.resize(1);
-      }
-      if (rc) return rc;
-      const auto c2 = clk::now();
-      apply(f0.q, f0.j, res);
-      if (hook_rc) return hook_rc;
-      int nq, nj;
-      have = next_job(qheap, [this](int qq) -> GoHeap<int>& { return jheaps[qq]; }, nq, nj);
-      fl.erase(fl.begin());
-      if (!fl.empty()) {
-        if (!have || nq != fl[0].q || nj != fl[0].j) {  // cannot happen: the speculation replays the loop head
-          for (const Flight& f : fl) {
-            kb_job_result drain;
-            (void)kb_job_finish(ctx, f.slot, nullptr, nullptr, &drain, 1);
+        if (rc) return rc;
+        const auto c2 = clk::now();
+        const bool cont = apply(f0.u, res);
+        if (hook_rc) return hook_rc;
+        Unit nu;
+        hv = advance(f0.u, cont, nu);
+        if (hv < 0) return hv;
+        fl.erase(fl.begin());
+        if (!fl.empty()) {
+          if (hv == 0 || !(nu == fl[0].u)) {  // cannot happen: the speculation replays the loop
+            for (const Flight& f : fl) {
+              kb_job_result drain;
+              (void)kb_job_finish(ctx, f.slot, nullptr, nullptr, &drain, 1);
+            }
+            ctx->err = "speculative unit does not match the loop order";
+            return KB_E_STATE;
           }
-          ctx->err = "speculative job does not match the loop order";
-          return KB_E_STATE;
+        } else if (hv > 0 && nu.fed == mode) {
+          const kb_job_req req = make_req(nu);
+          const int fs = free_slot();
+          if (int rc3 = kb_job_issue(ctx, &req, fs, nullptr)) return rc3;
+          fl.push_back(Flight{nu, fs, kb_job_pred{}});
+        }  // else the chain ends: no next unit, or the next one runs in the other mode (u, below)
+        if (hv > 0) u = nu;
+        if (trace) {
+          const auto c3 = clk::now();
+          t_spec += us(c0, c1), t_fin += us(c1, c2), t_apply += us(c2, c3);
+          ++n_iter;
         }
-      } else if (have) {
-        if (check_specs(nj)) return KB_E_INVALID;
-        const kb_job_req req = make_req(nj);
-        const int fs = free_slot();
-        if (int rc3 = kb_job_issue(ctx, &req, fs, nullptr)) return rc3;
-        fl.push_back(Flight{nq, nj, fs, kb_job_pred{}});
-      }
-      if (trace) {
-        const auto c3 = clk::now();
-        t_spec += us(c0, c1), t_fin += us(c1, c2), t_apply += us(c2, c3);
-        ++n_iter;
       }
     }
     loop_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - loop0).count();
@@ -800,13 +880,13 @@ struct Driver {
     out->n_events = n_events;
     const auto r3 = std::chrono::steady_clock::now();
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
-    if (fed) {
-      fed_end.on = false;
+    if (engine.on) {
+      engine.on = false;
       if (int rc = kb_fed_end(ctx)) return rc;
     }
     if (trace)
       fprintf(stderr, "kb_host_trace pre_ms=%.3f fed_begin_ms=%.3f post_ms=%.3f\n", us(r0, r1) * 1e-3,
-              us(r1, r2) * 1e-3, us(r3, clk::now()) * 1e-3);
+              fed_begin_ms, us(r3, clk::now()) * 1e-3);
     return KB_OK;
   }
 };

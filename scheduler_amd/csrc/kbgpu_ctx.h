@@ -31,6 +31,8 @@ struct kb_ctx {
   std::vector<char> spec_cap1;     // per spec: kSpecCap1 (a selection run with at most one Allocate per node)
   std::vector<int32_t> spec_cls;   // per spec: the class loop's finest dynamic slot (-1: not eligible)
   std::vector<int64_t> aff_slot_D;  // per topology slot: its domain count
+  std::vector<int32_t> spec_aff_class0;  // per spec: aff_class as kb_upload_specs got it (kb_upload_affinity marks
+                                         // specs with an empty affinity entry -1: they run as plain specs)
   uint32_t aff_n_tables = 0, aff_n_h = 0;  // kb_apply_affinity's bounds
   uint64_t* cls_lvl = nullptr;  // [kClsLevels][n] class loop scratch: keys after 1..kClsLevels commits
   int32_t* cls_amax = nullptr;  // [n] class loop scratch: Allocates before Idle stops fitting
@@ -239,6 +241,9 @@ extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, i
 // the engine can serve a cycle whose jobs have at most max_job_tasks tasks (past one selector's key plan only the
 // split engine, whose jobs are one segment)
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks);
+// the most tasks one engine command may carry: kFedSplitMaxTasks when the cycle would take the split engine, else 0
+// (no bound: the one-workgroup engine runs any number of segments per command)
+extern "C" __attribute__((visibility("hidden"))) uint32_t kb_fed_unit_cap(kb_ctx* c);
 // max_job_tasks: the most tasks any job of the cycle can place (the split engine takes one-segment jobs only)
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);

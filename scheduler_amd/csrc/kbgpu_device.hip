@@ -2882,7 +2882,8 @@ struct FedXchg {
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
   uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
-  uint64_t sphase[8];  // SHARD: the placer's exchange phases (kb_stats.shard_phase_ticks), ahead of sdiag
+  uint64_t sphase[8];  // SHARD: [0..5] the placer's exchange phases (kb_stats.shard_phase_ticks); every split launch:
+                       // [6] / [7] the placer's / selector 0's placement (kb_stats.fed_wg_place), ahead of sdiag
   uint64_t sdiag[16];  // KB_DIAG builds: [0..6] the selector's phases, [8..11] the placer's merge; [12..15] the placer's
                        // counters for kb_stats (every build: exchange wait / count, clock / realtime ticks)
 };
@@ -3521,6 +3522,12 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   if constexpr (SPLIT) {
+    if (tid == 0 && blockIdx.x <= 1) {  // where the placer and selector 0 run (XCC id, HW_ID: CU, SIMD, SE)
+      uint32_t xcc, hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      X->sphase[6 + blockIdx.x] = (uint64_t)xcc << 32 | hw;
+    }
     if (blockIdx.x >= 1) {
       fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
                        (int)blockIdx.x - 1, nsel, (uint32_t*)cand);

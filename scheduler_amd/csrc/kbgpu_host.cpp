@@ -525,8 +525,11 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
                        s.init_cpu < lim && s.init_mem >= 0 && s.init_mem < lim && s.nz_cpu >= 0 && s.nz_cpu < lim &&
                        s.nz_mem >= 0 && s.nz_mem < lim;
   }
-  for (uint32_t i = 0; i < in->m; ++i)
+  c->spec_aff_class0.assign(in->m, -1);
+  for (uint32_t i = 0; i < in->m; ++i) {
     c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
+    c->spec_aff_class0[i] = in->specs[i].aff_class;
+  }
   for (uint32_t i = 0; i < in->m; ++i) {
     int64_t sum = 0;
     for (uint32_t j = 0; j < in->specs[i].pref_term_cnt; ++j)
@@ -585,6 +588,10 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   }
   std::vector<kb_spec> specs(a->m);
   if (a->m) HIP_OK(c, hipMemcpy(specs.data(), c->P.specs, a->m * sizeof(kb_spec), hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < a->m; ++s) {  // as kb_upload_specs had them (an earlier upload may have marked some inert)
+    specs[s].aff_class = c->spec_aff_class0[s];
+    c->spec_needs_aff[s] = (specs[s].flags & KB_SPEC_POD_AFFINITY) || specs[s].aff_class >= 0;
+  }
   c->spec_dyn.assign(a->m, 0);
   c->spec_hist.assign(a->m, 0);
   c->spec_incr.assign(a->m, 0);
@@ -640,6 +647,22 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
     int rc_;
     if ((rc_ = upload(c, c->aff_mem, &c->cls_coff[F], off.data(), K + 1))) return rc_;
     if ((rc_ = upload(c, c->aff_mem, &c->cls_mem[F], mem.data(), mem.size()))) return rc_;
+  }
+  // A spec whose affinity entry is empty -- no checks, no InterPodAffinity histograms, no table its commits write,
+  // no batch score error -- is one the affinity stages leave alone: every node passes InterPodAffinityMatches, its
+  // InterPodAffinity counts are all 0 (score 0, interpod_affinity.go:219-241), and its commits move nothing. It
+  // gets KB_SPEC_POD_AFFINITY only because some other pod of the session has terms (the exporter's aff_in_play).
+  // Such specs run as plain ones (aff_class -1 on the device): the resident engine takes them (a mixed cycle's
+  // C2 jobs beside its affinity jobs).
+  for (uint32_t s = 0; s < a->m; ++s) {
+    const int32_t ac = specs[s].aff_class;
+    if (ac < 0 || c->spec_ipa_err[s]) continue;
+    const kb_aff_spec& e = a->specs[ac];
+    if (e.check_cnt || e.hist_cnt || e.lister_cnt || e.incr_cnt || (e.flags & KB_AFF_SELF_DYNAMIC)) continue;
+    specs[s].aff_class = -1;
+    c->spec_needs_aff[s] = 0;
+    c->aff_rd[s].clear();
+    c->aff_wr[s].clear();
   }
   if (a->m) HIP_OK(c, hipMemcpy(c->P.specs, specs.data(), a->m * sizeof(kb_spec), hipMemcpyHostToDevice));
   DevAff& A = c->P.A;
@@ -1636,6 +1659,10 @@ int kb_spec_fed_ok(kb_ctx* c, int spec) {
   return c->use_fed ? 1 : 0;
 }
 
+uint32_t kb_fed_unit_cap(kb_ctx* c) {
+  return c && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) ? (uint32_t)kFedSplitMaxTasks : 0u;
+}
+
 int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks) {
   if (!c) return 0;
   if (c->sharded && !(c->peer && c->use_fed_split && fed_split_ok(c->N.n, c->sharded) &&
@@ -1768,7 +1795,10 @@ int kb_fed_end(kb_ctx* c) {
     c->stats.fed_real_ticks += d[15];
     if (c->sharded)
       for (int k = 0; k < 6; ++k) c->stats.shard_phase_ticks[k] += ph[k];
+    c->stats.fed_wg_place[0] = ph[6];
+    c->stats.fed_wg_place[1] = ph[7];
   }
+  c->prev_listed = false;  // (the launch path's next sweep must not count on the engine's commit lists)
   // an idle exit after every job was served (a host stall before this call) loses nothing
   int32_t idle = 0;
   if (rc == KB_OK && c->any_busy() &&

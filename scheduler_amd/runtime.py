@@ -128,7 +128,8 @@ class kb_stats(C.Structure):
                 ("fed_sharded", C.c_uint64), ("shard_rezero", C.c_uint64), ("shard_xchg", C.c_uint64),
                 ("shard_wait_ticks", C.c_uint64), ("fed_clock_ticks", C.c_uint64), ("fed_real_ticks", C.c_uint64),
                 ("sweep_overlap", C.c_uint64), ("overlap_refused_tables", C.c_uint64),
-                ("shard_phase_ticks", C.c_uint64 * 6), ("peer_checks", C.c_uint64)]
+                ("shard_phase_ticks", C.c_uint64 * 6), ("peer_checks", C.c_uint64), ("fed_wg_place", C.c_uint64 * 2),
+                ("off_engine_units", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -404,7 +405,8 @@ class Context:
                 "shard_wait_ticks": st.shard_wait_ticks, "fed_clock_ticks": st.fed_clock_ticks,
                 "fed_real_ticks": st.fed_real_ticks, "sweep_overlap": st.sweep_overlap,
                 "overlap_refused_tables": st.overlap_refused_tables,
-                "shard_phase_ticks": list(st.shard_phase_ticks), "peer_checks": st.peer_checks}
+                "shard_phase_ticks": list(st.shard_phase_ticks), "peer_checks": st.peer_checks,
+                "off_engine_units": st.off_engine_units, "fed_wg_place": list(st.fed_wg_place)}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

@@ -5,6 +5,7 @@ C2  10k homogeneous nodes x 100k pods: 1k gang jobs x 100, resource fit + LeastR
 C3  20k heterogeneous nodes x 200k pods: GPU scalars, taints/tolerations, node selector/affinity
 C4  10k nodes x 100k pods with inter-pod (anti)affinity over hostname / zone / rack domains
 C5  50k nodes x 1M pods: the C2 shape scaled (the 8-GPU configuration)
+C2M the C2 shape with ~2% two-template (PS/worker) jobs and ~2% jobs with inter-pod anti-affinity (a mixed cycle)
 
 Every generator takes explicit sizes so tests can run "parity variants" (<= 1k x 5k) of the
 same shapes. There is no network: all data is synthetic.
@@ -215,6 +216,51 @@ def c4(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, n_zones=10, n_r
     return c4_parts(n_nodes, n_jobs, tasks_per_job, seed, n_zones, n_racks, n_pre, pre_job_size).cluster()
 
 
+def c2m_parts(n_nodes=10000, n_jobs=1000, tasks_per_job=100, seed=SEED, frac_multi=0.02, frac_aff=0.02,
+              fill=None) -> Parts:
+    """C2M: the C2 shape with a mixed job population: C2's nodes (plus a hostname label) and
+    per-job requests, where ~frac_multi of the jobs have two pod templates (a PS/worker job: 10% of its tasks are
+    'ps' pods with their own request, ordered before the workers -- two runs of two specs in one job) and ~frac_aff
+    of the jobs carry required pod anti-affinity to their own pods over hostname (one pod per node: inter-pod
+    terms, which the resident engine does not run). The rest are C2 jobs."""
+    rng = np.random.default_rng(seed)
+    cpu_cap, mem_cap = 64000, 256 * GI
+    cpus = rng.integers(1, 17, n_jobs) * 250
+    mems = rng.integers(1, 17, n_jobs) * (GI // 2)
+    kind = rng.random(n_jobs)
+    if fill is not None:  # as c2: node capacity for ~1/fill of the cpu the jobs ask for
+        cpu_cap = max(4000, int(float((cpus * tasks_per_job).sum()) / fill / n_nodes) // 1000 * 1000)
+    pt = Parts()
+    for i in range(n_nodes):
+        pt.nodes.append(M.Node(name=f"node-{i:05d}", alloc={M.CPU: cpu_cap, M.MEMORY: mem_cap, M.PODS: 110},
+                               labels={"kubernetes.io/hostname": f"node-{i:05d}"}))
+    _queue_pg_parts(pt, n_jobs, tasks_per_job)
+    n_ps = max(1, tasks_per_job // 10)
+    for j in range(n_jobs):
+        name = f"job{j:05d}"
+        req = {M.CPU: int(cpus[j]), M.MEMORY: int(mems[j])}
+        if kind[j] < frac_multi:  # PS / worker: two templates ("-ps-" sorts before "-wk-": ps pods first)
+            _block(pt, "ns", [f"{name}-ps-{t:04d}" for t in range(n_ps)], name, {M.CPU: 2000, M.MEMORY: 4 * GI},
+                   labels={"job": name, "role": "ps"})
+            _block(pt, "ns", [f"{name}-wk-{t:04d}" for t in range(tasks_per_job - n_ps)], name, req,
+                   labels={"job": name, "role": "worker"})
+        elif kind[j] < frac_multi + frac_aff:  # spread: one pod of the job per node
+            _block(pt, "ns", [f"{name}-{t:04d}" for t in range(tasks_per_job)], name, req, labels={"job": name},
+                   affinity={"podAntiAffinity": {"required": [
+                       {"labelSelector": {"matchLabels": {"job": name}}, "topologyKey": "kubernetes.io/hostname"}]}})
+        else:
+            _block(pt, "ns", [f"{name}-{t:04d}" for t in range(tasks_per_job)], name, req)
+    return pt
+
+
+def c2m(**kw) -> M.Cluster:
+    return c2m_parts(**kw).cluster()
+
+
+def c2m_columns(**kw):
+    return c2m_parts(**kw).columns()
+
+
 def c1_columns(**kw):
     """synth.c1's columns straight from the generator's draws (no per-pod objects: columns.columns_of_blocks)."""
     return c1_parts(**kw).columns()
@@ -228,8 +274,8 @@ def c4_columns(**kw):
     return c4_parts(**kw).columns()
 
 
-CONFIGS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4}
-COLUMNS = {"C1": c1_columns, "C3": c3_columns, "C4": c4_columns}
+CONFIGS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C2M": c2m}
+COLUMNS = {"C1": c1_columns, "C3": c3_columns, "C4": c4_columns, "C2M": c2m_columns}
 
 
 class ArraySnapshot:

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r05a}
-K=${K:-overlap or pipeline_parity or fed_split or loop_variants or survives or peer or progress or hazard}
+K=${K:-overlap or pipeline_parity or fed_split or loop_variants or survives or peer or progress or hazard or mixed}
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 mkdir -p gpurun_out
 step() {  # step <name> <timeout> <cmd...>
@@ -20,6 +20,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
     tests/test_gpu_parity.py tests/test_gpu_shard_peer.py tests/test_gpu_fed_queues.py -k "$K"
 fi
 step b2 200 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-eval
+step b2m 300 python bench.py --config C2M --steps 10 --warmup 2 --no-cpu-baseline --no-eval
 step b2coop 200 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-eval --opt fed_coop_launch
 step trace 300 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/${TAG}_trace" -o run --output-format csv -- \
   python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-eval

@@ -302,6 +302,8 @@ PIPE_CLUSTERS = CLUSTERS + [
     # is often the same job), and ready jobs compete with unready ones in the gang order
     ("C2-halfgang", _partial_gang(synth.c2(n_nodes=120, n_jobs=30, tasks_per_job=20, seed=31), 0.5)),
     ("C1-thirdgang", _partial_gang(synth.c1(n_nodes=100, n_jobs=20, tasks_per_job=24, seed=32), 0.34)),
+    # two-template jobs (two units per pop on the engine) and anti-affinity jobs (off the engine) among C2 jobs
+    ("C2M-mixed", synth.c2m(n_nodes=300, n_jobs=30, tasks_per_job=12, seed=33, frac_multi=0.3, frac_aff=0.2)),
 ]
 
 
@@ -392,8 +394,10 @@ def test_fed_split_engine_parity(name, cluster, split):
     assert len(got["events"]) > 0
 
 
-def test_fed_split_engine_steps_aside_for_long_jobs():
-    """A job of more than one segment (150 tasks) keeps the cycle on the one-workgroup engine."""
+def test_fed_split_engine_takes_long_jobs_as_units():
+    """A job of more than one segment (150 tasks) goes to the split engine as units of at most one segment (the
+    driver runs the job's next unit in the same pop when a unit places all its tasks without the job becoming
+    ready): the cycle stays on the split engine, with the oracle's placements."""
     cl = synth.c2(n_nodes=2200, n_jobs=8, tasks_per_job=150, seed=45)
     ref = pyoracle.allocate(cl)
     snap = E.Snapshot(cl)
@@ -404,8 +408,38 @@ def test_fed_split_engine_steps_aside_for_long_jobs():
         st = ctx.stats()
     finally:
         ctx.close()
-    assert st["fed_cycles"] == 1 and st["fed_split"] == 0
+    assert st["fed_cycles"] == 1 and st["fed_split"] == 1 and st["off_engine_units"] == 0, st
     _compare(ref, runtime.result_dict(snap, out))
+
+
+MIXED_CLUSTERS = [
+    # the split engine (n > 2048) with two-template jobs and anti-affinity jobs among C2 jobs
+    ("C2M-split", synth.c2m(n_nodes=2500, n_jobs=60, tasks_per_job=30, seed=61, frac_multi=0.15, frac_aff=0.15)),
+    # the one-workgroup engine, half gangs (jobs stop READY and come back mid-way through their units)
+    ("C2M-small-halfgang", _partial_gang(synth.c2m(n_nodes=600, n_jobs=40, tasks_per_job=20, seed=62,
+                                                   frac_multi=0.2, frac_aff=0.2), 0.5)),
+    # two-template jobs only: every unit on the engine, one launch for the cycle
+    ("C2M-multi-only", synth.c2m(n_nodes=2300, n_jobs=40, tasks_per_job=40, seed=63, frac_multi=0.5, frac_aff=0.0)),
+    # capacity for ~80% of the work: NO_FIT units on both paths
+    ("C2M-nofit", synth.c2m(n_nodes=2100, n_jobs=50, tasks_per_job=60, seed=64, frac_multi=0.2, frac_aff=0.1,
+                            fill=1.3)),
+]
+
+
+@pytest.mark.parametrize("name,cluster", MIXED_CLUSTERS, ids=[c[0] for c in MIXED_CLUSTERS])
+def test_mixed_cycle_matches_oracle(name, cluster):
+    """A cycle mixing engine units with units the engine does not take (inter-pod affinity): the driver stops the
+    engine for those, runs them on the launch path and starts it again for the next engine unit; a two-template job
+    is two units of one pop. Placements, statuses and FitErrors equal the oracle's."""
+    ref = pyoracle.allocate(cluster)
+    st = {}
+    got = runtime.allocate(cluster, stats_out=st)
+    _compare(ref, got)
+    assert st["fed_cycles"] >= 1, st
+    if name == "C2M-multi-only":
+        assert st["off_engine_units"] == 0 and st["fed_cycles"] == 1, st
+    else:
+        assert st["off_engine_units"] > 0, st
 
 
 def _ratio_cluster(seed=77, n_nodes=3000, n_specs=48):
