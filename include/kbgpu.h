@@ -219,7 +219,8 @@ typedef struct kb_opts {
   int32_t test_stall_ms; /* tests: with test_stall_job >= 0, a host stall of this long before that job */
   int64_t test_stall_job;/* tests: -1 off */
   uint32_t shard_epoch0; /* tests: the node-sharded engine's first cycle epoch (0; the inbox tags' wrap) */
-  uint32_t pad;
+  int32_t fed_xcc;       /* ABI 14: the split engine's workgroups: 0 = where the dispatcher puts them; k + 1 = on XCC k
+                            (a census at launch, kbgpu_device.hip fed_engine_kernel); -1 = the library's default */
 } kb_opts;
 
 typedef struct kb_ctx kb_ctx;
@@ -465,8 +466,9 @@ typedef struct kb_stats {
   uint64_t fed_wg_place[2];           /* the last split engine launch: where its placer [0] and selector 0 [1] ran,
                                          XCC id << 32 | HW_ID (CU id bits 11:8, SIMD 5:4, SE 15:13) */
   uint64_t off_engine_units;          /* kb_allocate units the resident engine does not take (inter-pod affinity,
-                                         host-evaluated reasons, ...), run on the launch path between two engine
-                                         launches of a cycle that otherwise runs on the engine */
+                                         host-evaluated reasons, ...), run on the launch path while the engine of a
+                                         cycle that otherwise runs on it is paused (or between two launches) */
+  uint64_t fed_pauses;                /* engine pauses for such units (the engine idles; its next command is fresh) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

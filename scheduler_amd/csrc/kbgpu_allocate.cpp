@@ -723,13 +723,15 @@ struct Driver {
     }
     const bool launch_pipe = pipe && !(ctx->sharded && !ctx->comm);
     const auto r1 = std::chrono::steady_clock::now();
-    struct FedEnd {  // the engine is stopped on every way out of the loop
+    using clk = std::chrono::steady_clock;
+    struct FedEnd {  // the engine is stopped on every way out of the loop (paused or not)
       kb_ctx* c;
-      bool on = false;
+      bool on = false, paused = false;
       ~FedEnd() {
         if (on) (void)kb_fed_end(c);
       }
     } engine{ctx};
+    clk::time_point pause_t0{};
     double fed_begin_ms = 0;
     Unit u;
     int hv;
@@ -748,7 +750,6 @@ struct Driver {
     const auto loop0 = std::chrono::steady_clock::now();
     double t_spec = 0, t_fin = 0, t_apply = 0;
     uint64_t n_iter = 0;
-    using clk = std::chrono::steady_clock;
     const auto us = [](clk::time_point a, clk::time_point b) {
       return std::chrono::duration<double, std::micro>(b - a).count();
     };
@@ -764,18 +765,28 @@ struct Driver {
     while (hv > 0) {
       // the unit's device mode: start the engine for a fed unit, stop it for the others (every unit in flight has
       // drained: the speculation never crosses a mode change)
+      // (a unit the engine does not take pauses it: the launch paths run beside the idle engine, whose next
+      // command comes fresh; a pause longer than kMaxPause ends the engine instead, before its idle exit)
+      constexpr auto kMaxPause = std::chrono::milliseconds(200);
       bool mode = u.fed;
-      if (mode && !engine.on) {
+      if (mode && engine.paused) {
+        if (int rc = kb_fed_resume(ctx)) return rc;
+        engine.paused = false;
+      } else if (mode && !engine.on) {
         const auto b0 = clk::now();
         if (int rc = kb_fed_begin(ctx, max_unit)) return rc;
         engine.on = true;
         fed_begin_ms += us(b0, clk::now()) * 1e-3;
-      } else if (!mode && engine.on) {
-        engine.on = false;
+      } else if (!mode && engine.on && !engine.paused) {
+        if (int rc = kb_fed_pause(ctx)) return rc;
+        engine.paused = true;
+        pause_t0 = clk::now();
+      } else if (!mode && engine.paused && clk::now() - pause_t0 > kMaxPause) {
+        engine.on = engine.paused = false;
         if (int rc = kb_fed_end(ctx)) return rc;
       }
-      if (!mode && fed_allowed) ctx->stats.off_engine_units++;
       if (!mode && !launch_pipe) {  // one kb_place_job per unit
+        if (fed_allowed) ctx->stats.off_engine_units++;
         const kb_job_req req = make_req(u);
         kb_job_result res;
         if (int rc = kb_place_job(ctx, &req, pn.data(), pk.data(), &res)) return rc;
@@ -810,7 +821,7 @@ struct Driver {
         int rc = kb_job_finish(ctx, f0.slot, pn.data(), pk.data(), &res, 0);
         if (rc == kFedIdleExit) {  // the engine idled out during a host stall: this unit and the rest of the chain
           rc = kb_fed_abandon(ctx);  // run on the launch path (the speculative units never ran)
-          engine.on = false;
+          engine.on = engine.paused = false;
           mode = false;
           fl.assign(1, f0);
           fl[0].slot = 0;
@@ -832,7 +843,7 @@ struct Driver {
             int rc2 = kb_job_finish(ctx, fl[i].slot, nullptr, nullptr, &skip, 1);
             if (rc2 == kFedIdleExit) {  // it never ran, nor did the ones after it: nothing to drain
               rc2 = kb_fed_abandon(ctx);
-              engine.on = false;
+              engine.on = engine.paused = false;
               mode = false;
               n_slots = 2;
               if (rc == KB_OK) rc = rc2;
@@ -844,6 +855,7 @@ struct Driver {
         }
         if (rc) return rc;
         const auto c2 = clk::now();
+        if (!f0.u.fed && fed_allowed) ctx->stats.off_engine_units++;
         const bool cont = apply(f0.u, res);
         if (hook_rc) return hook_rc;
         Unit nu;
@@ -881,7 +893,7 @@ struct Driver {
     const auto r3 = std::chrono::steady_clock::now();
     for (uint32_t t = 0; t < s.n_tasks; ++t) out->task_status[t] = task_status[t];
     if (engine.on) {
-      engine.on = false;
+      engine.on = engine.paused = false;
       if (int rc = kb_fed_end(ctx)) return rc;
     }
     if (trace)

@@ -158,12 +158,20 @@ struct kb_ctx {
   uint64_t* h_fed_ctrs = nullptr;  // pinned: the placer's counters at the end of fed_xchg, copied at kb_fed_end
   bool use_fed_split = true;  // !KB_OPT_NO_FED_SPLIT
   bool fed_split_now = false;  // the running fed cycle is on the split engine (its FedXchg counters)
+  // kb_fed_pause: the engine idles between two commands while launch-path units run on stream_alt (swapped into
+  // `stream` for the pause); the first command after kb_fed_resume is flagged fresh (FedCmd::fresh)
+  bool fed_paused = false, fed_fresh = false;
+  hipStream_t stream_alt = nullptr;
   // The resident engine waits for sweeps issued on stream_b: they must never queue behind it on one hardware queue.
   // stream_b is a CU-masked stream (a hardware queue of its own, never shared with other streams of the process),
   // and the engine a plain launch whose every workgroup fits the device at once (launch_fed_engine checks the
   // occupancy first). KB_OPT_FED_SHARED_QUEUES (tests): a plain stream_b, the hazard the dedicated queue removes.
   bool fed_dedicated = true;
   bool fed_coop = false;  // KB_OPT_FED_COOP_LAUNCH (A/B only): the default is a plain launch + residency check
+  // kb_opts.fed_xcc - 1: the split engine's XCC (-1: the dispatcher's placement). Default XCC 0: measured on C2
+  // (r05c), the placer and selector on XCC 0-3 run 17.0-17.1 us per job, on XCC 4-7 17.6-18.1 us, and a plain
+  // launch lands wherever the dispatcher's round robin stands
+  int fed_xcc = 0;
   // tests only (kb_opts.test_stall_job / test_stall_ms): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;
@@ -247,6 +255,9 @@ extern "C" __attribute__((visibility("hidden"))) uint32_t kb_fed_unit_cap(kb_ctx
 // max_job_tasks: the most tasks any job of the cycle can place (the split engine takes one-segment jobs only)
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks);
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_end(kb_ctx* c);
+// Launch-path units between two engine commands without ending the engine (nothing may be in flight either way)
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_pause(kb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_resume(kb_ctx* c);
 // kb_job_finish's code when the resident engine idled out before serving the job (see kb_fed_abandon)
 constexpr int kFedIdleExit = -100;
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_abandon(kb_ctx* c);

@@ -195,6 +195,7 @@ struct FedCmdArgs {
   int32_t op, spec, t_begin, t_count, ready0, minav0, gang0, slot;
   int32_t g_valid, g_stop, g_placed, g_ready;
   uint32_t seq;
+  int32_t fresh = 0;  // the first command after a pause (FedCmd::fresh)
 };
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
@@ -272,10 +273,13 @@ size_t shard_inbox_bytes();
 void launch_peer_put(uint64_t* dst, uint64_t v, void* stream);
 void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream);
 // coop: a cooperative launch (every workgroup co-resident, on the device's cooperative queue); returns the
-// launch's hipError_t. shard.world > 0: the node-sharded engine (split engine only).
+// launch's hipError_t. shard.world > 0: the node-sharded engine (split engine only). place_xcc >= 0 (split engine):
+// a grid of 8 x (1 + nsel) workgroups takes a census of their XCC ids and the placer and selectors are the ones on
+// XCC place_xcc (others where it has too few), the rest exit at once.
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard);
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard,
+                      int place_xcc = -1);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.

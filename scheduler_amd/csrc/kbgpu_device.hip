@@ -2449,7 +2449,10 @@ struct FedCmd {
   int32_t spec, t_begin, t_count, ready0, minav0, gang0, slot;
   int32_t g_valid, g_stop, g_placed, g_ready;  // SpecGuard on the previous job's outcome
   uint32_t seq;
-  int32_t pad[3];
+  int32_t fresh;  // the first command after the engine was paused (kb_fed_pause): the job's sweep ran after every
+                  // earlier job committed and after the launch-path units of the pause, whose commits the engine's
+                  // own bookkeeping (the previous jobs' sets, rows and commit lists) does not know: none is used
+  int32_t pad[2];
 };
 static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
 
@@ -2485,7 +2488,7 @@ void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   FedCmd cmd{};
   if (fed)
     cmd = FedCmd{fed->op, fed->spec, fed->t_begin, fed->t_count, fed->ready0, fed->minav0, fed->gang0, fed->slot,
-                 fed->g_valid, fed->g_stop, fed->g_placed, fed->g_ready, fed->seq, {0, 0, 0}};
+                 fed->g_valid, fed->g_stop, fed->g_placed, fed->g_ready, fed->seq, fed->fresh, {0, 0}};
   FedCmd* rg = fed ? (FedCmd*)ring : nullptr;
   if (aff)
     hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
@@ -2882,6 +2885,8 @@ struct FedXchg {
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
   uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
+  uint32_t census_n;                  // place_xcc: workgroups counted in (agent-scope atomic add)
+  uint32_t census_xcc[8 * (1 + kFedMaxSel)];  //   each workgroup's XCC id + 1
   uint64_t sphase[8];  // SHARD: [0..5] the placer's exchange phases (kb_stats.shard_phase_ticks); every split launch:
                        // [6] / [7] the placer's / selector 0's placement (kb_stats.fed_wg_place), ahead of sdiag
   uint64_t sdiag[16];  // KB_DIAG builds: [0..6] the selector's phases, [8..11] the placer's merge; [12..15] the placer's
@@ -2984,6 +2989,8 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       break;
     }
     const int slot = cm.slot, spec = cm.spec;
+    const bool fresh = cm.fresh != 0;  // (every earlier job is final: nothing to patch, no set to leave out)
+    if (fresh) slot2 = slot1 = -1;
     load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot] + base, n, n_pad);
     __syncthreads();
     KB_SSTAMP(1);
@@ -2993,7 +3000,9 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     const uint64_t* stat = S.stat[slot];
     if (tid == 0) {  // job m-2 done: its commit count, after its rows were written back
       int n2 = 0;
-      if (m >= 2) {
+      // (slot2 < 0: the previous command was fresh, and job m-2 committed before the pause, so before this sweep;
+      // its list is not this selector's to patch -- nor is it kept: slot2 names no slot)
+      if (m >= 2 && slot2 >= 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
           const uint64_t h = x_load64(&X->p_done[r2]);
@@ -3056,7 +3065,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     if (tid == 0) {  // job m-1's set (published at its node setup)
       int n1 = 0;
-      if (m >= 1) {
+      if (m >= 1 && slot1 >= 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
           const uint64_t h = x_load64(&X->p_head[r1]);
@@ -3503,7 +3512,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
                                                                  int32_t* exit_flag, FedXchg* X, int nsel_arg,
-                                                                 ShardPeers SP) {
+                                                                 ShardPeers SP, int place_xcc) {
   static_assert(!SHARD || SPLIT, "the node-sharded engine is the split engine");
   static_assert(MSEL == 1 || (SPLIT && MSEL <= kFedMaxSel), "range selectors belong to the split engine");
   const int nsel = MSEL == 1 ? 1 : nsel_arg;
@@ -3522,15 +3531,49 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint32_t* k32 = lds32;
   uint64_t* cand = (uint64_t*)(lds32 + n_pad);
   if constexpr (SPLIT) {
-    if (tid == 0 && blockIdx.x <= 1) {  // where the placer and selector 0 run (XCC id, HW_ID: CU, SIMD, SE)
-      uint32_t xcc, hw;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      X->sphase[6 + blockIdx.x] = (uint64_t)xcc << 32 | hw;
+    // role: 0 the placer, k >= 1 selector k - 1. place_xcc >= 0: a census of the grid's XCC ids (every workgroup is
+    // resident: launch_fed_engine's check) picks the workgroups on XCC place_xcc first, the others in block order
+    // after them; every workgroup computes the same assignment and the unpicked ones exit. A census that does not
+    // complete within idle_ticks leaves every workgroup out (the host sees the idle exit: launch path).
+    __shared__ int32_t s_role;
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (tid == 0) {
+      int role = (int)blockIdx.x;
+      if (place_xcc >= 0) {
+        const uint32_t G = gridDim.x;
+        __hip_atomic_store(&X->census_xcc[blockIdx.x], xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&X->census_n, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool all = false;
+        while (!(all = __hip_atomic_load(&X->census_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= G) &&
+               __builtin_amdgcn_s_memrealtime() - t0 <= idle_ticks)
+          __builtin_amdgcn_s_sleep(1);
+        role = -1;
+        if (all) {
+          int k = 0;  // roles in order: the target XCC's workgroups, then the rest (both in block order)
+          for (int pass = 0; pass < 2 && role < 0; ++pass)
+            for (uint32_t b = 0; b < G && k <= nsel && role < 0; ++b) {
+              const uint32_t x = __hip_atomic_load(&X->census_xcc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if ((x == (uint32_t)place_xcc + 1) == (pass == 0)) {
+                if (b == blockIdx.x) role = k;
+                ++k;
+              }
+            }
+        } else {
+          atomicMax(exit_flag, 1);
+        }
+      }
+      s_role = role;
+      if (role >= 0 && role <= 1) X->sphase[6 + role] = (uint64_t)xcc << 32 | hw;  // (kb_stats.fed_wg_place)
     }
-    if (blockIdx.x >= 1) {
+    __syncthreads();
+    const int role = s_role;
+    if (role < 0 || role > nsel) return;
+    if (role >= 1) {
       fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
-                       (int)blockIdx.x - 1, nsel, (uint32_t*)cand);
+                       role - 1, nsel, (uint32_t*)cand);
       return;
     }
   }
@@ -3663,6 +3706,11 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     const uint64_t rt0 = rt_wait0;
 #endif
     if constexpr (SHARD) t_job0 = __builtin_amdgcn_s_memrealtime();
+    if (cm.fresh) {  // after a pause: the sweep saw every earlier commit, and the launch path's units reused the slots
+      prev_slot[0] = prev_slot[1] = -1;
+      prev_ncommit[0] = prev_ncommit[1] = 0;
+      nbprev = 0;
+    }
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
     const int64_t* sci = P.sc_init + (size_t)spec * N.S;
@@ -3991,7 +4039,7 @@ bool fed_fits(int n) {
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
                     uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream) {
   FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
-             a.g_placed, a.g_ready, a.seq, {0, 0, 0}};
+             a.g_placed, a.g_ready, a.seq, a.fresh, {0, 0}};
   const int blocks = sweep ? (N.n + 63) / 64 : 1;
   hipLaunchKernelGGL(fed_cmd_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, idx_bits,
                      keys32, stat, cmd, (FedCmd*)ring, ctr, sweep ? 1 : 0);
@@ -4033,7 +4081,8 @@ void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream) {
 
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
-                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard) {
+                      int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard,
+                      int place_xcc) {
   FedSlots S;
   for (int s = 0; s < kJobSlots; ++s) {
     S.tgt[s] = tgt[s];
@@ -4052,8 +4101,9 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   const FedCmd* ring_c = (const FedCmd*)ring;
   FedXchg* X = (FedXchg*)xchg;
   ShardPeers SP = shard;
+  int pxcc = xchg && place_xcc >= 0 && place_xcc < 8 ? place_xcc : -1;
   void* args[] = {(void*)&N, (void*)&P, (void*)&C, (void*)&idx_bits, (void*)&S, (void*)&ring_c, (void*)&ctr,
-                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP};
+                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP, (void*)&pxcc};
   const bool sharded = SP.world > 0;
   if (sharded && !xchg) return (int)hipErrorInvalidValue;  // the node-sharded engine is the split engine
   const void* f = nullptr;
@@ -4082,7 +4132,8 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
 #undef KB_FED_QN
   if (!split) nsel = 1;
   if (sharded && !split) return (int)hipErrorInvalidValue;
-  const dim3 grid(split ? 1 + nsel : 1), block(kSelThreads);
+  if (!split) pxcc = -1;
+  const dim3 grid(split ? (pxcc >= 0 ? 8 : 1) * (1 + nsel) : 1), block(kSelThreads);
   if (coop) return (int)hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)bytes, (hipStream_t)stream);
   // A plain launch: its workgroups spin on each other, so every one of them must be resident at once. The
   // dispatcher places them as CUs free up (the sweeps they wait for run on another hardware queue and never wait

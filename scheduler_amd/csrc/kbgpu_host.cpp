@@ -258,6 +258,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
   if (opts && opts->eval_spb > 0) c->eval_spb = opts->eval_spb;
   if (opts) c->shard_epoch0 = opts->shard_epoch0;
+  if (opts && opts->fed_xcc >= 0) c->fed_xcc = opts->fed_xcc - 1;  // (< 0: the library's default, kbgpu_ctx.h)
   if (opts && opts->test_stall_job >= 0) {
     c->test_stall_job = opts->test_stall_job;
     if (opts->test_stall_ms > 0) c->test_stall_ms = opts->test_stall_ms;
@@ -318,6 +319,7 @@ void kb_destroy(kb_ctx* c) {
     if (c->commits[s]) (void)hipFree(c->commits[s]);
   }
   if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
+  if (c->stream_alt) (void)hipStreamDestroy(c->stream_alt);
   if (c->sweep_ctr) (void)hipFree(c->sweep_ctr);
   if (c->fed_ring) (void)hipFree(c->fed_ring);
   if (c->fed_ctr) (void)hipFree(c->fed_ctr);
@@ -1700,6 +1702,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   }
   c->fed_r = 0;
   c->fed_tasks = 0;
+  c->fed_fresh = false;
   c->fed_ev = nullptr;
   if (c->timing) {  // the engine is one launch per cycle: always timed
     const bool tn = c->timing_now;
@@ -1733,7 +1736,8 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
   const uint64_t idle = c->sharded ? 10 * c->fed_idle : c->fed_idle;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
-                                          c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP));
+                                          c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP,
+                                          c->fed_coop ? -1 : c->fed_xcc));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1760,7 +1764,47 @@ static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
   return KB_OK;
 }
 
+// Pause the resident engine between two of its commands (nothing in flight): the context's launch paths run on
+// stream_alt (a hardware queue of its own: the engine's launch keeps `stream`) while the engine idles, and
+// kb_fed_resume hands it the next command flagged fresh.
+int kb_fed_pause(kb_ctx* c) {
+  if (!c || !c->fed || c->fed_paused) return fail(c, KB_E_STATE, "fed engine not running");
+  if (c->any_busy()) return fail(c, KB_E_STATE, "fed engine: a job is still in flight");
+  if (!c->stream_alt) {
+    hipDeviceProp_t prop;
+    HIP_OK(c, hipGetDeviceProperties(&prop, c->device));
+    const int cus = std::max(prop.multiProcessorCount, 1);
+    std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+    HIP_OK(c, hipExtStreamCreateWithCUMask(&c->stream_alt, (uint32_t)mask.size(), mask.data()));
+  }
+  std::swap(c->stream, c->stream_alt);
+  c->fed = false;
+  c->fed_paused = true;
+  c->prev_listed = false;
+  c->stats.fed_pauses++;
+  return KB_OK;
+}
+
+int kb_fed_resume(kb_ctx* c) {
+  if (!c || !c->fed_paused) return fail(c, KB_E_STATE, "fed engine not paused");
+  if (c->any_busy()) return fail(c, KB_E_STATE, "a launch-path job is still in flight");
+  HIP_OK(c, hipStreamSynchronize(c->stream));  // the pause's last kernels (a table commit behind a publish)
+  std::swap(c->stream, c->stream_alt);
+  c->fed = true;
+  c->fed_paused = false;
+  c->fed_fresh = true;
+  c->prev_listed = false;
+  return KB_OK;
+}
+
 int kb_fed_end(kb_ctx* c) {
+  if (c && c->fed_paused) {  // (a pause ends with the engine: the next command is its EXIT)
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    std::swap(c->stream, c->stream_alt);
+    c->fed = true;
+    c->fed_paused = false;
+  }
   if (!c || !c->fed) return KB_OK;
   c->fed = false;
   FedCmdArgs a{KB_ENG_EXIT, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1811,6 +1855,12 @@ int kb_fed_end(kb_ctx* c) {
 // before the one the host waits for and none after. Leave fed mode; the caller re-issues the unserved job on
 // the launch path (the speculative one, never run, is dropped) and the cycle goes on there.
 int kb_fed_abandon(kb_ctx* c) {
+  if (c && c->fed_paused) {
+    (void)hipStreamSynchronize(c->stream);
+    std::swap(c->stream, c->stream_alt);
+    c->fed = true;
+    c->fed_paused = false;
+  }
   if (!c || !c->fed) return KB_OK;
   c->fed = false;
   if (c->sharded) {  // every rank would have to leave at the same job: fail loudly instead
@@ -1867,7 +1917,8 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     ((JobState*)S.h)->t_recv = 0;  // (the sharded placer's timeout note)
     FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
                  job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
-                 pred ? pred->ready : 0, ++c->seq};
+                 pred ? pred->ready : 0, ++c->seq, c->fed_fresh ? 1 : 0};
+    c->fed_fresh = false;
     if (c->issue_trace)
       fprintf(stderr, "kb_issue rank=%d seq=%u slot=%d spec=%d tasks=%u guard=%d stop=%d placed=%d ready=%d\n",
               c->sharded ? c->shard.rank : 0, c->seq, slot, job->task_specs[0], job->n_tasks, pred ? 1 : 0,
