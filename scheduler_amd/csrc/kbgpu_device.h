@@ -231,9 +231,10 @@ void launch_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int id
 // kernel (launch_fed_cmd, on the sweep stream) also posts the job's command to a kJobSlots-entry device ring and
 // counts its blocks in ctr[ring entry]; the engine serves commands in order until an EXIT command (or
 // idle_ticks without one: *exit_flag = 1).
-// Job slots: the fed engine keeps up to kJobSlots jobs in flight (the running one and two speculative ones);
-// the per-job launch path uses two of them.
-constexpr int kJobSlots = 3;
+// Job slots: the fed engine keeps up to kJobSlots jobs in flight (the running one and three speculative ones:
+// a job's sweep may predate the commits of the three before it -- the selector re-keys m-2's and m-3's rows, the
+// placer m-1's set); the per-job launch path uses two of them.
+constexpr int kJobSlots = 4;  // the fed engine's units in flight: the running one and three speculative ones
 struct FedSlotPtrs {
   uint32_t* keys[kJobSlots];
   uint64_t* stat[kJobSlots];
@@ -250,6 +251,7 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 // one job ahead (fed_split_ok(n)); nullptr: one workgroup.
 constexpr int kFedSplitMaxTasks = 100;  // one selection segment (kbgpu_device.hip kSegMax)
 size_t fed_xchg_bytes();
+size_t fed_census_bytes();  // FedXchg's census words, between wdiag and sphase (KB_DIAG's host read)
 bool fed_split_ok(int n, bool sharded);
 // selector workgroups of the split engine for n nodes (1: one holds every key; up to 4 node ranges past that;
 // 0: beyond the engine)

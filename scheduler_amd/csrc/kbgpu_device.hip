@@ -164,6 +164,34 @@ __device__ __forceinline__ Row load_row(const DevNodes& N, int n) {
   return r;
 }
 
+// The columns a commit changes, loaded around the vector L1 (sc1: agent-scope relaxed atomic loads). The selection
+// path's commits store them sc1 (store_back_row), so the fed selector reads the placer's commits once it has seen
+// the placer's tagged p_done word, without an agent-scope acquire per job (MI355X_MICROARCH.md, the hand-off
+// table's first row: sc1 stores, vmcnt(0) and one sc1 signal on the writer's side, sc1 loads on the reader's).
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Row load_row_sc1(const DevNodes& N, int n) {
+  Row r;
+  r.flags = N.flags[n];  // (flags, max_pods, allocatable: no commit changes them)
+  r.pod_count = ld_sc1(&N.pod_count[n]);
+  r.max_pods = N.max_pods[n];
+  r.idle_cpu = ld_sc1(&N.idle_cpu[n]);
+  r.idle_mem = ld_sc1(&N.idle_mem[n]);
+  r.rel_cpu = ld_sc1(&N.rel_cpu[n]);
+  r.rel_mem = ld_sc1(&N.rel_mem[n]);
+  r.nz_cpu = ld_sc1(&N.nz_cpu[n]);
+  r.nz_mem = ld_sc1(&N.nz_mem[n]);
+  r.alloc_cpu = N.alloc_cpu[n];
+  r.alloc_mem = N.alloc_mem[n];
+  return r;
+}
+
 // The columns a commit changes (idle / releasing cpu+mem, pod count, non-zero requests).
 __device__ __forceinline__ void store_row(const DevNodes& N, int n, const Row& r) {
   N.idle_cpu[n] = r.idle_cpu;
@@ -539,6 +567,19 @@ __device__ __forceinline__ void signal_skip(JobState* hjs, uint32_t seq) {
   do {                 \
   } while (0)
 #endif
+// KB_DIAG builds: fine stamps inside sel_run's e-sequences and winners (dg[8..12]: time, taken from the phase stamp
+// that follows) and counts (dg[13] e-sequence rounds, dg[14] winners threshold-search steps, dg[15] candidates K)
+#ifdef KB_DIAG
+#define KB_SEL_W(k) KB_STAMP(k)
+#define KB_SEL_COUNT(k, v) (dg[k] += (uint64_t)(v))
+#else
+#define KB_SEL_W(k) \
+  do {              \
+  } while (0)
+#define KB_SEL_COUNT(k, v) \
+  do {                     \
+  } while (0)
+#endif
 
 // Copy the buffered placements to the caller's pinned host buffer (coalesced, once per run / buffer).
 __device__ __forceinline__ void flush_placements(const uint64_t* pb, int cnt, int base, int32_t* hout, int lane) {
@@ -612,7 +653,7 @@ __global__ __launch_bounds__(512) void place_loop_kernel(DevNodes N, DevSpecs P,
   Row pr{};
   uint64_t pst = 0;
 #ifdef KB_DIAG
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1271,7 +1312,7 @@ __global__ __launch_bounds__(kPlaceThreads) void traj_place_kernel(
     int stop = KB_STOP_DONE, fail_task = -1, panic = 0, stopped = 0;
 #ifdef KB_DIAG
     // phases: 0 argmax, 1 commit, 2 chunk re-reduce, 3 chunk-max update, 4 unused, 5 loop, 6 fill
-    uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
     uint64_t dg_last = __builtin_amdgcn_s_memtime();
     dg[6] = dg_last - t_start;
 #endif
@@ -1598,13 +1639,14 @@ __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_sp
                                int c, int A, const Row& r0) {
   const int64_t a = c < A ? c : A;
   const int64_t p = c - a;
-  N.idle_cpu[w] = r0.idle_cpu - a * sp.req_cpu;
-  N.idle_mem[w] = r0.idle_mem - a * sp.req_mem;
-  N.rel_cpu[w] = r0.rel_cpu - p * sp.req_cpu;
-  N.rel_mem[w] = r0.rel_mem - p * sp.req_mem;
-  N.pod_count[w] = r0.pod_count + c;
-  N.nz_cpu[w] = r0.nz_cpu + (int64_t)c * sp.nz_cpu;
-  N.nz_mem[w] = r0.nz_mem + (int64_t)c * sp.nz_mem;
+  // (sc1 stores: the fed selector reads them with load_row_sc1, after the placer's p_done, without an acquire)
+  st_sc1(&N.idle_cpu[w], r0.idle_cpu - a * sp.req_cpu);
+  st_sc1(&N.idle_mem[w], r0.idle_mem - a * sp.req_mem);
+  st_sc1(&N.rel_cpu[w], r0.rel_cpu - p * sp.req_cpu);
+  st_sc1(&N.rel_mem[w], r0.rel_mem - p * sp.req_mem);
+  st_sc1(&N.pod_count[w], r0.pod_count + c);
+  st_sc1(&N.nz_cpu[w], r0.nz_cpu + (int64_t)c * sp.nz_cpu);
+  st_sc1(&N.nz_mem[w], r0.nz_mem + (int64_t)c * sp.nz_mem);
   uint64_t m = sp.req_sc_mask;
   while (m) {  // Sub on a nil scalar map is a no-op (resource_info.go:152-157)
     const int q = __builtin_ctzll(m);
@@ -1905,6 +1947,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         __syncthreads();
         const int na = sh.n_act;
         if (na == 0) break;
+        KB_SEL_COUNT(13, 1);
         // levels per active node this round: the largest power of two with na * L <= threads, at most 64
         int shift = 6;
         while (shift > 2 && (na << shift) > kSelThreads) --shift;
@@ -1967,6 +2010,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       uint32_t K, zero = 0, ztot;
       uint32_t pos = kc;
       sel_excl_scan2(sh, rp, pos, zero, &K, &ztot);
+      KB_SEL_W(8);  // candidate loads + count scan
+      KB_SEL_COUNT(15, K);
       if (K <= (uint32_t)KB_SEL_DENSE_MAX) {
 #pragma unroll
         for (int q = 0; q < 2 * kCandV; ++q)
@@ -1990,6 +2035,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           HN = umin32(HN, cs[q] ? h : 0xffffffffu);
         }
         sel_reduce3(sh, rp, kk, HX, HN);
+        KB_SEL_W(9);  // score range
         uint32_t lo = HN, hi = HX;  // K < T ends at lo = HN: every candidate
         while (lo < hi) {
           const uint32_t mid = lo + (hi - lo + 1) / 2;
@@ -1998,8 +2044,10 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           for (int q = 0; q < 2 * kCandV; ++q) c += cs[q] && (uint32_t)(cs[q] >> fs) >= mid;
           if (sel_sum(sh, rp, c) >= T) lo = mid;
           else hi = mid - 1;
+          KB_SEL_COUNT(14, 1);
         }
         const uint32_t thr = lo;
+        KB_SEL_W(10);  // threshold search
         if (wv == 0) {
           const int a = lane, b = lane + 64;
           const uint32_t ga = sel_cnt_ge(sh, cand, a, S, thr + 1, idx_bits);
@@ -2023,6 +2071,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           if (lane == 0) sh.s_count = (int)Kt;
         }
         __syncthreads();
+        KB_SEL_W(11);  // per-slot takes
         {  // rank of every taken element, 4 threads per element
           const int e2 = tid >> 2, part = tid & 3;
           const uint64_t v = sh.comp[e2];
@@ -2243,7 +2292,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_place_kernel(
   // phases: 0 sweep wait + key load + patch (from kernel entry), 1 node selection, 2 selected-node setup,
   // 3 e-sequences, 4 winners + order, 5 stop rules + commit, 6 no-fit histogram (thread 0 stamps after
   // the block barriers); diag[7]: realtime ticks from entry to the publish
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2355,7 +2404,7 @@ __global__ __launch_bounds__(kSelThreads) void engine_kernel(DevNodes N, DevSpec
   for (int i = n + tid; i < n_pad; i += kSelThreads) k32[i] = 0u;  // padding: infeasible, no reasons
   int rp = 0;
 #ifdef KB_DIAG
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
 #endif
   for (uint32_t want = seq0;; ++want) {
@@ -2565,7 +2614,7 @@ __global__ __launch_bounds__(kSelThreads) void shard_propose_kernel(DevNodes N, 
   }
   int ready = 0, placed = 0, stop = 0, fail_task = -1, panic = 0, stopped = 0, rp = 0;
 #ifdef KB_DIAG
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
 #endif
   __syncthreads();
@@ -2885,6 +2934,11 @@ struct FedXchg {
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
   uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
+  // (selector 0) the static cache of job m-1's set S(m-1) in its slot order (the placer's B candidates), from
+  // job m's sweep: the placer reads it here, behind the head, instead of from the sweep's buffer -- which would
+  // need an agent-scope acquire per job on the placer's CU (~1.7 us, MI355X_MICROARCH.md)
+  uint64_t s_bst[kJobSlots][128];
+  uint64_t wdiag[8];                  // KB_DIAG builds: the placer's fine sel_run stamps (dg[8..15])
   uint32_t census_n;                  // place_xcc: workgroups counted in (agent-scope atomic add)
   uint32_t census_xcc[8 * (1 + kFedMaxSel)];  //   each workgroup's XCC id + 1
   uint64_t sphase[8];  // SHARD: [0..5] the placer's exchange phases (kb_stats.shard_phase_ticks); every split launch:
@@ -2918,7 +2972,7 @@ __device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, cons
   for (int i = threadIdx.x; i < np; i += kSelThreads) {
     const int w = i < n0 ? l0[i] : l1[i - n0];
     if ((uint32_t)(w - base) >= (uint32_t)nk) continue;
-    const Row rr = load_row(N, w);
+    const Row rr = load_row_sc1(N, w);
     const uint64_t st = stat[w];
     const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
     k32[w - base] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
@@ -2965,12 +3019,13 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
   uint32_t tgt[kJobSlots];
 #pragma unroll
   for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
-  int slot2 = -1, slot1 = -1;  // slots of jobs m-2, m-1
+  int slot3 = -1, slot2 = -1, slot1 = -1;  // slots of jobs m-3, m-2, m-1
+  __shared__ int32_t s_n3;
   int rp = 0;
 #ifdef KB_DIAG
   // [0] wait for the command, [1] key load, [3] wait for job m-2 + patch, [2] wait for job m-1's set +
   // exclusion, [4] selection, [5] publish, [6] jobs
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
 #define KB_SSTAMP(k) KB_STAMP(k)
 #else
@@ -2990,24 +3045,30 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     const int slot = cm.slot, spec = cm.spec;
     const bool fresh = cm.fresh != 0;  // (every earlier job is final: nothing to patch, no set to leave out)
-    if (fresh) slot2 = slot1 = -1;
+    if (fresh) slot3 = slot2 = slot1 = -1;
     load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot] + base, n, n_pad);
     __syncthreads();
     KB_SSTAMP(1);
     const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
     const int r2 = r1 == 0 ? kJobSlots - 1 : r1 - 1;
+    const int r3 = r2 == 0 ? kJobSlots - 1 : r2 - 1;
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
-    if (tid == 0) {  // job m-2 done: its commit count, after its rows were written back
-      int n2 = 0;
+    // The host issues job m once job m - kJobSlots is read, so its sweep may predate the commits of jobs m-3, m-2
+    // and m-1: the placer re-keys m-1's set (B), this selector the rows m-2 and m-3 committed.
+    if (tid == 0) {  // jobs m-2 (and so m-3) done: their commit counts, after their rows were written back
+      int n2 = 0, n3 = 0;
       // (slot2 < 0: the previous command was fresh, and job m-2 committed before the pause, so before this sweep;
       // its list is not this selector's to patch -- nor is it kept: slot2 names no slot)
       if (m >= 2 && slot2 >= 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
+        for (int spin = 0;; ++spin) {
           const uint64_t h = x_load64(&X->p_done[r2]);
           if ((uint32_t)(h >> 32) == m - 1) {
             n2 = (int)(uint32_t)h;
+#ifdef KB_DIAG
+            dg[7] += spin == 0 ? 1 : 0;  // job m-2 had committed when the command came: the command gated this job
+#endif
             break;
           }
           if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
@@ -3017,15 +3078,25 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // its rows: no stale cached copies
+        // its rows: the main columns come through sc1 loads (load_row_sc1 of the placer's sc1 stores); a spec with
+        // scalar or host-port columns reads those with plain loads, after an agent acquire (~1.7 us)
+        if (sp.init_sc_mask | sp.req_sc_mask | sp.port_cnt | (sp.flags & (KB_SPEC_INIT_HAS_MAP | KB_SPEC_REQ_HAS_MAP)))
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      s_n1 = n2;
+      if (fresh) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the pause's launch-path kernels)
+      if (n2 >= 0 && m >= 3 && slot3 >= 0) {  // job m-3 published before m-2 (one placer): its word is there
+        const uint64_t h = x_load64(&X->p_done[r3]);
+        n3 = (uint32_t)(h >> 32) == m - 2 ? (int)(uint32_t)h : -1;
+        if (n3 < 0) atomicMax(exit_flag, 2);  // (cannot happen)
+      }
+      s_n1 = n3 < 0 ? -1 : n2;
+      s_n3 = n3 < 0 ? 0 : n3;
     }
     __syncthreads();
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
     // rows job m-2 committed (final), while job m-1 may still be choosing its set
-    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1, nullptr, 0,
-              base, n);
+    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1,
+              slot3 >= 0 ? S.commits[slot3] : nullptr, slot3 >= 0 ? s_n3 : 0, base, n);
     KB_SSTAMP(3);
     // the T best of this range outside job m-1's set are among its T + kSegMax best (the set holds at most kSegMax
     // nodes): chosen, ranked and their rows loaded before the set is known -- only the exclusion waits for it
@@ -3060,7 +3131,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     if (tid < (int)cnt) {
       wp = rnode[tid];
       wk = rkey[tid];
-      rw = load_row(N, wp + base);
+      rw = load_row_sc1(N, wp + base);
       stw = stat[wp + base];
     }
     if (tid == 0) {  // job m-1's set (published at its node setup)
@@ -3098,6 +3169,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       }
       const uint32_t w = (uint32_t)e - (uint32_t)base;
       if ((uint32_t)(e >> 32) == m && w < (uint32_t)n) k32[w] = 0u;
+      if (sel == 0 && (uint32_t)(e >> 32) == m) x_store64(&X->s_bst[r][tid], stat[(uint32_t)e]);  // (before the head)
     }
     __syncthreads();
     // candidates outside the set (a zeroed key: inside), in rank order; the first T go out
@@ -3124,13 +3196,14 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
 #ifdef KB_DIAG
     dg[6]++;
 #endif
+    slot3 = slot2;
     slot2 = slot1;
     slot1 = slot;
     __syncthreads();  // cm reused by the next command
   }
 #ifdef KB_DIAG
   if (tid == 0 && sel == 0)
-    for (int k = 0; k < 7; ++k) X->sdiag[k] = dg[k];
+    for (int k = 0; k < 8; ++k) X->sdiag[k] = dg[k];
 #endif
 #undef KB_SSTAMP
 }
@@ -3153,19 +3226,21 @@ __device__ __forceinline__ Row row_after(const kb_spec& sp, const Row& r0, int c
 
 // The no-fit FitErrors histogram (allocate.go:150-153, unschedule_info.go:57-79) of a table too large for the
 // placer's LDS: every node's key is the sweep's (keys, read from memory) unless its row changed since, on one of
-// the three commit lists; those are re-keyed. bits (LDS, n bits) marks them, so a node listed twice counts once
+// the four commit lists (the three jobs before and this one); those are re-keyed. bits (LDS, n bits) marks them, so a node listed twice counts once
 // and the streamed pass skips it. Ends after a barrier with the histogram in sh.hist.
 __device__ void fed_hist_stream(SelShared& sh, uint32_t* bits, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                                 const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
-                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2) {
+                                const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2, int n2,
+                                const int32_t* l3, int n3) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int n = N.n, nw = (n + 31) >> 5;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = tid; i < nw; i += kSelThreads) bits[i] = 0u;
   if (tid < KB_NUM_REASONS) sh.hist[tid] = 0;
   __syncthreads();
-  for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
-    const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : l2[i - n0 - n1]);
+  for (int i = tid; i < n0 + n1 + n2 + n3; i += kSelThreads) {
+    const int w = i < n0 ? l0[i]
+                         : (i < n0 + n1 ? l1[i - n0] : (i < n0 + n1 + n2 ? l2[i - n0 - n1] : l3[i - n0 - n1 - n2]));
     const uint32_t b = 1u << (w & 31);
     if (atomicOr(&bits[w >> 5], b) & b) continue;  // listed twice: its row is the same final row
     const uint32_t rs = row_reasons(N, P, C, sp, sci, load_row(N, w), stat[w], w);
@@ -3253,7 +3328,8 @@ static_assert(sizeof(ShardGather) <= 8 * kCandCap, "the gathered proposals fit t
 __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_t* cand, const ShardPeers& SP,
                                           uint32_t xn, const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                                           const kb_spec& sp, int spec, const uint64_t* stat, const uint32_t* keys,
-                                          const int32_t* l0, int n0, const int32_t* l1, int n1, int t_begin,
+                                          const int32_t* l0, int n0, const int32_t* l1, int n1, const int32_t* l2,
+                                          int n2, int t_begin,
                                           int t_count, int ready0, int minav, int gang, int idx_bits, int32_t* hout,
                                           JobState* js, JobState* hjs, int32_t* commit_out, uint64_t idle_ticks,
                                           int& stop, int& fail_task, int& placed, int& ready, int& panic, int& stopped,
@@ -3449,13 +3525,13 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     stopped = 1;
   } else if (kind == KB_STOP_NO_FIT) {
     // FitErrors over every rank's rows (allocate.go:150-153): each rank's histogram of its rows with the job's
-    // commits applied (as the one-GPU engine computes it: the sweep's keys, the rows the last two jobs and this one
+    // commits applied (as the one-GPU engine computes it: the sweep's keys, the rows the last three jobs and this one
     // wrote back re-keyed), then a second round of the exchange (17 tagged words per rank) and the sum
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores and the sweep's keys: fresh loads
     __syncthreads();
-    fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, keys, l0, n0, l1, n1, commit_out, sh.n_commit);
+    fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, keys, l0, n0, l1, n1, l2, n2, commit_out, sh.n_commit);
     if (tid < W * kShardNoFitR) {
       const int w = tid / kShardNoFitR, b = tid - w * kShardNoFitR;
       if (w == SP.rank && !SP.self_inbox) {
@@ -3585,9 +3661,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
   for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
   int last_stop = -1, last_placed = -1, last_ready = -1, last_panic = 1;  // no previous job: guards fail
-  // the commit lists of the previous two jobs ([0] the last one): a job's sweep may have run before either
-  // committed (the host issues a job once the job three back is read)
-  int prev_slot[2] = {-1, -1}, prev_ncommit[2] = {0, 0};
+  // the commit lists of the previous three jobs ([0] the last one): a job's sweep may have run before any of them
+  // committed (the host issues a job once the job kJobSlots back is read)
+  int prev_slot[3] = {-1, -1, -1}, prev_ncommit[3] = {0, 0, 0};
   int nbprev = 0;
   int rp = 0;
   // split, thread 0: the next job's command words and selector 0's head, then the other selectors' heads, loaded
@@ -3599,7 +3675,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
   // publish (fence + host writes)
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   uint64_t t_wait0 = dg_last, pub_prev = 0, rt_wait0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3619,6 +3695,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
         for (int q = 0; q < 16; ++q) have = have && (uint32_t)(pre[q] >> 32) == m + 1;
         uint64_t h = pre[16];
+#ifdef KB_DIAG
+        dg[12] += have ? 0 : 1;  // jobs whose head was not there at the previous job's end (kb_fed_placer_fine)
+#endif
         if (!have) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
@@ -3647,25 +3726,44 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
             s_na[k] = (int32_t)(uint32_t)hk;
           }
           if (c >= 0) {
+            // the selector stored the command's words before its head (vmcnt(0) between): all 16 loads issue at
+            // once, and the tags only confirm it (a word-by-word spin made this a chain of 16 L2 round trips
+            // whenever the prefetch at the end of the previous job came too early)
+            uint64_t wv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) wv[q] = have ? pre[q] : x_load64(&X->s_cmd[r][q]);
+            bool tagged = true;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) tagged = tagged && (uint32_t)(wv[q] >> 32) == m + 1;
+            if (!tagged) {
+#pragma unroll
+              for (int q = 0; q < 16; ++q) {
+                const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+                while ((uint32_t)(wv[q] >> 32) != m + 1) {  // the tag orders it
+                  if (__builtin_amdgcn_s_memrealtime() - t1 > idle_ticks) {  // (cannot happen: the head is last)
+                    c = -2;
+                    atomicMax(exit_flag, 3);
+                    break;
+                  }
+                  wv[q] = x_load64(&X->s_cmd[r][q]);
+                }
+              }
+            }
             uint32_t fields[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              uint64_t w = have ? pre[q] : x_load64(&X->s_cmd[r][q]);
-              const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-              while ((uint32_t)(w >> 32) != m + 1) {  // the tag orders it
-                if (__builtin_amdgcn_s_memrealtime() - t1 > idle_ticks) {  // (cannot happen: the head is last)
-                  c = -2;
-                  atomicMax(exit_flag, 3);
-                  break;
-                }
-                w = x_load64(&X->s_cmd[r][q]);
-              }
-              fields[q] = (uint32_t)w;
-            }
+            for (int q = 0; q < 16; ++q) fields[q] = (uint32_t)wv[q];
             __builtin_memcpy(&cm, fields, sizeof(FedCmd));
           }
-          // the sweep's static cache (another agent's release, which the selector has seen): fresh loads
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          // The placer's plain loads of global memory: the scalar / host-port columns of a spec that has them (rows
+          // its own commits wrote, and after a pause the launch path's), and everything after a pause. Those need
+          // an agent-scope acquire on this CU (~1.7 us); a plain spec's job reads nothing but the tagged hand-offs
+          // and its own LDS, so it skips it (the B candidates' static cache comes through the selector: s_bst).
+          if (c >= 0) {
+            const kb_spec& s0 = P.specs[cm.spec];
+            if (cm.fresh || (s0.flags & (KB_SPEC_INIT_HAS_MAP | KB_SPEC_REQ_HAS_MAP)) || s0.init_sc_mask ||
+                s0.req_sc_mask || s0.port_cnt)
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          }
         }
         if (c == -2) atomicMax(exit_flag, 1);
         s_cand = c;
@@ -3692,6 +3790,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         }
       }
       last_panic = 1;
+      prev_slot[2] = prev_slot[1], prev_ncommit[2] = prev_ncommit[1];
       prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
       prev_slot[0] = slot, prev_ncommit[0] = 0;
       nbprev = 0;
@@ -3707,8 +3806,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
     if constexpr (SHARD) t_job0 = __builtin_amdgcn_s_memrealtime();
     if (cm.fresh) {  // after a pause: the sweep saw every earlier commit, and the launch path's units reused the slots
-      prev_slot[0] = prev_slot[1] = -1;
-      prev_ncommit[0] = prev_ncommit[1] = 0;
+      prev_slot[0] = prev_slot[1] = prev_slot[2] = -1;
+      prev_ncommit[0] = prev_ncommit[1] = prev_ncommit[2] = 0;
       nbprev = 0;
     }
     const kb_spec sp = P.specs[spec];
@@ -3770,7 +3869,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       } else if (tid >= na && tid - na < nb) {
         const int j = tid - na, w = bprev[j];
         const Row rw = brow[j];
-        const uint64_t st = stat[w];
+        const uint64_t st = x_load64(&X->s_bst[r][j]);  // (selector 0's, behind its head: no acquire needed)
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, w);
         // an infeasible key (its reason mask) gets the B index below it, so B's keys are distinct: their ranks
         // are a permutation (still below every feasible key)
@@ -3863,12 +3962,17 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       KB_MSTAMP(3);
 #undef KB_MSTAMP
     } else {
-      // the previous two jobs' commits (final rows) re-keyed for this spec: their loads first
+      // the previous three jobs' commits (final rows) re-keyed for this spec: their loads first
       const int np0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0;
-      const int np = np0 + (prev_slot[1] >= 0 ? prev_ncommit[1] : 0);
+      const int np01 = np0 + (prev_slot[1] >= 0 ? prev_ncommit[1] : 0);
+      const int np = np01 + (prev_slot[2] >= 0 ? prev_ncommit[2] : 0);
       const int32_t* patch0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
       const int32_t* patch1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
-      const int pw = tid < np ? (tid < np0 ? patch0[tid] : patch1[tid - np0]) : -1;
+      const int32_t* patch2 = prev_slot[2] >= 0 ? S.commits[prev_slot[2]] : nullptr;
+      const auto prev_node = [&](int i) {
+        return i < np0 ? patch0[i] : (i < np01 ? patch1[i - np0] : patch2[i - np01]);
+      };
+      const int pw = tid < np ? prev_node(tid) : -1;
       Row prow;
       if (pw >= 0) prow = load_row(N, pw);
       const uint64_t pst = pw >= 0 ? stat[pw] : 0;
@@ -3880,7 +3984,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           k32[pw] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, prow, pst), pw), pw + N.base, idx_bits);
         }
         for (int i = tid + kSelThreads; i < np; i += kSelThreads) {
-          const int w = i < np0 ? patch0[i] : patch1[i - np0];
+          const int w = prev_node(i);
           const Row rr = load_row(N, w);
           const uint64_t st = stat[w];
           const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
@@ -3905,7 +4009,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                                  prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr,
                                  prev_slot[0] >= 0 ? prev_ncommit[0] : 0,
                                  prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr,
-                                 prev_slot[1] >= 0 ? prev_ncommit[1] : 0, cm.t_begin, cm.t_count, cm.ready0, minav,
+                                 prev_slot[1] >= 0 ? prev_ncommit[1] : 0,
+                                 prev_slot[2] >= 0 ? S.commits[prev_slot[2]] : nullptr,
+                                 prev_slot[2] >= 0 ? prev_ncommit[2] : 0, cm.t_begin, cm.t_count, cm.ready0, minav,
                                  gang, idx_bits, S.hout[slot], js, hjs, S.commits[slot], idle_ticks, stop, fail_task,
                                  placed, ready, panic, stopped, ph);
       t_job0 = __builtin_amdgcn_s_memrealtime();  // (the publish below counts as commit)
@@ -3939,8 +4045,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         __syncthreads();
         const int32_t* l0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
         const int32_t* l1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
+        const int32_t* l2 = prev_slot[2] >= 0 ? S.commits[prev_slot[2]] : nullptr;
         fed_hist_stream(sh, k32, N, P, C, sp, spec, stat, S.keys[slot], l0, prev_slot[0] >= 0 ? prev_ncommit[0] : 0,
-                        l1, prev_slot[1] >= 0 ? prev_ncommit[1] : 0, S.commits[slot], sh.n_commit);
+                        l1, prev_slot[1] >= 0 ? prev_ncommit[1] : 0, l2, prev_slot[2] >= 0 ? prev_ncommit[2] : 0,
+                        S.commits[slot], sh.n_commit);
         if (tid < KB_NUM_REASONS) {
           js->hist[tid] = sh.hist[tid];
           hjs->hist[tid] = sh.hist[tid];
@@ -3951,13 +4059,17 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot], n, n_pad);
         __syncthreads();
         const int n0 = prev_slot[0] >= 0 ? prev_ncommit[0] : 0, n1 = prev_slot[1] >= 0 ? prev_ncommit[1] : 0;
-        {  // the previous two jobs' commits and this job's own (one loop: two fed_patch calls here trip the
+        const int n2 = prev_slot[2] >= 0 ? prev_ncommit[2] : 0;
+        {  // the previous three jobs' commits and this job's own (one loop: two fed_patch calls here trip the
            // ROCm 7.2 inliner)
           const int32_t* l0 = prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr;
           const int32_t* l1 = prev_slot[1] >= 0 ? S.commits[prev_slot[1]] : nullptr;
-          const int n2 = sh.n_commit;
-          for (int i = tid; i < n0 + n1 + n2; i += kSelThreads) {
-            const int w = i < n0 ? l0[i] : (i < n0 + n1 ? l1[i - n0] : S.commits[slot][i - n0 - n1]);
+          const int32_t* l2 = prev_slot[2] >= 0 ? S.commits[prev_slot[2]] : nullptr;
+          const int n3 = sh.n_commit;
+          for (int i = tid; i < n0 + n1 + n2 + n3; i += kSelThreads) {
+            const int w = i < n0 ? l0[i]
+                                 : (i < n0 + n1 ? l1[i - n0]
+                                                : (i < n0 + n1 + n2 ? l2[i - n0 - n1] : S.commits[slot][i - n0 - n1 - n2]));
             const Row rr = load_row(N, w);
             const uint64_t st = stat[w];
             const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
@@ -4002,6 +4114,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     }
     if constexpr (SHARD) ph[4] += __builtin_amdgcn_s_memrealtime() - t_job0;
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
+    prev_slot[2] = prev_slot[1], prev_ncommit[2] = prev_ncommit[1];
     prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
     prev_slot[0] = slot, prev_ncommit[0] = ncommit;
     __syncthreads();  // cm / sh reused by the next command
@@ -4012,8 +4125,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #endif
   }
 #ifdef KB_DIAG
-  if (SPLIT && tid == 0)
+  if (SPLIT && tid == 0) {
     for (int k = 0; k < 4; ++k) X->sdiag[8 + k] = mg[k];
+    for (int k = 0; k < 8; ++k) X->wdiag[k] = dg[8 + k];
+  }
 #endif
   if (SPLIT && tid == 0) {  // for the host's stats: the exchange's cost (kb_stats.shard_wait_ticks / shard_xchg) and
                            // the shader clock over the launch (fed_clock_ticks / fed_real_ticks)
@@ -4047,6 +4162,7 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
 size_t fed_xchg_bytes() { return sizeof(FedXchg); }
+size_t fed_census_bytes() { return offsetof(FedXchg, sphase) - offsetof(FedXchg, census_n); }
 // Selector workgroups of the split engine for n nodes: one when every key fits one workgroup's plan, else the
 // fewest ranges of at most kFedSelNodes (kFedMaxSel at most); 0: the table is beyond the engine.
 int fed_nsel(int n) {
@@ -4552,7 +4668,7 @@ __global__ __launch_bounds__(kAffThreads) void aff_reg_kernel(
 #ifdef KB_DIAG_AFF
   // phases: 0 prologue, 1 counts + min/max, 2 keys + argmax, 3 commit (thread 0), 4 table updates,
   // 5 stop rules / flush, 6 no-fit histogram
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -5103,7 +5219,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_place_kernel(
 #ifdef KB_DIAG_AFF
   // phases: 0 prologue, 1 min / max + class keys + argmax, 2 commit (lane 0), 3 class rescan + counts,
   // 5 stop rules / flush, 6 no-fit histogram
-  uint64_t dg[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[16] = {};  // [0..6] phases; [8..15] sel_run's fine stamps (KB_SEL_W)
   uint64_t dg_last = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif

@@ -1826,12 +1826,22 @@ int kb_fed_end(kb_ctx* c) {
   if (ctrs && e == hipSuccess) {
     const uint64_t* ph = c->h_fed_ctrs;     // sphase
     const uint64_t* d = c->h_fed_ctrs + 8;  // sdiag
+    if (c->fed_diag && d[6]) {  // KB_DIAG builds: the placer's fine stamps (FedXchg::wdiag, ahead of census/sphase)
+      uint64_t w[8] = {};
+      const size_t off = fed_xchg_bytes() - kCtrWords * sizeof(uint64_t) - fed_census_bytes() - sizeof(w);
+      if (hipMemcpy(w, (char*)c->fed_xchg + off, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess && d[6])
+        fprintf(stderr, "kb_fed_placer_fine cycles/job cand_scan=%.0f range=%.0f thr_search=%.0f takes=%.0f "
+                "late_heads/job=%.3f rounds/job=%.2f search_steps/job=%.2f K/job=%.1f\n", (double)w[0] / d[6],
+                (double)w[1] / d[6], (double)w[2] / d[6], (double)w[3] / d[6], (double)w[4] / d[6],
+                (double)w[5] / d[6], (double)w[6] / d[6], (double)w[7] / d[6]);
+    }
     if (c->fed_diag && d[6]) {  // KB_DIAG builds: the selector's phases
       fprintf(stderr, "kb_fed_placer_merge cycles/job loads=%.0f b_order=%.0f union_rank=%.0f slots=%.0f\n",
               (double)d[8] / d[6], (double)d[9] / d[6], (double)d[10] / d[6], (double)d[11] / d[6]);
       fprintf(stderr, "kb_fed_selector jobs=%llu cycles/job wait_cmd=%.0f key_load=%.0f wait_set_exclude=%.0f "
-              "wait_done_patch=%.0f select=%.0f publish=%.0f\n", (unsigned long long)d[6], (double)d[0] / d[6],
-              (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6], (double)d[5] / d[6]);
+              "wait_done_patch=%.0f select=%.0f publish=%.0f cmd_gated/job=%.3f\n", (unsigned long long)d[6],
+              (double)d[0] / d[6], (double)d[1] / d[6], (double)d[2] / d[6], (double)d[3] / d[6], (double)d[4] / d[6],
+              (double)d[5] / d[6], (double)d[7] / d[6]);
     }
     c->stats.shard_wait_ticks += d[12];
     c->stats.shard_xchg += d[13];
