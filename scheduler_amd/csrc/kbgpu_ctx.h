@@ -31,6 +31,7 @@ struct kb_ctx {
   std::vector<char> spec_cap1;     // per spec: kSpecCap1 (a selection run with at most one Allocate per node)
   std::vector<int32_t> spec_cls;   // per spec: the class loop's finest dynamic slot (-1: not eligible)
   std::vector<int64_t> aff_slot_D;  // per topology slot: its domain count
+  std::vector<char> spec_rowcols;  // per spec: it reads scalar / host-port columns (the fed engine's acquire, FedCmd::acq)
   std::vector<int32_t> spec_aff_class0;  // per spec: aff_class as kb_upload_specs got it (kb_upload_affinity marks
                                          // specs with an empty affinity entry -1: they run as plain specs)
   uint32_t aff_n_tables = 0, aff_n_h = 0;  // kb_apply_affinity's bounds

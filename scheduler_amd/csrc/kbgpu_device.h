@@ -196,6 +196,7 @@ struct FedCmdArgs {
   int32_t g_valid, g_stop, g_placed, g_ready;
   uint32_t seq;
   int32_t fresh = 0;  // the first command after a pause (FedCmd::fresh)
+  int32_t acq = 0;    // FedCmd::acq
 };
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
@@ -252,6 +253,8 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 constexpr int kFedSplitMaxTasks = 100;  // one selection segment (kbgpu_device.hip kSegMax)
 size_t fed_xchg_bytes();
 size_t fed_census_bytes();  // FedXchg's census words, between wdiag and sphase (KB_DIAG's host read)
+size_t fed_trace_offset();  // KB_DIAG builds: FedXchg::tl (the per-job timeline), else 0
+int fed_trace_jobs();
 bool fed_split_ok(int n, bool sharded);
 // selector workgroups of the split engine for n nodes (1: one holds every key; up to 4 node ranges past that;
 // 0: beyond the engine)

@@ -854,7 +854,7 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
 // reciprocal estimate and corrected by one exact fma remainder, and Balanced keeps bra_score_inv's estimate with
 // its IEEE-division fallback near integers. Other rows take the int64 forms. Same values as eval_kernel on such
 // specs (tests/test_gpu_parity.py::test_eval_plain_equals_general, test_eval_plain_matches_oracle).
-constexpr int kEvalPlainSpecs = 32;
+constexpr int kEvalPlainSpecs = 64;  // (one resident round at 50k nodes needs 43: eval_plain_spb)
 constexpr double kPlainMax = 562949953421312.0;  // 2^49
 // leastRequestedScore (least_requested.go:36-53) on integers below 2^49 held in doubles. num = (cap - req) * 10
 // arrives as the node's (cap - nz_node) * 10 minus the spec's nz * 10 (exact), so req > cap is num < 0. The
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     // The loop body is branch-free, so the unrolled iterations' LDS reads and f64 chains interleave. Balanced's
     // IEEE-division fallback (f within 1e-9 of an integer, or a capacity <= 0) is deferred: the spec's bit in fb,
     // and the score is rewritten after the loop (the same thread's later store to the same word)
-    uint32_t fb = 0;
+    uint64_t fb = 0;
 #pragma unroll 4
     for (int j = 0; j < nj; ++j) {
       const double icpu = s_dreq[0][j], imem = s_dreq[1][j], nzc10 = s_dreq[2][j], nzm10 = s_dreq[3][j];
@@ -969,14 +969,19 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       const double fr = f - floor(f);
       const bool po = pos & over;
       const bool est = pos & !over & (fr > 1e-9) & (fr < 1.0 - 1e-9);
-      fb |= (uint32_t)(!est & !po) << j;
+      fb |= (uint64_t)(!est & !po) << j;
       // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
       const SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
       // uniform row bases: the stores take a scalar base and the lane's offset; non-temporal (the output is
       // streamed once, never read back by this kernel: no point keeping it in the caches)
       uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
       SCORE* srow = scores + (size_t)(j0 + j) * stride;
-#ifndef KB_EVAL_TEMPORAL
+#if defined(KB_EVAL_STOREONLY)  // (A/B builds: the stores alone, no compute -- the kernel's store bound)
+      __builtin_nontemporal_store((uint32_t)(n ^ j), rrow + n);
+      __builtin_nontemporal_store((SCORE)(n + j), srow + n);
+      (void)rs;
+      (void)score;
+#elif !defined(KB_EVAL_TEMPORAL)
       __builtin_nontemporal_store(rs, rrow + n);
       __builtin_nontemporal_store(score, srow + n);
 #else  // (A/B builds: the plain stores)
@@ -986,7 +991,7 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     }
     if (!C.nodeorder) fb = 0;
     while (fb) {  // the deferred Balanced fallbacks
-      const int j = __builtin_ctz(fb);
+      const int j = __builtin_ctzll(fb);
       fb &= fb - 1;
       const int lc = lr_score_f64(num_c - s_dreq[2][j], cap_c, lc_inv);
       const int lm = lr_score_f64(num_m - s_dreq[3][j], cap_m, lm_inv);
@@ -2179,7 +2184,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         if (rekey)
           k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
                                 idx_bits);
-        if (commit_out != nullptr) commit_out[atomicAdd(&sh.n_commit, 1)] = w;
+        if (commit_out != nullptr) st_sc1(&commit_out[atomicAdd(&sh.n_commit, 1)], (int32_t)w);  // (fed_patch: ld_sc1)
       }
       __syncthreads();
       KB_SEL_PH(5);
@@ -2501,7 +2506,9 @@ struct FedCmd {
   int32_t fresh;  // the first command after the engine was paused (kb_fed_pause): the job's sweep ran after every
                   // earlier job committed and after the launch-path units of the pause, whose commits the engine's
                   // own bookkeeping (the previous jobs' sets, rows and commit lists) does not know: none is used
-  int32_t pad[2];
+  int32_t acq;    // the job reads global columns the selection path stores plain (a spec with scalar or host-port
+                  // columns), or follows a pause: the selector and the placer take an agent acquire before it
+  int32_t pad;
 };
 static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
 
@@ -2537,7 +2544,7 @@ void launch_sel_sweep(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   FedCmd cmd{};
   if (fed)
     cmd = FedCmd{fed->op, fed->spec, fed->t_begin, fed->t_count, fed->ready0, fed->minav0, fed->gang0, fed->slot,
-                 fed->g_valid, fed->g_stop, fed->g_placed, fed->g_ready, fed->seq, fed->fresh, {0, 0}};
+                 fed->g_valid, fed->g_stop, fed->g_placed, fed->g_ready, fed->seq, fed->fresh, fed->acq, 0};
   FedCmd* rg = fed ? (FedCmd*)ring : nullptr;
   if (aff)
     hipLaunchKernelGGL(sel_sweep_kernel<true>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, spec, idx_bits,
@@ -2923,6 +2930,17 @@ constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
 constexpr int kFedMaxSel = 4;
 constexpr int kFedSelQ = 10;                          // key groups per thread of a range selector
 constexpr int kFedSelNodes = 4 * kSelThreads * kFedSelQ;  // 20480
+constexpr int kFedTraceJobs = 2048;  // KB_DIAG: the fed engine's per-job timeline (FedXchg::tl)
+#ifdef KB_DIAG
+#define KB_FED_TL(m, k)                                                      \
+  do {                                                                       \
+    if (tid == 0) X->tl[(m) & (kFedTraceJobs - 1)][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define KB_FED_TL(m, k) \
+  do {                  \
+  } while (0)
+#endif
 __host__ __device__ __forceinline__ int fed_sel_chunk(int n, int nsel) { return ((n + nsel - 1) / nsel + 3) & ~3; }
 struct FedXchg {
   uint64_t p_head[kJobSlots];        // placer -> selector (tagged, job number + 1): mode << 16 | count
@@ -2938,6 +2956,13 @@ struct FedXchg {
   // job m's sweep: the placer reads it here, behind the head, instead of from the sweep's buffer -- which would
   // need an agent-scope acquire per job on the placer's CU (~1.7 us, MI355X_MICROARCH.md)
   uint64_t s_bst[kJobSlots][128];
+#ifdef KB_DIAG
+  // KB_DIAG builds: per job (index & (kFedTraceJobs - 1)) s_memrealtime of [0] the selector's command arrival,
+  // [1] its patch done (after job m-2's p_done), [2] its selection done, [3] job m-1's set seen, [4] its head
+  // published; the placer's [5] job start (head and command read), [6] its set published, [7] p_done written,
+  // [8] its publish started (the drain before the release), [9] the release and host state done
+  uint64_t tl[kFedTraceJobs][10];
+#endif
   uint64_t wdiag[8];                  // KB_DIAG builds: the placer's fine sel_run stamps (dg[8..15])
   uint32_t census_n;                  // place_xcc: workgroups counted in (agent-scope atomic add)
   uint32_t census_xcc[8 * (1 + kFedMaxSel)];  //   each workgroup's XCC id + 1
@@ -2970,7 +2995,8 @@ __device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, cons
   const int np = n0 + n1;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = threadIdx.x; i < np; i += kSelThreads) {
-    const int w = i < n0 ? l0[i] : l1[i - n0];
+    // (sc1: the placer stores its commit lists sc1, and this selector takes no acquire per job)
+    const int w = i < n0 ? ld_sc1(&l0[i]) : ld_sc1(&l1[i - n0]);
     if ((uint32_t)(w - base) >= (uint32_t)nk) continue;
     const Row rr = load_row_sc1(N, w);
     const uint64_t st = stat[w];
@@ -3038,6 +3064,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     tgt[r] += blocks;
     fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
     KB_SSTAMP(0);
+    if (sel == 0) KB_FED_TL(m, 0);
     if (s_op != KB_ENG_RUN) {
       if (s_op == KB_ENG_EXIT && tid == 0 && sel == 0)  // the placer takes EXIT from here
         x_store64(&X->s_head[r][0], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
@@ -3078,12 +3105,11 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        // its rows: the main columns come through sc1 loads (load_row_sc1 of the placer's sc1 stores); a spec with
-        // scalar or host-port columns reads those with plain loads, after an agent acquire (~1.7 us)
-        if (sp.init_sc_mask | sp.req_sc_mask | sp.port_cnt | (sp.flags & (KB_SPEC_INIT_HAS_MAP | KB_SPEC_REQ_HAS_MAP)))
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      if (fresh) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the pause's launch-path kernels)
+      // its rows: the main columns and the commit lists come through sc1 loads (load_row_sc1 / ld_sc1 of the placer's
+      // sc1 stores); a spec with scalar or host-port columns reads those with plain loads, and after a pause the
+      // launch path's kernels wrote too: then an agent acquire (~1.7 us; the host's flag, FedCmd::acq)
+      if (cm.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (n2 >= 0 && m >= 3 && slot3 >= 0) {  // job m-3 published before m-2 (one placer): its word is there
         const uint64_t h = x_load64(&X->p_done[r3]);
         n3 = (uint32_t)(h >> 32) == m - 2 ? (int)(uint32_t)h : -1;
@@ -3097,6 +3123,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     // rows job m-2 committed (final), while job m-1 may still be choosing its set
     fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1,
               slot3 >= 0 ? S.commits[slot3] : nullptr, slot3 >= 0 ? s_n3 : 0, base, n);
+    if (sel == 0) KB_FED_TL(m, 1);
     KB_SSTAMP(3);
     // the T best of this range outside job m-1's set are among its T + kSegMax best (the set holds at most kSegMax
     // nodes): chosen, ranked and their rows loaded before the set is known -- only the exclusion waits for it
@@ -3123,6 +3150,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     __syncthreads();
     KB_SSTAMP(4);
+    if (sel == 0) KB_FED_TL(m, 2);
     // thread i: the rank-i candidate's row and static cache (final: job m-1 touches only its set)
     Row rw{};
     uint64_t stw = 0;
@@ -3156,6 +3184,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     }
     __syncthreads();
     KB_SSTAMP(2);
+    if (sel == 0) KB_FED_TL(m, 3);
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
     if (tid < s_n1) {  // job m-1's set is the placer's to re-key (every entry's tag checked: no store order)
       uint64_t e = x_load64(&X->p_node[r1][tid]);
@@ -3193,6 +3222,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     __syncthreads();
     if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | nout);
     KB_SSTAMP(5);
+    if (sel == 0) KB_FED_TL(m, 4);
 #ifdef KB_DIAG
     dg[6]++;
 #endif
@@ -3510,7 +3540,7 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
   if (tid < sh.n_sel && sh.fin[tid] > 0) {  // NodeInfo.AddTask x fin on this rank's row
     const int w = sh.node[tid];
     store_back_row(N, P, sp, P.sc_req + (size_t)spec * N.S, w, sh.fin[tid], sh.A[tid], sh.row[tid]);
-    commit_out[atomicAdd(&sh.n_commit, 1)] = w;
+    st_sc1(&commit_out[atomicAdd(&sh.n_commit, 1)], (int32_t)w);  // (fed_patch reads it ld_sc1)
   }
   placed = cut;
   ready = ready0 + G.n_alloc;
@@ -3600,6 +3630,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   __shared__ uint32_t bkey[128];  //   its keys for this job
   __shared__ int32_t s_feas;
   __shared__ int32_t s_na[MSEL];  // split: the selectors' candidate counts for this job
+  __shared__ int32_t s_pre_na;    // one selector: the next job's candidate count when its head was already there
   const int tid = threadIdx.x;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -3671,6 +3702,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t pre[16 + MSEL];
 #pragma unroll
   for (int q = 0; q < 16 + MSEL; ++q) pre[q] = 0;
+  // one selector: this thread's candidate entry of the next job, loaded at the end of this job when the next head was
+  // already there (its latency hides behind the publish), with the count it was loaded for (-1: none)
+  constexpr int kEntW = 2 + (int)(sizeof(Row) / 8);
+  uint64_t ent_pf[kEntW];
+#pragma unroll
+  for (int q = 0; q < kEntW; ++q) ent_pf[q] = 0;
+  int ent_pf_na = -1;
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -3758,12 +3796,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           // its own commits wrote, and after a pause the launch path's), and everything after a pause. Those need
           // an agent-scope acquire on this CU (~1.7 us); a plain spec's job reads nothing but the tagged hand-offs
           // and its own LDS, so it skips it (the B candidates' static cache comes through the selector: s_bst).
-          if (c >= 0) {
-            const kb_spec& s0 = P.specs[cm.spec];
-            if (cm.fresh || (s0.flags & (KB_SPEC_INIT_HAS_MAP | KB_SPEC_REQ_HAS_MAP)) || s0.init_sc_mask ||
-                s0.req_sc_mask || s0.port_cnt)
-              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          }
+          if (c >= 0 && cm.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the host's flag)
         }
         if (c == -2) atomicMax(exit_flag, 1);
         s_cand = c;
@@ -3790,6 +3823,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         }
       }
       last_panic = 1;
+      ent_pf_na = -1;  // (the prefetched entries were this skipped job's)
       prev_slot[2] = prev_slot[1], prev_ncommit[2] = prev_ncommit[1];
       prev_slot[1] = prev_slot[0], prev_ncommit[1] = prev_ncommit[0];
       prev_slot[0] = slot, prev_ncommit[0] = 0;
@@ -3801,6 +3835,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     for (int k = 0; k < 7; ++k) dg[k] = 0;
     dg_last = __builtin_amdgcn_s_memtime();
     const uint64_t wait_cycles = dg_last - t_wait0;  // wait for the command (+ guard)
+    if constexpr (SPLIT) KB_FED_TL(m, 5);
     dg[5] = pub_prev;
     const uint64_t rt0 = rt_wait0;
 #endif
@@ -3857,11 +3892,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       }
       if (list >= 0) {
         const uint64_t(*ent)[128] = X->s_ent[r][list];
-        const uint64_t e0 = x_load64(&ent[0][idx]);
-        const uint64_t st = x_load64(&ent[1][idx]);
+        // (prefetched at the previous job's end for this very head: the same count)
+        const bool pf = MSEL == 1 && ent_pf_na == na;
+        const uint64_t e0 = pf ? ent_pf[0] : x_load64(&ent[0][idx]);
+        const uint64_t st = pf ? ent_pf[1] : x_load64(&ent[1][idx]);
         uint64_t words[sizeof(Row) / 8];
 #pragma unroll
-        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = x_load64(&ent[2 + q][idx]);
+        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = pf ? ent_pf[2 + q] : x_load64(&ent[2 + q][idx]);
         __builtin_memcpy(&crow[tid], words, sizeof(Row));
         cst[tid] = st;
         cnd[tid] = (int)(e0 >> 32);
@@ -3994,6 +4031,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       }
     }
     KB_SEL_PH(0);
+    if constexpr (SPLIT) KB_FED_TL(m, 6);  // (sel_run publishes the set first thing)
     FedPub pub;
     if constexpr (SPLIT) {
       pub.head = &X->p_head[r];
@@ -4096,6 +4134,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #ifdef KB_DIAG
     const uint64_t t_pub = __builtin_amdgcn_s_memtime();
 #endif
+    if constexpr (SPLIT) KB_FED_TL(m, 8);
     if (SPLIT && tid == 0) {  // the next job's head and command: their latency hides in the drain below
       const int rn = r + 1 == kJobSlots ? 0 : r + 1;
 #pragma unroll
@@ -4104,14 +4143,31 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       for (int k = 0; k < MSEL; ++k) pre[16 + k] = k < nsel ? x_load64(&X->s_head[rn][k]) : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a barrier alone waits for LDS only)
+    if (SPLIT && MSEL == 1 && tid == 0) {  // the next job's head already there: its count, for the entry prefetch
+      const bool h_ok = (uint32_t)(pre[16] >> 32) == m + 2 && (int32_t)(uint32_t)pre[16] >= 0;
+      s_pre_na = h_ok ? (int32_t)(uint32_t)pre[16] : -1;
+    }
     __syncthreads();
     const int ncommit = sh.n_commit;
     if (tid == 0) {
       js->n_commit = ncommit;
       publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
+#ifdef KB_DIAG
+      if (SPLIT) X->tl[m & (kFedTraceJobs - 1)][9] = __builtin_amdgcn_s_memrealtime();
+#endif
       // after that release (the job's rows written back): the selector may re-key them
       if (SPLIT) tag_store(&X->p_done[r], m + 1, (uint32_t)ncommit);
     }
+    if constexpr (SPLIT && MSEL == 1) {  // every thread's entry of the next job: loads issued now (thread 0's after
+      ent_pf_na = s_pre_na;              // its publish), used at that job's merge
+      if (tid < ent_pf_na) {
+        const int rn = r + 1 == kJobSlots ? 0 : r + 1;
+        const uint64_t(*ent)[128] = X->s_ent[rn][0];
+#pragma unroll
+        for (int q = 0; q < kEntW; ++q) ent_pf[q] = x_load64(&ent[q][tid]);
+      }
+    }
+    if constexpr (SPLIT) KB_FED_TL(m, 7);
     if constexpr (SHARD) ph[4] += __builtin_amdgcn_s_memrealtime() - t_job0;
     last_stop = stop, last_placed = placed, last_ready = ready, last_panic = panic;
     prev_slot[2] = prev_slot[1], prev_ncommit[2] = prev_ncommit[1];
@@ -4154,7 +4210,7 @@ bool fed_fits(int n) {
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
                     uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream) {
   FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
-             a.g_placed, a.g_ready, a.seq, a.fresh, {0, 0}};
+             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, 0};
   const int blocks = sweep ? (N.n + 63) / 64 : 1;
   hipLaunchKernelGGL(fed_cmd_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, idx_bits,
                      keys32, stat, cmd, (FedCmd*)ring, ctr, sweep ? 1 : 0);
@@ -4163,6 +4219,12 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
 size_t fed_xchg_bytes() { return sizeof(FedXchg); }
 size_t fed_census_bytes() { return offsetof(FedXchg, sphase) - offsetof(FedXchg, census_n); }
+#ifdef KB_DIAG
+size_t fed_trace_offset() { return offsetof(FedXchg, tl); }
+#else
+size_t fed_trace_offset() { return 0; }
+#endif
+int fed_trace_jobs() { return kFedTraceJobs; }
 // Selector workgroups of the split engine for n nodes: one when every key fits one workgroup's plan, else the
 // fewest ranges of at most kFedSelNodes (kFedMaxSel at most); 0: the table is beyond the engine.
 int fed_nsel(int n) {

@@ -528,6 +528,12 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
                        s.nz_mem >= 0 && s.nz_mem < lim;
   }
   c->spec_aff_class0.assign(in->m, -1);
+  c->spec_rowcols.assign(in->m, 0);
+  for (uint32_t i = 0; i < in->m; ++i) {
+    const kb_spec& q = in->specs[i];
+    c->spec_rowcols[i] = (q.flags & (KB_SPEC_INIT_HAS_MAP | KB_SPEC_REQ_HAS_MAP)) || q.init_sc_mask || q.req_sc_mask ||
+                         q.port_cnt;
+  }
   for (uint32_t i = 0; i < in->m; ++i) {
     c->spec_needs_aff[i] = (in->specs[i].flags & KB_SPEC_POD_AFFINITY) || in->specs[i].aff_class >= 0;
     c->spec_aff_class0[i] = in->specs[i].aff_class;
@@ -1835,6 +1841,41 @@ int kb_fed_end(kb_ctx* c) {
                 (double)w[1] / d[6], (double)w[2] / d[6], (double)w[3] / d[6], (double)w[4] / d[6],
                 (double)w[5] / d[6], (double)w[6] / d[6], (double)w[7] / d[6]);
     }
+    if (c->fed_diag && d[6] && fed_trace_offset()) {  // KB_DIAG builds: the engine's per-job timeline
+      const int TJ = fed_trace_jobs();
+      constexpr int TW = 10;  // FedXchg::tl's words per job
+      std::vector<uint64_t> tl((size_t)TJ * TW);
+      const int jobs = (int)std::min<uint64_t>(d[6], (uint64_t)TJ);
+      if (hipMemcpy(tl.data(), (char*)c->fed_xchg + fed_trace_offset(), tl.size() * 8, hipMemcpyDeviceToHost) ==
+              hipSuccess && jobs > 8) {
+        // per job m (relative to the placer's end of job m-1 = when it wants job m's head): the selector's command
+        // arrival, patch done, selection done, set seen, head; the placer's start and end of job m
+        const char* names[10] = {"cmd", "patched", "selected", "set_seen", "head", "placer_start", "set_published",
+                                 "pub_start", "released", "placer_end"};
+        const int ks[10] = {0, 1, 2, 3, 4, 5, 6, 8, 9, 7};
+        std::vector<double> v[10], lv[10];
+        for (int m = 4; m < jobs - 1; ++m) {
+          const double E = (double)tl[(size_t)(m - 1) * TW + 7];
+          const bool late = tl[(size_t)m * TW + 4] > tl[(size_t)(m - 1) * TW + 7];
+          for (int k = 0; k < 10; ++k) {
+            const double x = ((double)tl[(size_t)m * TW + ks[k]] - E) * 0.01;  // us (100 MHz ticks)
+            v[k].push_back(x);
+            if (late) lv[k].push_back(x);
+          }
+        }
+        const auto pct = [](std::vector<double> x, double q) {
+          if (x.empty()) return 0.0;
+          std::sort(x.begin(), x.end());
+          return x[std::min(x.size() - 1, (size_t)(q * (double)x.size()))];
+        };
+        fprintf(stderr, "kb_fed_timeline us after the placer's end of job m-1 (p10/p50/p90; late heads %zu of %zu:"
+                " their p50)", lv[0].size(), v[0].size());
+        for (int k = 0; k < 10; ++k)
+          fprintf(stderr, " %s=%.2f/%.2f/%.2f[%.2f]", names[k], pct(v[k], 0.1), pct(v[k], 0.5), pct(v[k], 0.9),
+                  pct(lv[k], 0.5));
+        fprintf(stderr, "\n");
+      }
+    }
     if (c->fed_diag && d[6]) {  // KB_DIAG builds: the selector's phases
       fprintf(stderr, "kb_fed_placer_merge cycles/job loads=%.0f b_order=%.0f union_rank=%.0f slots=%.0f\n",
               (double)d[8] / d[6], (double)d[9] / d[6], (double)d[10] / d[6], (double)d[11] / d[6]);
@@ -1927,7 +1968,8 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     ((JobState*)S.h)->t_recv = 0;  // (the sharded placer's timeout note)
     FedCmdArgs a{KB_ENG_RUN, job->task_specs[0], 0, (int32_t)job->n_tasks, job->ready_num, job->min_available,
                  job->gang_ready, slot, pred ? 1 : 0, pred ? pred->stop : 0, pred ? pred->placed : 0,
-                 pred ? pred->ready : 0, ++c->seq, c->fed_fresh ? 1 : 0};
+                 pred ? pred->ready : 0, ++c->seq, c->fed_fresh ? 1 : 0,
+                 c->fed_fresh || c->spec_rowcols[job->task_specs[0]] ? 1 : 0};
     c->fed_fresh = false;
     if (c->issue_trace)
       fprintf(stderr, "kb_issue rank=%d seq=%u slot=%d spec=%d tasks=%u guard=%d stop=%d placed=%d ready=%d\n",

@@ -276,6 +276,7 @@ class Context:
         if self.ctx:
             self.lib.kb_destroy(self.ctx)
             self.ctx = None
+        self.forget_session()
 
     def __del__(self):
         try:
@@ -466,7 +467,12 @@ class Context:
         call on a session of the same size, whose arrays this cycle overwrites (a serving loop's reused result
         buffers: no fresh pages per cycle); by default new arrays."""
         nt, nj = len(snap.session_tasks), len(snap.jobs)
-        key = (id(snap),) + tuple(id(getattr(snap, a)) for a in SESSION_ARRAYS)
+        # The cached kb_session points into the snapshot's arrays: in-place edits of them are seen by the next call,
+        # a reassigned attribute or a changed scalar (counts, the total's scalar mask) rebuilds it. task_resreq is
+        # the one array the struct may hold a copy of (when the snapshot's is not C-contiguous): editing such an
+        # array in place needs forget_session().
+        key = ((id(snap), nt, nj, len(snap.acc_scalars), len(snap.queues), len(snap.s_tiers), int(snap.s_total_mask))
+               + tuple(id(getattr(snap, a)) for a in SESSION_ARRAYS))
         cached = getattr(self, "_ssn_cache", None)
         if cached is not None and cached[0] == key:  # the session arrays' struct, built once per snapshot and arrays
             ssn = cached[1]
@@ -496,6 +502,11 @@ class Context:
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
         return out
+
+    def forget_session(self):
+        """Drop the cached kb_session (and the snapshot it keeps alive): the next allocate() rebuilds it."""
+        self._ssn_cache = None
+        self._ssn_keep = None
 
     def _session_struct(self, snap, nt, nj):
         """kb_session over the snapshot's session arrays (kept alive with the struct in self._ssn_cache)."""
