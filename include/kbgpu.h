@@ -415,6 +415,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 #define KB_OPT_FED_COOP_LAUNCH (1u << 15)
 /* ABI 14, tests only: this rank's kb_set_shard_peer pre-flight words carry a wrong tag (every rank must fail). */
 #define KB_OPT_TEST_PEER_BADTAG (1u << 16)
+/* ABI 14: the split engine's per-job sweeps by sweep kernels on the CU-masked stream (round 4's path) instead of
+ * its resident sweepers (the spare workgroups of its census grid, fed commands through a pinned ring); A/B only. */
+#define KB_OPT_FED_KERNEL_SWEEPS (1u << 17)
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2

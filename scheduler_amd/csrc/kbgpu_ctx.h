@@ -173,6 +173,12 @@ struct kb_ctx {
   // (r05c), the placer and selector on XCC 0-3 run 17.0-17.1 us per job, on XCC 4-7 17.6-18.1 us, and a plain
   // launch lands wherever the dispatcher's round robin stands
   int fed_xcc = 0;
+  // the split engine's resident sweepers (launch_fed_engine's hring): commands go to a pinned ring (fed_hring,
+  // tags fed_epoch << 32 | fed_m + 1) instead of a sweep kernel per job; KB_OPT_FED_KERNEL_SWEEPS turns them off
+  bool fed_kernel_sweeps = false, fed_sweepers_now = false;
+  void* fed_hring = nullptr;      // pinned host ring (kJobSlots FedHostCmd)
+  void* fed_hring_dev = nullptr;  // its device address
+  uint32_t fed_epoch = 0, fed_m = 0;
   // tests only (kb_opts.test_stall_job / test_stall_ms): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;
@@ -181,6 +187,10 @@ struct kb_ctx {
   bool shard_self_inbox = false;  // KB_OPT_SHARD_SELF_INBOX
   bool test_peer_badtag = false;  // KB_OPT_TEST_PEER_BADTAG
   bool fed_diag = false;       // KB_OPT_FED_DIAG
+  // KB_OPT_FED_DIAG: host stamps per fed command (ns since kb_fed_begin): issue entry / exit, finish entry /
+  // result seen (kb_fed_end's kb_fed_host line, beside the engine's per-job timeline)
+  std::vector<int64_t> dg_iss0, dg_iss1, dg_fin0, dg_fin1;
+  std::chrono::steady_clock::time_point dg_t0;
   bool issue_trace = false;    // KB_HOST_TRACE: every fed job issue on stderr
   uint64_t fed_idle = 100000000ull;  // the engine's idle exit in s_memrealtime ticks (100 MHz): 1 s
   int eval_spb = 0;            // kb_opts.eval_spb (0: from cus)

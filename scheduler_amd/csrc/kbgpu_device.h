@@ -281,10 +281,21 @@ void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream);
 // launch's hipError_t. shard.world > 0: the node-sharded engine (split engine only). place_xcc >= 0 (split engine):
 // a grid of 8 x (1 + nsel) workgroups takes a census of their XCC ids and the placer and selectors are the ones on
 // XCC place_xcc (others where it has too few), the rest exit at once.
+// hring (pinned, kJobSlots FedHostCmd entries; place_xcc >= 0 only): the census grid's other workgroups stay as
+// resident sweepers (fed_sweeper) that take command m of this launch from hring[m % kJobSlots] once its tag is
+// epoch << 32 | m + 1 (fed_host_post) -- no sweep kernel per job; nullptr: they exit, and every command comes
+// through a sweep kernel (fed_post's launch_sel_sweep / launch_fed_cmd).
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
                       int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard,
-                      int place_xcc = -1);
+                      int place_xcc = -1, const void* hring = nullptr, uint32_t epoch = 0);
+// A command for the resident sweepers: the eight words, then the tag (release).
+struct FedHostCmd {
+  uint64_t w[8];
+  uint64_t tag;
+  uint64_t pad[7];
+};
+void fed_host_post(void* hring, int r, const FedCmdArgs& a, uint64_t tag);
 
 // Node sharding: per segment, the rank's local proposal (after launch_sel_sweep), then, after the
 // all-gather of every rank's ShardRec, the global merge + stop rules + commit of the rank's own rows.

@@ -854,6 +854,11 @@ __global__ __launch_bounds__(256) void eval_kernel(DevNodes N, DevSpecs P, DevCf
 // reciprocal estimate and corrected by one exact fma remainder, and Balanced keeps bra_score_inv's estimate with
 // its IEEE-division fallback near integers. Other rows take the int64 forms. Same values as eval_kernel on such
 // specs (tests/test_gpu_parity.py::test_eval_plain_equals_general, test_eval_plain_matches_oracle).
+#ifdef KB_EVAL_TEMPORAL
+constexpr int kEvalAux = 0;  // (A/B builds: ordinary stores)
+#else
+constexpr int kEvalAux = 2;  // buffer stores' cache policy: nt (the output is streamed once, never read back here)
+#endif
 constexpr int kEvalPlainSpecs = 64;  // (one resident round at 50k nodes needs 43: eval_plain_spb)
 constexpr double kPlainMax = 562949953421312.0;  // 2^49
 // leastRequestedScore (least_requested.go:36-53) on integers below 2^49 held in doubles. num = (cap - req) * 10
@@ -882,7 +887,10 @@ __device__ __forceinline__ int bra_score_f64(double rc, double ac, double rm, do
   const double cf = ac == 0.0 ? 1.0 : rc / ac, mf = am == 0.0 ? 1.0 : rm / am;
   return (cf >= 1.0 || mf >= 1.0) ? 0 : (int)((1.0 - fabs(cf - mf)) * 10.0);
 }
-template <class SCORE>
+// BUF: the output arrays take under 4 GiB (launch_eval_t): the loop's stores are buffer stores with the row's
+// offset in a scalar register (soffset) and the lane's node offset fixed in a VGPR -- no per-store 64-bit address
+// arithmetic on the VALU, which this kernel is bound by beside the stores.
+template <class SCORE, bool BUF = false>
 __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
                                                          int t, int spb, uint32_t* reasons, SCORE* scores) {
   __shared__ int64_t s_req[4][kEvalPlainSpecs];  // init cpu, init mem, non-zero cpu, non-zero mem
@@ -892,6 +900,10 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
   __shared__ SCORE s_tab[11 * 11];  // lr * w_lr + bra * w_bra for lr, bra in 0..10 (all 0 without nodeorder)
   const int j0 = blockIdx.y * spb;
   const int nj = t - j0 < spb ? t - j0 : spb;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  // the node's row first: its loads overlap the specs' staging (two dependent loads) below
+  Row r;
+  if (n < N.n) r = load_row(N, n);
   if ((int)threadIdx.x < nj) {
     const kb_spec sp = P.specs[spec_ids[j0 + threadIdx.x]];
     s_req[0][threadIdx.x] = sp.init_cpu;
@@ -911,9 +923,7 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     s_tab[q] = C.nodeorder ? (SCORE)(q / 11) * (SCORE)C.w_lr + (SCORE)(q % 11) * (SCORE)C.w_bra : (SCORE)0;
   }
   __syncthreads();
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N.n) return;
-  const Row r = load_row(N, n);
   // row_reasons after the resource check, per node: pod count, conditions (static_eval's pre), then the post
   // reasons (no taints: the one taint set is tolerated) -- memory pressure for BestEffort specs only
   uint32_t after = 0, post_be = 0;
@@ -952,6 +962,11 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     // IEEE-division fallback (f within 1e-9 of an integer, or a capacity <= 0) is deferred: the spec's bit in fb,
     // and the score is rewritten after the loop (the same thread's later store to the same word)
     uint64_t fb = 0;
+    // (BUF) the output arrays as buffer resources: raw, whole-array record counts (< 4 GiB: launch_eval_t)
+    const uint32_t out_pairs = (uint32_t)t * (uint32_t)stride;
+    const __amdgpu_buffer_rsrc_t rbuf = __builtin_amdgcn_make_buffer_rsrc(reasons, (short)0, (int)(out_pairs * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t sbuf =
+        __builtin_amdgcn_make_buffer_rsrc(scores, (short)0, (int)(out_pairs * (uint32_t)sizeof(SCORE)), 0x00020000);
 #pragma unroll 4
     for (int j = 0; j < nj; ++j) {
       const double icpu = s_dreq[0][j], imem = s_dreq[1][j], nzc10 = s_dreq[2][j], nzm10 = s_dreq[3][j];
@@ -974,6 +989,25 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       const SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
       // uniform row bases: the stores take a scalar base and the lane's offset; non-temporal (the output is
       // streamed once, never read back by this kernel: no point keeping it in the caches)
+      if constexpr (BUF) {
+        const uint32_t orow = (uint32_t)(j0 + j) * (uint32_t)stride;  // (uniform: scalar)
+#if defined(KB_EVAL_STOREONLY)
+        const uint32_t rs_v = (uint32_t)(n ^ j);
+        const SCORE sc_v = (SCORE)(n + j);
+#else
+        const uint32_t rs_v = rs;
+        const SCORE sc_v = score;
+#endif
+        __builtin_amdgcn_raw_buffer_store_b32(rs_v, rbuf, n * 4, (int)(orow * 4u), kEvalAux);
+        if constexpr (sizeof(SCORE) == 4) {
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)sc_v, sbuf, n * 4, (int)(orow * 4u), kEvalAux);
+        } else {
+          typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+          const v2u sv = {(unsigned)(uint64_t)sc_v, (unsigned)((uint64_t)sc_v >> 32)};
+          __builtin_amdgcn_raw_buffer_store_b64(sv, sbuf, n * 8, (int)(orow * 8u), kEvalAux);
+        }
+        continue;
+      }
       uint32_t* rrow = reasons + (size_t)(j0 + j) * stride;
       SCORE* srow = scores + (size_t)(j0 + j) * stride;
 #if defined(KB_EVAL_STOREONLY)  // (A/B builds: the stores alone, no compute -- the kernel's store bound)
@@ -2884,6 +2918,8 @@ bool sel_aff_pl_fits(int n, int t_count) {
 // kernel release and the next kernel's acquire (5.6 us median between place kernels) go away.
 // ===========================================================================
 
+constexpr int kFedGridMax = 256;  // the split engine's grid: placer, selectors, resident sweepers (one per CU)
+
 struct FedSlots {
   uint32_t* keys[kJobSlots];
   uint64_t* stat[kJobSlots];
@@ -2913,6 +2949,95 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
     // a non-sweeping command (EXIT) adds the whole count at once
     const uint32_t add = sweep ? 1u : (uint32_t)((N.n + 63) / 64);
     __hip_atomic_fetch_add(ctr, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The split engine's resident sweepers (the census grid's workgroups that are neither placer nor selector, off the
+// placer's XCC): the job's level-0 sweep without a kernel launch per job. The host writes command m of the launch
+// into the pinned ring entry m % kJobSlots (FedHostCmd: the command's eight words, then the tag epoch << 32 | m + 1,
+// a release store). Sweeper 0 polls that tag (system-scope loads, its thread 0) and relays the words and the tag to
+// device memory (sc1 stores, vmcnt(0), then the tag: MI355X_MICROARCH.md's hand-off table, first row), where the
+// other sweepers poll it (sc1 loads) -- one reader on the bus. Each sweeper then takes one agent-scope acquire (the
+// rows its loads read were committed by the placer and released at its publish, or by the launch path during a
+// pause), sweeps its share of the 64-node blocks into the slot's keys and static cache, releases, and adds its block
+// count to the ring counter the selector waits on -- the count the sweep kernel's blocks gave. Sweeper 0 also
+// writes the command into the device ring (before its release). EXIT ends the loop after its count; a sweeper
+// leaves too when the engine's exit flag is set or no command comes within idle_ticks.
+__device__ void fed_sweeper(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlots& S,
+                            const FedHostCmd* hring, uint32_t epoch, FedCmd* ring, uint32_t* ctr,
+                            uint64_t idle_ticks, int32_t* exit_flag, int sw, int nsw, uint64_t* relay_cmd,
+                            uint64_t* relay_go) {
+  __shared__ FedCmd s_cmd;
+  __shared__ int32_t s_go;
+  const int tid = threadIdx.x;
+  const uint32_t B = (uint32_t)((N.n + 63) / 64);
+  const uint32_t b0 = (uint32_t)((uint64_t)sw * B / (uint32_t)nsw), b1 = (uint32_t)((uint64_t)(sw + 1) * B / (uint32_t)nsw);
+  const int n0 = (int)b0 * 64, n1 = min((int)b1 * 64, N.n);
+  for (uint32_t m = 0;; ++m) {
+    const int r = (int)(m % (uint32_t)kJobSlots);
+    if (tid == 0) {
+      const uint64_t want = ((uint64_t)epoch << 32) | (uint64_t)(m + 1);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int go = 0;
+      // sweeper 0 polls the pinned ring over the bus; the others poll its relay in device memory (one bus reader)
+      const uint64_t* tagp = sw == 0 ? &hring[r].tag : &relay_go[r];
+      for (;;) {
+        if (__hip_atomic_load(tagp, __ATOMIC_RELAXED, sw == 0 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT) ==
+            want) {
+          go = 1;
+          break;
+        }
+        if (__hip_atomic_load(exit_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (go) {  // the words stored before the tag
+        uint64_t w[8];
+        if (sw == 0) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = __hip_atomic_load(&hring[r].w[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) st_sc1(&relay_cmd[r * 8 + q], w[q]);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          st_sc1(&relay_go[r], want);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = ld_sc1(&relay_cmd[r * 8 + q]);
+        }
+        __builtin_memcpy(&s_cmd, w, sizeof(FedCmd));
+        if (s_cmd.op == KB_ENG_RUN) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the barrier below holds the other waves' loads)
+        }
+      }
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) return;
+    const FedCmd cm = s_cmd;
+    if (cm.op == KB_ENG_RUN) {
+      const kb_spec sp = P.specs[cm.spec];
+      uint32_t* keys32 = S.keys[cm.slot];
+      uint64_t* stat = S.stat[cm.slot];
+      const int64_t* sci = P.sc_init + (size_t)cm.spec * N.S;
+      for (int n = n0 + tid; n < n1; n += kSelThreads) {
+        const Row rw = load_row(N, n);
+        const uint64_t st = static_eval<false>(N, P, C, sp, cm.spec, rw.flags, n, P.A.mm);
+        stat[n] = st;
+        const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, n);
+        keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rw, st), n), n + N.base, idx_bits);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      if (sw == 0) ring[r] = cm;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&ctr[r], b1 - b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (cm.op != KB_ENG_RUN) return;
+    __syncthreads();  // (s_cmd / s_go are rewritten by the next poll)
   }
 }
 
@@ -2963,9 +3088,12 @@ struct FedXchg {
   // [8] its publish started (the drain before the release), [9] the release and host state done
   uint64_t tl[kFedTraceJobs][10];
 #endif
+  // resident sweepers: sweeper 0 relays each host command (its eight words sc1, then the tag) to the others
+  uint64_t sw_cmd[kJobSlots][8];
+  uint64_t sw_go[kJobSlots];
   uint64_t wdiag[8];                  // KB_DIAG builds: the placer's fine sel_run stamps (dg[8..15])
   uint32_t census_n;                  // place_xcc: workgroups counted in (agent-scope atomic add)
-  uint32_t census_xcc[8 * (1 + kFedMaxSel)];  //   each workgroup's XCC id + 1
+  uint32_t census_xcc[kFedGridMax];   //   each workgroup's XCC id + 1
   uint64_t sphase[8];  // SHARD: [0..5] the placer's exchange phases (kb_stats.shard_phase_ticks); every split launch:
                        // [6] / [7] the placer's / selector 0's placement (kb_stats.fed_wg_place), ahead of sdiag
   uint64_t sdiag[16];  // KB_DIAG builds: [0..6] the selector's phases, [8..11] the placer's merge; [12..15] the placer's
@@ -3618,7 +3746,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
                                                                  FedSlots S, const FedCmd* ring,
                                                                  const uint32_t* ctr, uint64_t idle_ticks,
                                                                  int32_t* exit_flag, FedXchg* X, int nsel_arg,
-                                                                 ShardPeers SP, int place_xcc) {
+                                                                 ShardPeers SP, int place_xcc,
+                                                                 const FedHostCmd* hring, uint32_t epoch) {
   static_assert(!SHARD || SPLIT, "the node-sharded engine is the split engine");
   static_assert(MSEL == 1 || (SPLIT && MSEL <= kFedMaxSel), "range selectors belong to the split engine");
   const int nsel = MSEL == 1 ? 1 : nsel_arg;
@@ -3642,41 +3771,65 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     // resident: launch_fed_engine's check) picks the workgroups on XCC place_xcc first, the others in block order
     // after them; every workgroup computes the same assignment and the unpicked ones exit. A census that does not
     // complete within idle_ticks leaves every workgroup out (the host sees the idle exit: launch path).
-    __shared__ int32_t s_role;
+    __shared__ int32_t s_role, s_nsw, s_all;
+    __shared__ uint8_t s_cx[kFedGridMax];  // (XCC id + 1; bit 7: role taken -- the static LDS budget is tight)
     uint32_t xcc, hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t G = gridDim.x;
     if (tid == 0) {
-      int role = (int)blockIdx.x;
+      int all = 1;
       if (place_xcc >= 0) {
-        const uint32_t G = gridDim.x;
         __hip_atomic_store(&X->census_xcc[blockIdx.x], xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(&X->census_n, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        bool all = false;
         while (!(all = __hip_atomic_load(&X->census_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= G) &&
                __builtin_amdgcn_s_memrealtime() - t0 <= idle_ticks)
           __builtin_amdgcn_s_sleep(1);
+        if (!all) atomicMax(exit_flag, 1);
+      }
+      s_all = all;
+    }
+    __syncthreads();
+    if (place_xcc >= 0 && s_all && tid < (int)G)  // every entry in one round trip (agent-scope loads)
+      s_cx[tid] = (uint8_t)__hip_atomic_load(&X->census_xcc[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (tid == 0) {
+      // roles: 0 the placer, 1..nsel the selectors -- the workgroups on XCC place_xcc first, then the others, both in
+      // block order; then (resident sweepers) every other workgroup NOT on the placer's XCC, in block order: a
+      // sweeper's stores and its per-job release would dirty and write back that XCC's L2 under the placer
+      // (measured: C2 19.2 us per job with sweepers there, r05r). The rest exit.
+      int role = (int)blockIdx.x, nsw = 0;
+      if (place_xcc >= 0) {
         role = -1;
-        if (all) {
-          int k = 0;  // roles in order: the target XCC's workgroups, then the rest (both in block order)
-          for (int pass = 0; pass < 2 && role < 0; ++pass)
-            for (uint32_t b = 0; b < G && k <= nsel && role < 0; ++b) {
-              const uint32_t x = __hip_atomic_load(&X->census_xcc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((x == (uint32_t)place_xcc + 1) == (pass == 0)) {
+        if (s_all) {
+          int k = 0;
+          for (int pass = 0; pass < 2; ++pass)
+            for (uint32_t b = 0; b < G && k <= nsel; ++b)
+              if (!(s_cx[b] & 0x80u) && ((uint32_t)s_cx[b] == (uint32_t)place_xcc + 1) == (pass == 0)) {
                 if (b == blockIdx.x) role = k;
+                s_cx[b] |= 0x80u;  // (taken)
                 ++k;
               }
-            }
-        } else {
-          atomicMax(exit_flag, 1);
+          if (hring != nullptr)
+            for (uint32_t b = 0; b < G; ++b)
+              if (!(s_cx[b] & 0x80u) && s_cx[b] != (uint32_t)place_xcc + 1) {
+                if (b == blockIdx.x) role = nsel + 1 + nsw;
+                ++nsw;
+              }
         }
       }
       s_role = role;
+      s_nsw = nsw;
       if (role >= 0 && role <= 1) X->sphase[6 + role] = (uint64_t)xcc << 32 | hw;  // (kb_stats.fed_wg_place)
     }
     __syncthreads();
     const int role = s_role;
+    if (role > nsel) {  // resident sweepers
+      fed_sweeper(N, P, C, idx_bits, S, hring, epoch, const_cast<FedCmd*>(ring), const_cast<uint32_t*>(ctr),
+                  idle_ticks, exit_flag, role - nsel - 1, s_nsw, &X->sw_cmd[0][0], X->sw_go);
+      return;
+    }
     if (role < 0 || role > nsel) return;
     if (role >= 1) {
       fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
@@ -3709,6 +3862,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
   for (int q = 0; q < kEntW; ++q) ent_pf[q] = 0;
   int ent_pf_na = -1;
+  uint64_t bst_pf = 0;  // likewise this thread's B entry's static cache (s_bst, written before the same head)
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -3890,10 +4044,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         if (tid >= na && tid < na + c) list = k, idx = tid - na;
         na += c;
       }
+      // (prefetched at the previous job's end for this very head: the same count)
+      const bool pf = MSEL == 1 && ent_pf_na == na;
       if (list >= 0) {
         const uint64_t(*ent)[128] = X->s_ent[r][list];
-        // (prefetched at the previous job's end for this very head: the same count)
-        const bool pf = MSEL == 1 && ent_pf_na == na;
         const uint64_t e0 = pf ? ent_pf[0] : x_load64(&ent[0][idx]);
         const uint64_t st = pf ? ent_pf[1] : x_load64(&ent[1][idx]);
         uint64_t words[sizeof(Row) / 8];
@@ -3906,7 +4060,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       } else if (tid >= na && tid - na < nb) {
         const int j = tid - na, w = bprev[j];
         const Row rw = brow[j];
-        const uint64_t st = x_load64(&X->s_bst[r][j]);  // (selector 0's, behind its head: no acquire needed)
+        // (selector 0's, behind its head: no acquire needed)
+        const uint64_t st = pf ? bst_pf : x_load64(&X->s_bst[r][j]);
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, w);
         // an infeasible key (its reason mask) gets the B index below it, so B's keys are distinct: their ranks
         // are a permutation (still below every feasible key)
@@ -4160,11 +4315,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     }
     if constexpr (SPLIT && MSEL == 1) {  // every thread's entry of the next job: loads issued now (thread 0's after
       ent_pf_na = s_pre_na;              // its publish), used at that job's merge
+      const int rn = r + 1 == kJobSlots ? 0 : r + 1;
       if (tid < ent_pf_na) {
-        const int rn = r + 1 == kJobSlots ? 0 : r + 1;
         const uint64_t(*ent)[128] = X->s_ent[rn][0];
 #pragma unroll
         for (int q = 0; q < kEntW; ++q) ent_pf[q] = x_load64(&ent[q][tid]);
+      } else if (ent_pf_na >= 0 && tid - ent_pf_na < nbprev) {  // (the thread that takes that B entry)
+        bst_pf = x_load64(&X->s_bst[rn][tid - ent_pf_na]);
       }
     }
     if constexpr (SPLIT) KB_FED_TL(m, 7);
@@ -4217,6 +4374,15 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 }
 
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
+void fed_host_post(void* hring, int r, const FedCmdArgs& a, uint64_t tag) {
+  FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
+             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, 0};
+  FedHostCmd* h = (FedHostCmd*)hring + r;
+  uint64_t w[8];
+  __builtin_memcpy(w, &cmd, sizeof(cmd));
+  for (int q = 0; q < 8; ++q) __atomic_store_n(&h->w[q], w[q], __ATOMIC_RELAXED);
+  __atomic_store_n(&h->tag, tag, __ATOMIC_RELEASE);  // (x86: the words are visible first)
+}
 size_t fed_xchg_bytes() { return sizeof(FedXchg); }
 size_t fed_census_bytes() { return offsetof(FedXchg, sphase) - offsetof(FedXchg, census_n); }
 #ifdef KB_DIAG
@@ -4260,7 +4426,7 @@ void launch_peer_get(const uint64_t* src, int n, uint64_t* out, void* stream) {
 int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlotPtrs& sp,
                       const void* ring, const uint32_t* ctr, const uint32_t* tgt, uint64_t idle_ticks,
                       int32_t* exit_flag, void* xchg, void* stream, bool coop, const ShardPeers& shard,
-                      int place_xcc) {
+                      int place_xcc, const void* hring, uint32_t epoch) {
   FedSlots S;
   for (int s = 0; s < kJobSlots; ++s) {
     S.tgt[s] = tgt[s];
@@ -4280,8 +4446,10 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   FedXchg* X = (FedXchg*)xchg;
   ShardPeers SP = shard;
   int pxcc = xchg && place_xcc >= 0 && place_xcc < 8 ? place_xcc : -1;
+  const FedHostCmd* hr = (const FedHostCmd*)hring;
   void* args[] = {(void*)&N, (void*)&P, (void*)&C, (void*)&idx_bits, (void*)&S, (void*)&ring_c, (void*)&ctr,
-                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP, (void*)&pxcc};
+                  (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP, (void*)&pxcc,
+                  (void*)&hr, (void*)&epoch};
   const bool sharded = SP.world > 0;
   if (sharded && !xchg) return (int)hipErrorInvalidValue;  // the node-sharded engine is the split engine
   const void* f = nullptr;
@@ -4311,7 +4479,18 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   if (!split) nsel = 1;
   if (sharded && !split) return (int)hipErrorInvalidValue;
   if (!split) pxcc = -1;
-  const dim3 grid(split ? (pxcc >= 0 ? 8 : 1) * (1 + nsel) : 1), block(kSelThreads);
+  if (pxcc < 0 || coop) hr = nullptr;  // resident sweepers: with the census grid only
+  // with sweepers, enough workgroups for about one sweeper thread per node off the placer's XCC (a sweeper's
+  // nodes are latency-bound loads and static checks: C3's 20k nodes over 14 sweepers ran 39 us per job, r05q);
+  // the dispatcher deals blocks round robin over the 8 XCCs, so ~7/8 of the grid lands off it
+  int g = split ? (pxcc >= 0 ? 8 : 1) * (1 + nsel) : 1;
+  if (hr != nullptr) {
+    const int want_sw = (N.n + kSelThreads - 1) / kSelThreads;
+    const int g_sw = ((want_sw * 8 + 6) / 7 + 7) / 8 * 8;
+    g = g_sw > g ? g_sw : g;
+    if (g > kFedGridMax) g = kFedGridMax;
+  }
+  const dim3 grid(g), block(kSelThreads);
   if (coop) return (int)hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)bytes, (hipStream_t)stream);
   // A plain launch: its workgroups spin on each other, so every one of them must be resident at once. The
   // dispatcher places them as CUs free up (the sweeps they wait for run on another hardware queue and never wait
@@ -6327,8 +6506,8 @@ void launch_traj_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, in
 // eval_plain_kernel's resident blocks per CU (its occupancy: the instance's registers decide it), per instance
 int eval_plain_blocks_per_cu(bool i32) {
   int nb = 0;
-  const hipError_t e = i32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int32_t>, 256, 0)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int64_t>, 256, 0);
+  const hipError_t e = i32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int32_t, true>, 256, 0)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain_kernel<int64_t, true>, 256, 0);
   return e == hipSuccess && nb > 0 ? nb : 2;
 }
 
@@ -6354,8 +6533,13 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
   if (plain) {
     const int spb = eval_plain_spb(N.n, t, cus & 0xffff, cus >> 16, spb_opt);
     dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
-    hipLaunchKernelGGL(eval_plain_kernel<SCORE>, grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t, spb,
-                       reasons, scores);
+    // buffer stores when every output offset fits 32 bits (the record count is a 32-bit byte count)
+    if ((uint64_t)t * (uint64_t)N.n * sizeof(SCORE) < (1ull << 31))
+      hipLaunchKernelGGL((eval_plain_kernel<SCORE, true>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+                         spb, reasons, scores);
+    else
+      hipLaunchKernelGGL((eval_plain_kernel<SCORE, false>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids,
+                         t, spb, reasons, scores);
     return;
   }
   dim3 grid((N.n + 255) / 256, (t + kEvalSpecs - 1) / kEvalSpecs);

@@ -253,6 +253,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->fed_coop = c->fed_dedicated && (fl & KB_OPT_FED_COOP_LAUNCH) && !(fl & KB_OPT_FED_PLAIN_LAUNCH);
   c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
   c->test_peer_badtag = (fl & KB_OPT_TEST_PEER_BADTAG) != 0;
+  c->fed_kernel_sweeps = (fl & KB_OPT_FED_KERNEL_SWEEPS) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
@@ -326,6 +327,7 @@ void kb_destroy(kb_ctx* c) {
   if (c->fed_exit) (void)hipFree(c->fed_exit);
   if (c->fed_xchg) (void)hipFree(c->fed_xchg);
   if (c->h_fed_ctrs) (void)hipHostFree(c->h_fed_ctrs);
+  if (c->fed_hring) (void)hipHostFree(c->fed_hring);
   if (c->h_eval) (void)hipHostFree(c->h_eval);
   (void)hipFree(c->eval_ids);
   (void)hipFree(c->eval_r);
@@ -1563,6 +1565,10 @@ static int place_finish(kb_ctx* c, int si, int32_t* placed_node, int32_t* placed
   const JobState* hs = (const JobState*)S.h;
   const auto t_wait = std::chrono::steady_clock::now();
   if (int rc = wait_seq(c, hs, S.seq)) return rc;
+  if (c->fed && c->fed_diag) {
+    c->dg_fin0.push_back((t_wait - c->dg_t0).count());
+    c->dg_fin1.push_back((std::chrono::steady_clock::now() - c->dg_t0).count());
+  }
   // host time spent in the device path for this job: issuing it plus waiting for it (jobs overlap when
   // pipelined, so issue-to-finish walls would count the overlap twice)
   const double wall =
@@ -1709,6 +1715,13 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   c->fed_r = 0;
   c->fed_tasks = 0;
   c->fed_fresh = false;
+  if (c->fed_diag) {
+    c->dg_iss0.clear();
+    c->dg_iss1.clear();
+    c->dg_fin0.clear();
+    c->dg_fin1.clear();
+    c->dg_t0 = std::chrono::steady_clock::now();
+  }
   c->fed_ev = nullptr;
   if (c->timing) {  // the engine is one launch per cycle: always timed
     const bool tn = c->timing_now;
@@ -1741,9 +1754,19 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   }
   // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
   const uint64_t idle = c->sharded ? 10 * c->fed_idle : c->fed_idle;
+  // resident sweepers: the census grid's spare workgroups (split engine, placed on an XCC, plain launch)
+  c->fed_sweepers_now = xchg && !c->fed_coop && c->fed_xcc >= 0 && c->fed_xcc < 8 && !c->fed_kernel_sweeps;
+  if (c->fed_sweepers_now && !c->fed_hring) {
+    HIP_OK(c, hipHostMalloc(&c->fed_hring, kJobSlots * sizeof(FedHostCmd), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->fed_hring, 0, kJobSlots * sizeof(FedHostCmd));
+    HIP_OK(c, hipHostGetDevicePointer(&c->fed_hring_dev, c->fed_hring, 0));
+  }
+  c->fed_epoch++;
+  c->fed_m = 0;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
                                           c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP,
-                                          c->fed_coop ? -1 : c->fed_xcc));
+                                          c->fed_coop ? -1 : c->fed_xcc,
+                                          c->fed_sweepers_now ? c->fed_hring_dev : nullptr, c->fed_epoch));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
   c->prev_listed = false;
@@ -1754,7 +1777,10 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
 static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
   const int r = c->fed_r;
   void* entry = (char*)c->fed_ring + r * (fed_ring_bytes() / kJobSlots);
-  if (sweep) {  // the job's level-0 sweep (the launch path's own sweep kernel) carries the command
+  if (c->fed_sweepers_now) {  // the resident sweepers take it from the pinned ring: no launch
+    fed_host_post(c->fed_hring, r, a, ((uint64_t)c->fed_epoch << 32) | (uint64_t)(c->fed_m + 1));
+    c->fed_m++;
+  } else if (sweep) {  // the job's level-0 sweep (the launch path's own sweep kernel) carries the command
     hipEvent_t ea;
     c->ev_begin(&ea, c->stream_b);
     launch_sel_sweep(c->N, c->P, c->cfg, a.spec, c->idx_bits, c->sel_keys[si], c->sel_stat[si], nullptr, false,
@@ -1874,6 +1900,44 @@ int kb_fed_end(kb_ctx* c) {
           fprintf(stderr, " %s=%.2f/%.2f/%.2f[%.2f]", names[k], pct(v[k], 0.1), pct(v[k], 0.5), pct(v[k], 0.9),
                   pct(lv[k], 0.5));
         fprintf(stderr, "\n");
+        // the late heads by job index mod the slot count and their runs; the host's side of the same jobs: the
+        // issue call, the gap from seeing job m-kJobSlots's result to issuing job m, and the result intervals
+        int bym[8] = {}, run = 0, maxrun = 0, runs = 0;
+        std::vector<char> late_m((size_t)jobs, 0);
+        for (int m = 4; m < jobs - 1; ++m) {
+          const bool late = tl[(size_t)m * TW + 4] > tl[(size_t)(m - 1) * TW + 7];
+          late_m[(size_t)m] = late;
+          if (late) {
+            bym[m % kJobSlots]++;
+            runs += run == 0;
+            maxrun = std::max(maxrun, ++run);
+          } else {
+            run = 0;
+          }
+        }
+        fprintf(stderr, "kb_fed_late by m%%%d:", kJobSlots);
+        for (int k = 0; k < kJobSlots; ++k) fprintf(stderr, " %d", bym[k]);
+        fprintf(stderr, " runs=%d longest=%d\n", runs, maxrun);
+        const size_t nh = std::min({c->dg_iss0.size(), c->dg_iss1.size(), (size_t)jobs});
+        if (nh > 8 && c->dg_fin1.size() + kJobSlots >= nh) {
+          std::vector<double> iss, gap, fin, lgap, liss;
+          for (size_t m = kJobSlots; m < nh; ++m) {
+            const double is = (double)(c->dg_iss1[m] - c->dg_iss0[m]) * 1e-3;
+            const double gp = (double)(c->dg_iss0[m] - c->dg_fin1[m - kJobSlots]) * 1e-3;
+            iss.push_back(is);
+            gap.push_back(gp);
+            if (m < c->dg_fin1.size()) fin.push_back((double)(c->dg_fin1[m] - c->dg_fin1[m - 1]) * 1e-3);
+            if (m < late_m.size() && late_m[m]) {
+              lgap.push_back(gp);
+              liss.push_back(is);
+            }
+          }
+          fprintf(stderr, "kb_fed_host us (p10/p50/p90/max [late heads' p50]) issue=%.2f/%.2f/%.2f/%.2f[%.2f] "
+                  "seen_m-%d_to_issue=%.2f/%.2f/%.2f/%.2f[%.2f] result_interval=%.2f/%.2f/%.2f/%.2f\n",
+                  pct(iss, 0.1), pct(iss, 0.5), pct(iss, 0.9), pct(iss, 0.999), pct(liss, 0.5), kJobSlots,
+                  pct(gap, 0.1), pct(gap, 0.5), pct(gap, 0.9), pct(gap, 0.999), pct(lgap, 0.5), pct(fin, 0.1),
+                  pct(fin, 0.5), pct(fin, 0.9), pct(fin, 0.999));
+        }
       }
     }
     if (c->fed_diag && d[6]) {  // KB_DIAG builds: the selector's phases
@@ -1963,6 +2027,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     if (!kb_spec_fed_ok(c, job->task_specs[0])) return fail(c, KB_E_INVALID, "fed engine: spec not eligible");
     kb_ctx::JobSlot& S = c->slot[slot];
     S.t_issue = std::chrono::steady_clock::now();
+    if (c->fed_diag) c->dg_iss0.push_back((S.t_issue - c->dg_t0).count());
     c->timing_now = c->timing && (c->issue_count++ % c->timing_every == 0);  // the job's sweep
     memset(((JobState*)S.h)->diag, 0, sizeof(((JobState*)S.h)->diag));
     ((JobState*)S.h)->t_recv = 0;  // (the sharded placer's timeout note)
@@ -1981,6 +2046,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     S.seq = c->seq;
     S.busy = true;
     S.issue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - S.t_issue).count();
+    if (c->fed_diag) c->dg_iss1.push_back((std::chrono::steady_clock::now() - c->dg_t0).count());
     return KB_OK;
   }
   SpecGuard g{nullptr, 0, 0, 0};

@@ -17,11 +17,16 @@ pick() { grep -o '"value": [0-9.]*\|"us_per_job": [0-9.]*\|"ms_per_step": [0-9.]
 step tests 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 600 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_gpu_digest.py tests/test_gpu_shard_peer.py tests/test_gpu_fed_queues.py \
   -k "${K:-mixed or pipeline_parity or takes_long or fed_split or survives or full_size or peer_engine or progress}"
-for i in 1 2; do step b2_$i 200 python bench.py --steps 20 --warmup 2 --no-eval --no-cpu-baseline; pick b2_$i; done
+for i in 1 2 3; do step b2_$i 200 python bench.py --steps 20 --warmup 2 --no-eval --no-cpu-baseline; pick b2_$i; done
 KBGPU_LIB=scheduler_amd/libkbgpu_diag.so step diag2 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-eval --opt fed_diag
-grep -h "kb_fed_timeline\|kb_fed_placer_fine" "gpurun_out/${TAG}_diag2.log" | tail -2; grep -o '"diag_place_phases": {[^}]*}' "gpurun_out/${TAG}_diag2.log"
+grep -h "kb_fed_timeline\|kb_fed_placer_fine\|kb_fed_late\|kb_fed_host\|kb_fed_placer_merge" "gpurun_out/${TAG}_diag2.log" | tail -5; grep -o '"diag_place_phases": {[^}]*}' "gpurun_out/${TAG}_diag2.log"
 step b5 300 python bench.py --config C5 --steps 3 --warmup 1 --no-eval --no-cpu-baseline; pick b5
 step b2m 300 python bench.py --config C2M --steps 10 --warmup 2 --no-eval --no-cpu-baseline; pick b2m
 step b3 300 python bench.py --config C3 --steps 5 --warmup 1 --no-eval --no-cpu-baseline; pick b3
-if [ -n "${EVALP:-}" ]; then step evalp 200 python scripts/eval_probe.py; cat "gpurun_out/${TAG}_evalp.log"; fi
+if [ -n "${EVALP:-}" ]; then
+  step evalp 200 python scripts/eval_probe.py 0; cat "gpurun_out/${TAG}_evalp.log"
+  for v in evalso evalt; do
+    KBGPU_LIB=scheduler_amd/libkbgpu_$v.so step evalp_$v 200 python scripts/eval_probe.py 0; cat "gpurun_out/${TAG}_evalp_$v.log"
+  done
+fi
 echo "=== done"

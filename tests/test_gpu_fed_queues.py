@@ -24,11 +24,12 @@ from test_gpu_parity import _compare
 pytestmark = pytest.mark.gpu
 
 
-def _child(q, shared):
+def _child(q, shared, kernel_sweeps):
     """One fresh process: torch's HIP runtime first (as in bench.py's ranks), then the library's."""
     try:
-        # a stall shows as an abandon within the test's time; shared: the sweep stream without its own queue
-        options = {"fed_idle_ms": 300, "fed_shared_queues": shared}
+        # a stall shows as an abandon within the test's time; shared: the sweep stream without its own queue;
+        # kernel_sweeps: the per-job sweep kernels on that stream (else the engine's resident sweepers)
+        options = {"fed_idle_ms": 300, "fed_shared_queues": shared, "fed_kernel_sweeps": kernel_sweeps}
         import torch
         import torch.distributed as dist
         with socket.socket() as sk:
@@ -69,11 +70,11 @@ def _child(q, shared):
         q.put((None, repr(e)))
 
 
-def _run(shared):
+def _run(shared, kernel_sweeps=True):
     import torch.multiprocessing as mp
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
-    p = ctxm.Process(target=_child, args=(q, shared))
+    p = ctxm.Process(target=_child, args=(q, shared, kernel_sweeps))
     p.start()
     res, err = q.get(timeout=240)
     p.join(timeout=60)
@@ -81,16 +82,19 @@ def _run(shared):
     return res
 
 
-def test_fed_engine_progress_beside_other_streams():
+@pytest.mark.parametrize("kernel_sweeps", [True, False], ids=["sweep-kernels", "resident-sweepers"])
+def test_fed_engine_progress_beside_other_streams(kernel_sweeps):
+    """Both ways the split engine gets its sweeps: the per-job sweep kernels on the CU-masked stream, and the
+    engine's resident sweepers (no per-job launch at all)."""
     ref = pyoracle.allocate(synth.c2(n_nodes=3000, n_jobs=40, tasks_per_job=40, seed=51), workers=8)
-    for extra, cycles, abandon, got in _run(shared=False):
+    for extra, cycles, abandon, got in _run(shared=False, kernel_sweeps=kernel_sweeps):
         assert cycles == 1 and abandon == 0, (extra, cycles, abandon)
         _compare(ref, got)
 
 
 def test_shared_queues_hazard_is_real():
-    """The same process layout with the sweep stream from the shared pool
-    (option fed_shared_queues): the hazard is observable -- some layouts stall the engine into its idle exit --
+    """The same process layout with the sweep kernels' stream from the shared pool
+    (options fed_shared_queues, fed_kernel_sweeps): the hazard is observable -- some layouts stall the engine into its idle exit --
     and the cycle still ends with the oracle's placements on the launch path (correct, 300 ms slower)."""
     ref = pyoracle.allocate(synth.c2(n_nodes=3000, n_jobs=40, tasks_per_job=40, seed=51), workers=8)
     res = _run(shared=True)

@@ -372,16 +372,18 @@ SPLIT_CLUSTERS = [
 ]
 
 
-@pytest.mark.parametrize("split", [True, False], ids=["split", "one-workgroup"])
+@pytest.mark.parametrize("mode", ["split", "split-kernel-sweeps", "one-workgroup"])
 @pytest.mark.parametrize("name,cluster", SPLIT_CLUSTERS, ids=[c[0] for c in SPLIT_CLUSTERS])
-def test_fed_split_engine_parity(name, cluster, split):
+def test_fed_split_engine_parity(name, cluster, mode):
     """The split fed engine (n > 2048, every job one segment): a second workgroup selects each job's
     candidate nodes one job ahead, leaving out the nodes the job before may commit to, which the placer
     re-keys and merges in. Same placements, statuses and FitErrors as the oracle, and as the one-workgroup
-    engine (option no_fed_split)."""
+    engine (option no_fed_split). The split engine's sweeps come from its resident sweepers (commands through a
+    pinned ring), or per job from sweep kernels (option fed_kernel_sweeps)."""
+    split = mode != "one-workgroup"
     ref = pyoracle.allocate(cluster)
     snap = E.Snapshot(cluster)
-    ctx = runtime.Context(0, options={"no_fed_split": not split})
+    ctx = runtime.Context(0, options={"no_fed_split": not split, "fed_kernel_sweeps": mode == "split-kernel-sweeps"})
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)
