@@ -259,8 +259,8 @@ class Tables:
         # (satisfiesExistingPodsAntiAffinity errors before it looks at any term, predicates.go:1302-1313)
         self.xb_pods = sorted((u, first_invalid(paff(pod).req_anti)) for pod, _, uids in lister
                               if first_invalid(paff(pod).req_anti) for u in uids)
-        self.xb_spec = {s: first_invalid(paff(spec_pod[s]).req_anti) for s in range(m)
-                        if first_invalid(paff(spec_pod[s]).req_anti)}
+        xb_spec = ((s, first_invalid(paff(spec_pod[s]).req_anti)) for s in range(m))
+        self.xb_spec = {s: inv for s, inv in xb_spec if inv}
         if self.xb_pods or self.xb_spec:
             xb = self.table(("XB",), (), AFF_ERROR)
             for s in range(m):
@@ -366,8 +366,9 @@ class Tables:
         spec_by_ident = defaultdict(list)
         for s, ident in enumerate(spec_ids):
             spec_by_ident[ident].append(s)
+        universe = set(lid) | set(spec_ids)  # (once: every table's candidates come out of it)
         for tid, terms in bc.items():
-            for ident in _candidates(terms, index, set(lid) | set(spec_ids)):
+            for ident in _candidates(terms, index, universe):
                 ns, labels = ident[0], dict(ident[1])
                 if not _all_match(terms, ns, labels):
                     continue

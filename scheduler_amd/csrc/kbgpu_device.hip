@@ -900,7 +900,11 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
   __shared__ SCORE s_tab[11 * 11];  // lr * w_lr + bra * w_bra for lr, bra in 0..10 (all 0 without nodeorder)
   const int j0 = blockIdx.y * spb;
   const int nj = t - j0 < spb ? t - j0 : spb;
+#ifdef KB_EVAL_NPT2
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;  // (A/B store probe: two nodes per lane)
+#else
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
+#endif
   // the node's row first: its loads overlap the specs' staging (two dependent loads) below
   Row r;
   if (n < N.n) r = load_row(N, n);
@@ -991,6 +995,18 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       // streamed once, never read back by this kernel: no point keeping it in the caches)
       if constexpr (BUF) {
         const uint32_t orow = (uint32_t)(j0 + j) * (uint32_t)stride;  // (uniform: scalar)
+#if defined(KB_EVAL_STOREONLY) && defined(KB_EVAL_NPT2)
+        {
+          typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+          const v2u rv = {(unsigned)(n ^ j), (unsigned)((n + 1) ^ j)};
+          const v2u sv = {(unsigned)(n + j), (unsigned)(n + 1 + j)};
+          __builtin_amdgcn_raw_buffer_store_b64(rv, rbuf, n * 4, (int)(orow * 4u), kEvalAux);
+          __builtin_amdgcn_raw_buffer_store_b64(sv, sbuf, n * 4, (int)(orow * 4u), kEvalAux);
+          (void)rs;
+          (void)score;
+          continue;
+        }
+#endif
 #if defined(KB_EVAL_STOREONLY)
         const uint32_t rs_v = (uint32_t)(n ^ j);
         const SCORE sc_v = (SCORE)(n + j);
@@ -3055,8 +3071,11 @@ constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
 constexpr int kFedMaxSel = 4;
 constexpr int kFedSelQ = 10;                          // key groups per thread of a range selector
 constexpr int kFedSelNodes = 4 * kSelThreads * kFedSelQ;  // 20480
-constexpr int kFedTraceJobs = 2048;  // KB_DIAG: the fed engine's per-job timeline (FedXchg::tl)
-#ifdef KB_DIAG
+constexpr int kFedTraceJobs = 2048;  // KB_DIAG / KB_TIMELINE: the fed engine's per-job timeline (FedXchg::tl)
+#if defined(KB_DIAG) && !defined(KB_TIMELINE)
+#define KB_TIMELINE
+#endif
+#ifdef KB_TIMELINE
 #define KB_FED_TL(m, k)                                                      \
   do {                                                                       \
     if (tid == 0) X->tl[(m) & (kFedTraceJobs - 1)][k] = __builtin_amdgcn_s_memrealtime(); \
@@ -3081,12 +3100,12 @@ struct FedXchg {
   // job m's sweep: the placer reads it here, behind the head, instead of from the sweep's buffer -- which would
   // need an agent-scope acquire per job on the placer's CU (~1.7 us, MI355X_MICROARCH.md)
   uint64_t s_bst[kJobSlots][128];
-#ifdef KB_DIAG
-  // KB_DIAG builds: per job (index & (kFedTraceJobs - 1)) s_memrealtime of [0] the selector's command arrival,
+#ifdef KB_TIMELINE
+  // KB_DIAG / KB_TIMELINE builds (KB_TIMELINE: the stamps alone, without the phase counters' registers): per job (index & (kFedTraceJobs - 1)) s_memrealtime of [0] the selector's command arrival,
   // [1] its patch done (after job m-2's p_done), [2] its selection done, [3] job m-1's set seen, [4] its head
   // published; the placer's [5] job start (head and command read), [6] its set published, [7] p_done written,
   // [8] its publish started (the drain before the release), [9] the release and host state done
-  uint64_t tl[kFedTraceJobs][10];
+  uint64_t tl[kFedTraceJobs][12];  // ... [10] the placer's command decoded (thread 0), [11] its loop top
 #endif
   // resident sweepers: sweeper 0 relays each host command (its eight words sc1, then the tag) to the others
   uint64_t sw_cmd[kJobSlots][8];
@@ -3880,6 +3899,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   uint64_t t_job0 = 0;
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
+      KB_FED_TL(m, 11);
       if (tid == 0) {
         int c = -2;
         // the head and command prefetched at the end of the previous job, when they were already there
@@ -3890,6 +3910,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #ifdef KB_DIAG
         dg[12] += have ? 0 : 1;  // jobs whose head was not there at the previous job's end (kb_fed_placer_fine)
 #endif
+        // (every load below is consumed inside its own branch -- asm operand uses: the compiler's wait counting
+        // merges branches, so a load pending past a merge made the prefetched path wait there too, for every
+        // earlier load and store of the wave including the previous job's host release: ~0.9 us per job, r05x)
         if (!have) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
@@ -3898,6 +3921,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
             if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
             __builtin_amdgcn_s_sleep(1);
           }
+          asm volatile("" ::"v"(h));
         }
         if ((uint32_t)(h >> 32) == m + 1) {
           c = (int32_t)(uint32_t)h;
@@ -3914,6 +3938,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
               }
               __builtin_amdgcn_s_sleep(1);
               hk = x_load64(&X->s_head[r][k]);
+              asm volatile("" ::"v"(hk));
             }
             s_na[k] = (int32_t)(uint32_t)hk;
           }
@@ -3921,29 +3946,37 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
             // the selector stored the command's words before its head (vmcnt(0) between): all 16 loads issue at
             // once, and the tags only confirm it (a word-by-word spin made this a chain of 16 L2 round trips
             // whenever the prefetch at the end of the previous job came too early)
-            uint64_t wv[16];
+            uint32_t fields[16];
+            if (have) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) wv[q] = have ? pre[q] : x_load64(&X->s_cmd[r][q]);
-            bool tagged = true;
+              for (int q = 0; q < 16; ++q) fields[q] = (uint32_t)pre[q];
+            } else {
+              uint64_t wv[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) tagged = tagged && (uint32_t)(wv[q] >> 32) == m + 1;
-            if (!tagged) {
+              for (int q = 0; q < 16; ++q) wv[q] = x_load64(&X->s_cmd[r][q]);
+              bool tagged = true;
 #pragma unroll
-              for (int q = 0; q < 16; ++q) {
-                const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-                while ((uint32_t)(wv[q] >> 32) != m + 1) {  // the tag orders it
-                  if (__builtin_amdgcn_s_memrealtime() - t1 > idle_ticks) {  // (cannot happen: the head is last)
-                    c = -2;
-                    atomicMax(exit_flag, 3);
-                    break;
+              for (int q = 0; q < 16; ++q) tagged = tagged && (uint32_t)(wv[q] >> 32) == m + 1;
+              if (!tagged) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+                  while ((uint32_t)(wv[q] >> 32) != m + 1) {  // the tag orders it
+                    if (__builtin_amdgcn_s_memrealtime() - t1 > idle_ticks) {  // (cannot happen: the head is last)
+                      c = -2;
+                      atomicMax(exit_flag, 3);
+                      break;
+                    }
+                    wv[q] = x_load64(&X->s_cmd[r][q]);
                   }
-                  wv[q] = x_load64(&X->s_cmd[r][q]);
                 }
               }
-            }
-            uint32_t fields[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) fields[q] = (uint32_t)wv[q];
+              for (int q = 0; q < 16; ++q) {
+                asm volatile("" ::"v"(wv[q]));
+                fields[q] = (uint32_t)wv[q];
+              }
+            }
             __builtin_memcpy(&cm, fields, sizeof(FedCmd));
           }
           // The placer's plain loads of global memory: the scalar / host-port columns of a spec that has them (rows
@@ -3952,6 +3985,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           // and its own LDS, so it skips it (the B candidates' static cache comes through the selector: s_bst).
           if (c >= 0 && cm.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the host's flag)
         }
+        KB_FED_TL(m, 10);
         if (c == -2) atomicMax(exit_flag, 1);
         s_cand = c;
         s_op = c >= 0 ? KB_ENG_RUN : (c == kSelExit ? KB_ENG_EXIT : KB_ENG_EXIT_IDLE);
@@ -4298,23 +4332,24 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       for (int k = 0; k < MSEL; ++k) pre[16 + k] = k < nsel ? x_load64(&X->s_head[rn][k]) : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a barrier alone waits for LDS only)
+    if constexpr (SPLIT) {
+      // the head and command words are in now (the wait above): a use here, on every path (not under tid == 0:
+      // the compiler's wait counting merges the lanes' paths), ends its tracking of their loads, so the next job's
+      // decode at the loop top waits for nothing -- else it waited there for every later load and store of the
+      // wave, the release's host store included (~1 us per job, r05v-w)
+#pragma unroll
+      for (int q = 0; q < 16 + MSEL; ++q) asm volatile("" ::"v"(pre[q]));
+    }
     if (SPLIT && MSEL == 1 && tid == 0) {  // the next job's head already there: its count, for the entry prefetch
       const bool h_ok = (uint32_t)(pre[16] >> 32) == m + 2 && (int32_t)(uint32_t)pre[16] >= 0;
       s_pre_na = h_ok ? (int32_t)(uint32_t)pre[16] : -1;
     }
     __syncthreads();
-    const int ncommit = sh.n_commit;
-    if (tid == 0) {
-      js->n_commit = ncommit;
-      publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
-#ifdef KB_DIAG
-      if (SPLIT) X->tl[m & (kFedTraceJobs - 1)][9] = __builtin_amdgcn_s_memrealtime();
-#endif
-      // after that release (the job's rows written back): the selector may re-key them
-      if (SPLIT) tag_store(&X->p_done[r], m + 1, (uint32_t)ncommit);
-    }
-    if constexpr (SPLIT && MSEL == 1) {  // every thread's entry of the next job: loads issued now (thread 0's after
-      ent_pf_na = s_pre_na;              // its publish), used at that job's merge
+    if constexpr (SPLIT && MSEL == 1) {
+      // every thread's entry of the next job, its head already seen: loads issued before this job's publish, so
+      // their latency runs beside the release (which waits for them in thread 0's wave) instead of stalling the
+      // next job's start (issued after it, the loop top's wait took ~1 us, r05v)
+      ent_pf_na = s_pre_na;
       const int rn = r + 1 == kJobSlots ? 0 : r + 1;
       if (tid < ent_pf_na) {
         const uint64_t(*ent)[128] = X->s_ent[rn][0];
@@ -4323,6 +4358,16 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       } else if (ent_pf_na >= 0 && tid - ent_pf_na < nbprev) {  // (the thread that takes that B entry)
         bst_pf = x_load64(&X->s_bst[rn][tid - ent_pf_na]);
       }
+    }
+    const int ncommit = sh.n_commit;
+    if (tid == 0) {
+      js->n_commit = ncommit;
+      publish_state(js, hjs, stopped, stop, fail_task, placed, ready, minav, gang, panic, cm.seq);
+#ifdef KB_TIMELINE
+      if (SPLIT) X->tl[m & (kFedTraceJobs - 1)][9] = __builtin_amdgcn_s_memrealtime();
+#endif
+      // after that release (the job's rows written back): the selector may re-key them
+      if (SPLIT) tag_store(&X->p_done[r], m + 1, (uint32_t)ncommit);
     }
     if constexpr (SPLIT) KB_FED_TL(m, 7);
     if constexpr (SHARD) ph[4] += __builtin_amdgcn_s_memrealtime() - t_job0;
@@ -4385,7 +4430,7 @@ void fed_host_post(void* hring, int r, const FedCmdArgs& a, uint64_t tag) {
 }
 size_t fed_xchg_bytes() { return sizeof(FedXchg); }
 size_t fed_census_bytes() { return offsetof(FedXchg, sphase) - offsetof(FedXchg, census_n); }
-#ifdef KB_DIAG
+#ifdef KB_TIMELINE
 size_t fed_trace_offset() { return offsetof(FedXchg, tl); }
 #else
 size_t fed_trace_offset() { return 0; }
@@ -6532,7 +6577,11 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
                           void* stream) {
   if (plain) {
     const int spb = eval_plain_spb(N.n, t, cus & 0xffff, cus >> 16, spb_opt);
+#ifdef KB_EVAL_NPT2
+    dim3 grid((N.n + 511) / 512, (t + spb - 1) / spb);
+#else
     dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
+#endif
     // buffer stores when every output offset fits 32 bits (the record count is a 32-bit byte count)
     if ((uint64_t)t * (uint64_t)N.n * sizeof(SCORE) < (1ull << 31))
       hipLaunchKernelGGL((eval_plain_kernel<SCORE, true>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,

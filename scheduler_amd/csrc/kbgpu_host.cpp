@@ -1867,23 +1867,24 @@ int kb_fed_end(kb_ctx* c) {
                 (double)w[1] / d[6], (double)w[2] / d[6], (double)w[3] / d[6], (double)w[4] / d[6],
                 (double)w[5] / d[6], (double)w[6] / d[6], (double)w[7] / d[6]);
     }
-    if (c->fed_diag && d[6] && fed_trace_offset()) {  // KB_DIAG builds: the engine's per-job timeline
+    if (c->fed_diag && fed_trace_offset()) {  // KB_DIAG / KB_TIMELINE builds: the engine's per-job timeline
       const int TJ = fed_trace_jobs();
-      constexpr int TW = 10;  // FedXchg::tl's words per job
+      constexpr int TW = 12;  // FedXchg::tl's words per job
       std::vector<uint64_t> tl((size_t)TJ * TW);
-      const int jobs = (int)std::min<uint64_t>(d[6], (uint64_t)TJ);
+      const int jobs = (int)std::min<uint64_t>(d[6] ? d[6] : (uint64_t)c->dg_iss0.size(), (uint64_t)TJ);
       if (hipMemcpy(tl.data(), (char*)c->fed_xchg + fed_trace_offset(), tl.size() * 8, hipMemcpyDeviceToHost) ==
               hipSuccess && jobs > 8) {
         // per job m (relative to the placer's end of job m-1 = when it wants job m's head): the selector's command
         // arrival, patch done, selection done, set seen, head; the placer's start and end of job m
-        const char* names[10] = {"cmd", "patched", "selected", "set_seen", "head", "placer_start", "set_published",
-                                 "pub_start", "released", "placer_end"};
-        const int ks[10] = {0, 1, 2, 3, 4, 5, 6, 8, 9, 7};
-        std::vector<double> v[10], lv[10];
+        constexpr int NK = 12;
+        const char* names[NK] = {"cmd", "patched", "selected", "set_seen", "head", "loop_top", "cmd_decoded",
+                                 "placer_start", "set_published", "pub_start", "released", "placer_end"};
+        const int ks[NK] = {0, 1, 2, 3, 4, 11, 10, 5, 6, 8, 9, 7};
+        std::vector<double> v[NK], lv[NK];
         for (int m = 4; m < jobs - 1; ++m) {
           const double E = (double)tl[(size_t)(m - 1) * TW + 7];
           const bool late = tl[(size_t)m * TW + 4] > tl[(size_t)(m - 1) * TW + 7];
-          for (int k = 0; k < 10; ++k) {
+          for (int k = 0; k < NK; ++k) {
             const double x = ((double)tl[(size_t)m * TW + ks[k]] - E) * 0.01;  // us (100 MHz ticks)
             v[k].push_back(x);
             if (late) lv[k].push_back(x);
@@ -1896,7 +1897,7 @@ int kb_fed_end(kb_ctx* c) {
         };
         fprintf(stderr, "kb_fed_timeline us after the placer's end of job m-1 (p10/p50/p90; late heads %zu of %zu:"
                 " their p50)", lv[0].size(), v[0].size());
-        for (int k = 0; k < 10; ++k)
+        for (int k = 0; k < NK; ++k)
           fprintf(stderr, " %s=%.2f/%.2f/%.2f[%.2f]", names[k], pct(v[k], 0.1), pct(v[k], 0.5), pct(v[k], 0.9),
                   pct(lv[k], 0.5));
         fprintf(stderr, "\n");
