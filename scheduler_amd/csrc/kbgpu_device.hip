@@ -2934,7 +2934,10 @@ bool sel_aff_pl_fits(int n, int t_count) {
 // kernel release and the next kernel's acquire (5.6 us median between place kernels) go away.
 // ===========================================================================
 
-constexpr int kFedGridMax = 256;  // the split engine's grid: placer, selectors, resident sweepers (one per CU)
+constexpr int kFedGridMax = 256;
+// a selector entry's first word: key (bits 0..31), node (32..55: the split engine's tables are below 2^24 nodes,
+// kFedMaxSel * kFedSelNodes), the node's rank among the list's first T (56..62)
+constexpr uint64_t kEntNodeMask = 0xffffffull;  // the split engine's grid: placer, selectors, resident sweepers (one per CU)
 
 struct FedSlots {
   uint32_t* keys[kJobSlots];
@@ -3071,6 +3074,7 @@ constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
 constexpr int kFedMaxSel = 4;
 constexpr int kFedSelQ = 10;                          // key groups per thread of a range selector
 constexpr int kFedSelNodes = 4 * kSelThreads * kFedSelQ;  // 20480
+static_assert((uint64_t)kFedMaxSel * kFedSelNodes <= kEntNodeMask, "selector entries pack the node in 24 bits");
 constexpr int kFedTraceJobs = 2048;  // KB_DIAG / KB_TIMELINE: the fed engine's per-job timeline (FedXchg::tl)
 #if defined(KB_DIAG) && !defined(KB_TIMELINE)
 #define KB_TIMELINE
@@ -3353,9 +3357,18 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     const bool keep = pos != 0;
     sel_excl_scan2(sh, rp, pos, zero, &kept, &ztot);
     const uint32_t nout = kept < T ? kept : T;
+    // each outgoing entry's rank by node among the first nout: the placer's slot order when the T best of the
+    // union are exactly these (its merge's fast path: no node ranking there)
+    if (keep && pos < T) cnode[pos] = wp + base;
+    __syncthreads();
+    uint32_t nrank = 0;
+    if (keep && pos < T) {
+      const int me = wp + base;
+      for (uint32_t q = 0; q < nout; ++q) nrank += cnode[q] < me ? 1u : 0u;
+    }
     if (keep && pos < T) {
       uint64_t(*ent)[128] = X->s_ent[r][sel];
-      x_store64(&ent[0][pos], (uint64_t)wk | ((uint64_t)(uint32_t)(wp + base) << 32));
+      x_store64(&ent[0][pos], (uint64_t)wk | ((uint64_t)(uint32_t)(wp + base) << 32) | ((uint64_t)nrank << 56));
       x_store64(&ent[1][pos], stw);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
@@ -3777,6 +3790,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   __shared__ int32_t bprev[128];  // split: the previous job's selected set, slot order
   __shared__ uint32_t bkey[128];  //   its keys for this job
   __shared__ int32_t s_feas;
+  __shared__ uint32_t s_bmax;  // split: the largest B key of the job (the merge's fast path)
   __shared__ int32_t s_na[MSEL];  // split: the selectors' candidate counts for this job
   __shared__ int32_t s_pre_na;    // one selector: the next job's candidate count when its head was already there
   const int tid = threadIdx.x;
@@ -4043,6 +4057,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       sh.n_commit = 0;
       sh.need_hist = 0;
       s_feas = 0;
+      s_bmax = 0;
     }
     if constexpr (SPLIT) {
       // candidates: A, the selector's T best outside the previous job's set (key order, with their static cache
@@ -4080,22 +4095,40 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       }
       // (prefetched at the previous job's end for this very head: the same count)
       const bool pf = MSEL == 1 && ent_pf_na == na;
+      int a_nrank = 0;  // an A entry's rank by node among A's first T (the selector's, entry bits 56..62)
+      uint32_t bk_mine = 0;  // a B entry's key (0 elsewhere)
       if (list >= 0) {
         const uint64_t(*ent)[128] = X->s_ent[r][list];
-        const uint64_t e0 = pf ? ent_pf[0] : x_load64(&ent[0][idx]);
-        const uint64_t st = pf ? ent_pf[1] : x_load64(&ent[1][idx]);
+        // (the loads of the unprefetched path are consumed inside it: see the command decode above)
+        uint64_t ew[kEntW];
+        if (pf) {
+#pragma unroll
+          for (int q = 0; q < kEntW; ++q) ew[q] = ent_pf[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < kEntW; ++q) ew[q] = x_load64(&ent[q][idx]);
+#pragma unroll
+          for (int q = 0; q < kEntW; ++q) asm volatile("" ::"v"(ew[q]));
+        }
+        const uint64_t e0 = ew[0];
+        const uint64_t st = ew[1];
         uint64_t words[sizeof(Row) / 8];
 #pragma unroll
-        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = pf ? ent_pf[2 + q] : x_load64(&ent[2 + q][idx]);
+        for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) words[q] = ew[2 + q];
         __builtin_memcpy(&crow[tid], words, sizeof(Row));
         cst[tid] = st;
-        cnd[tid] = (int)(e0 >> 32);
+        cnd[tid] = (int)((e0 >> 32) & kEntNodeMask);
+        a_nrank = (int)(e0 >> 56);
         akey[list * 128 + idx] = (uint32_t)e0;
       } else if (tid >= na && tid - na < nb) {
         const int j = tid - na, w = bprev[j];
         const Row rw = brow[j];
         // (selector 0's, behind its head: no acquire needed)
-        const uint64_t st = pf ? bst_pf : x_load64(&X->s_bst[r][j]);
+        uint64_t st = bst_pf;
+        if (!pf) {
+          st = x_load64(&X->s_bst[r][j]);
+          asm volatile("" ::"v"(st));
+        }
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, w);
         // an infeasible key (its reason mask) gets the B index below it, so B's keys are distinct: their ranks
         // are a permutation (still below every feasible key)
@@ -4105,10 +4138,28 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         cst[na + j] = st;
         cnd[na + j] = w;
         if (rs == 0) atomicAdd(&s_feas, 1);
+        bk_mine = bkey[j];
+      }
+      {  // the largest B key: per wave, then one LDS atomic per wave (100 on one word cost ~3k cycles, r05A)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bk_mine = umax32(bk_mine, (uint32_t)__shfl_xor((int)bk_mine, o, 64));
+        if ((tid & 63) == 0 && bk_mine) atomicMax(&s_bmax, bk_mine);
       }
       if (tid >= nb && tid < 128) bkey[tid] = 0u;  // padding ranks below every key
       __syncthreads();
       KB_MSTAMP(0);
+      // Fast path (one selector list): every B key below A's T-th key -- the previous job's nodes, just loaded,
+      // rank below the selector's T best, as they mostly do -- makes the T best of the union A's first T, in A's
+      // order: no B order, no union ranks (~1.4 us of barrier-separated LDS ranking, r05z)
+      const bool fast_a = MSEL == 1 && na >= (int)T && s_bmax < akey[T - 1];
+      int pos = -1;
+      uint32_t key = 0;
+      if (fast_a) {
+        if (tid < na) {
+          pos = idx;
+          key = akey[idx];
+        }
+      } else {
       // B's keys in descending order (rank among B: 4 threads per entry; the keys are distinct)
       {
         const int j = tid >> 2, part = tid & 3;
@@ -4128,8 +4179,6 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       // rank in the union (keys carry the node: distinct): the own index plus, in every other list, the entries
       // above the key (binary search)
       const int nc = na + nb;
-      int pos = -1;
-      uint32_t key = 0;
       if (tid < nc) {
         key = tid < na ? akey[list * 128 + idx] : bkey[tid - na];
         // entries above the key in every list (its own list included: there that is its index), all searches
@@ -4154,28 +4203,31 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
 #pragma unroll
         for (int k = 0; k <= MSEL; ++k) pos += c[k];
       }
+      }  // (the general merge)
       // the T best feasible (A is all feasible; infeasible keys rank below every feasible one), slots in node
       // order: the winners' tie rule on equal score fields takes lower slots first, which must be lower nodes
       const int nsel_t = min((int)T, na + s_feas);
       const bool sel = pos >= 0 && pos < nsel_t;
-      __syncthreads();  // the lists read
-      if (sel) bprev[pos] = cnd[tid];  // scratch: the selected nodes by rank
-      if (tid >= nsel_t && tid < 128) bprev[tid] = 0x7fffffff;  // padding: above every node
-      __syncthreads();
-      KB_MSTAMP(2);
-      {
-        const int e = tid >> 2, part = tid & 3;
-        const int w = e < nsel_t ? bprev[e] : 0;
-        uint32_t c = 0;
+      if (!fast_a) {  // (fast path: the selector's node ranks of its first T entries are the slots)
+        __syncthreads();  // the lists read
+        if (sel) bprev[pos] = cnd[tid];  // scratch: the selected nodes by rank
+        if (tid >= nsel_t && tid < 128) bprev[tid] = 0x7fffffff;  // padding: above every node
+        __syncthreads();
+        KB_MSTAMP(2);
+        {
+          const int e = tid >> 2, part = tid & 3;
+          const int w = e < nsel_t ? bprev[e] : 0;
+          uint32_t c = 0;
 #pragma unroll
-        for (int q = 0; q < 32; ++q) c += bprev[part * 32 + q] < w;
-        c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
-        c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
-        if (part == 0 && e < nsel_t) sh.gen[e] = (int)c;  // scratch: slot of the rank-e node
+          for (int q = 0; q < 32; ++q) c += bprev[part * 32 + q] < w;
+          c += dpp_src<0xb1>(0u, c);  // quad_perm [1,0,3,2]
+          c += dpp_src<0x4e>(0u, c);  // quad_perm [2,3,0,1]
+          if (part == 0 && e < nsel_t) sh.gen[e] = (int)c;  // scratch: slot of the rank-e node
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (sel) {
-        const int slot_s = sh.gen[pos];
+        const int slot_s = fast_a ? a_nrank : sh.gen[pos];
         sh.node[slot_s] = cnd[tid];
         sh.key0[slot_s] = key;
         sh.row[slot_s] = crow[tid];
