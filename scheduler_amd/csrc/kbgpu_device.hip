@@ -2215,6 +2215,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       // ---- commit: placements, rows, keys ----
       const int cut = sh.cut;
       const int kind = sh.stop_kind;
+      const int base_c = sh.n_commit;  // (read before the barrier below: thread 0 rewrites it after it)
       if (tid < cut) {
         const uint64_t o = sh.ord[tid];
         const int s = sel_slot(o), j = sel_level(o);
@@ -2228,14 +2229,23 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       // the touched nodes' keys matter only to a later segment or to the no-fit histogram; commit_out
       // lists the rows for the next job, whose level-0 sweep ran before these stores (kb_job_issue)
       const bool rekey = !CAND && (kind == KB_STOP_NO_FIT || (kind == -1 && done_tasks + cut < t_count));
-      if (tid < (int)S && sh.fin[tid] > 0) {
+      // the commit list's positions: slot order, from two ballots (S <= 128 slots: waves 0 and 1) -- an LDS
+      // atomic counter serialised ~100 lanes on one word (~1 us per job)
+      const bool has = tid < (int)S && sh.fin[tid] > 0;
+      const uint64_t b_lo = __ballot(lane < (int)S && sh.fin[lane] > 0);
+      const uint64_t b_hi = __ballot(lane + 64 < (int)S && sh.fin[lane + 64] > 0);
+      if (has) {
         const int w = sh.node[tid], c = sh.fin[tid], A = sh.A[tid];
         store_back_row(N, P, sp, scr, w, c, A, sh.row[tid]);
         if (rekey)
           k32[w] = compress_key(traj_key64(N, P, C, sp, sci, scr, sh.row[tid], sh.stat[tid], w, c, A), w + N.base,
                                 idx_bits);
-        if (commit_out != nullptr) st_sc1(&commit_out[atomicAdd(&sh.n_commit, 1)], (int32_t)w);  // (fed_patch: ld_sc1)
+        if (commit_out != nullptr) {
+          const int at_c = base_c + (wv == 0 ? __popcll(b_lo & lt) : __popcll(b_lo) + __popcll(b_hi & lt));
+          st_sc1(&commit_out[at_c], (int32_t)w);  // (fed_patch: ld_sc1)
+        }
       }
+      if (tid == 0) sh.n_commit = base_c + __popcll(b_lo) + __popcll(b_hi);
       __syncthreads();
       KB_SEL_PH(5);
       ready += sh.n_alloc;
@@ -3696,11 +3706,20 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     hout[2 * (t_begin + tid) + 1] = (int32_t)((uint32_t)nk >> 30);
     if (node >= N.base && node < N.base + N.n) atomicAdd(&sh.fin[sel_slot(sh.ord[tid])], 1);
   }
+  const int base_c = sh.n_commit;  // (read before the barrier: thread 0 rewrites it after)
   __syncthreads();
-  if (tid < sh.n_sel && sh.fin[tid] > 0) {  // NodeInfo.AddTask x fin on this rank's row
-    const int w = sh.node[tid];
-    store_back_row(N, P, sp, P.sc_req + (size_t)spec * N.S, w, sh.fin[tid], sh.A[tid], sh.row[tid]);
-    st_sc1(&commit_out[atomicAdd(&sh.n_commit, 1)], (int32_t)w);  // (fed_patch reads it ld_sc1)
+  {  // the commit list in slot order from two ballots (an LDS atomic counter serialises the lanes on one word)
+    const int ns = sh.n_sel;
+    const uint64_t lt_ = (1ull << lane) - 1;
+    const uint64_t b_lo = __ballot(lane < ns && sh.fin[lane] > 0);
+    const uint64_t b_hi = __ballot(lane + 64 < ns && sh.fin[lane + 64] > 0);
+    if (tid < ns && sh.fin[tid] > 0) {  // NodeInfo.AddTask x fin on this rank's row
+      const int w = sh.node[tid];
+      store_back_row(N, P, sp, P.sc_req + (size_t)spec * N.S, w, sh.fin[tid], sh.A[tid], sh.row[tid]);
+      const int at_c = base_c + (wv == 0 ? __popcll(b_lo & lt_) : __popcll(b_lo) + __popcll(b_hi & lt_));
+      st_sc1(&commit_out[at_c], (int32_t)w);  // (fed_patch reads it ld_sc1)
+    }
+    if (tid == 0) sh.n_commit = base_c + __popcll(b_lo) + __popcll(b_hi);
   }
   placed = cut;
   ready = ready0 + G.n_alloc;
@@ -4097,6 +4116,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       const bool pf = MSEL == 1 && ent_pf_na == na;
       int a_nrank = 0;  // an A entry's rank by node among A's first T (the selector's, entry bits 56..62)
       uint32_t bk_mine = 0;  // a B entry's key (0 elsewhere)
+      bool b_feas = false;   // a B entry's key is feasible
       if (list >= 0) {
         const uint64_t(*ent)[128] = X->s_ent[r][list];
         // (the loads of the unprefetched path are consumed inside it: see the command decode above)
@@ -4137,13 +4157,16 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         crow[na + j] = rw;
         cst[na + j] = st;
         cnd[na + j] = w;
-        if (rs == 0) atomicAdd(&s_feas, 1);
+        b_feas = rs == 0;
         bk_mine = bkey[j];
       }
-      {  // the largest B key: per wave, then one LDS atomic per wave (100 on one word cost ~3k cycles, r05A)
+      {  // the largest B key and B's feasible count: per wave, then one LDS atomic per wave (100 lanes on one word
+         // cost ~3k cycles, r05A)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) bk_mine = umax32(bk_mine, (uint32_t)__shfl_xor((int)bk_mine, o, 64));
+        const int nf = __popcll(__ballot(b_feas));
         if ((tid & 63) == 0 && bk_mine) atomicMax(&s_bmax, bk_mine);
+        if ((tid & 63) == 0 && nf) atomicAdd(&s_feas, nf);
       }
       if (tid >= nb && tid < 128) bkey[tid] = 0u;  // padding ranks below every key
       __syncthreads();

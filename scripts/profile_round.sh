@@ -31,7 +31,9 @@ for C in $CONFIGS; do
   [ "$C" = C2 ] && EVAL=""
   run ${C}_trace 300 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/${C}_trace" -o run --output-format csv -- python3 bench.py --config $C --steps 3 --warmup 1 --no-timing --no-cpu-baseline --no-eval --opt $PLAIN
   NOFED=""
-  [ "$C" != C4 ] && NOFED=,no_fed
+  # FEDPMC=1: the PMC passes on the fed engine itself (its resident sweepers take the commands from a pinned ring:
+  # no other-stream dispatch for the profiler's serialisation to stall; the pass counts the engine's one dispatch)
+  [ "$C" != C4 ] && [ "${FEDPMC:-0}" != 1 ] && NOFED=,no_fed
   # (the PMC passes keep the sweep stream in the shared queue pool: with a dedicated CU-masked queue the profiler's
   # serialisation leaves the launch path's place kernel waiting for its overlapped sweep)
   run ${C}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$PWD/$OUT/${C}_fetch" -o run --output-format csv -- python3 bench.py --config $C --steps 1 --warmup 0 --no-timing --no-cpu-baseline $EVAL --opt $PLAIN,fed_shared_queues$NOFED
