@@ -343,7 +343,7 @@ def roofline_of(st, args, cfg):
     if tr is not None:
         out["traffic"] = tr["bytes_per_launch"]
         out["traffic_source"] = tr["source"]
-        out["traffic_is_proxy"] = fed
+        out["traffic_is_proxy"] = tr.get("proxy", fed)
         out["cycle_traffic_bytes"] = tr["cycle_bytes"]
         if avg_ms > 0:
             out["measured_frac"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
@@ -620,6 +620,14 @@ def pmc_cycle_traffic(config, kernel):
         cyc = sum(e["hbm_bytes_per_launch"] * e["pmc_dispatches"] for k, e in ks.items()
                   if k in CYCLE_KERNELS and "hbm_bytes_per_launch" in e and "pmc_dispatches" in e) / cycles
         src = os.path.relpath(f, ROOT)
+        fe = ks.get("fed_engine_kernel", {})
+        if kernel == "fed_engine_kernel" and "hbm_bytes_per_launch" in fe:
+            # round 5: the engine's own counters (its resident sweepers take the commands from a pinned ring, so
+            # the profiler's dispatch serialisation has no other-stream sweep to stall: scripts/profile_round.sh
+            # FEDPMC=1) -- one dispatch per cycle
+            return {"bytes_per_launch": fe["hbm_bytes_per_launch"], "cycle_bytes": round(cyc, 1), "proxy": False,
+                    "source": f"{src}: the engine's own PMC counts (FETCH_SIZE x2 + WRITE_SIZE), one dispatch per "
+                              f"cycle"}
         if kernel == "fed_engine_kernel":
             return {"bytes_per_launch": round(cyc, 1), "cycle_bytes": round(cyc, 1),
                     "source": f"PROXY, not the engine's own counters: {src}: the same cycle on the per-job launch path "

@@ -3369,10 +3369,11 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     const uint32_t nout = kept < T ? kept : T;
     // each outgoing entry's rank by node among the first nout: the placer's slot order when the T best of the
     // union are exactly these (its merge's fast path: no node ranking there)
-    if (keep && pos < T) cnode[pos] = wp + base;
+    // (one selector only: the placer's fast path takes a single list)
+    if (nsel == 1 && keep && pos < T) cnode[pos] = wp + base;
     __syncthreads();
     uint32_t nrank = 0;
-    if (keep && pos < T) {
+    if (nsel == 1 && keep && pos < T) {
       const int me = wp + base;
       for (uint32_t q = 0; q < nout; ++q) nrank += cnode[q] < me ? 1u : 0u;
     }
