@@ -376,6 +376,11 @@ def shard_fields(st, args):
            "shard_exchange_us_per_job": (round(st["shard_wait_ticks"] / 100.0 / st["shard_xchg"], 3)
                                          if st["shard_xchg"] else None),
            "shard_exchanges_per_step": st["shard_xchg"] / args.steps}
+    ph = st.get("shard_phase_ticks")
+    if ph is not None and st["shard_xchg"]:  # the placer's s_memrealtime per phase of a sharded job (kb_stats)
+        names = ("proposal", "xgmi_write", "peer_wait", "merge_stop_rules", "commit", "nofit_round")
+        out["shard_phase_us_per_job"] = {nm: round(float(ph[i]) / 100.0 / st["shard_xchg"], 3)
+                                         for i, nm in enumerate(names)}
     k = runtime.KERNELS.index("shard_exchange")
     if st["launches"][k]:
         out["launch_path_exchange_us_per_segment"] = round(st["kernel_ms"][k] * 1e3 / st["launches"][k], 2)
