@@ -145,8 +145,13 @@ __device__ __forceinline__ double frac_cap(int64_t req, int64_t cap) {
 struct Row {
   uint32_t flags;
   int32_t pod_count, max_pods;
+  // (the padding word before the int64 columns) the split engine's hand-off: a selector entry's A (allocations
+  // before the node's Idle stops fitting the job's spec, allocs_before_full), -1 where the placer computes it; no
+  // node column, never stored back
+  int32_t aux;
   int64_t idle_cpu, idle_mem, rel_cpu, rel_mem, nz_cpu, nz_mem, alloc_cpu, alloc_mem;
 };
+static_assert(sizeof(Row) == 80, "Row: aux fills the padding word");
 
 __device__ __forceinline__ Row load_row(const DevNodes& N, int n) {
   Row r;
@@ -1946,7 +1951,9 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           sh.row[tid] = r;
           sh.stat[tid] = stat[w];
         }
-        sh.A[tid] = allocs_before_full(N, sp, sci, scr, r, w);
+        // (CAND: the selector computed A for its entries one job ahead -- off this chain; the previous set's rows
+        // come with aux -1)
+        sh.A[tid] = CAND && r.aux >= 0 ? r.aux : allocs_before_full(N, sp, sci, scr, r, w);
         sh.recip[0][tid] = 1.0 / (double)r.alloc_cpu;
         sh.recip[1][tid] = 1.0 / (double)r.alloc_mem;
         sh.cnt[tid] = 0;
@@ -3381,6 +3388,8 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       uint64_t(*ent)[128] = X->s_ent[r][sel];
       x_store64(&ent[0][pos], (uint64_t)wk | ((uint64_t)(uint32_t)(wp + base) << 32) | ((uint64_t)nrank << 56));
       x_store64(&ent[1][pos], stw);
+      // the entry's A for the placer's node setup (allocs_before_full: off the placer's chain)
+      rw.aux = allocs_before_full(N, sp, P.sc_init + (size_t)spec * N.S, P.sc_req + (size_t)spec * N.S, rw, wp + base);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
@@ -4156,6 +4165,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         bkey[j] = rs ? (rs << 7) | (uint32_t)j
                      : compress_key(make_key(0, row_score(C, sp, rw, st), w), w + N.base, idx_bits);
         crow[na + j] = rw;
+        crow[na + j].aux = -1;  // (A computed at the node setup)
         cst[na + j] = st;
         cnd[na + j] = w;
         b_feas = rs == 0;
