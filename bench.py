@@ -668,15 +668,40 @@ def diag_summary(d, tasks, kernel):
             "clock_mhz": round(clock_mhz, 1) if clock_mhz else None}
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup's CPU quota (cgroup v2 cpu.max, else v1 cfs quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0 and per > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(cluster, sample_tasks, config):
     """The oracle (C++ restatement of the reference, ParallelizeUntil-style pool) on the first `sample_tasks`
     placements of the same workload: 16 workers (the reference's ParallelizeUntil(..., 16, ...)), and beside it the
     same sample on every core this process may run on ("Also report an all-cores run")."""
     from oracle import pyoracle
     try:
-        avail = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        avail = os.cpu_count() or 1
+        affinity = os.cpu_count() or 1
+    # the cores this process may actually use: its affinity, capped by the cgroup's CPU quota (the GPU box shows all
+    # 256 CPUs of the host but grants 16; 256 workers there thrashed: 80 pods/s against 2,280 on 16, r05j)
+    quota = cgroup_cpus()
+    avail = min(affinity, quota) if quota else affinity
     label = "CPU restatement of the reference algorithm (oracle/oracle.cpp), not the Go reference"
 
     def run(workers):
@@ -692,7 +717,7 @@ def cpu_baseline(cluster, sample_tasks, config):
            "sample": f"first {out['attempts']} task placements of the {config} cycle "
                      f"({placed} placed in {secs:.2f} s, {cores} worker threads, "
                      f"reference-structured full predicate+score sweep per task)",
-           "host": {"nproc_visible": os.cpu_count(), "affinity_cpus": avail}}
+           "host": {"nproc_visible": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota}}
     if avail > cores:
         out2, placed2, secs2 = run(avail)
         res["all_cores"] = {"value": round(placed2 / secs2, 1) if secs2 > 0 else None, "unit": "pods/s",
@@ -700,7 +725,8 @@ def cpu_baseline(cluster, sample_tasks, config):
                                                       f"threads ({secs2:.2f} s)"}
     else:
         res["all_cores"] = {"value": res["value"], "cores": cores,
-                            "sample": "this process may run on no more than the 16 cores above"}
+                            "sample": f"this process may run on no more than the {cores} cores above (affinity "
+                                      f"{affinity}, cgroup quota {quota})"}
     return res
 
 
