@@ -701,6 +701,8 @@ def cpu_baseline(cluster, sample_tasks, config):
     # the cores this process may actually use: its affinity, capped by the cgroup's CPU quota (the GPU box shows all
     # 256 CPUs of the host but grants 16; 256 workers there thrashed: 80 pods/s against 2,280 on 16, r05j)
     quota = cgroup_cpus()
+    if not quota and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        quota = int(os.environ["OMP_NUM_THREADS"])  # (the pool's stated CPU share when no cgroup quota is visible)
     avail = min(affinity, quota) if quota else affinity
     label = "CPU restatement of the reference algorithm (oracle/oracle.cpp), not the Go reference"
 
