@@ -1995,6 +1995,19 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       //         segmented prefix-min across the node's lanes ----
       const bool cut0 = S == T;  // level 0 of S fills the segment: elements below theta0 cannot rank < T
       __syncthreads();
+      if constexpr (CAND) {
+        // level 0 without a lane: every slot's own key is a candidate (the merge took feasible keys only, and when
+        // S == T theta0 is the least of them), so the first round starts at level 1 and covers one level more per
+        // node -- fewer jobs need a second round
+        if (tid < (int)S) {
+          cand[sh.off[tid]] = ((uint64_t)sh.key0[tid] << 14) | ((uint64_t)(127 - tid) << 7) | 127u;
+          sh.cnt[tid] = 1;
+          sh.emin[tid] = sh.key0[tid];
+          sh.gen[tid] = 1;
+          if (sh.lmax[tid] <= 1) sh.done[tid] = 1;
+        }
+        __syncthreads();
+      }
       KB_SEL_PH(2);
       for (;;) {
         if (wv == 0) {
