@@ -32,7 +32,9 @@ for C in $CONFIGS; do
   run ${C}_trace 300 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/${C}_trace" -o run --output-format csv -- python3 bench.py --config $C --steps 3 --warmup 1 --no-timing --no-cpu-baseline --no-eval --opt $PLAIN
   NOFED=""
   # FEDPMC=1: the PMC passes on the fed engine itself (its resident sweepers take the commands from a pinned ring:
-  # no other-stream dispatch for the profiler's serialisation to stall; the pass counts the engine's one dispatch)
+  # no other-stream dispatch for the profiler's serialisation to stall; the pass counts the engine's one dispatch).
+  # Split-engine configurations only (C2, C3, C5): C1's 1k-node table runs the one-workgroup engine, fed by sweep
+  # kernels, which the serialisation stalls into its idle exit (r05m)
   [ "$C" != C4 ] && [ "${FEDPMC:-0}" != 1 ] && NOFED=,no_fed
   # (the PMC passes keep the sweep stream in the shared queue pool: with a dedicated CU-masked queue the profiler's
   # serialisation leaves the launch path's place kernel waiting for its overlapped sweep)
