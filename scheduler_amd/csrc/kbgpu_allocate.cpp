@@ -299,46 +299,29 @@ struct Driver {
     for (auto& q : queues) {
       q.deserved.S = q.allocated.S = q.request.S = S;
     }
+    // one pass over the tasks: the jobs' counts and DRF allocations, and (proportion) the queues' allocated /
+    // request sums -- the latter in task order with cpu and memory in registers while the queue stays the same (the
+    // same float additions in the same order as one add_raw per task)
+    const bool prop = has[KB_PLUGIN_PROPORTION];
+    int cq = -1;
+    double ac = 0, am = 0, rc = 0, rm = 0;
+    const auto flush = [&]() {
+      if (cq < 0) return;
+      queues[cq].allocated.v[0] = ac;
+      queues[cq].allocated.v[1] = am;
+      queues[cq].request.v[0] = rc;
+      queues[cq].request.v[1] = rm;
+    };
     for (uint32_t t = 0; t < s.n_tasks; ++t) {
       int j = s.task_job[t], st = task_status[t];
-      if (allocated_status(st) || st == KB_ST_SUCCEEDED) jobs[j].ready++;
+      const bool al = allocated_status(st);
+      if (al || st == KB_ST_SUCCEEDED) jobs[j].ready++;
       if (st == KB_ST_PIPELINED) jobs[j].waiting++;
-      if (allocated_status(st) || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
+      if (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
       if (st == KB_ST_ALLOCATED) job_allocated[j].push_back((int)t);
-      if (allocated_status(st)) jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
-    }
-    const auto i1 = std::chrono::steady_clock::now();
-    for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
-    const auto i2 = std::chrono::steady_clock::now();
-    if (has[KB_PLUGIN_PROPORTION]) open_proportion();
-    if (ctx->issue_trace)
-      fprintf(stderr, "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f\n",
-              std::chrono::duration<double, std::milli>(i1 - i0).count(),
-              std::chrono::duration<double, std::milli>(i2 - i1).count(),
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count());
-    return KB_OK;
-  }
-
-  // proportion.OnSessionOpen (proportion.go:58-169); queues visited in UID order.
-  void open_proportion() {
-    std::vector<char> in_use(s.n_queues, 0);
-    for (uint32_t j = 0; j < s.n_jobs; ++j) in_use[s.job_queue[j]] = 1;
-    {  // the queues' sums in task order, cpu and memory kept in registers while the queue stays the same (the same
-       // float additions in the same order as one add_raw per task: 0.24 -> ~0.05 ms per C2 cycle)
-      int cq = -1;
-      double ac = 0, am = 0, rc = 0, rm = 0;
-      const auto flush = [&]() {
-        if (cq < 0) return;
-        queues[cq].allocated.v[0] = ac;
-        queues[cq].allocated.v[1] = am;
-        queues[cq].request.v[0] = rc;
-        queues[cq].request.v[1] = rm;
-      };
-      for (uint32_t t = 0; t < s.n_tasks; ++t) {
-        const int st = task_status[t];
-        const bool al = allocated_status(st);
-        if (!al && st != KB_ST_PENDING) continue;
-        const int qi = s.job_queue[s.task_job[t]];
+      if (al) jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
+      if (prop && (al || st == KB_ST_PENDING)) {  // proportion.go:72-81 (OnSessionOpen's task walk)
+        const int qi = s.job_queue[j];
         if (qi != cq) {
           flush();
           cq = qi;
@@ -358,8 +341,25 @@ struct Driver {
         rm += p[1];
         queues[qi].request.add_scalars(p, m);
       }
-      flush();
     }
+    flush();
+    const auto i1 = std::chrono::steady_clock::now();
+    for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
+    const auto i2 = std::chrono::steady_clock::now();
+    if (prop) open_proportion();
+    if (ctx->issue_trace)
+      fprintf(stderr, "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f\n",
+              std::chrono::duration<double, std::milli>(i1 - i0).count(),
+              std::chrono::duration<double, std::milli>(i2 - i1).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count());
+    return KB_OK;
+  }
+
+  // proportion.OnSessionOpen (proportion.go:58-169); queues visited in UID order.
+  void open_proportion() {
+    std::vector<char> in_use(s.n_queues, 0);
+    for (uint32_t j = 0; j < s.n_jobs; ++j) in_use[s.job_queue[j]] = 1;
+    // (the queues' allocated / request sums come from init()'s task pass)
     std::vector<int> order;
     for (uint32_t q = 0; q < s.n_queues; ++q)
       if (in_use[q]) order.push_back((int)q);

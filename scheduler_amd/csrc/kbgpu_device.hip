@@ -2006,13 +2006,9 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           sh.gen[tid] = 1;
           if (sh.lmax[tid] <= 1) sh.done[tid] = 1;
         }
-        __syncthreads();
-      }
-      KB_SEL_PH(2);
-      for (;;) {
-        if (wv == 0) {
-          const bool a0 = lane < (int)S && !sh.done[lane];
-          const bool a1 = lane + 64 < (int)S && !sh.done[lane + 64];
+        if (wv == 0) {  // the first round's active list beside it (active: lmax > 1), under the same barrier
+          const bool a0 = lane < (int)S && sh.lmax[lane] > 1;
+          const bool a1 = lane + 64 < (int)S && sh.lmax[lane + 64] > 1;
           const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
           const int c0 = __popcll(m0);
           if (a0) sh.act[__popcll(m0 & lt)] = lane;
@@ -2020,6 +2016,21 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
           if (lane == 0) sh.n_act = c0 + __popcll(m1);
         }
         __syncthreads();
+      }
+      KB_SEL_PH(2);
+      for (bool first = CAND;; first = false) {
+        if (!first) {
+          if (wv == 0) {
+            const bool a0 = lane < (int)S && !sh.done[lane];
+            const bool a1 = lane + 64 < (int)S && !sh.done[lane + 64];
+            const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
+            const int c0 = __popcll(m0);
+            if (a0) sh.act[__popcll(m0 & lt)] = lane;
+            if (a1) sh.act[c0 + __popcll(m1 & lt)] = lane + 64;
+            if (lane == 0) sh.n_act = c0 + __popcll(m1);
+          }
+          __syncthreads();
+        }
         const int na = sh.n_act;
         if (na == 0) break;
         KB_SEL_COUNT(13, 1);
