@@ -517,7 +517,7 @@ EVAL_SPECS, EVAL_NODES = 256, 50000
 EVAL_OUT_BYTES = 8  # kb_eval32: u32 reason mask + i32 score per (spec, node)
 
 
-EVAL_WARMUP, EVAL_TIMED = 200, 20
+EVAL_WARMUP, EVAL_TIMED = 200, 200
 
 
 def eval_side(device):
