@@ -907,6 +907,8 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
   const int nj = t - j0 < spb ? t - j0 : spb;
 #ifdef KB_EVAL_NPT2
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;  // (A/B store probe: two nodes per lane)
+#elif defined(KB_EVAL_RUN4)
+  const int n = blockIdx.x * blockDim.x * 4 + threadIdx.x;  // (A/B store probe: 4 nodes per lane, 256 apart)
 #else
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
 #endif
@@ -1011,6 +1013,19 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
           (void)score;
           continue;
         }
+#endif
+#if defined(KB_EVAL_STOREONLY) && defined(KB_EVAL_RUN4)
+        // (one 4 KB run per spec row per workgroup instead of 1 KB)
+        for (int k = 0; k < 4; ++k) {
+          const int nk = n + k * 256;
+          if (nk < N.n) {
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(nk ^ j), rbuf, nk * 4, (int)(orow * 4u), kEvalAux);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(nk + j), sbuf, nk * 4, (int)(orow * 4u), kEvalAux);
+          }
+        }
+        (void)rs;
+        (void)score;
+        continue;
 #endif
 #if defined(KB_EVAL_STOREONLY)
         const uint32_t rs_v = (uint32_t)(n ^ j);
@@ -6689,6 +6704,8 @@ static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C,
     const int spb = eval_plain_spb(N.n, t, cus & 0xffff, cus >> 16, spb_opt);
 #ifdef KB_EVAL_NPT2
     dim3 grid((N.n + 511) / 512, (t + spb - 1) / spb);
+#elif defined(KB_EVAL_RUN4)
+    dim3 grid((N.n + 1023) / 1024, (t + spb - 1) / spb);
 #else
     dim3 grid((N.n + 255) / 256, (t + spb - 1) / spb);
 #endif
