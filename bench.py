@@ -365,7 +365,12 @@ def engine_of(st):
     return {"kernel": "fed_engine_kernel", "bound": "latency (per-job dependent chain in one workgroup)",
             "avg_launch_us": round(us, 3), "launches": st["launches"][k], "jobs_per_launch": round(jobs, 1),
             "us_per_job": round(us / max(1.0, jobs), 3), "clock_mhz": round(clk, 1) if clk else None,
-            "placement": {"placer": place[0], "selector": place[1]}}
+            "placement": {"placer": place[0], "selector": place[1]},
+            "depth": st["fed_last_depth"], "sweepers": st["fed_last_sweepers"],
+            "mispredicts_per_step": round(st["fed_mispredicts"] / launches, 2),
+            "skipped_per_step": round(st["fed_skipped"] / launches, 2),
+            "nofit_predicted_per_step": round(st["nofit_predicted"] / launches, 2),
+            "units_per_step": round(st["fed_units"] / launches, 1)}
 
 
 def shard_fields(st, args):

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 14
+#define KBGPU_ABI_VERSION 15
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -219,8 +219,12 @@ typedef struct kb_opts {
   int32_t test_stall_ms; /* tests: with test_stall_job >= 0, a host stall of this long before that job */
   int64_t test_stall_job;/* tests: -1 off */
   uint32_t shard_epoch0; /* tests: the node-sharded engine's first cycle epoch (0; the inbox tags' wrap) */
-  int32_t fed_xcc;       /* ABI 14: the split engine's workgroups: 0 = where the dispatcher puts them; k + 1 = on XCC k
-                            (a census at launch, kbgpu_device.hip fed_engine_kernel); -1 = the library's default */
+  int32_t fed_xcc;       /* ABI 15: the split engine's workgroups: 0 = the library's default (XCC 0, resident sweepers);
+                            k + 1 = on XCC k (a census at launch, kbgpu_device.hip fed_engine_kernel); -1 = where the
+                            dispatcher puts them (no census, so per-job sweep kernels). A zero-initialised kb_opts gets
+                            the production path. */
+  int32_t fed_depth;     /* ABI 15: the fed engine's units in flight (the running one + speculative ones), 2..4;
+                            0 = chosen per cycle by the driver (kbgpu_allocate.cpp) */
 } kb_opts;
 
 typedef struct kb_ctx kb_ctx;
@@ -418,6 +422,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 /* ABI 14: the split engine's per-job sweeps by sweep kernels on the CU-masked stream (round 4's path) instead of
  * its resident sweepers (the spare workgroups of its census grid, fed commands through a pinned ring); A/B only. */
 #define KB_OPT_FED_KERNEL_SWEEPS (1u << 17)
+/* ABI 15, tests only: the split engine's census reads every workgroup as on the placer's XCC (a one-XCC device or
+ * partition), so its resident sweepers share that XCC */
+#define KB_OPT_TEST_ONE_XCC (1u << 18)
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -472,6 +479,17 @@ typedef struct kb_stats {
                                          host-evaluated reasons, ...), run on the launch path while the engine of a
                                          cycle that otherwise runs on it is paused (or between two launches) */
   uint64_t fed_pauses;                /* engine pauses for such units (the engine idles; its next command is fresh) */
+  /* ABI 15 */
+  uint64_t fed_mispredicts;           /* pipelined driver: units whose outcome differed from the prediction their
+                                         successor was guarded on (the speculative chain behind them drained) */
+  uint64_t fed_skipped;               /* ... speculative units skipped (guard failed) and drained */
+  uint64_t fed_units;                 /* units finished by the pipelined driver in its fed (engine) mode */
+  uint64_t nofit_predicted;           /* speculative issues behind a unit predicted NO_FIT (its spec, or a smaller one
+                                         of its feasibility class, already found no node this cycle) */
+  int32_t fed_last_depth;             /* the last engine cycle's units in flight (kb_opts.fed_depth or the driver's
+                                         choice) */
+  int32_t fed_last_sweepers;          /* the last split engine launch: resident sweeper workgroups (0: sweep
+                                         kernels) */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

@@ -561,6 +561,7 @@ struct Driver {
     if (res.stop == KB_STOP_NO_FIT) {
       const int ft = js.pending[js.cursor];
       out->job_fail_task[j] = ft;
+      note_dead(s.task_spec[ft]);
       memcpy(out->job_reason_hist + (size_t)j * KB_NUM_REASONS, res.reason_hist, sizeof(res.reason_hist));
       // host-evaluated stages: the caller turns the KB_R_HOST_ERROR bucket into its per-node strings from
       // the reason masks at this state (nothing has run since the failing task)
@@ -582,10 +583,16 @@ struct Driver {
   // The place call's outcome when every task it places is Allocated (the stop rules of the place
   // kernels): a gang job stops READY at the task that brings ready to minAvailable, a job without the
   // gang JobReady check after its first task; otherwise every task places and the call ends DONE.
-  void predict(const Unit& u, int& stop, int& placed) const {
+  // A unit whose first task's spec is dead (below) stops NO_FIT before placing anything.
+  void predict(const Unit& u, int& stop, int& placed) {
     const int j = u.j;
     const JobS& js = jobs[j];
     const int nt = (int)u.len;
+    if (is_dead(s.task_spec[js.pending[u.cur]])) {
+      stop = KB_STOP_NO_FIT;
+      placed = 0;
+      return;
+    }
     if (!gang_ready_on) {
       stop = KB_STOP_READY;
       placed = 1;
@@ -594,6 +601,52 @@ struct Driver {
     const int need = std::max(1, s.job_min_available[j] - js.ready);
     stop = need <= nt ? KB_STOP_READY : KB_STOP_DONE;
     placed = std::min(need, nt);
+  }
+
+  // NO_FIT prediction. A spec that stopped a unit NO_FIT found no node at that state; within the cycle every node's
+  // Idle, Releasing, pod count and used host ports only move toward failure (Allocate / Pipeline commits, session.go:
+  // 199-297), so it finds none later either, and neither does a spec of its feasibility class (kb_upload_specs: the
+  // same PredicateFn inputs apart from InitResreq) whose InitResreq is at least as large in every resource
+  // (resource_info.go:253-276). Such units are predicted NO_FIT with no placement, so the speculative chain behind
+  // them survives (C3: each NO_FIT job used to drain the chain). Specs with inter-pod terms (required affinity can
+  // turn true as pods land) or host-evaluated reasons have no class. dead[c]: the minimal dead specs of class c.
+  std::vector<std::vector<int>> dead;
+  std::vector<int8_t> spec_dead;  // per spec: 0 unknown, 1 dead
+  bool dead_any = false;
+  bool dead_eligible(int sp) const {
+    return sp >= 0 && (size_t)sp < ctx->spec_fclass.size() && ctx->spec_fclass[sp] >= 0 &&
+           !(ctx->aff_ok && ctx->spec_needs_aff[sp]) && !ctx->host_reasons(sp);
+  }
+  bool init_geq(int a, int b) const {  // InitResreq(a) >= InitResreq(b) in every resource b requests
+    const uint64_t ma = ctx->spec_init_mask[a], mb = ctx->spec_init_mask[b];
+    if (mb & ~ma) return false;
+    const size_t w = 2 + (size_t)ctx->N.S;
+    const int64_t* va = ctx->spec_init.data() + (size_t)a * w;
+    const int64_t* vb = ctx->spec_init.data() + (size_t)b * w;
+    if (va[0] < vb[0] || va[1] < vb[1]) return false;
+    for (uint64_t m = mb; m; m &= m - 1)
+      if (va[2 + __builtin_ctzll(m)] < vb[2 + __builtin_ctzll(m)]) return false;
+    return true;
+  }
+  void note_dead(int sp) {
+    if (!dead_eligible(sp)) return;
+    std::vector<int>& d = dead[(size_t)ctx->spec_fclass[sp]];
+    for (int x : d)
+      if (init_geq(sp, x)) return;  // implied by a smaller dead spec
+    d.erase(std::remove_if(d.begin(), d.end(), [&](int x) { return init_geq(x, sp); }), d.end());
+    d.push_back(sp);
+    spec_dead[(size_t)sp] = 1;
+    dead_any = true;
+  }
+  bool is_dead(int sp) {
+    if (!dead_any || !dead_eligible(sp)) return false;
+    if (spec_dead[(size_t)sp]) return true;
+    for (int x : dead[(size_t)ctx->spec_fclass[sp]])
+      if (init_geq(sp, x)) {
+        spec_dead[(size_t)sp] = 1;
+        return true;
+      }
+    return false;
   }
 
   // Units in flight on the device (pipelined driver), oldest first. Entry i > 0 was issued speculatively, guarded on
@@ -643,6 +696,7 @@ struct Driver {
       Flight& f = fl[i];
       int stop, placed;
       predict(f.u, stop, placed);
+      if (stop == KB_STOP_NO_FIT && i + 1 == fl.size()) ctx->stats.nofit_predicted++;
       JobS& js = jobs[f.u.j];
       bool seen = false;
       for (const auto& e : saved_jobs) seen = seen || e.j == f.u.j;
@@ -704,11 +758,17 @@ struct Driver {
     return 1;
   }
 
+  // The engine's units in flight (the running one + speculative ones): kb_opts.fed_depth, else kJobSlots.
+  int fed_depth() const { return ctx->fed_depth >= 2 ? ctx->fed_depth : kbgpu::kJobSlots; }
+
   int run() {
     const auto r0 = std::chrono::steady_clock::now();
     qheap.less = [this](const int& a, const int& b) { return queue_less(a, b); };
     sq.less = qheap.less;
     jheaps.assign(s.n_queues, GoHeap<int>());
+    dead.assign((size_t)ctx->n_fclass, {});
+    spec_dead.assign(ctx->spec_fclass.size(), 0);
+    dead_any = false;
     for (auto& h : jheaps) h.less = [this](const int& a, const int& b) { return job_less(a, b); };
     gang_ready_on = has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY);
     std::vector<int> jorder(s.n_jobs);
@@ -843,7 +903,8 @@ struct Driver {
         continue;
       }
       // pipelined (the fed engine: two units ahead, kJobSlots slots; the launch path: one ahead, two slots)
-      n_slots = mode ? kbgpu::kJobSlots : 2;
+      n_slots = mode ? fed_depth() : 2;
+      if (mode) ctx->stats.fed_last_depth = n_slots;
       fl.clear();
       {
         const kb_job_req req = make_req(u);
@@ -881,7 +942,12 @@ struct Driver {
         const bool match = chained && rc == KB_OK && res.stop == pred.stop && (int)res.n_placed == pred.placed &&
                            jobs[f0.u.j].ready + (int)std::count(pk.begin(), pk.begin() + res.n_placed,
                                                                 (int32_t)KB_PLACE_ALLOCATE) == pred.ready;
+        if (mode) ctx->stats.fed_units++;
         if (chained && !match) {  // every later guard fails on the device as well: drain the skipped units
+          if (mode) {
+            ctx->stats.fed_mispredicts++;
+            ctx->stats.fed_skipped += fl.size() - 1;
+          }
           for (size_t i = 1; i < fl.size(); ++i) {
             kb_job_result skip;
             int rc2 = kb_job_finish(ctx, fl[i].slot, nullptr, nullptr, &skip, 1);

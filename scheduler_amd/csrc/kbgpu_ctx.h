@@ -31,6 +31,12 @@ struct kb_ctx {
   std::vector<char> spec_cap1;     // per spec: kSpecCap1 (a selection run with at most one Allocate per node)
   std::vector<int32_t> spec_cls;   // per spec: the class loop's finest dynamic slot (-1: not eligible)
   std::vector<int64_t> aff_slot_D;  // per topology slot: its domain count
+  // per spec: its feasibility class (kb_upload_specs; -1: inter-pod terms, no class) and InitResreq (cpu, mem, then
+  // the scalar slots; spec_init_mask the slots present): the driver's NO_FIT prediction (kbgpu_allocate.cpp)
+  std::vector<int32_t> spec_fclass;
+  std::vector<int64_t> spec_init;
+  std::vector<uint64_t> spec_init_mask;
+  int32_t n_fclass = 0;
   std::vector<char> spec_rowcols;  // per spec: it reads scalar / host-port columns (the fed engine's acquire, FedCmd::acq)
   std::vector<int32_t> spec_aff_class0;  // per spec: aff_class as kb_upload_specs got it (kb_upload_affinity marks
                                          // specs with an empty affinity entry -1: they run as plain specs)
@@ -169,6 +175,8 @@ struct kb_ctx {
   // occupancy first). KB_OPT_FED_SHARED_QUEUES (tests): a plain stream_b, the hazard the dedicated queue removes.
   bool fed_dedicated = true;
   bool fed_coop = false;  // KB_OPT_FED_COOP_LAUNCH (A/B only): the default is a plain launch + residency check
+  // kb_opts.fed_depth: the engine's units in flight, 2..kJobSlots (0: the driver's per-cycle choice, kbgpu_allocate.cpp)
+  int fed_depth = 0;
   // kb_opts.fed_xcc - 1: the split engine's XCC (-1: the dispatcher's placement). Default XCC 0: measured on C2
   // (r05c), the placer and selector on XCC 0-3 run 17.0-17.1 us per job, on XCC 4-7 17.6-18.1 us, and a plain
   // launch lands wherever the dispatcher's round robin stands
@@ -176,6 +184,7 @@ struct kb_ctx {
   // the split engine's resident sweepers (launch_fed_engine's hring): commands go to a pinned ring (fed_hring,
   // tags fed_epoch << 32 | fed_m + 1) instead of a sweep kernel per job; KB_OPT_FED_KERNEL_SWEEPS turns them off
   bool fed_kernel_sweeps = false, fed_sweepers_now = false;
+  bool test_one_xcc = false;  // KB_OPT_TEST_ONE_XCC
   void* fed_hring = nullptr;      // pinned host ring (kJobSlots FedHostCmd)
   void* fed_hring_dev = nullptr;  // its device address
   uint32_t fed_epoch = 0, fed_m = 0;

@@ -3878,10 +3878,13 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     const uint32_t G = gridDim.x;
+    // (bit 8 of place_xcc, tests only: every workgroup's census entry reads as the placer's XCC -- a one-XCC layout)
+    const bool one_xcc = place_xcc >= 0 && (place_xcc & 0x100) != 0;
+    const int pxc = place_xcc >= 0 ? (place_xcc & 0xff) : -1;
     if (tid == 0) {
       int all = 1;
-      if (place_xcc >= 0) {
-        __hip_atomic_store(&X->census_xcc[blockIdx.x], xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pxc >= 0) {
+        __hip_atomic_store(&X->census_xcc[blockIdx.x], (one_xcc ? (uint32_t)pxc : xcc) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(&X->census_n, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (!(all = __hip_atomic_load(&X->census_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= G) &&
@@ -3892,7 +3895,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       s_all = all;
     }
     __syncthreads();
-    if (place_xcc >= 0 && s_all && tid < (int)G)  // every entry in one round trip (agent-scope loads)
+    if (pxc >= 0 && s_all && tid < (int)G)  // every entry in one round trip (agent-scope loads)
       s_cx[tid] = (uint8_t)__hip_atomic_load(&X->census_xcc[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tid == 0) {
@@ -3901,28 +3904,44 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       // sweeper's stores and its per-job release would dirty and write back that XCC's L2 under the placer
       // (measured: C2 19.2 us per job with sweepers there, r05r). The rest exit.
       int role = (int)blockIdx.x, nsw = 0;
-      if (place_xcc >= 0) {
+      if (pxc >= 0) {
         role = -1;
         if (s_all) {
           int k = 0;
           for (int pass = 0; pass < 2; ++pass)
             for (uint32_t b = 0; b < G && k <= nsel; ++b)
-              if (!(s_cx[b] & 0x80u) && ((uint32_t)s_cx[b] == (uint32_t)place_xcc + 1) == (pass == 0)) {
+              if (!(s_cx[b] & 0x80u) && ((uint32_t)s_cx[b] == (uint32_t)pxc + 1) == (pass == 0)) {
                 if (b == blockIdx.x) role = k;
                 s_cx[b] |= 0x80u;  // (taken)
                 ++k;
               }
-          if (hring != nullptr)
+          if (hring != nullptr) {
             for (uint32_t b = 0; b < G; ++b)
-              if (!(s_cx[b] & 0x80u) && s_cx[b] != (uint32_t)place_xcc + 1) {
+              if (!(s_cx[b] & 0x80u) && s_cx[b] != (uint32_t)pxc + 1) {
                 if (b == blockIdx.x) role = nsel + 1 + nsw;
                 ++nsw;
               }
+            // no workgroup off the placer's XCC (a one-XCC device or partition): the sweepers share its XCC rather
+            // than leave the host ring undrained (the selector would wait out its idle bound for every command)
+            if (nsw == 0)
+              for (uint32_t b = 0; b < G; ++b)
+                if (!(s_cx[b] & 0x80u)) {
+                  if (b == blockIdx.x) role = nsel + 1 + nsw;
+                  ++nsw;
+                }
+            // still none (a grid of placer and selectors only, which launch_fed_engine never sizes): every role leaves
+            // with the exit flag set, so the host finishes the cycle on the launch path instead of waiting
+            if (nsw == 0) {
+              role = -1;
+              atomicMax(exit_flag, 1);
+            }
+          }
         }
       }
       s_role = role;
       s_nsw = nsw;
-      if (role >= 0 && role <= 1) X->sphase[6 + role] = (uint64_t)xcc << 32 | hw;  // (kb_stats.fed_wg_place)
+      // (kb_stats.fed_wg_place; the placer's word also carries the sweeper count, kb_stats.fed_last_sweepers)
+      if (role >= 0 && role <= 1) X->sphase[6 + role] = (uint64_t)xcc << 32 | hw | (role == 0 ? (uint64_t)nsw << 40 : 0ull);
     }
     __syncthreads();
     const int role = s_role;
@@ -4615,7 +4634,8 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   const FedCmd* ring_c = (const FedCmd*)ring;
   FedXchg* X = (FedXchg*)xchg;
   ShardPeers SP = shard;
-  int pxcc = xchg && place_xcc >= 0 && place_xcc < 8 ? place_xcc : -1;
+  // (bit 8: the tests' one-XCC census, fed_engine_kernel)
+  int pxcc = xchg && place_xcc >= 0 && (place_xcc & 0xff) < 8 ? place_xcc : -1;
   const FedHostCmd* hr = (const FedHostCmd*)hring;
   void* args[] = {(void*)&N, (void*)&P, (void*)&C, (void*)&idx_bits, (void*)&S, (void*)&ring_c, (void*)&ctr,
                   (void*)&idle_ticks, (void*)&exit_flag, (void*)&X, (void*)&nsel, (void*)&SP, (void*)&pxcc,

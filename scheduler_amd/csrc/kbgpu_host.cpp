@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kbgpu_ctx.h"
@@ -254,12 +255,16 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->shard_self_inbox = (fl & KB_OPT_SHARD_SELF_INBOX) != 0;
   c->test_peer_badtag = (fl & KB_OPT_TEST_PEER_BADTAG) != 0;
   c->fed_kernel_sweeps = (fl & KB_OPT_FED_KERNEL_SWEEPS) != 0;
+  c->test_one_xcc = (fl & KB_OPT_TEST_ONE_XCC) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
   if (opts && opts->eval_spb > 0) c->eval_spb = opts->eval_spb;
   if (opts) c->shard_epoch0 = opts->shard_epoch0;
-  if (opts && opts->fed_xcc >= 0) c->fed_xcc = opts->fed_xcc - 1;  // (< 0: the library's default, kbgpu_ctx.h)
+  // kb_opts.fed_xcc (ABI 15): 0 the library's default (kbgpu_ctx.h), k + 1 XCC k, < 0 the dispatcher's placement
+  if (opts && opts->fed_xcc > 0) c->fed_xcc = opts->fed_xcc - 1;
+  if (opts && opts->fed_xcc < 0) c->fed_xcc = -1;
+  if (opts && opts->fed_depth >= 2) c->fed_depth = std::min(opts->fed_depth, (int)kJobSlots);
   if (opts && opts->test_stall_job >= 0) {
     c->test_stall_job = opts->test_stall_job;
     if (opts->test_stall_ms > 0) c->test_stall_ms = opts->test_stall_ms;
@@ -546,6 +551,46 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
       sum += std::llabs((long long)in->terms[in->specs[i].pref_term_off + j].weight);
     c->max_pref_weight = std::max(c->max_pref_weight, sum);
     c->spec_pref_weight[i] = sum;
+  }
+  // Feasibility classes (the driver's NO_FIT prediction, kbgpu_allocate.cpp): two specs share a class when everything
+  // PredicateFn reads of them other than InitResreq is equal -- flags, tolerations, the selector and required node
+  // affinity terms (by content), host ports. Within a class feasibility is monotone in InitResreq
+  // (resource_info.go:253-276: LessEqual per resource), and within an allocate cycle every node's Idle, Releasing,
+  // pod count and used ports only move toward failure, so a spec that found no node stays without one, and so does
+  // every spec of its class whose request is at least as large in every resource.
+  {
+    std::unordered_map<std::string, int32_t> ids;
+    c->spec_fclass.assign(in->m, -1);
+    c->spec_init.assign((size_t)in->m * (2 + S), 0);
+    c->spec_init_mask.assign(in->m, 0);
+    std::string k;
+    auto put = [&k](const void* p, size_t b) { k.append((const char*)p, b); };
+    auto put_term = [&](uint32_t t) {
+      const kb_term& tm = in->terms[t];
+      put(&tm.req_cnt, 4);
+      for (uint32_t q = 0; q < tm.req_cnt; ++q) {
+        const kb_req& r = in->reqs[tm.req_off + q];
+        put(&r.key, 4), put(&r.op, 4), put(&r.val_cnt, 4), put(&r.ival, 8);
+        put(in->vals + r.val_off, 4 * (size_t)r.val_cnt);
+      }
+    };
+    for (uint32_t i = 0; i < in->m; ++i) {
+      const kb_spec& q = in->specs[i];
+      int64_t* v = c->spec_init.data() + (size_t)i * (2 + S);
+      v[0] = q.init_cpu, v[1] = q.init_mem;
+      for (uint32_t r = 0; r < S; ++r) v[2 + r] = in->sc_init[(size_t)i * S + r];
+      c->spec_init_mask[i] = q.init_sc_mask;
+      if ((q.flags & (KB_SPEC_POD_AFFINITY | KB_SPEC_IPA_ERROR)) || q.aff_class >= 0) continue;
+      k.clear();
+      put(&q.flags, 4), put(&q.tol_set, 4);
+      if (q.flags & KB_SPEC_HAS_SELECTOR) put_term(q.sel_term);
+      put(&q.req_term_cnt, 4);
+      for (uint32_t t = 0; t < q.req_term_cnt; ++t) put_term(q.req_term_off + t);
+      put(&q.port_cnt, 4);
+      put(in->ports + q.port_off, sizeof(kb_port) * (size_t)q.port_cnt);
+      c->spec_fclass[i] = ids.emplace(k, (int32_t)ids.size()).first->second;
+    }
+    c->n_fclass = (int32_t)ids.size();
   }
   kb_update_traj_ok(c);
   c->specs_ok = true;
@@ -1765,7 +1810,7 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
   c->fed_m = 0;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
                                           c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP,
-                                          c->fed_coop ? -1 : c->fed_xcc,
+                                          c->fed_coop || c->fed_xcc < 0 ? -1 : c->fed_xcc | (c->test_one_xcc ? 0x100 : 0),
                                           c->fed_sweepers_now ? c->fed_hring_dev : nullptr, c->fed_epoch));
   HIP_OK(c, hipGetLastError());
   c->fed = true;
@@ -1955,8 +2000,10 @@ int kb_fed_end(kb_ctx* c) {
     c->stats.fed_real_ticks += d[15];
     if (c->sharded)
       for (int k = 0; k < 6; ++k) c->stats.shard_phase_ticks[k] += ph[k];
-    c->stats.fed_wg_place[0] = ph[6];
+    // (the placer's word carries the resident sweeper count in bits 40..47)
+    c->stats.fed_wg_place[0] = ph[6] & ~(0xffull << 40);
     c->stats.fed_wg_place[1] = ph[7];
+    c->stats.fed_last_sweepers = (int32_t)((ph[6] >> 40) & 0xffu);
   }
   c->prev_listed = false;  // (the launch path's next sweep must not count on the engine's commit lists)
   // an idle exit after every job was served (a host stall before this call) loses nothing

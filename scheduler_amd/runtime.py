@@ -91,7 +91,7 @@ def shard_range(n_total: int, rank: int, world: int):
 class kb_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("timing_every", C.c_uint32), ("fed_idle_ms", C.c_int32),
                 ("eval_spb", C.c_int32), ("test_stall_ms", C.c_int32), ("test_stall_job", C.c_int64),
-                ("shard_epoch0", C.c_uint32), ("fed_xcc", C.c_int32)]
+                ("shard_epoch0", C.c_uint32), ("fed_xcc", C.c_int32), ("fed_depth", C.c_int32)]
 
 
 class kb_job_req(C.Structure):
@@ -129,7 +129,9 @@ class kb_stats(C.Structure):
                 ("shard_wait_ticks", C.c_uint64), ("fed_clock_ticks", C.c_uint64), ("fed_real_ticks", C.c_uint64),
                 ("sweep_overlap", C.c_uint64), ("overlap_refused_tables", C.c_uint64),
                 ("shard_phase_ticks", C.c_uint64 * 6), ("peer_checks", C.c_uint64), ("fed_wg_place", C.c_uint64 * 2),
-                ("off_engine_units", C.c_uint64), ("fed_pauses", C.c_uint64)]
+                ("off_engine_units", C.c_uint64), ("fed_pauses", C.c_uint64),
+                ("fed_mispredicts", C.c_uint64), ("fed_skipped", C.c_uint64), ("fed_units", C.c_uint64),
+                ("nofit_predicted", C.c_uint64), ("fed_last_depth", C.c_int32), ("fed_last_sweepers", C.c_int32)]
 
 
 KB_OPT_TIMING = 1
@@ -141,8 +143,9 @@ KB_OPT_ENGINE = 8
 OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6, "no_aff_reg": 1 << 7,
                 "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
                 "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14,
-                "fed_coop_launch": 1 << 15, "test_peer_badtag": 1 << 16, "fed_kernel_sweeps": 1 << 17}
-OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0", "fed_xcc")
+                "fed_coop_launch": 1 << 15, "test_peer_badtag": 1 << 16, "fed_kernel_sweeps": 1 << 17,
+                "test_one_xcc": 1 << 18}
+OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0", "fed_xcc", "fed_depth")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
            "shard_propose_kernel", "shard_exchange", "shard_commit_kernel", "fed_engine_kernel", "cls_place_kernel")
@@ -154,7 +157,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 14  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 15  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -229,7 +232,7 @@ def make_opts(device: int = 0, timing: bool = False, path: str = "select", timin
     options = dict(options or {})
     flags = (KB_OPT_TIMING if timing else 0) | PATHS[path]
     vals = {"fed_idle_ms": 0, "eval_spb": 0, "test_stall_job": -1, "test_stall_ms": 0, "shard_epoch0": 0,
-            "fed_xcc": -1}
+            "fed_xcc": 0, "fed_depth": 0}
     for k, v in options.items():
         if k in OPTION_FLAGS:
             flags |= OPTION_FLAGS[k] if v else 0
@@ -238,7 +241,7 @@ def make_opts(device: int = 0, timing: bool = False, path: str = "select", timin
         else:
             raise KbError(KB_E_INVALID, f"unknown context option {k!r}")
     return kb_opts(device, flags, timing_every, vals["fed_idle_ms"], vals["eval_spb"], vals["test_stall_ms"],
-                   vals["test_stall_job"], vals["shard_epoch0"], vals["fed_xcc"])
+                   vals["test_stall_job"], vals["shard_epoch0"], vals["fed_xcc"], vals["fed_depth"])
 
 
 def parse_options(text: str | None) -> dict:
@@ -409,7 +412,10 @@ class Context:
                 "overlap_refused_tables": st.overlap_refused_tables,
                 "shard_phase_ticks": list(st.shard_phase_ticks), "peer_checks": st.peer_checks,
                 "off_engine_units": st.off_engine_units, "fed_wg_place": list(st.fed_wg_place),
-                "fed_pauses": st.fed_pauses}
+                "fed_pauses": st.fed_pauses, "fed_mispredicts": st.fed_mispredicts, "fed_skipped": st.fed_skipped,
+                "fed_units": st.fed_units, "nofit_predicted": st.nofit_predicted,
+                "fed_last_depth": st.fed_last_depth,
+                "fed_last_sweepers": st.fed_last_sweepers}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

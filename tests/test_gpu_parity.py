@@ -372,18 +372,31 @@ SPLIT_CLUSTERS = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["split", "split-kernel-sweeps", "one-workgroup"])
+SPLIT_MODES = {
+    "split": {},
+    "split-kernel-sweeps": {"fed_kernel_sweeps": True},
+    "one-workgroup": {"no_fed_split": True},
+    # a one-XCC census (a one-XCC device or partition): the resident sweepers share the placer's XCC
+    "split-one-xcc": {"test_one_xcc": True},
+    # the speculative chain two and three units deep (kb_opts.fed_depth; the default is the driver's choice)
+    "split-depth2": {"fed_depth": 2},
+    "split-depth3": {"fed_depth": 3},
+}
+
+
+@pytest.mark.parametrize("mode", list(SPLIT_MODES))
 @pytest.mark.parametrize("name,cluster", SPLIT_CLUSTERS, ids=[c[0] for c in SPLIT_CLUSTERS])
 def test_fed_split_engine_parity(name, cluster, mode):
     """The split fed engine (n > 2048, every job one segment): a second workgroup selects each job's
     candidate nodes one job ahead, leaving out the nodes the job before may commit to, which the placer
     re-keys and merges in. Same placements, statuses and FitErrors as the oracle, and as the one-workgroup
     engine (option no_fed_split). The split engine's sweeps come from its resident sweepers (commands through a
-    pinned ring), or per job from sweep kernels (option fed_kernel_sweeps)."""
+    pinned ring) -- off the placer's XCC, or on it when the census finds one XCC only -- or per job from sweep
+    kernels (option fed_kernel_sweeps); the driver keeps two to four units in flight (fed_depth)."""
     split = mode != "one-workgroup"
     ref = pyoracle.allocate(cluster)
     snap = E.Snapshot(cluster)
-    ctx = runtime.Context(0, options={"no_fed_split": not split, "fed_kernel_sweeps": mode == "split-kernel-sweeps"})
+    ctx = runtime.Context(0, options=SPLIT_MODES[mode])
     try:
         ctx.upload(snap)
         out = ctx.allocate(snap)
@@ -391,6 +404,13 @@ def test_fed_split_engine_parity(name, cluster, mode):
     finally:
         ctx.close()
     assert st["fed_cycles"] == 1 and st["fed_split"] == (1 if split else 0)
+    assert st["fed_abandon"] == 0, st
+    if mode in ("split", "split-one-xcc", "split-depth2", "split-depth3"):
+        assert st["fed_last_sweepers"] > 0, st
+    if mode == "split-kernel-sweeps":
+        assert st["fed_last_sweepers"] == 0, st
+    if mode.startswith("split-depth"):
+        assert st["fed_last_depth"] == int(mode[-1]), st
     got = runtime.result_dict(snap, out)
     _compare(ref, got)
     assert len(got["events"]) > 0
