@@ -608,7 +608,8 @@ struct Driver {
   // 199-297), so it finds none later either, and neither does a spec of its feasibility class (kb_upload_specs: the
   // same PredicateFn inputs apart from InitResreq) whose InitResreq is at least as large in every resource
   // (resource_info.go:253-276). Such units are predicted NO_FIT with no placement, so the speculative chain behind
-  // them survives (C3: each NO_FIT job used to drain the chain). Specs with inter-pod terms (required affinity can
+  // them survives (C3: each NO_FIT job used to drain the chain). A dead spec of a parent class (kb_upload_specs: the
+  // same filters without the selector or the required node affinity) kills likewise. Specs with inter-pod terms (required affinity can
   // turn true as pods land) or host-evaluated reasons have no class. dead[c]: the minimal dead specs of class c.
   std::vector<std::vector<int>> dead;
   std::vector<int8_t> spec_dead;  // per spec: 0 unknown, 1 dead
@@ -641,11 +642,16 @@ struct Driver {
   bool is_dead(int sp) {
     if (!dead_any || !dead_eligible(sp)) return false;
     if (spec_dead[(size_t)sp]) return true;
-    for (int x : dead[(size_t)ctx->spec_fclass[sp]])
-      if (init_geq(sp, x)) {
-        spec_dead[(size_t)sp] = 1;
-        return true;
-      }
+    // its own class, then the parent classes (kb_upload_specs: fewer node filters, so a superset of its nodes)
+    for (int k = -1; k < 3; ++k) {
+      const int c = k < 0 ? ctx->spec_fclass[sp] : ctx->spec_fparent[(size_t)sp * 3 + k];
+      if (c < 0) continue;
+      for (int x : dead[(size_t)c])
+        if (init_geq(sp, x)) {
+          spec_dead[(size_t)sp] = 1;
+          return true;
+        }
+    }
     return false;
   }
 
@@ -836,6 +842,16 @@ struct Driver {
       }
     } engine{ctx};
     clk::time_point pause_t0{};
+    uint64_t pause_units = 0;  // off-engine units run since the pause began
+    // A pause ends the engine instead of resuming it once it has gone on too long (the engine's idle exit is 1 s, 10 s
+    // node-sharded). One GPU: 200 ms of wall clock. Node-sharded: every rank must end and relaunch its engine at the
+    // same unit (a relaunch bumps the exchange epoch), so the bound is a unit count, which every rank's driver sees
+    // alike -- never a rank's own clock.
+    constexpr auto kMaxPause = std::chrono::milliseconds(200);
+    constexpr uint64_t kMaxPauseUnitsSharded = 64;
+    const auto pause_over = [&]() {
+      return ctx->sharded ? pause_units >= kMaxPauseUnitsSharded : clk::now() - pause_t0 > kMaxPause;
+    };
     double fed_begin_ms = 0;
     Unit u;
     int hv;
@@ -871,7 +887,6 @@ struct Driver {
       // drained: the speculation never crosses a mode change)
       // (a unit the engine does not take pauses it: the launch paths run beside the idle engine, whose next
       // command comes fresh; a pause longer than kMaxPause ends the engine instead, before its idle exit)
-      constexpr auto kMaxPause = std::chrono::milliseconds(200);
       bool mode = u.fed;
       if (mode && engine.paused) {
         if (int rc = kb_fed_resume(ctx)) return rc;
@@ -885,10 +900,12 @@ struct Driver {
         if (int rc = kb_fed_pause(ctx)) return rc;
         engine.paused = true;
         pause_t0 = clk::now();
-      } else if (!mode && engine.paused && clk::now() - pause_t0 > kMaxPause) {
+        pause_units = 0;
+      } else if (!mode && engine.paused && pause_over()) {
         engine.on = engine.paused = false;
         if (int rc = kb_fed_end(ctx)) return rc;
       }
+      if (!mode && engine.paused) ++pause_units;
       if (!mode && !launch_pipe) {  // one kb_place_job per unit
         if (fed_allowed) ctx->stats.off_engine_units++;
         const kb_job_req req = make_req(u);
@@ -913,7 +930,10 @@ struct Driver {
       }
       while (!fl.empty()) {
         const auto c0 = clk::now();
-        for (;;) {  // top up the speculative chain
+        // (a launch-path chain during a pause stops growing once the pause is over: it drains, and the loop top
+        // ends the engine before its idle exit)
+        const bool grow = mode || !engine.paused || !pause_over();
+        for (; grow;) {  // top up the speculative chain
           const int fs = (int)fl.size() < n_slots ? free_slot() : -1;
           if (fs < 0 || !speculate(fs, mode)) break;
         }
@@ -981,7 +1001,7 @@ struct Driver {
             ctx->err = "speculative unit does not match the loop order";
             return KB_E_STATE;
           }
-        } else if (hv > 0 && nu.fed == mode) {
+        } else if (hv > 0 && nu.fed == mode && (mode || !engine.paused || !pause_over())) {
           const kb_job_req req = make_req(nu);
           const int fs = free_slot();
           if (int rc3 = kb_job_issue(ctx, &req, fs, nullptr)) return rc3;

@@ -34,6 +34,7 @@ struct kb_ctx {
   // per spec: its feasibility class (kb_upload_specs; -1: inter-pod terms, no class) and InitResreq (cpu, mem, then
   // the scalar slots; spec_init_mask the slots present): the driver's NO_FIT prediction (kbgpu_allocate.cpp)
   std::vector<int32_t> spec_fclass;
+  std::vector<int32_t> spec_fparent;  // [m][3]: the classes with the selector / required terms / both dropped (-1)
   std::vector<int64_t> spec_init;
   std::vector<uint64_t> spec_init_mask;
   int32_t n_fclass = 0;

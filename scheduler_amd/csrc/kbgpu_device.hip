@@ -3294,10 +3294,21 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       int n2 = 0, n3 = 0;
       // (slot2 < 0: the previous command was fresh, and job m-2 committed before the pause, so before this sweep;
       // its list is not this selector's to patch -- nor is it kept: slot2 names no slot)
+      // A guarded command right behind a skipped job is skipped as well (the placer's guard fails once the previous
+      // job was skipped: it leaves last_panic set). When job m-1's head already reads skipped -- the rest of a
+      // speculative chain after a misprediction -- this job publishes its command and an empty candidate list at
+      // once instead of a whole selection the placer would throw away (C3: two or three per NO_FIT the driver did
+      // not predict). Its head is loaded beside job m-2's done word: no round trip of its own.
+      const bool may_skip = cm.g_valid && slot1 >= 0;
       if (m >= 2 && slot2 >= 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int spin = 0;; ++spin) {
           const uint64_t h = x_load64(&X->p_done[r2]);
+          const uint64_t h1 = may_skip ? x_load64(&X->p_head[r1]) : 0ull;
+          if (may_skip && (uint32_t)(h1 >> 32) == m && (h1 >> 16 & 0xffffu) == kPubModeSkipped) {
+            n2 = -2;  // (job m-2 is done too: the placer published m-1 after it)
+            break;
+          }
           if ((uint32_t)(h >> 32) == m - 1) {
             n2 = (int)(uint32_t)h;
 #ifdef KB_DIAG
@@ -3316,7 +3327,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       // its rows: the main columns and the commit lists come through sc1 loads (load_row_sc1 / ld_sc1 of the placer's
       // sc1 stores); a spec with scalar or host-port columns reads those with plain loads, and after a pause the
       // launch path's kernels wrote too: then an agent acquire (~1.7 us; the host's flag, FedCmd::acq)
-      if (cm.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (cm.acq && n2 != -2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (n2 >= 0 && m >= 3 && slot3 >= 0) {  // job m-3 published before m-2 (one placer): its word is there
         const uint64_t h = x_load64(&X->p_done[r3]);
         n3 = (uint32_t)(h >> 32) == m - 2 ? (int)(uint32_t)h : -1;
@@ -3326,6 +3337,18 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       s_n3 = n3 < 0 ? 0 : n3;
     }
     __syncthreads();
+    if (s_n1 == -2) {  // skipped behind a skipped job: the command and an empty list
+      if (sel == 0 && tid < 16) tag_store(&X->s_cmd[r][tid], m + 1, ((const uint32_t*)&cm)[tid]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | 0u);
+      if (sel == 0) KB_FED_TL(m, 4);
+      slot3 = slot2;
+      slot2 = slot1;
+      slot1 = slot;
+      __syncthreads();  // cm reused by the next command
+      continue;
+    }
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
     // rows job m-2 committed (final), while job m-1 may still be choosing its set
     fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1,

@@ -557,10 +557,13 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
   // affinity terms (by content), host ports. Within a class feasibility is monotone in InitResreq
   // (resource_info.go:253-276: LessEqual per resource), and within an allocate cycle every node's Idle, Releasing,
   // pod count and used ports only move toward failure, so a spec that found no node stays without one, and so does
-  // every spec of its class whose request is at least as large in every resource.
+  // every spec of its class whose request is at least as large in every resource. A class's parents are the classes
+  // of the same signature with its nodeSelector and / or its required node affinity dropped (predicates.go:
+  // PodMatchNodeSelector ANDs both): a parent's feasible nodes are a superset, so a dead parent spec kills too.
   {
     std::unordered_map<std::string, int32_t> ids;
     c->spec_fclass.assign(in->m, -1);
+    c->spec_fparent.assign((size_t)in->m * 3, -1);
     c->spec_init.assign((size_t)in->m * (2 + S), 0);
     c->spec_init_mask.assign(in->m, 0);
     std::string k;
@@ -574,21 +577,42 @@ int kb_upload_specs(kb_ctx* c, const kb_specs* in) {
         put(in->vals + r.val_off, 4 * (size_t)r.val_cnt);
       }
     };
+    // the signature with the selector (drop & 1) and / or the required terms (drop & 2) left out
+    auto sig = [&](const kb_spec& q, int drop) {
+      k.clear();
+      uint32_t fl = q.flags;
+      if (drop & 1) fl &= ~KB_SPEC_HAS_SELECTOR;
+      if (drop & 2) fl &= ~KB_SPEC_HAS_REQUIRED;
+      put(&fl, 4), put(&q.tol_set, 4);
+      if (fl & KB_SPEC_HAS_SELECTOR) put_term(q.sel_term);
+      const uint32_t nreq = (fl & KB_SPEC_HAS_REQUIRED) ? q.req_term_cnt : 0u;
+      put(&nreq, 4);
+      for (uint32_t t = 0; t < nreq; ++t) put_term(q.req_term_off + t);
+      put(&q.port_cnt, 4);
+      put(in->ports + q.port_off, sizeof(kb_port) * (size_t)q.port_cnt);
+      return k;
+    };
+    auto eligible = [](const kb_spec& q) {
+      return !((q.flags & (KB_SPEC_POD_AFFINITY | KB_SPEC_IPA_ERROR)) || q.aff_class >= 0);
+    };
     for (uint32_t i = 0; i < in->m; ++i) {
       const kb_spec& q = in->specs[i];
       int64_t* v = c->spec_init.data() + (size_t)i * (2 + S);
       v[0] = q.init_cpu, v[1] = q.init_mem;
       for (uint32_t r = 0; r < S; ++r) v[2 + r] = in->sc_init[(size_t)i * S + r];
       c->spec_init_mask[i] = q.init_sc_mask;
-      if ((q.flags & (KB_SPEC_POD_AFFINITY | KB_SPEC_IPA_ERROR)) || q.aff_class >= 0) continue;
-      k.clear();
-      put(&q.flags, 4), put(&q.tol_set, 4);
-      if (q.flags & KB_SPEC_HAS_SELECTOR) put_term(q.sel_term);
-      put(&q.req_term_cnt, 4);
-      for (uint32_t t = 0; t < q.req_term_cnt; ++t) put_term(q.req_term_off + t);
-      put(&q.port_cnt, 4);
-      put(in->ports + q.port_off, sizeof(kb_port) * (size_t)q.port_cnt);
-      c->spec_fclass[i] = ids.emplace(k, (int32_t)ids.size()).first->second;
+      if (!eligible(q)) continue;
+      c->spec_fclass[i] = ids.emplace(sig(q, 0), (int32_t)ids.size()).first->second;
+    }
+    for (uint32_t i = 0; i < in->m; ++i) {
+      const kb_spec& q = in->specs[i];
+      if (!eligible(q)) continue;
+      for (int drop = 1; drop <= 3; ++drop) {
+        if (((drop & 1) && !(q.flags & KB_SPEC_HAS_SELECTOR)) || ((drop & 2) && !(q.flags & KB_SPEC_HAS_REQUIRED)))
+          continue;  // (the same signature)
+        const auto it = ids.find(sig(q, drop));
+        if (it != ids.end()) c->spec_fparent[(size_t)i * 3 + (drop - 1)] = it->second;
+      }
     }
     c->n_fclass = (int32_t)ids.size();
   }

@@ -231,3 +231,71 @@ def test_peer_preflight_fails_loudly(world):
         assert got[r] is not None, f"rank {r} passed the pre-flight"
         code, msg = got[r]
         assert code == runtime.KB_E_STATE and "pre-flight" in msg and "from rank 1" in msg, (r, msg)
+
+
+def _mixed_rank_main(rank, world, port, q, cluster):
+    import torch
+    import torch.distributed as dist
+    from scheduler_amd import export as E
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.tolist()) for o in outs)
+    try:
+        snap = E.Snapshot(cluster)
+        ctx = runtime.Context(0)
+        try:
+            ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
+            ctx.upload(snap)
+            out = []
+            for _ in range(2):
+                ctx.restore()
+                dist.barrier()
+                r = runtime.result_dict(snap, ctx.allocate(snap))
+                out.append({k: r[k] for k in ("events", "binds", "fit_errors")})
+            st = ctx.stats()
+        finally:
+            ctx.close()
+        q.put((rank, (out, st["fed_sharded"], st["fed_pauses"], st["off_engine_units"], st["fed_abandon"]), None))
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_engine_mixed_cycle_two_ranks():
+    """A node-sharded mixed cycle (C2M shape: two-template jobs, which stay on the engine as units, and jobs with
+    required anti-affinity over hostname, which pause every rank's engine and run through the host-staged exchange):
+    both ranks equal the oracle, twice, and every rank pauses at the same units -- the pause's bound is a unit
+    count, not a rank's own clock, so no rank relaunches its engine (a new exchange epoch) while a peer resumes."""
+    import torch.multiprocessing as mp
+    from oracle import pyoracle
+    world = 2
+    cl = synth.c2m(n_nodes=2100 * world + 300, n_jobs=50, tasks_per_job=30, seed=62, frac_multi=0.15, frac_aff=0.2)
+    ref = pyoracle.allocate(cl)
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_mixed_rank_main, args=(r, world, port, q, cl)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, f"rank {rank}: {err}"
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        out, n_sharded, n_pauses, n_off, n_abandon = got[r]
+        assert n_abandon == 0 and n_sharded >= 2 and n_off > 0, (r, n_sharded, n_pauses, n_off)
+        assert (n_sharded, n_pauses, n_off) == got[0][1:4], (r, got[r][1:], got[0][1:])
+        for c in out:
+            for k in ("events", "binds", "fit_errors"):
+                assert c[k] == ref[k], (r, k)
