@@ -425,6 +425,9 @@ int kb_restore_nodes(kb_ctx* ctx);
 /* ABI 15, tests only: the split engine's census reads every workgroup as on the placer's XCC (a one-XCC device or
  * partition), so its resident sweepers share that XCC */
 #define KB_OPT_TEST_ONE_XCC (1u << 18)
+/* ABI 15: the split engine without the resident sweepers' level records (the placer computes every e-sequence level
+ * itself, round 5's path); A/B only */
+#define KB_OPT_FED_NO_LEVELS (1u << 19)
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2

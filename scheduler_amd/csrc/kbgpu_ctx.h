@@ -147,6 +147,7 @@ struct kb_ctx {
   // read back by the host when job i is issued (two slots), so the sweep needs no stream dependency; the
   // place kernel waits on sweep_ctr[slot] reaching sweep_target[slot] (device counter, no events).
   uint32_t* sel_keys[kbgpu::kJobSlots] = {};
+  uint32_t* sel_lvl[kbgpu::kJobSlots] = {};  // the resident sweepers' level records (kb_fed_begin, lazily)
   uint64_t* sel_stat[kbgpu::kJobSlots] = {};
   int32_t* commits[kbgpu::kJobSlots] = {};
   int32_t sel_n = -1;       // node count the per-slot buffers were sized for
@@ -186,9 +187,11 @@ struct kb_ctx {
   // tags fed_epoch << 32 | fed_m + 1) instead of a sweep kernel per job; KB_OPT_FED_KERNEL_SWEEPS turns them off
   bool fed_kernel_sweeps = false, fed_sweepers_now = false;
   bool test_one_xcc = false;  // KB_OPT_TEST_ONE_XCC
+  bool no_lvl = false;        // KB_OPT_FED_NO_LEVELS
   void* fed_hring = nullptr;      // pinned host ring (kJobSlots FedHostCmd)
   void* fed_hring_dev = nullptr;  // its device address
   uint32_t fed_epoch = 0, fed_m = 0;
+  uint32_t fed_cmd_m = 0, fed_fresh_m = 0;  // commands posted this launch; the last fresh one's index (FedCmd::fresh_m)
   // tests only (kb_opts.test_stall_job / test_stall_ms): kb_allocate's driver sleeps before
   // finishing job test_stall_job, a host stall longer than the engine's idle bound
   int64_t test_stall_job = -1;

@@ -197,6 +197,7 @@ struct FedCmdArgs {
   uint32_t seq;
   int32_t fresh = 0;  // the first command after a pause (FedCmd::fresh)
   int32_t acq = 0;    // FedCmd::acq
+  int32_t fresh_m = 0;  // FedCmd::fresh_m (fed_post fills it in)
 };
 
 // Selection path (kbgpu_device.hip): the run's tasks as a parallel top-T selection over the level-0
@@ -243,7 +244,11 @@ struct FedSlotPtrs {
   JobState* js[kJobSlots];
   JobState* hjs[kJobSlots];
   int32_t* hout[kJobSlots];
+  uint32_t* lvl[kJobSlots];  // the resident sweepers' level records per slot (kLvlW words per node), nullptr: none
 };
+// the split engine's level records (kbgpu_device.hip fed_sweeper): a node's keys after 1..kPreLevels commits, then A
+constexpr int kPreLevels = 7;
+constexpr int kLvlW = 8;
 size_t fed_ring_bytes();
 bool fed_fits(int n);  // the engine's LDS plan fits n nodes
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,

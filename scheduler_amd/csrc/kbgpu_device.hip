@@ -1186,7 +1186,7 @@ __device__ __forceinline__ int allocs_before_full(const DevNodes& N, const kb_sp
 // Full 64-bit key of node n after j commits of the spec (A allocations at most, the rest pipelined).
 // INV: the score from the node's reciprocal capacities ic / im (row_score_inv: the same value).
 template <bool INV = false>
-__device__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
+__device__ __forceinline__ uint64_t traj_key64(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
                                const int64_t* sci, const int64_t* scr, const Row& r0, uint64_t st, int n, int j,
                                int A, double ic = 0.0, double im = 0.0) {
   const int64_t a = j < A ? j : A;
@@ -1918,7 +1918,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
                                         int& placed, int& stop, int& fail_task, int& panic, int& stopped,
                                         int32_t* hout, JobState* js, JobState* hjs, int& rp,
                                         ShardRec* rec, int32_t* commit_out SEL_DIAG_PARAMS,
-                                        FedPub pub = FedPub{}, uint32_t* pl = nullptr) {
+                                        FedPub pub = FedPub{}, uint32_t* pl = nullptr, const uint32_t* clv = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = N.n;
   const int Q4 = QN > 0 ? QN : (n + 4 * kSelThreads - 1) / (4 * kSelThreads);
@@ -2015,13 +2015,39 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         // S == T theta0 is the least of them), so the first round starts at level 1 and covers one level more per
         // node -- fewer jobs need a second round
         if (tid < (int)S) {
-          cand[sh.off[tid]] = ((uint64_t)sh.key0[tid] << 14) | ((uint64_t)(127 - tid) << 7) | 127u;
-          sh.cnt[tid] = 1;
-          sh.emin[tid] = sh.key0[tid];
-          sh.gen[tid] = 1;
-          if (sh.lmax[tid] <= 1) sh.done[tid] = 1;
+          const int lm = sh.lmax[tid];
+          uint32_t e = sh.key0[tid];
+          cand[sh.off[tid]] = ((uint64_t)e << 14) | ((uint64_t)(127 - tid) << 7) | 127u;
+          int c = 1, g = 1, dn = lm <= 1;
+          const uint64_t ci = clv != nullptr ? sh.comp[tid] : 0ull;
+          if (ci != 0 && !dn) {
+            // levels 1.. from the sweep's record (clv, the same closed-form keys the rounds below compute): the
+            // prefix minimum while it stays feasible and above the cut-off, as a round would take them
+            const uint4* lr = (const uint4*)(clv + (ci - 1) * kLvlW);
+            const uint4 a = lr[0], b = lr[1];
+            const uint32_t lv[kPreLevels] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z};
+            const int jm = lm < kPreLevels + 1 ? lm : kPreLevels + 1;
+            const uint32_t th = cut0 ? sh.theta0 : 0u;
+            int j = 1;
+#pragma unroll
+            for (int q = 0; q < kPreLevels; ++q) {
+              if (j != q + 1 || j >= jm) continue;  // (stopped)
+              const uint32_t ee = lv[q] < e ? lv[q] : e;
+              if (!(ee >> 31) || ee < th) continue;
+              cand[sh.off[tid] + c] = ((uint64_t)ee << 14) | ((uint64_t)(127 - tid) << 7) | (uint64_t)(127 - j);
+              ++c;
+              e = ee;
+              ++j;
+            }
+            g = j;
+            dn = j < jm || j >= lm;
+          }
+          sh.cnt[tid] = c;
+          sh.emin[tid] = e;
+          sh.gen[tid] = g;
+          if (dn) sh.done[tid] = 1;
         }
-        if (wv == 0) {  // the first round's active list beside it (active: lmax > 1), under the same barrier
+        if (wv == 0 && clv == nullptr) {  // the first round's active list beside it (active: lmax > 1), under the same barrier
           const bool a0 = lane < (int)S && sh.lmax[lane] > 1;
           const bool a1 = lane + 64 < (int)S && sh.lmax[lane + 64] > 1;
           const uint64_t m0 = __ballot(a0), m1 = __ballot(a1);
@@ -2033,7 +2059,8 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         __syncthreads();
       }
       KB_SEL_PH(2);
-      for (bool first = CAND;; first = false) {
+      // (with level records the first round's active list needs the emission's done flags: built in the loop)
+      for (bool first = CAND && clv == nullptr;; first = false) {
         if (!first) {
           if (wv == 0) {
             const bool a0 = lane < (int)S && !sh.done[lane];
@@ -2614,7 +2641,7 @@ struct FedCmd {
                   // own bookkeeping (the previous jobs' sets, rows and commit lists) does not know: none is used
   int32_t acq;    // the job reads global columns the selection path stores plain (a spec with scalar or host-port
                   // columns), or follows a pause: the selector and the placer take an agent acquire before it
-  int32_t pad;
+  int32_t fresh_m;  // the launch's most recent fresh command at or before this one: every earlier command is final
 };
 static_assert(sizeof(FedCmd) == 64, "the split engine's selector forwards commands as 8 words");
 
@@ -2991,6 +3018,11 @@ bool sel_aff_pl_fits(int n, int t_count) {
 // ===========================================================================
 
 constexpr int kFedGridMax = 256;
+// Level records (split engine with resident sweepers): for every feasible node the sweep also computes its keys after
+// 1..kPreLevels commits of the job's spec (traj_key64, the e-sequences' levels) and A (allocs_before_full), kLvlW words
+// per node; the selector forwards them with its candidates, so the placer's first e-sequence round is a prefix
+// minimum over loaded values instead of kPreLevels closed-form keys per slot on its critical chain.
+// (kPreLevels, kLvlW: kbgpu_device.h)
 // a selector entry's first word: key (bits 0..31), node (32..55: the split engine's tables are below 2^24 nodes,
 // kFedMaxSel * kFedSelNodes), the node's rank among the list's first T (56..62)
 constexpr uint64_t kEntNodeMask = 0xffffffull;  // the split engine's grid: placer, selectors, resident sweepers (one per CU)
@@ -3003,6 +3035,9 @@ struct FedSlots {
   JobState* hjs[kJobSlots];  // pinned host job state per slot (device addresses)
   int32_t* hout[kJobSlots];  // pinned host placements per slot (device addresses)
   uint32_t tgt[kJobSlots];   // ring counters' targets at launch
+  // the resident sweepers' level records per slot ([n][kLvlW]: the node's keys after 1..kPreLevels commits, then A),
+  // nullptr when the sweeps come from sweep kernels (no records)
+  uint32_t* lvl[kJobSlots];
 };
 
 // A command without a sweep (EXIT): the ring entry and the whole block count at once.
@@ -3038,37 +3073,48 @@ __global__ __launch_bounds__(64) void fed_cmd_sweep_kernel(DevNodes N, DevSpecs 
 // count to the ring counter the selector waits on -- the count the sweep kernel's blocks gave. Sweeper 0 also
 // writes the command into the device ring (before its release). EXIT ends the loop after its count; a sweeper
 // leaves too when the engine's exit flag is set or no command comes within idle_ticks.
-__device__ void fed_sweeper(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlots& S,
+// Groups: the sweepers form kSweepGroups groups that take the commands in turn (command m: group m % G), each sweeping
+// the whole table with its own members, so a group has G job times for a sweep -- one sweep's latency chain (the
+// relay, the acquire, the row loads, the level records, the release) is longer than one placer job (r06f: with the
+// level records one group fell behind the placer, the selector's commands came 6 us later). Each group's first member
+// polls the host ring for its commands and relays them; the group that takes EXIT raises sw_exit for the others.
+constexpr int kSweepGroups = 2;
+__device__ __forceinline__ void fed_sweeper(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, const FedSlots& S,
                             const FedHostCmd* hring, uint32_t epoch, FedCmd* ring, uint32_t* ctr,
                             uint64_t idle_ticks, int32_t* exit_flag, int sw, int nsw, uint64_t* relay_cmd,
-                            uint64_t* relay_go) {
+                            uint64_t* relay_go, uint32_t* sw_exit) {
+  static_assert(kJobSlots % kSweepGroups == 0, "a ring entry belongs to one sweeper group");
   __shared__ FedCmd s_cmd;
   __shared__ int32_t s_go;
   const int tid = threadIdx.x;
+  const int G = nsw >= 2 * kSweepGroups ? kSweepGroups : 1;
+  const int g = sw % G, sg = sw / G, ng = (nsw - g + G - 1) / G;  // group, index in it, its members
   const uint32_t B = (uint32_t)((N.n + 63) / 64);
-  const uint32_t b0 = (uint32_t)((uint64_t)sw * B / (uint32_t)nsw), b1 = (uint32_t)((uint64_t)(sw + 1) * B / (uint32_t)nsw);
+  const uint32_t b0 = (uint32_t)((uint64_t)sg * B / (uint32_t)ng), b1 = (uint32_t)((uint64_t)(sg + 1) * B / (uint32_t)ng);
   const int n0 = (int)b0 * 64, n1 = min((int)b1 * 64, N.n);
-  for (uint32_t m = 0;; ++m) {
+  const bool lead = sg == 0;
+  for (uint32_t m = (uint32_t)g;; m += (uint32_t)G) {
     const int r = (int)(m % (uint32_t)kJobSlots);
     if (tid == 0) {
       const uint64_t want = ((uint64_t)epoch << 32) | (uint64_t)(m + 1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       int go = 0;
-      // sweeper 0 polls the pinned ring over the bus; the others poll its relay in device memory (one bus reader)
-      const uint64_t* tagp = sw == 0 ? &hring[r].tag : &relay_go[r];
+      // the group's first member polls the pinned ring over the bus; the others poll its relay in device memory
+      const uint64_t* tagp = lead ? &hring[r].tag : &relay_go[r];
       for (;;) {
-        if (__hip_atomic_load(tagp, __ATOMIC_RELAXED, sw == 0 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT) ==
+        if (__hip_atomic_load(tagp, __ATOMIC_RELAXED, lead ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT) ==
             want) {
           go = 1;
           break;
         }
         if (__hip_atomic_load(exit_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        if (__hip_atomic_load(sw_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
         __builtin_amdgcn_s_sleep(2);
       }
       if (go) {  // the words stored before the tag
         uint64_t w[8];
-        if (sw == 0) {
+        if (lead) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) w[q] = __hip_atomic_load(&hring[r].w[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
@@ -3095,21 +3141,37 @@ __device__ void fed_sweeper(const DevNodes& N, const DevSpecs& P, const DevCfg& 
       uint32_t* keys32 = S.keys[cm.slot];
       uint64_t* stat = S.stat[cm.slot];
       const int64_t* sci = P.sc_init + (size_t)cm.spec * N.S;
+      uint32_t* lvl = S.lvl[cm.slot];
+      const int64_t* scr = P.sc_req + (size_t)cm.spec * N.S;
       for (int n = n0 + tid; n < n1; n += kSelThreads) {
         const Row rw = load_row(N, n);
         const uint64_t st = static_eval<false>(N, P, C, sp, cm.spec, rw.flags, n, P.A.mm);
         stat[n] = st;
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, n);
         keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rw, st), n), n + N.base, idx_bits);
+        if (lvl != nullptr && rs == 0) {  // (an infeasible node is never a candidate: no record)
+          // the e-sequence levels exactly as sel_run computes them (same row, static cache, A and reciprocals)
+          // (one level at a time, each stored as it comes: the sweeper role must not raise the kernel's register
+          // count, which the placer's chain pays for)
+          const int A = allocs_before_full(N, sp, sci, scr, rw, n);
+          const double ic = 1.0 / (double)rw.alloc_cpu, im = 1.0 / (double)rw.alloc_mem;
+          uint32_t* o = lvl + (size_t)n * kLvlW;
+#pragma unroll 1
+          for (int j = 1; j <= kPreLevels; ++j)
+            o[j - 1] = compress_key(traj_key64<true>(N, P, C, sp, sci, scr, rw, st, n, j, A, ic, im), n + N.base,
+                                    idx_bits);
+          o[kLvlW - 1] = (uint32_t)A;
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      if (sw == 0) ring[r] = cm;
+      if (lead) ring[r] = cm;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(&ctr[r], b1 - b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cm.op != KB_ENG_RUN && lead) __hip_atomic_store(sw_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (cm.op != KB_ENG_RUN) return;
     __syncthreads();  // (s_cmd / s_go are rewritten by the next poll)
@@ -3128,6 +3190,8 @@ constexpr int32_t kSelExit = -3;  // selector -> placer: the command was EXIT
 // workgroup each (grid 1 + nsel): each publishes the T best of its range, and the placer merges the lists. Every
 // range is a multiple of 4 nodes (16-byte key loads) and holds at most kFedSelNodes keys.
 constexpr int kFedMaxSel = 4;
+constexpr int kFedParity = 2;  // selector workgroups per node range, taking the jobs in turn (fed_selector)
+constexpr int kEntWords = 2 + (int)(sizeof(Row) / 8) + 4;  // a selector entry: key/node, static cache, row, levels
 constexpr int kFedSelQ = 10;                          // key groups per thread of a range selector
 constexpr int kFedSelNodes = 4 * kSelThreads * kFedSelQ;  // 20480
 static_assert((uint64_t)kFedMaxSel * kFedSelNodes <= kEntNodeMask, "selector entries pack the node in 24 bits");
@@ -3155,7 +3219,9 @@ struct FedXchg {
   uint64_t s_cmd[kJobSlots][16];     //   (selector 0) the job's command (FedCmd), one tagged word per field
   // selector k's candidates in key order (descending), word-major so that a wave's stores and loads of one word
   // are contiguous: [0] key | node << 32, [1] static cache, [2..] the row
-  uint64_t s_ent[kJobSlots][kFedMaxSel][2 + sizeof(Row) / 8][128];
+  // [2 + Row/8 ..] the entry's level record: levels 1..kPreLevels (two per word), the last word's high half 1 when
+  // the record is valid (the node's row is the sweep's: not on the commit lists the selector patched)
+  uint64_t s_ent[kJobSlots][kFedMaxSel][kEntWords][128];
   // (selector 0) the static cache of job m-1's set S(m-1) in its slot order (the placer's B candidates), from
   // job m's sweep: the placer reads it here, behind the head, instead of from the sweep's buffer -- which would
   // need an agent-scope acquire per job on the placer's CU (~1.7 us, MI355X_MICROARCH.md)
@@ -3170,6 +3236,8 @@ struct FedXchg {
   // resident sweepers: sweeper 0 relays each host command (its eight words sc1, then the tag) to the others
   uint64_t sw_cmd[kJobSlots][8];
   uint64_t sw_go[kJobSlots];
+  uint32_t sw_exit;  // the sweeper group that took EXIT tells the other groups
+  uint32_t sel_exit;  // the parity selector that took EXIT tells the other
   uint64_t wdiag[8];                  // KB_DIAG builds: the placer's fine sel_run stamps (dg[8..15])
   uint32_t census_n;                  // place_xcc: workgroups counted in (agent-scope atomic add)
   uint32_t census_xcc[kFedGridMax];   //   each workgroup's XCC id + 1
@@ -3196,9 +3264,10 @@ __device__ __forceinline__ bool fed_wait_word(const uint32_t* w, uint32_t want, 
 
 // Re-key the rows on two commit lists (n0 entries of l0, then n1 of l1) for `spec` into k32 (positions node - base;
 // nodes outside [base, base + nk) are another selector's). Ends after a barrier.
+// pbits (LDS, nk bits, zeroed; nullptr: none): marks every re-keyed node, whose level record is stale.
 __device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, const DevSpecs& P, const DevCfg& C, const kb_spec& sp,
                           int spec, const uint64_t* stat, int idx_bits, const int32_t* l0, int n0, const int32_t* l1,
-                          int n1, int base, int nk) {
+                          int n1, int base, int nk, uint32_t* pbits = nullptr) {
   const int np = n0 + n1;
   const int64_t* sci = P.sc_init + (size_t)spec * N.S;
   for (int i = threadIdx.x; i < np; i += kSelThreads) {
@@ -3209,18 +3278,33 @@ __device__ __forceinline__ void fed_patch(uint32_t* k32, const DevNodes& N, cons
     const uint64_t st = stat[w];
     const uint32_t rs = row_reasons(N, P, C, sp, sci, rr, st, w);
     k32[w - base] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st), w), w + N.base, idx_bits);
+    if (pbits != nullptr) atomicOr(&pbits[(w - base) >> 5], 1u << ((w - base) & 31));
   }
   __syncthreads();
 }
 
 // Thread 0: wait for ring entry r's command and keys (acquire), bounded by idle_ticks; s_op = its op.
+// done (the split engine's parity selectors): a word another selector sets when it took EXIT -- this one's next command
+// never comes; it leaves as if EXIT had (s_op KB_ENG_EXIT without a command).
 __device__ __forceinline__ void fed_wait_cmd(const uint32_t* ctr, uint32_t tgt, const FedCmd* ring, FedCmd& cm,
-                                             int32_t& s_op, uint64_t idle_ticks, int32_t* exit_flag) {
+                                             int32_t& s_op, uint64_t idle_ticks, int32_t* exit_flag,
+                                             const uint32_t* done = nullptr) {
   if (threadIdx.x == 0) {
     int op = KB_ENG_EXIT_IDLE;
-    if (fed_wait_word(ctr, tgt, idle_ticks)) {
-      cm = *ring;
-      op = cm.op;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (v - tgt <= 0x7fffffffu) {
+        cm = *ring;
+        op = cm.op;
+        break;
+      }
+      if (done != nullptr && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        op = -KB_ENG_EXIT;  // (another selector's EXIT)
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+      __builtin_amdgcn_s_sleep(1);
     }
     s_op = op;
     if (op == KB_ENG_EXIT_IDLE) atomicMax(exit_flag, 1);
@@ -3236,13 +3320,14 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
                                              const FedSlots& S, const FedCmd* ring, const uint32_t* ctr,
                                              uint64_t idle_ticks, int32_t* exit_flag, FedXchg* X, uint32_t* k32,
                                              SelShared& sh, FedCmd& cm, int32_t& s_op, int32_t& s_n1, int sel,
-                                             int nsel, uint32_t* scratch) {
+                                             int nsel, uint32_t* scratch, int par) {
   const int tid = threadIdx.x;
   // candidate lists (scratch: 4 x 256 words of the candidate space, unused by a selector): by position, by rank
   int32_t* cnode = (int32_t*)scratch;
   uint32_t* ckey = scratch + 256;
   int32_t* rnode = (int32_t*)scratch + 512;
   uint32_t* rkey = scratch + 768;
+  uint32_t* pbits = scratch + 1024;  // the nodes fed_patch re-keyed this job (their level records are stale)
   const int chunk = fed_sel_chunk(N.n, nsel);
   const int base = sel * chunk;
   const int n = N.n - base < chunk ? N.n - base : chunk;  // this selector's nodes
@@ -3252,8 +3337,7 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
   uint32_t tgt[kJobSlots];
 #pragma unroll
   for (int k = 0; k < kJobSlots; ++k) tgt[k] = S.tgt[k];
-  int slot3 = -1, slot2 = -1, slot1 = -1;  // slots of jobs m-3, m-2, m-1
-  __shared__ int32_t s_n3;
+  __shared__ int32_t s_n3, s_ns2, s_ns3;
   int rp = 0;
 #ifdef KB_DIAG
   // [0] wait for the command, [1] key load, [3] wait for job m-2 + patch, [2] wait for job m-1's set +
@@ -3266,21 +3350,33 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
   do {               \
   } while (0)
 #endif
-  uint32_t m = 0;
-  for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
+  // Parity selectors: two selector workgroups per node range take the jobs in turn (this one: m = par, par + 2, ...),
+  // so each has two placer jobs of time for its own chain (keys, patches, selection, exclusion, publication), and
+  // the selection of job m starts as soon as job m-2 is done, not when job m-1's selection is. Jobs they did not
+  // select themselves are known through the placer's tagged words (sets, done words): nothing per job is kept here.
+  uint32_t m = (uint32_t)par;
+  for (int r = par;; r = (r + kFedParity) % kJobSlots, m += kFedParity) {
     tgt[r] += blocks;
-    fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag);
+    fed_wait_cmd(&ctr[r], tgt[r], &ring[r], cm, s_op, idle_ticks, exit_flag, &X->sel_exit);
     KB_SSTAMP(0);
     if (sel == 0) KB_FED_TL(m, 0);
     if (s_op != KB_ENG_RUN) {
-      if (s_op == KB_ENG_EXIT && tid == 0 && sel == 0)  // the placer takes EXIT from here
-        x_store64(&X->s_head[r][0], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
+      if (s_op == KB_ENG_EXIT && tid == 0) {
+        if (sel == 0)  // the placer takes EXIT from here
+          x_store64(&X->s_head[r][0], ((uint64_t)(m + 1) << 32) | (uint32_t)kSelExit);
+        __hip_atomic_store(&X->sel_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (the other parity)
+      }
       break;
     }
     const int slot = cm.slot, spec = cm.spec;
-    const bool fresh = cm.fresh != 0;  // (every earlier job is final: nothing to patch, no set to leave out)
-    if (fresh) slot3 = slot2 = slot1 = -1;
+    // the jobs before the launch's last fresh command (the first after a pause, at or before this one) are final: their
+    // commits predate this sweep -- nothing to patch, no set to leave out
+    const uint32_t fm = (uint32_t)cm.fresh_m;
+    const bool has1 = m >= 1 && m - 1 >= fm, has2 = m >= 2 && m - 2 >= fm, has3 = m >= 3 && m - 3 >= fm;
     load_keys_lds<(QN > 0 ? QN : kSelQ4)>(k32, S.keys[slot] + base, n, n_pad);
+    const uint32_t* lvl = S.lvl[slot];
+    if (lvl != nullptr)
+      for (int i = tid; i < (n + 31) >> 5; i += kSelThreads) pbits[i] = 0u;
     __syncthreads();
     KB_SSTAMP(1);
     const int r1 = r == 0 ? kJobSlots - 1 : r - 1;
@@ -3289,18 +3385,94 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     const kb_spec sp = P.specs[spec];
     const uint64_t* stat = S.stat[slot];
     // The host issues job m once job m - kJobSlots is read, so its sweep may predate the commits of jobs m-3, m-2
-    // and m-1: the placer re-keys m-1's set (B), this selector the rows m-2 and m-3 committed.
-    if (tid == 0) {  // jobs m-2 (and so m-3) done: their commit counts, after their rows were written back
-      int n2 = 0, n3 = 0;
-      // (slot2 < 0: the previous command was fresh, and job m-2 committed before the pause, so before this sweep;
-      // its list is not this selector's to patch -- nor is it kept: slot2 names no slot)
+    // and m-1: the placer re-keys m-1's set (B), this selector the rows m-3 and m-2 committed. Job m-3's are final
+    // long before this selector needs them (patched from its commit list first, off the critical path). Job m-2's
+    // commits come from its selected set S(m-2) -- published at its start, and seen here as job m-1's set -- so the
+    // set's static caches for this job are loaded before m-2 ends, and after its done word only the rows' loads and
+    // the keys remain (every node of the set re-keyed: an unchanged row gives its unchanged key). That chain, from
+    // m-2's done word to this selection, was the engine's critical loop (r06g: 5 us of patch after the done word).
+    if (tid == 0) {
+      int n3 = 0, ns2 = 0, ns3 = 0;
+      if (has3) {  // job m-3 done
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const uint64_t h = x_load64(&X->p_done[r3]);
+          if ((uint32_t)(h >> 32) == m - 2) {
+            n3 = (int)(uint32_t)h;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            n3 = -1;
+            atomicMax(exit_flag, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (n3 >= 0 && has3) {  // S(m-3): its head (published before its done word)
+        const uint64_t h = x_load64(&X->p_head[r3]);
+        ns3 = (uint32_t)(h >> 32) == m - 2 && (h >> 16 & 0xffffu) == kPubModeSet ? (int)(h & 0xffffu) : 0;
+        if ((uint32_t)(h >> 32) != m - 2) n3 = -1;  // (cannot happen)
+      }
+      if (n3 >= 0 && has2) {  // S(m-2): its head
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const uint64_t h = x_load64(&X->p_head[r2]);
+          if ((uint32_t)(h >> 32) == m - 1) {
+            ns2 = (h >> 16 & 0xffffu) == kPubModeSet ? (int)(h & 0xffffu) : 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            n3 = -1;
+            atomicMax(exit_flag, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      // the rows' main columns and the commit lists come through sc1 loads (load_row_sc1 / ld_sc1 of the placer's sc1
+      // stores); a spec with scalar or host-port columns reads those with plain loads, and after a pause the launch
+      // path's kernels wrote too: then an agent acquire (~1.7 us; the host's flag, FedCmd::acq) -- here for m-3's
+      // rows, and again below for m-2's
+      if (cm.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      s_n3 = n3;
+      s_ns2 = ns2;
+      s_ns3 = ns3;
+    }
+    __syncthreads();
+    if (s_n3 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
+    // this thread's node of S(m-2) / S(m-3) in this selector's range, and its static cache for this job (the sets'
+    // words: tagged, the heads stored after them)
+    int w2 = -1, w3 = -1;
+    uint64_t st2 = 0, st3 = 0;
+    if (tid < s_ns2) {
+      const uint64_t e = x_load64(&X->p_node[r2][tid]);
+      if ((uint32_t)(e >> 32) != m - 1) atomicMax(exit_flag, 2);  // (cannot happen: the head is stored last)
+      else if ((uint32_t)e - (uint32_t)base < (uint32_t)n) w2 = (int)(uint32_t)e;
+    }
+    if (tid < s_ns3) {
+      const uint64_t e = x_load64(&X->p_node[r3][tid]);
+      if ((uint32_t)(e >> 32) != m - 2) atomicMax(exit_flag, 2);
+      else if ((uint32_t)e - (uint32_t)base < (uint32_t)n) w3 = (int)(uint32_t)e;
+    }
+    if (w2 >= 0) st2 = stat[w2];
+    if (w3 >= 0) {  // S(m-3) re-keyed from its final rows (job m-3 is done)
+      st3 = stat[w3];
+      const Row rr = load_row_sc1(N, w3);
+      const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, rr, st3, w3);
+      k32[w3 - base] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st3), w3), w3 + N.base, idx_bits);
+      if (lvl != nullptr) atomicOr(&pbits[(w3 - base) >> 5], 1u << ((w3 - base) & 31));
+    }
+    __syncthreads();
+    if (tid == 0) {  // job m-2 done: its rows are written back
+      int n2 = 0;
       // A guarded command right behind a skipped job is skipped as well (the placer's guard fails once the previous
       // job was skipped: it leaves last_panic set). When job m-1's head already reads skipped -- the rest of a
       // speculative chain after a misprediction -- this job publishes its command and an empty candidate list at
       // once instead of a whole selection the placer would throw away (C3: two or three per NO_FIT the driver did
       // not predict). Its head is loaded beside job m-2's done word: no round trip of its own.
-      const bool may_skip = cm.g_valid && slot1 >= 0;
-      if (m >= 2 && slot2 >= 0) {
+      const bool may_skip = cm.g_valid && has1;
+      if (has2) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int spin = 0;; ++spin) {
           const uint64_t h = x_load64(&X->p_done[r2]);
@@ -3324,17 +3496,8 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
           __builtin_amdgcn_s_sleep(1);
         }
       }
-      // its rows: the main columns and the commit lists come through sc1 loads (load_row_sc1 / ld_sc1 of the placer's
-      // sc1 stores); a spec with scalar or host-port columns reads those with plain loads, and after a pause the
-      // launch path's kernels wrote too: then an agent acquire (~1.7 us; the host's flag, FedCmd::acq)
-      if (cm.acq && n2 != -2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (n2 >= 0 && m >= 3 && slot3 >= 0) {  // job m-3 published before m-2 (one placer): its word is there
-        const uint64_t h = x_load64(&X->p_done[r3]);
-        n3 = (uint32_t)(h >> 32) == m - 2 ? (int)(uint32_t)h : -1;
-        if (n3 < 0) atomicMax(exit_flag, 2);  // (cannot happen)
-      }
-      s_n1 = n3 < 0 ? -1 : n2;
-      s_n3 = n3 < 0 ? 0 : n3;
+      if (cm.acq && n2 >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      s_n1 = n2;
     }
     __syncthreads();
     if (s_n1 == -2) {  // skipped behind a skipped job: the command and an empty list
@@ -3343,16 +3506,17 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       __syncthreads();
       if (tid == 0) x_store64(&X->s_head[r][sel], ((uint64_t)(m + 1) << 32) | 0u);
       if (sel == 0) KB_FED_TL(m, 4);
-      slot3 = slot2;
-      slot2 = slot1;
-      slot1 = slot;
       __syncthreads();  // cm reused by the next command
       continue;
     }
     if (s_n1 < 0) break;  // the placer stopped answering: leave (the host sees the exit flag)
-    // rows job m-2 committed (final), while job m-1 may still be choosing its set
-    fed_patch(k32, N, P, C, sp, spec, stat, idx_bits, slot2 >= 0 ? S.commits[slot2] : nullptr, s_n1,
-              slot3 >= 0 ? S.commits[slot3] : nullptr, slot3 >= 0 ? s_n3 : 0, base, n);
+    if (w2 >= 0) {  // S(m-2) re-keyed from its final rows (while job m-1 may still be choosing its set)
+      const Row rr = load_row_sc1(N, w2);
+      const uint32_t rs = row_reasons(N, P, C, sp, P.sc_init + (size_t)spec * N.S, rr, st2, w2);
+      k32[w2 - base] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rr, st2), w2), w2 + N.base, idx_bits);
+      if (lvl != nullptr) atomicOr(&pbits[(w2 - base) >> 5], 1u << ((w2 - base) & 31));
+    }
+    __syncthreads();
     if (sel == 0) KB_FED_TL(m, 1);
     KB_SSTAMP(3);
     // the T best of this range outside job m-1's set are among its T + kSegMax best (the set holds at most kSegMax
@@ -3386,15 +3550,21 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
     uint64_t stw = 0;
     int wp = 0;
     uint32_t wk = 0;
+    uint4 lv0 = make_uint4(0u, 0u, 0u, 0u), lv1 = lv0;  // its level record (the sweep's), loaded beside the row
     if (tid < (int)cnt) {
       wp = rnode[tid];
       wk = rkey[tid];
       rw = load_row_sc1(N, wp + base);
       stw = stat[wp + base];
+      if (lvl != nullptr) {
+        const uint4* lr = (const uint4*)(lvl + (size_t)(wp + base) * kLvlW);
+        lv0 = lr[0];
+        lv1 = lr[1];
+      }
     }
     if (tid == 0) {  // job m-1's set (published at its node setup)
       int n1 = 0;
-      if (m >= 1 && slot1 >= 0) {
+      if (has1) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
           const uint64_t h = x_load64(&X->p_head[r1]);
@@ -3450,12 +3620,21 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
       uint64_t(*ent)[128] = X->s_ent[r][sel];
       x_store64(&ent[0][pos], (uint64_t)wk | ((uint64_t)(uint32_t)(wp + base) << 32) | ((uint64_t)nrank << 56));
       x_store64(&ent[1][pos], stw);
-      // the entry's A for the placer's node setup (allocs_before_full: off the placer's chain)
-      rw.aux = allocs_before_full(N, sp, P.sc_init + (size_t)spec * N.S, P.sc_req + (size_t)spec * N.S, rw, wp + base);
+      // the entry's A for the placer's node setup (allocs_before_full: off the placer's chain) -- the sweep's, with
+      // its levels, unless this job's patch re-keyed the node (its row changed after the sweep read it)
+      const bool lv_ok = lvl != nullptr && !((pbits[wp >> 5] >> (wp & 31)) & 1u);
+      rw.aux = lv_ok ? (int32_t)lv1.w
+                     : allocs_before_full(N, sp, P.sc_init + (size_t)spec * N.S, P.sc_req + (size_t)spec * N.S, rw,
+                                          wp + base);
       uint64_t words[sizeof(Row) / 8];
       __builtin_memcpy(words, &rw, sizeof(Row));
 #pragma unroll
       for (int q = 0; q < (int)(sizeof(Row) / 8); ++q) x_store64(&ent[2 + q][pos], words[q]);
+      constexpr int kL = 2 + (int)(sizeof(Row) / 8);
+      x_store64(&ent[kL][pos], (uint64_t)lv0.x | ((uint64_t)lv0.y << 32));
+      x_store64(&ent[kL + 1][pos], (uint64_t)lv0.z | ((uint64_t)lv0.w << 32));
+      x_store64(&ent[kL + 2][pos], (uint64_t)lv1.x | ((uint64_t)lv1.y << 32));
+      x_store64(&ent[kL + 3][pos], (uint64_t)lv1.z | ((uint64_t)(lv_ok ? 1u : 0u) << 32));
     } else if (sel == 0 && tid >= 256 && tid < 256 + 16) {  // the command, for the placer (tagged: prefetched)
       tag_store(&X->s_cmd[r][tid - 256], m + 1, ((const uint32_t*)&cm)[tid - 256]);
     }
@@ -3468,13 +3647,10 @@ __device__ __forceinline__ void fed_selector(const DevNodes& N, const DevSpecs& 
 #ifdef KB_DIAG
     dg[6]++;
 #endif
-    slot3 = slot2;
-    slot2 = slot1;
-    slot1 = slot;
     __syncthreads();  // cm reused by the next command
   }
 #ifdef KB_DIAG
-  if (tid == 0 && sel == 0)
+  if (tid == 0 && sel == 0 && par == 0)
     for (int k = 0; k < 8; ++k) X->sdiag[k] = dg[k];
 #endif
 #undef KB_SSTAMP
@@ -3922,7 +4098,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       s_cx[tid] = (uint8_t)__hip_atomic_load(&X->census_xcc[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tid == 0) {
-      // roles: 0 the placer, 1..nsel the selectors -- the workgroups on XCC place_xcc first, then the others, both in
+      // roles: 0 the placer, 1..kFedParity*nsel the selectors -- the workgroups on XCC place_xcc first, then the others, both in
       // block order; then (resident sweepers) every other workgroup NOT on the placer's XCC, in block order: a
       // sweeper's stores and its per-job release would dirty and write back that XCC's L2 under the placer
       // (measured: C2 19.2 us per job with sweepers there, r05r). The rest exit.
@@ -3932,7 +4108,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         if (s_all) {
           int k = 0;
           for (int pass = 0; pass < 2; ++pass)
-            for (uint32_t b = 0; b < G && k <= nsel; ++b)
+            for (uint32_t b = 0; b < G && k <= kFedParity * nsel; ++b)
               if (!(s_cx[b] & 0x80u) && ((uint32_t)s_cx[b] == (uint32_t)pxc + 1) == (pass == 0)) {
                 if (b == blockIdx.x) role = k;
                 s_cx[b] |= 0x80u;  // (taken)
@@ -3941,7 +4117,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
           if (hring != nullptr) {
             for (uint32_t b = 0; b < G; ++b)
               if (!(s_cx[b] & 0x80u) && s_cx[b] != (uint32_t)pxc + 1) {
-                if (b == blockIdx.x) role = nsel + 1 + nsw;
+                if (b == blockIdx.x) role = kFedParity * nsel + 1 + nsw;
                 ++nsw;
               }
             // no workgroup off the placer's XCC (a one-XCC device or partition): the sweepers share its XCC rather
@@ -3949,7 +4125,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
             if (nsw == 0)
               for (uint32_t b = 0; b < G; ++b)
                 if (!(s_cx[b] & 0x80u)) {
-                  if (b == blockIdx.x) role = nsel + 1 + nsw;
+                  if (b == blockIdx.x) role = kFedParity * nsel + 1 + nsw;
                   ++nsw;
                 }
             // still none (a grid of placer and selectors only, which launch_fed_engine never sizes): every role leaves
@@ -3968,15 +4144,15 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     }
     __syncthreads();
     const int role = s_role;
-    if (role > nsel) {  // resident sweepers
+    if (role > kFedParity * nsel) {  // resident sweepers
       fed_sweeper(N, P, C, idx_bits, S, hring, epoch, const_cast<FedCmd*>(ring), const_cast<uint32_t*>(ctr),
-                  idle_ticks, exit_flag, role - nsel - 1, s_nsw, &X->sw_cmd[0][0], X->sw_go);
+                  idle_ticks, exit_flag, role - kFedParity * nsel - 1, s_nsw, &X->sw_cmd[0][0], X->sw_go, &X->sw_exit);
       return;
     }
-    if (role < 0 || role > nsel) return;
-    if (role >= 1) {
+    if (role < 0) return;
+    if (role >= 1) {  // selector (role - 1) % nsel of the node ranges, parity (role - 1) / nsel
       fed_selector<QN>(N, P, C, idx_bits, S, ring, ctr, idle_ticks, exit_flag, X, k32, sh, cm, s_op, s_cand,
-                       role - 1, nsel, (uint32_t*)cand);
+                       (role - 1) % nsel, nsel, (uint32_t*)cand, (role - 1) / nsel);
       return;
     }
   }
@@ -4000,12 +4176,15 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   for (int q = 0; q < 16 + MSEL; ++q) pre[q] = 0;
   // one selector: this thread's candidate entry of the next job, loaded at the end of this job when the next head was
   // already there (its latency hides behind the publish), with the count it was loaded for (-1: none)
-  constexpr int kEntW = 2 + (int)(sizeof(Row) / 8);
+  constexpr int kEntW = kEntWords - 4;  // (the level words are loaded at the merge, not prefetched: registers)
   uint64_t ent_pf[kEntW];
 #pragma unroll
   for (int q = 0; q < kEntW; ++q) ent_pf[q] = 0;
   int ent_pf_na = -1;
   uint64_t bst_pf = 0;  // likewise this thread's B entry's static cache (s_bst, written before the same head)
+  // ... and its entry's level words, moved into the LDS records (clv) at the next loop top -- not held in registers
+  // through the next job's merge, where the kernel's register budget is spent
+  uint64_t lw_pf[4] = {0, 0, 0, 0};
 #ifdef KB_DIAG
   uint64_t mg[4] = {0, 0, 0, 0};  // split: the merge's steps (loads, B order, union rank, slots)
   // per job: the KB_SEL_PH phases; [0] also takes the wait for this job's command, [6] the previous job's
@@ -4024,6 +4203,11 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
   for (int r = 0;; r = r + 1 == kJobSlots ? 0 : r + 1, ++m) {
     if constexpr (SPLIT) {  // the selector's publication carries the command (and EXIT)
       KB_FED_TL(m, 11);
+      if (MSEL == 1 && tid < ent_pf_na) {  // the prefetched entry's level words (they came in during the publish)
+        uint4* o = (uint4*)(k32 + 128 + (size_t)tid * kLvlW);  // (clv, below)
+        o[0] = make_uint4((uint32_t)lw_pf[0], (uint32_t)(lw_pf[0] >> 32), (uint32_t)lw_pf[1], (uint32_t)(lw_pf[1] >> 32));
+        o[1] = make_uint4((uint32_t)lw_pf[2], (uint32_t)(lw_pf[2] >> 32), (uint32_t)lw_pf[3], (uint32_t)(lw_pf[3] >> 32));
+      }
       if (tid == 0) {
         int c = -2;
         // the head and command prefetched at the end of the previous job, when they were already there
@@ -4169,6 +4353,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       s_feas = 0;
       s_bmax = 0;
     }
+    // split engine with resident sweepers: the selected slots' level records (sh.comp: clv index + 1, 0 none)
+    const bool lvl_on = SPLIT && S.lvl[slot] != nullptr;
+    const uint32_t* lvl_lds = nullptr;
     if constexpr (SPLIT) {
       // candidates: A, the selector's T best outside the previous job's set (key order, with their static cache
       // and rows); B, that set re-keyed from the final rows kept in brow. Every rank below is a count over at
@@ -4196,6 +4383,10 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       Row* crow = MSEL == 1 ? brow + 128 : (Row*)(k32 + MSEL * 128);
       uint64_t* cst = (uint64_t*)(crow + (MSEL == 1 ? 256 : 128 * (MSEL + 1)));
       int32_t* cnd = (int32_t*)(cst + 128 * (MSEL + 1));
+      // the A entries' level records (kLvlW words each, by list position), in key space the split placer leaves free
+      uint32_t* clv = MSEL == 1 ? k32 + 128 : (uint32_t*)(cnd + 128 * (MSEL + 1));
+      lvl_lds = clv;
+      uint64_t lw[4] = {0, 0, 0, 0};  // this thread's A entry's level words (its record, valid flag in lw[3] >> 32)
       int na = 0, list = -1, idx = 0;
 #pragma unroll
       for (int k = 0; k < MSEL; ++k) {
@@ -4229,6 +4420,12 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         __builtin_memcpy(&crow[tid], words, sizeof(Row));
         cst[tid] = st;
         cnd[tid] = (int)((e0 >> 32) & kEntNodeMask);
+        if (lvl_on && !pf) {  // its level record (valid flag in the last word): loaded now, stored to LDS after the
+                              // merge (prefetched: in LDS already, the loop top)
+          constexpr int kL = 2 + (int)(sizeof(Row) / 8);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) lw[q] = x_load64(&ent[kL + q][idx]);
+        }
         a_nrank = (int)(e0 >> 56);
         akey[list * 128 + idx] = (uint32_t)e0;
       } else if (tid >= na && tid - na < nb) {
@@ -4341,6 +4538,14 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         }
         __syncthreads();
       }
+      // the selected A entries' level records into LDS (their loads had the merge to arrive; prefetched: there already,
+      // the valid flag in the record's last word)
+      const bool lv_ok = list >= 0 && (pf ? clv[(size_t)tid * kLvlW + kLvlW - 1] != 0u : (lw[3] >> 32) != 0);
+      if (sel && lv_ok && !pf) {
+        uint4* o = (uint4*)(clv + (size_t)tid * kLvlW);
+        o[0] = make_uint4((uint32_t)lw[0], (uint32_t)(lw[0] >> 32), (uint32_t)lw[1], (uint32_t)(lw[1] >> 32));
+        o[1] = make_uint4((uint32_t)lw[2], (uint32_t)(lw[2] >> 32), (uint32_t)lw[3], 1u);
+      }
       if (sel) {
         const int slot_s = fast_a ? a_nrank : sh.gen[pos];
         sh.node[slot_s] = cnd[tid];
@@ -4348,6 +4553,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         sh.row[slot_s] = crow[tid];
         sh.stat[slot_s] = cst[tid];
         sh.lmax[slot_s] = (int)T - pos;
+        sh.comp[slot_s] = lv_ok ? (uint64_t)(tid + 1) : 0ull;  // (sel_run: the slot's level record, clv[comp - 1])
         if (pos == nsel_t - 1) sh.theta0 = key;
       }
       if (tid == 0) sh.n_sel = nsel_t;
@@ -4397,7 +4603,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     if constexpr (SHARD) {
       sel_run<true, QN, true>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,
                               gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp, nullptr,
-                              S.commits[slot] SEL_DIAG_ARGS, pub);
+                              S.commits[slot] SEL_DIAG_ARGS, pub, nullptr, lvl_on ? lvl_lds : nullptr);
       ph[0] += __builtin_amdgcn_s_memrealtime() - t_job0;
       const int rc = shard_place(sh, k32, cand, SP, xn++, N, P, C, sp, spec, stat, S.keys[slot],
                                  prev_slot[0] >= 0 ? S.commits[prev_slot[0]] : nullptr,
@@ -4423,7 +4629,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
     } else {
       sel_run<false, QN, SPLIT>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready,
                                 minav, gang, placed, stop, fail_task, panic, stopped, S.hout[slot], js, hjs, rp,
-                                nullptr, S.commits[slot] SEL_DIAG_ARGS, pub);
+                                nullptr, S.commits[slot] SEL_DIAG_ARGS, pub, nullptr, lvl_on ? lvl_lds : nullptr);
     }
     if constexpr (SPLIT) {
       __syncthreads();
@@ -4522,6 +4728,8 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         const uint64_t(*ent)[128] = X->s_ent[rn][0];
 #pragma unroll
         for (int q = 0; q < kEntW; ++q) ent_pf[q] = x_load64(&ent[q][tid]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lw_pf[q] = x_load64(&ent[kEntW + q][tid]);
       } else if (ent_pf_na >= 0 && tid - ent_pf_na < nbprev) {  // (the thread that takes that B entry)
         bst_pf = x_load64(&X->s_bst[rn][tid - ent_pf_na]);
       }
@@ -4579,7 +4787,7 @@ bool fed_fits(int n) {
 void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int idx_bits, uint32_t* keys32,
                     uint64_t* stat, const FedCmdArgs& a, void* ring, uint32_t* ctr, bool sweep, void* stream) {
   FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
-             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, 0};
+             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, a.fresh_m};
   const int blocks = sweep ? (N.n + 63) / 64 : 1;
   hipLaunchKernelGGL(fed_cmd_sweep_kernel<false>, dim3(blocks), dim3(64), 0, (hipStream_t)stream, N, P, C, idx_bits,
                      keys32, stat, cmd, (FedCmd*)ring, ctr, sweep ? 1 : 0);
@@ -4588,7 +4796,7 @@ void launch_fed_cmd(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int i
 size_t fed_ring_bytes() { return kJobSlots * sizeof(FedCmd); }
 void fed_host_post(void* hring, int r, const FedCmdArgs& a, uint64_t tag) {
   FedCmd cmd{a.op, a.spec, a.t_begin, a.t_count, a.ready0, a.minav0, a.gang0, a.slot, a.g_valid, a.g_stop,
-             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, 0};
+             a.g_placed, a.g_ready, a.seq, a.fresh, a.acq, a.fresh_m};
   FedHostCmd* h = (FedHostCmd*)hring + r;
   uint64_t w[8];
   __builtin_memcpy(w, &cmd, sizeof(cmd));
@@ -4648,6 +4856,7 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
     S.js[s] = sp.js[s];
     S.hjs[s] = sp.hjs[s];
     S.hout[s] = sp.hout[s];
+    S.lvl[s] = sp.lvl[s];
   }
   // past one workgroup's key plan: nsel range selectors of kFedSelQ key groups each (split engine only)
   int nsel = xchg ? fed_nsel(N.n) : 1;
@@ -4696,9 +4905,9 @@ int launch_fed_engine(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int
   // with sweepers, enough workgroups for about one sweeper thread per node off the placer's XCC (a sweeper's
   // nodes are latency-bound loads and static checks: C3's 20k nodes over 14 sweepers ran 39 us per job, r05q);
   // the dispatcher deals blocks round robin over the 8 XCCs, so ~7/8 of the grid lands off it
-  int g = split ? (pxcc >= 0 ? 8 : 1) * (1 + nsel) : 1;
+  int g = split ? (pxcc >= 0 ? 8 : 1) * (1 + kFedParity * nsel) : 1;
   if (hr != nullptr) {
-    const int want_sw = (N.n + kSelThreads - 1) / kSelThreads;
+    const int want_sw = kSweepGroups * ((N.n + kSelThreads - 1) / kSelThreads);  // (fed_sweeper's groups)
     const int g_sw = ((want_sw * 8 + 6) / 7 + 7) / 8 * 8;
     g = g_sw > g ? g_sw : g;
     if (g > kFedGridMax) g = kFedGridMax;

@@ -256,6 +256,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->test_peer_badtag = (fl & KB_OPT_TEST_PEER_BADTAG) != 0;
   c->fed_kernel_sweeps = (fl & KB_OPT_FED_KERNEL_SWEEPS) != 0;
   c->test_one_xcc = (fl & KB_OPT_TEST_ONE_XCC) != 0;
+  c->no_lvl = (fl & KB_OPT_FED_NO_LEVELS) != 0;
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
@@ -322,6 +323,7 @@ void kb_destroy(kb_ctx* c) {
   for (int s = 0; s < kJobSlots; ++s) {
     if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
     if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
+    if (c->sel_lvl[s]) (void)hipFree(c->sel_lvl[s]);
     if (c->commits[s]) (void)hipFree(c->commits[s]);
   }
   if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
@@ -1381,8 +1383,10 @@ static int ensure_sel_bufs(kb_ctx* c) {
     for (int s = 0; s < kJobSlots; ++s) {
       if (c->sel_keys[s]) (void)hipFree(c->sel_keys[s]);
       if (c->sel_stat[s]) (void)hipFree(c->sel_stat[s]);
+      if (c->sel_lvl[s]) (void)hipFree(c->sel_lvl[s]);
       c->sel_keys[s] = nullptr;
       c->sel_stat[s] = nullptr;
+      c->sel_lvl[s] = nullptr;
     }
     c->sel_n = -1;
     const size_t n = (size_t)std::max(c->N.n, 1);
@@ -1830,8 +1834,15 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     memset(c->fed_hring, 0, kJobSlots * sizeof(FedHostCmd));
     HIP_OK(c, hipHostGetDevicePointer(&c->fed_hring_dev, c->fed_hring, 0));
   }
+  // the sweepers' level records (the selector forwards them with its candidates; sweep kernels write none)
+  const bool lvl_on = c->fed_sweepers_now && !c->no_lvl;
+  for (int s = 0; s < kJobSlots; ++s) {
+    if (lvl_on && !c->sel_lvl[s]) HIP_OK(c, hipMalloc((void**)&c->sel_lvl[s], (size_t)std::max(c->N.n, 1) * kLvlW * 4));
+    sp.lvl[s] = lvl_on ? c->sel_lvl[s] : nullptr;
+  }
   c->fed_epoch++;
   c->fed_m = 0;
+  c->fed_cmd_m = c->fed_fresh_m = 0;
   HIP_OK(c, (hipError_t)launch_fed_engine(c->N, c->P, c->cfg, c->idx_bits, sp, c->fed_ring, c->fed_ctr,
                                           c->fed_count, idle, c->fed_exit, xchg, c->stream, c->fed_coop, SP,
                                           c->fed_coop || c->fed_xcc < 0 ? -1 : c->fed_xcc | (c->test_one_xcc ? 0x100 : 0),
@@ -1843,8 +1854,13 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
 }
 
 // Post a command to the engine (sweep: the job's level-0 keys into its slot buffers first).
-static int fed_post(kb_ctx* c, const FedCmdArgs& a, int si, bool sweep) {
+static int fed_post(kb_ctx* c, const FedCmdArgs& a0, int si, bool sweep) {
   const int r = c->fed_r;
+  // the launch's most recent fresh command (the parity selectors: every command before it is final)
+  FedCmdArgs a = a0;
+  if (a.fresh) c->fed_fresh_m = c->fed_cmd_m;
+  a.fresh_m = (int32_t)c->fed_fresh_m;
+  c->fed_cmd_m++;
   void* entry = (char*)c->fed_ring + r * (fed_ring_bytes() / kJobSlots);
   if (c->fed_sweepers_now) {  // the resident sweepers take it from the pinned ring: no launch
     fed_host_post(c->fed_hring, r, a, ((uint64_t)c->fed_epoch << 32) | (uint64_t)(c->fed_m + 1));

@@ -144,7 +144,7 @@ OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6,
                 "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
                 "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14,
                 "fed_coop_launch": 1 << 15, "test_peer_badtag": 1 << 16, "fed_kernel_sweeps": 1 << 17,
-                "test_one_xcc": 1 << 18}
+                "test_one_xcc": 1 << 18, "fed_no_levels": 1 << 19}
 OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0", "fed_xcc", "fed_depth")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",

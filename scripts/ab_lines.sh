@@ -28,7 +28,7 @@ print(f"{sys.argv[2]:>14} {d['config']['workload'][:18]:>18} {d['value']/1e6:7.3
 EOF
 }
 if [ -n "${TESTS:-}" ]; then
-  step tests 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 600 --timeout-method thread tests -k "$TESTS"
+  step tests 900 python -u -m pytest -m gpu -v -s -x -p no:cacheprovider --timeout 600 --timeout-method thread tests -k "$TESTS"
   grep -E "passed|failed" "gpurun_out/${TAG}_tests.log" | tail -1
 fi
 for spec in ${LINES:-}; do

@@ -375,6 +375,8 @@ SPLIT_CLUSTERS = [
 SPLIT_MODES = {
     "split": {},
     "split-kernel-sweeps": {"fed_kernel_sweeps": True},
+    # the placer computes every e-sequence level itself (no level records from the sweepers)
+    "split-no-levels": {"fed_no_levels": True},
     "one-workgroup": {"no_fed_split": True},
     # a one-XCC census (a one-XCC device or partition): the resident sweepers share the placer's XCC
     "split-one-xcc": {"test_one_xcc": True},
@@ -405,7 +407,7 @@ def test_fed_split_engine_parity(name, cluster, mode):
         ctx.close()
     assert st["fed_cycles"] == 1 and st["fed_split"] == (1 if split else 0)
     assert st["fed_abandon"] == 0, st
-    if mode in ("split", "split-one-xcc", "split-depth2", "split-depth3"):
+    if mode in ("split", "split-one-xcc", "split-depth2", "split-depth3", "split-no-levels"):
         assert st["fed_last_sweepers"] > 0, st
     if mode == "split-kernel-sweeps":
         assert st["fed_last_sweepers"] == 0, st
