@@ -1712,6 +1712,9 @@ __device__ __forceinline__ int sel_level(uint64_t o) { return 127 - (int)(o & 12
 // write_back_row does them).
 __device__ void store_back_row(const DevNodes& N, const DevSpecs& P, const kb_spec& sp, const int64_t* scr, int w,
                                int c, int A, const Row& r0) {
+#ifdef KB_WA_NO_ROWS  // (write-accounting A/B build only: the committed rows are not written back -- wrong placements)
+  return;
+#endif
   const int64_t a = c < A ? c : A;
   const int64_t p = c - a;
   // (sc1 stores: the fed selector reads them with load_row_sc1, after the placer's p_done, without an acquire)
@@ -1886,6 +1889,16 @@ __device__ void sel_hist(SelShared& sh, const uint4* k32v, int Q4) {
 // Tagged words: (tag << 32 | payload), written and read as write-through agent-scope atomics. A reader
 // takes a word once its tag is the one it waits for, so a publication needs no store ordering (no waits on
 // the writer's side) and a stale word from an earlier job reads as not there yet.
+#ifdef KB_TIMELINE
+#define KB_PUB_TL(k)                                                                          \
+  do {                                                                                        \
+    if (CAND && pub.tl != nullptr && threadIdx.x == 0) pub.tl[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define KB_PUB_TL(k) \
+  do {               \
+  } while (0)
+#endif
 __device__ __forceinline__ void tag_store(uint64_t* w, uint32_t tag, uint32_t v) {
   __hip_atomic_store(w, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1902,6 +1915,7 @@ struct FedPub {
   uint64_t* head = nullptr;  // tag << 32 | mode << 16 | count; nullptr: nothing to publish
   uint64_t* node = nullptr;  // [128] tag << 32 | node
   uint32_t tag = 0;
+  uint64_t* tl = nullptr;    // KB_TIMELINE builds: the job's timeline row (FedXchg::tl)
   __device__ void set_node(int i, int w) const { tag_store(&node[i], tag, (uint32_t)w); }
   __device__ void set_head(uint32_t mode, int cnt) const { tag_store(head, tag, (mode << 16) | (uint32_t)cnt); }
 };
@@ -2059,6 +2073,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         __syncthreads();
       }
       KB_SEL_PH(2);
+      KB_PUB_TL(13);
       // (with level records the first round's active list needs the emission's done flags: built in the loop)
       for (bool first = CAND && clv == nullptr;; first = false) {
         if (!first) {
@@ -2123,6 +2138,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
         __syncthreads();
       }
       KB_SEL_PH(3);
+      KB_PUB_TL(14);
       // ---- 4. the T winners in pick order: rank every candidate when they fit one per thread, else a
       //         threshold on the score field plus per-slot takes, then rank the T taken ones ----
       uint64_t cs[2 * kCandV];
@@ -2213,6 +2229,7 @@ __device__ __forceinline__ void sel_run(SelShared& sh, uint32_t* k32, uint64_t* 
       }
       __syncthreads();
       KB_SEL_PH(4);
+      KB_PUB_TL(15);
       if constexpr (PROPOSE && CAND) {
         // the node-sharded fed engine's placer: the proposal stays in sh.ord[0..s_count) for the caller's exchange
         // and merge (shard_place)
@@ -3127,7 +3144,9 @@ __device__ __forceinline__ void fed_sweeper(const DevNodes& N, const DevSpecs& P
         }
         __builtin_memcpy(&s_cmd, w, sizeof(FedCmd));
         if (s_cmd.op == KB_ENG_RUN) {
+#ifndef KB_WA_NO_SWACQ  // (write-accounting A/B builds only: scripts/write_account.sh)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the barrier below holds the other waves' loads)
         }
       }
@@ -3135,20 +3154,31 @@ __device__ __forceinline__ void fed_sweeper(const DevNodes& N, const DevSpecs& P
     }
     __syncthreads();
     if (!s_go) return;
-    const FedCmd cm = s_cmd;
-    if (cm.op == KB_ENG_RUN) {
-      const kb_spec sp = P.specs[cm.spec];
-      uint32_t* keys32 = S.keys[cm.slot];
-      uint64_t* stat = S.stat[cm.slot];
-      const int64_t* sci = P.sc_init + (size_t)cm.spec * N.S;
-      uint32_t* lvl = S.lvl[cm.slot];
-      const int64_t* scr = P.sc_req + (size_t)cm.spec * N.S;
+    // (the fields the sweep uses, as scalars: a private copy of the whole command went to scratch, and every
+    // sweeper's per-job release then wrote those dirty scratch lines back to memory -- 56 B per lane per job, most of
+    // the engine's WRITE_SIZE before round 6's write accounting found it)
+    const int op = s_cmd.op, cspec = s_cmd.spec, cslot = s_cmd.slot;
+    if (op == KB_ENG_RUN) {
+      const kb_spec sp = P.specs[cspec];
+      uint32_t* keys32 = S.keys[cslot];
+      uint64_t* stat = S.stat[cslot];
+      const int64_t* sci = P.sc_init + (size_t)cspec * N.S;
+      uint32_t* lvl = S.lvl[cslot];
+      const int64_t* scr = P.sc_req + (size_t)cspec * N.S;
       for (int n = n0 + tid; n < n1; n += kSelThreads) {
+#ifdef KB_WA_NO_SWROWS  // (write-accounting A/B: the sweep without its row loads -- wrong keys)
+        Row rw{};
+        rw.alloc_cpu = rw.alloc_mem = rw.idle_cpu = rw.idle_mem = 1ll << 40;
+        rw.max_pods = 110;
+#else
         const Row rw = load_row(N, n);
-        const uint64_t st = static_eval<false>(N, P, C, sp, cm.spec, rw.flags, n, P.A.mm);
-        stat[n] = st;
+#endif
+        const uint64_t st = static_eval<false>(N, P, C, sp, cspec, rw.flags, n, P.A.mm);
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, n);
+#ifndef KB_WA_NO_SWSTORES  // (write-accounting A/B: no key / static-cache stores -- stale keys)
+        stat[n] = st;
         keys32[n] = compress_key(make_key(rs, rs ? 0 : row_score(C, sp, rw, st), n), n + N.base, idx_bits);
+#endif
         if (lvl != nullptr && rs == 0) {  // (an infeasible node is never a candidate: no record)
           // the e-sequence levels exactly as sel_run computes them (same row, static cache, A and reciprocals)
           // (one level at a time, each stored as it comes: the sweeper role must not raise the kernel's register
@@ -3167,13 +3197,13 @@ __device__ __forceinline__ void fed_sweeper(const DevNodes& N, const DevSpecs& P
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      if (lead) ring[r] = cm;
+      if (lead) ring[r] = s_cmd;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(&ctr[r], b1 - b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cm.op != KB_ENG_RUN && lead) __hip_atomic_store(sw_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (op != KB_ENG_RUN && lead) __hip_atomic_store(sw_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (cm.op != KB_ENG_RUN) return;
+    if (op != KB_ENG_RUN) return;
     __syncthreads();  // (s_cmd / s_go are rewritten by the next poll)
   }
 }
@@ -3231,7 +3261,8 @@ struct FedXchg {
   // [1] its patch done (after job m-2's p_done), [2] its selection done, [3] job m-1's set seen, [4] its head
   // published; the placer's [5] job start (head and command read), [6] its set published, [7] p_done written,
   // [8] its publish started (the drain before the release), [9] the release and host state done
-  uint64_t tl[kFedTraceJobs][12];  // ... [10] the placer's command decoded (thread 0), [11] its loop top
+  uint64_t tl[kFedTraceJobs][16];  // ... [10] the placer's command decoded (thread 0), [11] its loop top, [12] its merge's
+                                   // entries in LDS, in sel_run [13] node setup, [14] e-sequences, [15] winners done
 #endif
   // resident sweepers: sweeper 0 relays each host command (its eight words sc1, then the tag) to the others
   uint64_t sw_cmd[kJobSlots][8];
@@ -4460,6 +4491,7 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       if (tid >= nb && tid < 128) bkey[tid] = 0u;  // padding ranks below every key
       __syncthreads();
       KB_MSTAMP(0);
+      KB_FED_TL(m, 12);
       // Fast path (one selector list): every B key below A's T-th key -- the previous job's nodes, just loaded,
       // rank below the selector's T best, as they mostly do -- makes the T best of the union A's first T, in A's
       // order: no B order, no union ranks (~1.4 us of barrier-separated LDS ranking, r05z)
@@ -4599,6 +4631,9 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
       pub.head = &X->p_head[r];
       pub.node = X->p_node[r];
       pub.tag = m + 1;
+#ifdef KB_TIMELINE
+      pub.tl = X->tl[m & (kFedTraceJobs - 1)];
+#endif
     }
     if constexpr (SHARD) {
       sel_run<true, QN, true>(sh, k32, cand, N, P, C, sp, spec, cm.t_begin, cm.t_count, idx_bits, stat, ready, minav,

@@ -1954,17 +1954,18 @@ int kb_fed_end(kb_ctx* c) {
     }
     if (c->fed_diag && fed_trace_offset()) {  // KB_DIAG / KB_TIMELINE builds: the engine's per-job timeline
       const int TJ = fed_trace_jobs();
-      constexpr int TW = 12;  // FedXchg::tl's words per job
+      constexpr int TW = 16;  // FedXchg::tl's words per job
       std::vector<uint64_t> tl((size_t)TJ * TW);
       const int jobs = (int)std::min<uint64_t>(d[6] ? d[6] : (uint64_t)c->dg_iss0.size(), (uint64_t)TJ);
       if (hipMemcpy(tl.data(), (char*)c->fed_xchg + fed_trace_offset(), tl.size() * 8, hipMemcpyDeviceToHost) ==
               hipSuccess && jobs > 8) {
         // per job m (relative to the placer's end of job m-1 = when it wants job m's head): the selector's command
         // arrival, patch done, selection done, set seen, head; the placer's start and end of job m
-        constexpr int NK = 12;
+        constexpr int NK = 16;
         const char* names[NK] = {"cmd", "patched", "selected", "set_seen", "head", "loop_top", "cmd_decoded",
-                                 "placer_start", "set_published", "pub_start", "released", "placer_end"};
-        const int ks[NK] = {0, 1, 2, 3, 4, 11, 10, 5, 6, 8, 9, 7};
+                                 "placer_start", "merge_loads", "set_published", "node_setup", "e_seq", "winners",
+                                 "pub_start", "released", "placer_end"};
+        const int ks[NK] = {0, 1, 2, 3, 4, 11, 10, 5, 12, 6, 13, 14, 15, 8, 9, 7};
         std::vector<double> v[NK], lv[NK];
         for (int m = 4; m < jobs - 1; ++m) {
           const double E = (double)tl[(size_t)(m - 1) * TW + 7];
