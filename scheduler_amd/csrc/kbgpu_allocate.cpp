@@ -6,6 +6,8 @@
 // host-side job / share state the ordering reads.
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +20,64 @@
 #include "kbgpu_ctx.h"
 
 namespace {
+
+// One host helper thread per process: kb_allocate builds the cycle's pending lists on it while its own thread walks the
+// tasks for the plugins' session-open state (two independent passes over the session's task arrays, ~0.2 ms each on
+// C2's 100k tasks, before the first job can be issued). A driver that finds it busy (another context's cycle in
+// another thread) runs the work itself.
+class HostHelper {
+ public:
+  static HostHelper& get() {
+    static HostHelper h;
+    return h;
+  }
+  bool post(std::function<void()> f) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (busy_) return false;
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    job_ = std::move(f);
+    busy_ = true;
+    cv_.notify_one();
+    return true;
+  }
+  void join() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return !busy_; });
+  }
+  ~HostHelper() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || job_ != nullptr; });
+        if (stop_) return;
+        f = std::move(job_);
+        job_ = nullptr;
+      }
+      f();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        busy_ = false;
+      }
+      done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::function<void()> job_;
+  bool busy_ = false, stop_ = false;
+  std::thread th_;
+};
 
 constexpr double kMinMilliCPU = 10, kMinMemory = 10 * 1024 * 1024, kMinMilliScalar = 10;  // resource_info.go:70-72
 constexpr uint64_t kHasMap = 1ull << 63;
@@ -283,6 +343,8 @@ struct Driver {
 
   int init() {
     const auto i0 = std::chrono::steady_clock::now();
+    // the pending lists (run()) on the helper thread, beside this task pass (both only read the session)
+    const bool helped = HostHelper::get().post([this] { build_pend(); });
     for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
       int p = s.tier_plugins[i].plugin;
       if (p >= 0 && p < 8) has[p] = true;
@@ -343,6 +405,8 @@ struct Driver {
       }
     }
     flush();
+    if (helped) HostHelper::get().join();
+    else build_pend();
     const auto i1 = std::chrono::steady_clock::now();
     for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
     const auto i2 = std::chrono::steady_clock::now();
@@ -430,6 +494,37 @@ struct Driver {
 
   // ---- the allocate loop (actions/allocate/allocate.go:40-176) ----
   double loop_ms = 0;  // KB_HOST_TRACE: time in the job loop of run()
+  // The jobs in UID order and every job's Pending tasks as one CSR array, with the cycle's largest pending list and
+  // the pending tasks with requests (pend_all), of which the fed engine takes pend_eng. Reads only the session (the
+  // input task statuses: init() copies them beside it) and the context's per-spec eligibility, so it runs on the
+  // host helper thread during init()'s task pass.
+  std::vector<int> jorder;
+  uint32_t max_pending = 1;
+  uint64_t pend_all = 0, pend_eng = 0;
+  void build_pend() {
+    jorder.resize(s.n_jobs);
+    for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
+    std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
+    pend_off.assign(s.n_jobs + 1, 0);
+    for (uint32_t t = 0; t < s.n_tasks; ++t)
+      if (s.task_status[t] == KB_ST_PENDING) ++pend_off[s.task_job[t] + 1];
+    max_pending = 1;
+    for (uint32_t j = 0; j < s.n_jobs; ++j) {
+      max_pending = std::max<uint32_t>(max_pending, pend_off[j + 1]);
+      pend_off[j + 1] += pend_off[j];
+    }
+    pend.resize(pend_off[s.n_jobs]);
+    pend_all = pend_eng = 0;
+    std::vector<uint32_t> cur(pend_off.begin(), pend_off.end() - 1);
+    for (uint32_t t = 0; t < s.n_tasks; ++t)
+      if (s.task_status[t] == KB_ST_PENDING) {
+        pend[cur[s.task_job[t]]++] = (int)t;
+        if (!task_res_empty(t)) {
+          ++pend_all;
+          pend_eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
+        }
+      }
+  }
   GoHeap<int> qheap;
   std::vector<GoHeap<int>> jheaps;
   // each job's Pending tasks in task order, as one CSR array (job j: pend[pend_off[j] .. pend_off[j + 1]))
@@ -777,30 +872,7 @@ struct Driver {
     dead_any = false;
     for (auto& h : jheaps) h.less = [this](const int& a, const int& b) { return job_less(a, b); };
     gang_ready_on = has[KB_PLUGIN_GANG] && enabled(KB_PLUGIN_GANG, KB_EN_JOB_READY);
-    std::vector<int> jorder(s.n_jobs);
-    for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
-    std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
-    pend_off.assign(s.n_jobs + 1, 0);
-    for (uint32_t t = 0; t < s.n_tasks; ++t)
-      if (task_status[t] == KB_ST_PENDING) ++pend_off[s.task_job[t] + 1];
-    uint32_t max_pending = 1;
-    for (uint32_t j = 0; j < s.n_jobs; ++j) {
-      max_pending = std::max<uint32_t>(max_pending, pend_off[j + 1]);
-      pend_off[j + 1] += pend_off[j];
-    }
-    pend.resize(pend_off[s.n_jobs]);
-    uint64_t pend_all = 0, pend_eng = 0;  // pending tasks with requests, and those the fed engine takes (below)
-    {
-      std::vector<uint32_t> cur(pend_off.begin(), pend_off.end() - 1);
-      for (uint32_t t = 0; t < s.n_tasks; ++t)
-        if (task_status[t] == KB_ST_PENDING) {
-          pend[cur[s.task_job[t]]++] = (int)t;
-          if (!task_res_empty(t)) {
-            ++pend_all;
-            pend_eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
-          }
-        }
-    }
+    // (jorder, pend_off / pend, max_pending, pend_all, pend_eng: build_pend, during init)
     for (int j : jorder) {
       if (s.job_pg_pending[j]) continue;                                              // allocate.go:50-52
       if (has[KB_PLUGIN_GANG] && jobs[j].valid < s.job_min_available[j]) continue;  // JobValid, gang.go:48-69
