@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KBGPU_ABI_VERSION 15
+#define KBGPU_ABI_VERSION 16
 
 /* ---- return codes ---- */
 #define KB_OK 0
@@ -428,6 +428,10 @@ int kb_restore_nodes(kb_ctx* ctx);
 /* ABI 15: the split engine without the resident sweepers' level records (the placer computes every e-sequence level
  * itself, round 5's path); A/B only */
 #define KB_OPT_FED_NO_LEVELS (1u << 19)
+/* ABI 16: inter-pod-affinity units stay off the resident engine (round 5's path: they run on the launch path while
+ * the engine pauses); A/B only. By default kb_allocate's engine takes the affinity units whose inputs its sweep can
+ * fold in: selection runs whose own commits leave their inputs alone, and the cap-1 runs. */
+#define KB_OPT_FED_NO_AFF (1u << 20)
 #define KB_KERNEL_SWEEP 0
 #define KB_KERNEL_PLACE 1
 #define KB_KERNEL_EVAL 2
@@ -493,6 +497,11 @@ typedef struct kb_stats {
                                          choice) */
   int32_t fed_last_sweepers;          /* the last split engine launch: resident sweeper workgroups (0: sweep
                                          kernels) */
+  /* ABI 16 */
+  uint64_t fed_aff_units;             /* engine units of specs with inter-pod terms (their table commits in the
+                                         placer) */
+  uint64_t fed_aff_waits;             /* engine units issued only after the units in flight finished: their sweep
+                                         reads affinity tables an earlier unit's commits write */
 } kb_stats;
 int kb_get_stats(kb_ctx* ctx, kb_stats* out, int reset);
 

@@ -587,12 +587,46 @@ struct Driver {
   };
   bool fed_allowed = false;  // the cycle may run units on the resident engine
   uint32_t unit_cap = 0;     // kb_fed_unit_cap: 0 = any length
-  std::vector<int8_t> spec_fed;  // per spec: -1 not asked yet, else kb_spec_fed_ok
+  // per spec: -1 not asked yet, else kb_spec_fed_ok_pre (affinity specs with histograms: as if their min / max were
+  // prepared; run() prepares them, or drops the ones whose histograms the cycle's commits write: prepare_fed_aff)
+  std::vector<int8_t> spec_fed;
   bool spec_fed_ok(int sp) {
     if (sp < 0) return false;
     if ((size_t)sp >= spec_fed.size()) spec_fed.resize(sp + 1, -1);
-    if (spec_fed[sp] < 0) spec_fed[sp] = (int8_t)kb_spec_fed_ok(ctx, sp);
+    if (spec_fed[sp] < 0) spec_fed[sp] = (int8_t)kb_spec_fed_ok_pre(ctx, sp);
     return spec_fed[sp] != 0;
+  }
+  // The engine's affinity units with InterPodAffinity histograms: their sweep normalises by the min / max over the
+  // nodes (interpod_affinity.go:221-238) as the tables stand when the unit runs. Computed once, before the engine's
+  // launch, they stay exact through the cycle when no pending spec's commits write the histograms they read
+  // (aff_wr / aff_rd, kb_upload_affinity); the other such specs run on the launch path (its own min / max pass per
+  // run). Returns the first error.
+  int prepare_fed_aff() {
+    ctx->mm_spec_ok.assign(ctx->mm_spec_ok.size(), 0);
+    if (!ctx->aff_ok) return KB_OK;
+    std::vector<char> seen(ctx->spec_needs_aff.size(), 0);
+    std::vector<int> cyc;  // the cycle's distinct pending specs
+    for (int t : pend) {
+      const int sp = s.task_spec[t];
+      if (sp < 0 || (size_t)sp >= seen.size() || seen[sp]) continue;
+      seen[sp] = 1;
+      cyc.push_back(sp);
+    }
+    std::vector<uint32_t> w_all;  // every table / histogram the cycle's commits may write
+    for (int sp : cyc)
+      if ((size_t)sp < ctx->aff_wr.size()) w_all.insert(w_all.end(), ctx->aff_wr[sp].begin(), ctx->aff_wr[sp].end());
+    std::sort(w_all.begin(), w_all.end());
+    w_all.erase(std::unique(w_all.begin(), w_all.end()), w_all.end());
+    std::vector<int32_t> prep;
+    for (int sp : cyc) {
+      if (!ctx->spec_needs_aff[sp] || !ctx->spec_hist[sp] || !spec_fed_ok(sp)) continue;
+      bool clash = false;
+      for (uint32_t x : ctx->aff_rd[sp])
+        if ((x >> 31) && std::binary_search(w_all.begin(), w_all.end(), x)) clash = true;
+      if (clash) spec_fed[sp] = 0;
+      else prep.push_back(sp);
+    }
+    return kb_fed_ipa_prepare(ctx, prep.data(), (uint32_t)prep.size());
   }
   // the unit job j's pending list has at its cursor (j popped from queue q)
   Unit unit_at(int q, int j) {
@@ -823,6 +857,14 @@ struct Driver {
       if (ok && i + 1 < fl.size()) ok = nu == fl[i + 1].u;  // issued by the same replay
     }
     ok = ok && nu.fed == mode_fed;
+    // an engine unit whose sweep reads affinity tables a unit in flight commits to waits for the chain to drain (it is
+    // issued after the last one is read: the placer commits the tables before it publishes)
+    if (ok && mode_fed && ctx->aff_ok) {
+      const int sb = s.task_spec[jobs[nu.j].pending[nu.cur]];
+      for (const Flight& f : fl)
+        if (!kb_fed_units_indep(ctx, s.task_spec[jobs[f.u.j].pending[f.u.cur]], sb)) ok = false;
+      if (!ok) ctx->stats.fed_aff_waits++;
+    }
     if (ok) {
       const kb_job_req req = make_req(nu);
       ok = kb_job_guardable(ctx, &req) != 0;
@@ -899,6 +941,8 @@ struct Driver {
     // worth it when most of the cycle's tasks are engine units: every switch costs an engine stop and relaunch (C4:
     // ~20% eligible jobs stay on the launch path); the counts come from the pending-list pass above
     if (fed_allowed) fed_allowed = 2 * pend_eng > pend_all;
+    if (fed_allowed)
+      if (int rc = prepare_fed_aff()) return rc;
     const bool launch_pipe = pipe && !(ctx->sharded && !ctx->comm);
     const auto r1 = std::chrono::steady_clock::now();
     if (ctx->issue_trace)

@@ -55,6 +55,12 @@ struct kb_ctx {
   bool use_aff_reg = true;
   int64_t* mm_eval = nullptr;   // [2 * chunk] per-spec IPA min / max for kb_eval
   uint32_t mm_eval_cap = 0;
+  // the fed engine's affinity units (kb_spec_fed_ok): !KB_OPT_FED_NO_AFF; per spec, whether kb_fed_ipa_prepare has
+  // filled its InterPodAffinity min / max (DevAff::mm_spec) this cycle (kb_allocate's driver clears and refills them)
+  bool use_fed_aff = true;
+  std::vector<char> mm_spec_ok;
+  int32_t* d_mm_ids = nullptr;  // kb_fed_ipa_prepare's spec list (device)
+  uint32_t mm_ids_cap = 0;
   uint64_t* keys = nullptr;  // [n] packed argmax keys of the current spec
   uint64_t* cmax = nullptr;  // [ceil(n/64)] chunk maxima
   uint64_t* stat = nullptr;  // [n] static predicate / NodeAffinity cache of the current spec
@@ -270,6 +276,15 @@ extern "C" __attribute__((visibility("hidden"))) int kb_job_reserve(kb_ctx* c, u
 // (kb_spec_fed_ok): kb_fed_begin after kb_job_reserve, then kb_job_issue / kb_job_finish as usual (each
 // issue launches only the job's sweep kernel), kb_fed_end before anything else runs on the context.
 extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok(kb_ctx* c, int spec);
+// Affinity units on the engine (kb_spec_fed_ok takes specs with inter-pod terms whose sweep folds them in). A spec with
+// InterPodAffinity histograms needs its min / max over the nodes as the cycle has them: kb_fed_ipa_prepare computes
+// them for `n` specs into DevAff::mm_spec (on `stream`, before kb_fed_begin), and kb_spec_fed_ok refuses such a spec
+// until then -- kb_spec_fed_ok_pre answers as if it were prepared (the driver's pending-list pass). The driver keeps
+// the min / max exact: it prepares only specs whose histograms no unit of the cycle writes. kb_fed_units_indep: the
+// commits of a unit of spec a leave every input of a sweep of spec b alone (b may be in flight behind a).
+extern "C" __attribute__((visibility("hidden"))) int kb_spec_fed_ok_pre(kb_ctx* c, int spec);
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_ipa_prepare(kb_ctx* c, const int32_t* specs, uint32_t n);
+extern "C" __attribute__((visibility("hidden"))) int kb_fed_units_indep(const kb_ctx* c, int a, int b);
 // the engine can serve a cycle whose jobs have at most max_job_tasks tasks (past one selector's key plan only the
 // split engine, whose jobs are one segment)
 extern "C" __attribute__((visibility("hidden"))) int kb_fed_cycle_ok(kb_ctx* c, uint32_t max_job_tasks);

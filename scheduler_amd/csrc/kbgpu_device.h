@@ -61,6 +61,7 @@ struct DevAff {
   int32_t* h;           // mutable
   kb_ipa_incr* incr;
   int64_t* mm;          // [2] InterPodAffinity min / max count of the current run's spec
+  int64_t* mm_spec;     // [2 x specs] the same per spec, for the fed engine's sweeps (kb_fed_ipa_prepare)
 };
 
 struct DevSpecs {
@@ -162,10 +163,11 @@ int place_loop_lds_bytes(int n);
 constexpr int kTrajMaxJ = 64;
 constexpr int kTrajDefaultJ = 16;  // trajectory depth per run; deeper commits are computed in place
 // Inter-pod affinity (kbgpu_device.hip): min / max InterPodAffinity count over all nodes for each of
-// `count` specs (spec_ids, or the single `spec` when spec_ids is null) into mm[2 * i], and the
-// block-wide re-sweep place loop for specs whose own commits change their affinity inputs.
+// `count` specs (spec_ids, or the single `spec` when spec_ids is null) into mm[2 * i] (by_spec: mm[2 * spec], the
+// per-spec array DevAff::mm_spec), and the block-wide re-sweep place loop for specs whose own commits change their
+// affinity inputs.
 void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec_ids, int spec, int count,
-                       int64_t* mm, const JobState* js, void* stream);
+                       int64_t* mm, const JobState* js, void* stream, int by_spec = 0);
 void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,
                       uint64_t* base, uint64_t* stat, JobState* js, int first, int ready0, int minav0, int gang0,
                       int32_t* hout, JobState* hjs, uint32_t seq, void* stream);

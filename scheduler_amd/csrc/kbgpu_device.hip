@@ -228,7 +228,7 @@ __device__ __forceinline__ int32_t ld_cnt(const int32_t* p) {
 }
 
 template <bool COH = false>
-__device__ uint32_t aff_reasons(const DevAff& A, const kb_aff_spec& as, int n) {
+__device__ __forceinline__ uint32_t aff_reasons(const DevAff& A, const kb_aff_spec& as, int n) {
   for (uint32_t i = 0; i < as.check_cnt; ++i) {
     const kb_aff_check c = A.checks[as.check_off + i];
     const kb_aff_table t = A.tables[c.table];
@@ -3173,7 +3173,16 @@ __device__ __forceinline__ void fed_sweeper(const DevNodes& N, const DevSpecs& P
 #else
         const Row rw = load_row(N, n);
 #endif
-        const uint64_t st = static_eval<false>(N, P, C, sp, cspec, rw.flags, n, P.A.mm);
+        // an affinity unit (kb_spec_fed_ok: its inputs stay as they are through the run) folds the inter-pod checks
+        // and its InterPodAffinity score, normalised by the min / max the host prepared for its spec, into the
+        // static cache, as the launch path's selection sweep does
+        // (inlined: as a call it put the kernel's by-value arguments in scratch)
+        uint64_t st;
+        if (sp.aff_class >= 0) {
+          [[clang::always_inline]] st = static_eval<true>(N, P, C, sp, cspec, rw.flags, n, P.A.mm_spec + 2 * (size_t)cspec);
+        } else {
+          [[clang::always_inline]] st = static_eval<false>(N, P, C, sp, cspec, rw.flags, n, nullptr);
+        }
         const uint32_t rs = row_reasons(N, P, C, sp, sci, rw, st, n);
 #ifndef KB_WA_NO_SWSTORES  // (write-accounting A/B: no key / static-cache stores -- stale keys)
         stat[n] = st;
@@ -4674,6 +4683,14 @@ __global__ __launch_bounds__(kSelThreads) void fed_engine_kernel(DevNodes N, Dev
         bprev[tid] = sh.node[tid];
         brow[tid] = row_after(sp, sh.row[tid], sh.fin[tid], sh.A[tid]);
       }
+      // an affinity unit's commits into the global tables (the first min(fin, A) commits on a node are Allocates,
+      // which join the lister tables; every commit adds to the histograms), before the publish below: the host issues
+      // a unit whose sweep reads them only after this one is read (the driver's dependency check)
+      if constexpr (!SHARD)
+        if (sp.aff_class >= 0 && tid < ns && sh.fin[tid] > 0) {
+          // (inlined: as a call it put the kernel's by-value arguments in scratch)
+          [[clang::always_inline]] apply_commit_tables(P.A, sp, sh.node[tid], min(sh.fin[tid], sh.A[tid]), sh.fin[tid]);
+        }
       nbprev = ns;
       if (sh.need_hist && MSEL > 1 && nsel > 1) {  // no fit, the table past one key plan: the histogram streamed (below)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this job's row stores, not stale cached rows
@@ -5015,7 +5032,8 @@ __device__ void block_ipa_minmax(const DevAff& A, const kb_aff_spec& as, int n, 
 
 // One block per spec: min / max of its InterPodAffinity counts over all nodes into mm[2 * block].
 __global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, DevSpecs P, const int32_t* spec_ids,
-                                                                 int spec, int64_t* mm, const JobState* js) {
+                                                                 int spec, int64_t* mm, const JobState* js,
+                                                                 int by_spec) {
   __shared__ int64_t rmin[16], rmax[16];
   if (js != nullptr && js->stopped) return;
   const int s = spec_ids ? spec_ids[blockIdx.x] : spec;
@@ -5064,9 +5082,10 @@ __global__ __launch_bounds__(kAffThreads) void ipa_minmax_kernel(DevNodes N, Dev
       }
     }
   }
-  if (threadIdx.x == 0) {
-    mm[2 * blockIdx.x] = mn;
-    mm[2 * blockIdx.x + 1] = mx;
+  if (threadIdx.x == 0) {  // (by_spec: into the spec's own pair, mm_spec)
+    const size_t o = by_spec ? (size_t)s : (size_t)blockIdx.x;
+    mm[2 * o] = mn;
+    mm[2 * o + 1] = mx;
   }
 }
 
@@ -5738,9 +5757,9 @@ static const void* const kAffRegFns[] = {KB_AFF_REG_FN(2), KB_AFF_REG_FN(4), KB_
 #undef KB_AFF_REG_NE
 
 void launch_ipa_minmax(const DevNodes& N, const DevSpecs& P, const int32_t* spec_ids, int spec, int count,
-                       int64_t* mm, const JobState* js, void* stream) {
+                       int64_t* mm, const JobState* js, void* stream, int by_spec) {
   hipLaunchKernelGGL(ipa_minmax_kernel, dim3(count), dim3(kAffThreads), 0, (hipStream_t)stream, N, P, spec_ids, spec,
-                     mm, js);
+                     mm, js, by_spec);
 }
 
 void launch_aff_place(const DevNodes& N, const DevSpecs& P, const DevCfg& C, int spec, int t_begin, int t_count,

@@ -93,6 +93,9 @@ void drop_affinity(kb_ctx* c) {
   c->spec_aff_err.clear();
   c->mm_eval = nullptr;
   c->mm_eval_cap = 0;
+  c->d_mm_ids = nullptr;
+  c->mm_ids_cap = 0;
+  c->mm_spec_ok.clear();
   c->spec_cap1.clear();
   c->spec_cls.clear();
   c->cls_coff.clear();
@@ -257,6 +260,7 @@ kb_ctx* kb_create(const kb_opts* opts) {
   c->fed_kernel_sweeps = (fl & KB_OPT_FED_KERNEL_SWEEPS) != 0;
   c->test_one_xcc = (fl & KB_OPT_TEST_ONE_XCC) != 0;
   c->no_lvl = (fl & KB_OPT_FED_NO_LEVELS) != 0;
+  c->use_fed_aff = !(fl & KB_OPT_FED_NO_AFF);
   c->fed_diag = (fl & KB_OPT_FED_DIAG) != 0;
   c->issue_trace = getenv("KB_HOST_TRACE") != nullptr;
   if (opts && opts->fed_idle_ms > 0) c->fed_idle = (uint64_t)opts->fed_idle_ms * 100000ull;
@@ -761,6 +765,13 @@ int kb_upload_affinity(kb_ctx* c, const kb_affinity* a) {
   int64_t* mm = nullptr;
   if ((rc = upload(c, c->aff_mem, &mm, (const int64_t*)nullptr, 2, false))) return rc;
   A.mm = mm;
+  int64_t* mm_spec = nullptr;  // (the fed engine's: kb_fed_ipa_prepare)
+  if ((rc = upload(c, c->aff_mem, &mm_spec, (const int64_t*)nullptr, 2 * (size_t)std::max<uint32_t>(a->m, 1), false)))
+    return rc;
+  A.mm_spec = mm_spec;
+  c->mm_spec_ok.assign(a->m, 0);
+  if ((rc = upload(c, c->aff_mem, &c->d_mm_ids, (const int32_t*)nullptr, std::max<uint32_t>(a->m, 1), false))) return rc;
+  c->mm_ids_cap = a->m;
   A.n = (int32_t)n;
   if (c->sharded) A.topo_dom += c->N.base;  // (aff_mem keeps the allocation's own pointer)
   // pristine copies of the mutable tables (kb_restore_nodes re-opens the session)
@@ -1734,16 +1745,59 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
   return ensure_slots(c, std::max<uint32_t>(max_tasks, 1), true);
 }
 
-int kb_spec_fed_ok(kb_ctx* c, int spec) {
+// A spec with inter-pod terms on the resident engine (kb_spec_fed_ok): one selection run whose own commits leave its
+// affinity inputs alone (or the cap-1 closed form, traj_key64), on the split engine with resident sweepers (which fold
+// the terms into the static cache with the spec's prepared min / max: fed_sweeper), one GPU. Its table commits are the
+// placer's (fed_engine_kernel, before the job's publish).
+static bool fed_aff_ok(const kb_ctx* c, int spec, bool need_mm) {
+  if (!c->use_fed_aff || c->sharded || !c->use_fed_split || !fed_split_ok(c->N.n, false)) return false;
+  if (c->fed_coop || c->fed_xcc < 0 || c->fed_xcc >= 8 || c->fed_kernel_sweeps) return false;  // (fed_sweepers_now)
+  if (c->spec_dyn[spec] && !c->cap1(spec)) return false;
+  if (c->spec_aff_err[spec] || c->spec_ipa_err[spec]) return false;
+  if (need_mm && c->spec_hist[spec] && !((size_t)spec < c->mm_spec_ok.size() && c->mm_spec_ok[spec])) return false;
+  return true;
+}
+
+static int spec_fed_ok_impl(kb_ctx* c, int spec, bool need_mm) {
   if (!c || spec < 0 || spec >= c->P.m) return 0;
   if ((c->sharded && !c->peer) || c->use_engine || !c->use_sel || !c->spec_traj_ok[spec]) return 0;
   if (c->sharded && !(c->use_fed_split && fed_split_ok(c->N.n, c->sharded))) return 0;  // the sharded engine is the split one
   const int ns = fed_nsel(c->N.n);  // past one workgroup's key plan: range selectors (split engine only)
   if (ns == 0 || (ns > 1 && !c->use_fed_split)) return 0;
   if (ns == 1 && (!c->sel_ok || !c->traj)) return 0;
-  if (c->aff_ok && c->spec_needs_aff[spec]) return 0;
+  if (c->aff_ok && c->spec_needs_aff[spec] && !fed_aff_ok(c, spec, need_mm)) return 0;
   if (c->host_reasons(spec)) return 0;  // its NO_FIT needs a mid-cycle kb_node_reasons (not beside the engine)
   return c->use_fed ? 1 : 0;
+}
+
+int kb_spec_fed_ok(kb_ctx* c, int spec) { return spec_fed_ok_impl(c, spec, true); }
+int kb_spec_fed_ok_pre(kb_ctx* c, int spec) { return spec_fed_ok_impl(c, spec, false); }
+
+int kb_fed_ipa_prepare(kb_ctx* c, const int32_t* specs, uint32_t n) {
+  if (!c) return KB_E_INVALID;
+  if (!c->aff_ok || n == 0) return KB_OK;
+  if (c->fed || c->fed_paused) return fail(c, KB_E_STATE, "kb_fed_ipa_prepare: the engine is running");
+  for (uint32_t i = 0; i < n; ++i)
+    if (specs[i] < 0 || specs[i] >= c->P.m) return fail(c, KB_E_INVALID, "kb_fed_ipa_prepare: spec %d", specs[i]);
+  if (n > c->mm_ids_cap) return fail(c, KB_E_INVALID, "kb_fed_ipa_prepare: %u specs, %u uploaded", n, c->mm_ids_cap);
+  HIP_OK(c, hipMemcpyAsync(c->d_mm_ids, specs, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  hipEvent_t ea;
+  c->ev_begin(&ea);
+  launch_ipa_minmax(c->N, c->P, c->d_mm_ids, 0, (int)n, c->P.A.mm_spec, nullptr, c->stream, 1);
+  c->ev_end(ea, KB_KERNEL_IPA_MINMAX, (uint64_t)c->N.n * n);
+  HIP_OK(c, hipGetLastError());
+  // (the engine's launch queues behind it on `stream`; the copy's host buffer is read before the call returns)
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (c->mm_spec_ok.size() < (size_t)c->P.m) c->mm_spec_ok.resize(c->P.m, 0);
+  for (uint32_t i = 0; i < n; ++i) c->mm_spec_ok[specs[i]] = 1;
+  return KB_OK;
+}
+
+int kb_fed_units_indep(const kb_ctx* c, int a, int b) {
+  if (!c->aff_ok || a < 0 || b < 0) return 1;
+  if ((size_t)b >= c->aff_rd.size() || c->aff_rd[b].empty()) return 1;  // b's sweep reads no table
+  if ((size_t)a >= c->aff_wr.size() || c->aff_wr[a].empty()) return 1;  // a's commits write none
+  return aff_sweep_indep(c, a, b) ? 1 : 0;
 }
 
 uint32_t kb_fed_unit_cap(kb_ctx* c) {
@@ -2114,6 +2168,7 @@ int kb_job_issue(kb_ctx* c, const kb_job_req* job, int slot, const kb_job_pred* 
     for (uint32_t i = 1; i < job->n_tasks; ++i)
       if (job->task_specs[i] != job->task_specs[0]) return fail(c, KB_E_INVALID, "fed engine: one run per job");
     if (!kb_spec_fed_ok(c, job->task_specs[0])) return fail(c, KB_E_INVALID, "fed engine: spec not eligible");
+    if (c->aff_ok && c->spec_needs_aff[job->task_specs[0]]) c->stats.fed_aff_units++;
     kb_ctx::JobSlot& S = c->slot[slot];
     S.t_issue = std::chrono::steady_clock::now();
     if (c->fed_diag) c->dg_iss0.push_back((S.t_issue - c->dg_t0).count());

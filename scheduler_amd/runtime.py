@@ -131,7 +131,8 @@ class kb_stats(C.Structure):
                 ("shard_phase_ticks", C.c_uint64 * 6), ("peer_checks", C.c_uint64), ("fed_wg_place", C.c_uint64 * 2),
                 ("off_engine_units", C.c_uint64), ("fed_pauses", C.c_uint64),
                 ("fed_mispredicts", C.c_uint64), ("fed_skipped", C.c_uint64), ("fed_units", C.c_uint64),
-                ("nofit_predicted", C.c_uint64), ("fed_last_depth", C.c_int32), ("fed_last_sweepers", C.c_int32)]
+                ("nofit_predicted", C.c_uint64), ("fed_last_depth", C.c_int32), ("fed_last_sweepers", C.c_int32),
+                ("fed_aff_units", C.c_uint64), ("fed_aff_waits", C.c_uint64)]
 
 
 KB_OPT_TIMING = 1
@@ -144,7 +145,7 @@ OPTION_FLAGS = {"no_fed": 1 << 4, "no_fed_split": 1 << 5, "no_pipeline": 1 << 6,
                 "no_cap1": 1 << 8, "no_cls": 1 << 9, "no_eval_plain": 1 << 10, "fed_shared_queues": 1 << 11,
                 "fed_plain_launch": 1 << 12, "shard_self_inbox": 1 << 13, "fed_diag": 1 << 14,
                 "fed_coop_launch": 1 << 15, "test_peer_badtag": 1 << 16, "fed_kernel_sweeps": 1 << 17,
-                "test_one_xcc": 1 << 18, "fed_no_levels": 1 << 19}
+                "test_one_xcc": 1 << 18, "fed_no_levels": 1 << 19, "fed_no_aff": 1 << 20}
 OPTION_VALUES = ("fed_idle_ms", "eval_spb", "test_stall_job", "test_stall_ms", "shard_epoch0", "fed_xcc", "fed_depth")
 KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_kernel", "traj_place_kernel",
            "aff_place_kernel", "ipa_minmax_kernel", "sel_place_kernel", "engine_kernel", "sel_sweep_kernel",
@@ -157,7 +158,7 @@ KERNELS = ("sweep_keys_kernel", "place_loop_kernel", "eval_kernel", "traj_sweep_
 PATHS = {"select": 0, "engine": KB_OPT_ENGINE, "trajectory": KB_OPT_NO_SELECT,
          "rekey": KB_OPT_NO_SELECT | KB_OPT_NO_TRAJECTORY}
 
-ABI_VERSION = 15  # include/kbgpu.h KBGPU_ABI_VERSION
+ABI_VERSION = 16  # include/kbgpu.h KBGPU_ABI_VERSION
 
 EXPORTS = ["kb_abi_version", "kb_create", "kb_destroy", "kb_last_error", "kb_set_config", "kb_upload_nodes",
            "kb_upload_specs", "kb_place_job", "kb_eval", "kb_eval32", "kb_read_nodes", "kb_allocate", "kb_restore_nodes",
@@ -415,7 +416,8 @@ class Context:
                 "fed_pauses": st.fed_pauses, "fed_mispredicts": st.fed_mispredicts, "fed_skipped": st.fed_skipped,
                 "fed_units": st.fed_units, "nofit_predicted": st.nofit_predicted,
                 "fed_last_depth": st.fed_last_depth,
-                "fed_last_sweepers": st.fed_last_sweepers}
+                "fed_last_sweepers": st.fed_last_sweepers, "fed_aff_units": st.fed_aff_units,
+                "fed_aff_waits": st.fed_aff_waits}
 
     def eval(self, spec_ids):
         ids = np.ascontiguousarray(np.asarray(spec_ids, dtype=np.int32))

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 15
+    assert runtime.load_library().kb_abi_version() == runtime.ABI_VERSION == 16
 
 
 def test_struct_layouts_match_header():

@@ -450,21 +450,27 @@ MIXED_CLUSTERS = [
 ]
 
 
+@pytest.mark.parametrize("aff_path", ["engine", "pause"])
 @pytest.mark.parametrize("name,cluster", MIXED_CLUSTERS, ids=[c[0] for c in MIXED_CLUSTERS])
-def test_mixed_cycle_matches_oracle(name, cluster):
-    """A cycle mixing engine units with units the engine does not take (inter-pod affinity): the driver pauses the
-    engine for those (nothing in flight), runs them on the launch path beside the idle engine, and hands the engine
-    its next unit flagged fresh (its bookkeeping of the previous jobs is void); a two-template job is two units of
-    one pop. Placements, statuses and FitErrors equal the oracle's."""
+def test_mixed_cycle_matches_oracle(name, cluster, aff_path):
+    """A cycle mixing plain units with inter-pod-affinity units (cap-1: required anti-affinity to the job's own pods
+    over hostname). On the split engine they are engine units by default (aff_path "engine": the resident sweepers fold
+    the terms into the static cache, the placer commits the tables before its publish). With option
+    fed_no_aff, and on the one-workgroup engine, the driver pauses the engine for them (nothing in flight), runs them
+    on the launch path beside the idle engine, and hands the engine its next unit flagged fresh. A two-template job
+    is two units of one pop. Placements, statuses and FitErrors equal the oracle's."""
     ref = pyoracle.allocate(cluster)
     st = {}
-    got = runtime.allocate(cluster, stats_out=st)
+    got = runtime.allocate(cluster, stats_out=st, options={"fed_no_aff": aff_path == "pause"})
     _compare(ref, got)
-    assert st["fed_cycles"] >= 1, st
+    assert st["fed_cycles"] == 1, st
+    split = st["fed_split"] >= 1
     if name == "C2M-multi-only":
-        assert st["off_engine_units"] == 0 and st["fed_cycles"] == 1, st
+        assert st["off_engine_units"] == 0 and st["fed_aff_units"] == 0, st
+    elif aff_path == "engine" and split:  # every affinity unit on the engine: no pause
+        assert st["off_engine_units"] == 0 and st["fed_pauses"] == 0 and st["fed_aff_units"] > 0, st
     else:  # the affinity units ran while the engine was paused (one launch for the whole cycle)
-        assert st["off_engine_units"] > 0 and st["fed_pauses"] > 0 and st["fed_cycles"] == 1, st
+        assert st["off_engine_units"] > 0 and st["fed_pauses"] > 0 and st["fed_aff_units"] == 0, st
 
 
 def _ratio_cluster(seed=77, n_nodes=3000, n_specs=48):
@@ -547,3 +553,81 @@ def test_affinity_sweep_overlap(kind):
         assert st["sweep_overlap"] > 0 and st["overlap_refused_tables"] == 0, st
     else:
         assert st["overlap_refused_tables"] > 0, st
+
+
+def _fed_aff_cluster(seed=91, n_nodes=2200, n_jobs=48, tasks=24):
+    """The split engine's affinity units and their limits, with every kind of inter-pod input:
+    own-job hostname anti-affinity (cap-1, independent units), a team anti-affinity shared by several jobs (a unit's
+    sweep reads the table an earlier unit's commits write: it waits for the chain to drain), required zone affinity
+    to running services (static checks), noisy pods that a running pod's preferred anti-affinity scores (a static
+    histogram: min / max prepared before the launch), and preferred rack affinity to another pending job's pods (a
+    histogram the cycle's commits write: those units stay on the launch path, the engine pauses)."""
+    rng = np.random.default_rng(seed)
+    GI = 1024 ** 3
+    cl = m.Cluster()
+    for i in range(n_nodes):
+        rack = i * 40 // n_nodes
+        cl.nodes.append(m.Node(name=f"n{i:05d}", alloc={m.CPU: 16000, m.MEMORY: 64 * GI, m.PODS: 110},
+                               labels={"kubernetes.io/hostname": f"n{i:05d}", "zone": f"z{rack // 8}",
+                                       "rack": f"r{rack}"}))
+    cl.queues.append(m.Queue(name="q"))
+    noisy_sel = {"labelSelector": {"matchLabels": {"noisy": "true"}}}
+    for k in range(30):  # running services in the first two zones; one carries the noisy terms
+        aff = None
+        if k == 0:
+            aff = {"podAntiAffinity": {"preferred": [{"weight": 10, "podAffinityTerm": dict(noisy_sel,
+                                                                                            topologyKey="zone")}]}}
+        node = int(rng.integers(0, n_nodes // 5 * 2))
+        cl.pods.append(m.Pod(ns="s", name=f"svc{k}", uid=f"s-svc{k}", node=f"n{node:05d}", phase="Running",
+                             labels={"app": "svc"}, affinity=aff,
+                             containers=[m.Container(req={m.CPU: 500, m.MEMORY: GI})]))
+    for j in range(n_jobs):
+        name = f"j{j:03d}"
+        cl.pod_groups.append(m.PodGroup(ns="t", name=name, queue="q", min_member=tasks // 2))
+        req = {m.CPU: int(rng.integers(1, 5)) * 250, m.MEMORY: int(rng.integers(1, 5)) * GI // 2}
+        labels = {"job": name}
+        kind = j % 6
+        aff = None
+        if kind == 0:
+            aff = {"podAntiAffinity": {"required": [{"labelSelector": {"matchLabels": {"job": name}},
+                                                     "topologyKey": "kubernetes.io/hostname"}]}}
+        elif kind == 1:
+            labels["team"] = "blue"
+            aff = {"podAntiAffinity": {"required": [{"labelSelector": {"matchLabels": {"team": "blue"}},
+                                                     "topologyKey": "kubernetes.io/hostname"}]}}
+        elif kind == 2:
+            aff = {"podAffinity": {"required": [{"labelSelector": {"matchLabels": {"app": "svc"}},
+                                                 "topologyKey": "zone"}]}}
+        elif kind == 3:
+            labels["noisy"] = "true"
+        elif kind == 4:
+            labels["team"] = "green"
+            aff = {"podAffinity": {"preferred": [{"weight": 30, "podAffinityTerm": {
+                "labelSelector": {"matchLabels": {"team": "red"}}, "topologyKey": "rack"}}]}}
+        else:
+            labels["team"] = "red"
+        for t in range(tasks):
+            cl.pods.append(m.Pod(ns="t", name=f"{name}-{t:03d}", uid=f"t-{name}-{t:03d}", group=name,
+                                 labels=dict(labels), affinity=aff, containers=[m.Container(req=dict(req))]))
+    return cl
+
+
+def test_fed_affinity_units_match_oracle():
+    """Affinity units on the resident engine against the oracle: placements, statuses and FitErrors equal, the
+    independent ones in flight together, the team units waiting for the chain, the green units (their histograms
+    move with the red jobs' commits) on the launch path while the engine pauses; and the same with the engine's
+    affinity units off (option fed_no_aff: every unit of this cycle has inter-pod inputs, so it runs without the
+    engine)."""
+    cl = _fed_aff_cluster()
+    ref = pyoracle.allocate(cl)
+    st = {}
+    got = runtime.allocate(cl, stats_out=st)
+    _compare(ref, got)
+    assert st["fed_cycles"] == 1 and st["fed_split"] == 1, st
+    assert st["fed_aff_units"] > 0 and st["fed_aff_waits"] > 0, st
+    assert st["off_engine_units"] > 0 and st["fed_pauses"] > 0, st
+    st2 = {}
+    got2 = runtime.allocate(cl, stats_out=st2, options={"fed_no_aff": True})
+    _compare(ref, got2)
+    # (every unit of this cycle has inter-pod inputs: without them the engine has nothing, the cycle is launch path)
+    assert st2["fed_aff_units"] == 0 and st2["fed_cycles"] == 0, st2
