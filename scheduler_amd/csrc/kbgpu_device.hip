@@ -4009,6 +4009,13 @@ __device__ __forceinline__ int shard_place(SelShared& sh, uint32_t* k32, uint64_
     }
     if (tid == 0) sh.n_commit = base_c + __popcll(b_lo) + __popcll(b_hi);
   }
+  // an affinity unit's table commits, on every rank for every placement (the count tables and histograms are
+  // replicated: topo_dom covers the whole cluster from this rank's first row), before the job's publish
+  if (sp.aff_class >= 0 && tid < cut) {
+    const int nk = ordnk[tid];
+    [[clang::always_inline]] apply_commit_tables(P.A, sp, (nk & 0x3fffffff) - N.base,
+                                                 ((uint32_t)nk >> 30) == KB_PLACE_ALLOCATE ? 1 : 0, 1);
+  }
   placed = cut;
   ready = ready0 + G.n_alloc;
   const uint64_t t_hist0 = __builtin_amdgcn_s_memrealtime();

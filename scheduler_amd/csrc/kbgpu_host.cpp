@@ -1750,7 +1750,10 @@ int kb_job_reserve(kb_ctx* c, uint32_t max_tasks) {
 // the terms into the static cache with the spec's prepared min / max: fed_sweeper), one GPU. Its table commits are the
 // placer's (fed_engine_kernel, before the job's publish).
 static bool fed_aff_ok(const kb_ctx* c, int spec, bool need_mm) {
-  if (!c->use_fed_aff || c->sharded || !c->use_fed_split || !fed_split_ok(c->N.n, false)) return false;
+  if (!c->use_fed_aff || !c->use_fed_split || !fed_split_ok(c->N.n, c->sharded)) return false;
+  // node-sharded: the peer engine (replicated tables: every rank commits every placement's increments); a spec with
+  // histograms needs the whole-cluster min / max, reduced through the host all-gather (kb_fed_ipa_prepare)
+  if (c->sharded && (!c->peer || (c->spec_hist[spec] && !c->ag_fn))) return false;
   if (c->fed_coop || c->fed_xcc < 0 || c->fed_xcc >= 8 || c->fed_kernel_sweeps) return false;  // (fed_sweepers_now)
   if (c->spec_dyn[spec] && !c->cap1(spec)) return false;
   if (c->spec_aff_err[spec] || c->spec_ipa_err[spec]) return false;
@@ -1788,6 +1791,29 @@ int kb_fed_ipa_prepare(kb_ctx* c, const int32_t* specs, uint32_t n) {
   HIP_OK(c, hipGetLastError());
   // (the engine's launch queues behind it on `stream`; the copy's host buffer is read before the call returns)
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (c->sharded) {  // each rank's min / max over its own rows, then the min of the minima and the max of the maxima
+    if (!c->ag_fn) return fail(c, KB_E_STATE, "kb_fed_ipa_prepare: node-sharded without the host all-gather");
+    const int W = c->shard.world;
+    const size_t m2 = 2 * (size_t)std::max(c->P.m, 1);
+    std::vector<int64_t> all(m2), mine(2 * (size_t)n), got(2 * (size_t)n * W);
+    HIP_OK(c, hipMemcpy(all.data(), c->P.A.mm_spec, m2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) {
+      mine[2 * i] = all[2 * (size_t)specs[i]];
+      mine[2 * i + 1] = all[2 * (size_t)specs[i] + 1];
+    }
+    if (int rc = c->ag_fn(c->ag_user, mine.data(), got.data(), mine.size() * sizeof(int64_t)))
+      return fail(c, KB_E_HIP, "all-gather callback failed (%d)", rc);
+    for (uint32_t i = 0; i < n; ++i) {
+      int64_t mn = got[2 * i], mx = got[2 * i + 1];
+      for (int w = 1; w < W; ++w) {
+        mn = std::min(mn, got[2 * ((size_t)w * n + i)]);
+        mx = std::max(mx, got[2 * ((size_t)w * n + i) + 1]);
+      }
+      all[2 * (size_t)specs[i]] = mn;
+      all[2 * (size_t)specs[i] + 1] = mx;
+    }
+    HIP_OK(c, hipMemcpy(c->P.A.mm_spec, all.data(), m2 * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
   if (c->mm_spec_ok.size() < (size_t)c->P.m) c->mm_spec_ok.resize(c->P.m, 0);
   for (uint32_t i = 0; i < n; ++i) c->mm_spec_ok[specs[i]] = 1;
   return KB_OK;

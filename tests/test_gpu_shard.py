@@ -400,6 +400,7 @@ def _aff_rank_main(rank, world, port, q, peer=False):
                 ctx.upload(snap)
                 r = runtime.result_dict(snap, ctx.allocate(snap))
                 res[name] = {k: r[k] for k in ("events", "binds", "fit_errors")}
+                res[name]["fed_aff_units"] = ctx.stats()["fed_aff_units"]
             finally:
                 ctx.close()
         q.put((rank, res, None))
@@ -413,7 +414,9 @@ def _aff_rank_main(rank, world, port, q, peer=False):
 def test_sharded_affinity_matches_oracle(world, exchange):
     """Replicated count tables and histograms, one whole-cluster IPA min / max per run (or per task), every
     commit applied on every rank: the oracle's events, binds and FitErrors on every affinity cluster (C4 shapes,
-    the edge clusters, the self-affinity clusters whose specs run one task per segment or as cap-1 runs)."""
+    the edge clusters, the self-affinity clusters whose specs run one task per segment or as cap-1 runs). peer: the
+    affinity units the node-sharded engine takes run on it (each rank commits every placement's
+    table increments; the histogram specs' min / max reduced over the ranks before the launch)."""
     import torch.multiprocessing as mp
     from oracle import pyoracle
     ref = {name: pyoracle.allocate(cl) for name, cl in _aff_cases().items()}
@@ -434,3 +437,6 @@ def test_sharded_affinity_matches_oracle(world, exchange):
         for name, o in ref.items():
             for k in ("events", "binds", "fit_errors"):
                 assert got[r][name][k] == o[k], (world, r, name, k)
+            assert got[r][name]["fed_aff_units"] == got[0][name]["fed_aff_units"], (r, name)
+    if exchange == "peer":
+        assert sum(v["fed_aff_units"] for v in got[0].values()) > 0, {k: v["fed_aff_units"] for k, v in got[0].items()}

@@ -233,7 +233,7 @@ def test_peer_preflight_fails_loudly(world):
         assert code == runtime.KB_E_STATE and "pre-flight" in msg and "from rank 1" in msg, (r, msg)
 
 
-def _mixed_rank_main(rank, world, port, q, cluster):
+def _mixed_rank_main(rank, world, port, q, cluster, options=None):
     import torch
     import torch.distributed as dist
     from scheduler_amd import export as E
@@ -247,7 +247,7 @@ def _mixed_rank_main(rank, world, port, q, cluster):
         return b"".join(bytes(o.tolist()) for o in outs)
     try:
         snap = E.Snapshot(cluster)
-        ctx = runtime.Context(0)
+        ctx = runtime.Context(0, options=options)
         try:
             ctx.set_shard(rank, world, snap.n_nodes, allgather=allgather, peer=True)
             ctx.upload(snap)
@@ -260,18 +260,22 @@ def _mixed_rank_main(rank, world, port, q, cluster):
             st = ctx.stats()
         finally:
             ctx.close()
-        q.put((rank, (out, st["fed_sharded"], st["fed_pauses"], st["off_engine_units"], st["fed_abandon"]), None))
+        q.put((rank, (out, st["fed_sharded"], st["fed_pauses"], st["off_engine_units"], st["fed_abandon"],
+                      st["fed_aff_units"]), None))
     except Exception as e:  # report, do not hang the parent
         q.put((rank, None, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_peer_engine_mixed_cycle_two_ranks():
+@pytest.mark.parametrize("aff_path", ["engine", "pause"])
+def test_peer_engine_mixed_cycle_two_ranks(aff_path):
     """A node-sharded mixed cycle (C2M shape: two-template jobs, which stay on the engine as units, and jobs with
-    required anti-affinity over hostname, which pause every rank's engine and run through the host-staged exchange):
-    both ranks equal the oracle, twice, and every rank pauses at the same units -- the pause's bound is a unit
-    count, not a rank's own clock, so no rank relaunches its engine (a new exchange epoch) while a peer resumes."""
+    required anti-affinity over hostname): both ranks equal the oracle, twice. engine: the anti-affinity jobs are
+    cap-1 units of the peer engine too (every rank commits every placement's table increments), no
+    pause. pause (option fed_no_aff): they pause every rank's engine and run through the host-staged exchange, and
+    every rank pauses at the same units -- the pause's bound is a unit count, not a rank's own clock, so no rank
+    relaunches its engine (a new exchange epoch) while a peer resumes."""
     import torch.multiprocessing as mp
     from oracle import pyoracle
     world = 2
@@ -280,7 +284,8 @@ def test_peer_engine_mixed_cycle_two_ranks():
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_mixed_rank_main, args=(r, world, port, q, cl)) for r in range(world)]
+    opts = {"fed_no_aff": aff_path == "pause"}
+    procs = [ctxm.Process(target=_mixed_rank_main, args=(r, world, port, q, cl, opts)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -293,9 +298,13 @@ def test_peer_engine_mixed_cycle_two_ranks():
         for p in procs:
             p.join(timeout=60)
     for r in range(world):
-        out, n_sharded, n_pauses, n_off, n_abandon = got[r]
-        assert n_abandon == 0 and n_sharded >= 2 and n_off > 0, (r, n_sharded, n_pauses, n_off)
-        assert (n_sharded, n_pauses, n_off) == got[0][1:4], (r, got[r][1:], got[0][1:])
+        out, n_sharded, n_pauses, n_off, n_abandon, n_aff = got[r]
+        assert n_abandon == 0 and n_sharded >= 2, (r, n_sharded, n_pauses, n_off)
+        if aff_path == "pause":
+            assert n_off > 0 and n_aff == 0, (r, n_sharded, n_pauses, n_off, n_aff)
+        else:
+            assert n_off == 0 and n_pauses == 0 and n_aff > 0, (r, n_sharded, n_pauses, n_off, n_aff)
+        assert got[r][1:] == got[0][1:], (r, got[r][1:], got[0][1:])
         for c in out:
             for k in ("events", "binds", "fit_errors"):
                 assert c[k] == ref[k], (r, k)
