@@ -21,62 +21,75 @@
 
 namespace {
 
-// One host helper thread per process: kb_allocate builds the cycle's pending lists on it while its own thread walks the
-// tasks for the plugins' session-open state (two independent passes over the session's task arrays, ~0.2 ms each on
-// C2's 100k tasks, before the first job can be issued). A driver that finds it busy (another context's cycle in
-// another thread) runs the work itself.
-class HostHelper {
+// Host helper threads (two per process): kb_allocate builds the cycle's pending lists on one and walks the second
+// half of the tasks for the session-open state on the other while its own thread walks the first half (independent
+// passes over the session's task arrays, ~0.2 ms each on C2's 100k tasks, before the first job can be issued). A
+// driver that finds no worker free (another context's cycle in another thread) runs the work itself.
+class HostPool {
  public:
-  static HostHelper& get() {
-    static HostHelper h;
+  static constexpr int kWorkers = 2;
+  static HostPool& get() {
+    static HostPool h;
     return h;
   }
-  bool post(std::function<void()> f) {
-    std::unique_lock<std::mutex> lk(mu_);
-    if (busy_) return false;
-    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
-    job_ = std::move(f);
-    busy_ = true;
-    cv_.notify_one();
-    return true;
+  // the worker that takes f, or -1 (none free: run it yourself)
+  int post(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < kWorkers; ++i) {
+      Worker& w = w_[i];
+      if (w.busy) continue;
+      if (!w.th.joinable()) w.th = std::thread([this, i] { loop(i); });
+      w.job = std::move(f);
+      w.busy = true;
+      cv_.notify_all();
+      return i;
+    }
+    return -1;
   }
-  void join() {
+  void join(int i) {
+    if (i < 0) return;
     std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [this] { return !busy_; });
+    done_.wait(lk, [&] { return !w_[i].busy; });
   }
-  ~HostHelper() {
+  ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
     }
-    cv_.notify_one();
-    if (th_.joinable()) th_.join();
+    cv_.notify_all();
+    for (Worker& w : w_)
+      if (w.th.joinable()) w.th.join();
   }
 
  private:
-  void loop() {
+  struct Worker {
+    std::thread th;
+    std::function<void()> job;
+    bool busy = false;
+  };
+  void loop(int i) {
+    Worker& w = w_[i];
     for (;;) {
       std::function<void()> f;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return stop_ || job_ != nullptr; });
+        cv_.wait(lk, [&] { return stop_ || w.job != nullptr; });
         if (stop_) return;
-        f = std::move(job_);
-        job_ = nullptr;
+        f = std::move(w.job);
+        w.job = nullptr;
       }
       f();
       {
         std::lock_guard<std::mutex> lk(mu_);
-        busy_ = false;
+        w.busy = false;
       }
       done_.notify_all();
     }
   }
   std::mutex mu_;
   std::condition_variable cv_, done_;
-  std::function<void()> job_;
-  bool busy_ = false, stop_ = false;
-  std::thread th_;
+  Worker w_[kWorkers];
+  bool stop_ = false;
 };
 
 constexpr double kMinMilliCPU = 10, kMinMemory = 10 * 1024 * 1024, kMinMilliScalar = 10;  // resource_info.go:70-72
@@ -341,14 +354,68 @@ struct Driver {
     return queues[q].deserved.less_equal(queues[q].allocated);
   }
 
+  // init()'s task pass over the second half of the tasks, on a helper thread: the jobs' counts, the allocated-status
+  // tasks (their DRF sums and Allocated lists are replayed in task order by init()), and the queues' proportion sums
+  // of this half. exact: every cpu / memory request summed here is a non-negative integer and none has scalars --
+  // then, with the totals below 2^53, every partial sum is exact and first half + second half equals the task-order
+  // sum bit for bit; else init() sums this half again in task order.
+  struct TailPass {
+    uint32_t t0 = 0, t1 = 0;
+    std::vector<int32_t> ready, waiting, valid;
+    std::vector<int> alloc;
+    std::vector<double> q;  // per queue: allocated cpu, memory, request cpu, memory
+    bool exact = true;
+  } tail;
+  static bool exact_int(double x) { return x >= 0 && x < 9007199254740992.0 && x == (double)(int64_t)x; }
+  void tail_pass(bool prop) {
+    TailPass& T = tail;
+    T.ready.assign(s.n_jobs, 0);
+    T.waiting.assign(s.n_jobs, 0);
+    T.valid.assign(s.n_jobs, 0);
+    T.alloc.clear();
+    T.q.assign(4 * (size_t)s.n_queues, 0.0);
+    bool exact = true;
+    const uint64_t sc_bits = S >= 64 ? ~0ull : (1ull << S) - 1;  // (add_scalars reads these bits only)
+    for (uint32_t t = T.t0; t < T.t1; ++t) {
+      const int j = s.task_job[t], st = s.task_status[t];
+      const bool al = allocated_status(st);
+      T.ready[j] += (al || st == KB_ST_SUCCEEDED) ? 1 : 0;
+      T.waiting[j] += st == KB_ST_PIPELINED ? 1 : 0;
+      T.valid[j] += (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) ? 1 : 0;
+      if (al) T.alloc.push_back((int)t);
+      if (prop && (al || st == KB_ST_PENDING)) {
+        const double* p = task_req(t);
+        double* q = T.q.data() + 4 * (size_t)s.job_queue[j];
+        exact = exact && exact_int(p[0]) && exact_int(p[1]) && (s.task_resreq_mask[t] & sc_bits) == 0;
+        if (al) {
+          q[0] += p[0];
+          q[1] += p[1];
+        }
+        q[2] += p[0];
+        q[3] += p[1];
+      }
+    }
+    T.exact = exact;
+  }
+
   int init() {
     const auto i0 = std::chrono::steady_clock::now();
-    // the pending lists (run()) on the helper thread, beside this task pass (both only read the session)
-    const bool helped = HostHelper::get().post([this] { build_pend(); });
+    // the pending lists (run()) on a helper thread, beside this task pass (both only read the session)
+    const int w_pend = HostPool::get().post([this] { build_pend(); });
     for (uint32_t i = 0; i < s.n_tier_plugins; ++i) {
       int p = s.tier_plugins[i].plugin;
       if (p >= 0 && p < 8) has[p] = true;
       if (p == KB_PLUGIN_PRIORITY && (s.tier_plugins[i].enable & KB_EN_TASK_ORDER)) task_prio = true;
+    }
+    const bool prop = has[KB_PLUGIN_PROPORTION];
+    // the second half of the task pass on the other helper (large sessions: the split pays for the thread hand-off)
+    uint32_t h = s.n_tasks;
+    int w_tail = -1;
+    if (s.n_tasks >= 32768) {
+      tail.t0 = h = s.n_tasks / 2;
+      tail.t1 = s.n_tasks;
+      w_tail = HostPool::get().post([this, prop] { tail_pass(prop); });
+      if (w_tail < 0) h = s.n_tasks;  // (no worker free: one pass)
     }
     total.S = S;
     for (int i = 0; i < 2 + S; ++i) total.v[i] = s.total_alloc[i];
@@ -364,9 +431,9 @@ struct Driver {
     // one pass over the tasks: the jobs' counts and DRF allocations, and (proportion) the queues' allocated /
     // request sums -- the latter in task order with cpu and memory in registers while the queue stays the same (the
     // same float additions in the same order as one add_raw per task)
-    const bool prop = has[KB_PLUGIN_PROPORTION];
     int cq = -1;
     double ac = 0, am = 0, rc = 0, rm = 0;
+    bool exact = true;  // (as TailPass::exact, for this half's cpu / memory sums)
     const auto flush = [&]() {
       if (cq < 0) return;
       queues[cq].allocated.v[0] = ac;
@@ -374,7 +441,30 @@ struct Driver {
       queues[cq].request.v[0] = rc;
       queues[cq].request.v[1] = rm;
     };
-    for (uint32_t t = 0; t < s.n_tasks; ++t) {
+    // proportion.go:72-81 (OnSessionOpen's task walk): task t's requests into its queue's sums
+    const auto prop_add = [&](uint32_t t, int j, bool al) {
+      const int qi = s.job_queue[j];
+      if (qi != cq) {
+        flush();
+        cq = qi;
+        ac = queues[qi].allocated.v[0];
+        am = queues[qi].allocated.v[1];
+        rc = queues[qi].request.v[0];
+        rm = queues[qi].request.v[1];
+      }
+      const double* p = task_req(t);
+      const uint64_t m = s.task_resreq_mask[t];
+      exact = exact && exact_int(p[0]) && exact_int(p[1]);
+      if (al) {
+        ac += p[0];
+        am += p[1];
+        queues[qi].allocated.add_scalars(p, m);
+      }
+      rc += p[0];
+      rm += p[1];
+      queues[qi].request.add_scalars(p, m);
+    };
+    for (uint32_t t = 0; t < h; ++t) {
       int j = s.task_job[t], st = task_status[t];
       const bool al = allocated_status(st);
       if (al || st == KB_ST_SUCCEEDED) jobs[j].ready++;
@@ -382,40 +472,60 @@ struct Driver {
       if (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
       if (st == KB_ST_ALLOCATED) job_allocated[j].push_back((int)t);
       if (al) jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
-      if (prop && (al || st == KB_ST_PENDING)) {  // proportion.go:72-81 (OnSessionOpen's task walk)
-        const int qi = s.job_queue[j];
-        if (qi != cq) {
-          flush();
-          cq = qi;
-          ac = queues[qi].allocated.v[0];
-          am = queues[qi].allocated.v[1];
-          rc = queues[qi].request.v[0];
-          rm = queues[qi].request.v[1];
-        }
-        const double* p = task_req(t);
-        const uint64_t m = s.task_resreq_mask[t];
-        if (al) {
-          ac += p[0];
-          am += p[1];
-          queues[qi].allocated.add_scalars(p, m);
-        }
-        rc += p[0];
-        rm += p[1];
-        queues[qi].request.add_scalars(p, m);
-      }
+      if (prop && (al || st == KB_ST_PENDING)) prop_add(t, j, al);
     }
     flush();
-    if (helped) HostHelper::get().join();
+    if (h < s.n_tasks) {  // the second half's results, in task order where order matters
+      HostPool::get().join(w_tail);
+      for (uint32_t j = 0; j < s.n_jobs; ++j) {
+        jobs[j].ready += tail.ready[j];
+        jobs[j].waiting += tail.waiting[j];
+        jobs[j].valid += tail.valid[j];
+      }
+      for (int t : tail.alloc) {
+        const int j = s.task_job[t];
+        if (task_status[t] == KB_ST_ALLOCATED) job_allocated[j].push_back(t);
+        jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
+      }
+      if (prop) {
+        bool ok = exact && tail.exact;
+        if (ok)
+          for (uint32_t q = 0; q < s.n_queues && ok; ++q) {
+            const double* x = tail.q.data() + 4 * (size_t)q;
+            ok = exact_int(queues[q].allocated.v[0] + x[0]) && exact_int(queues[q].allocated.v[1] + x[1]) &&
+                 exact_int(queues[q].request.v[0] + x[2]) && exact_int(queues[q].request.v[1] + x[3]);
+          }
+        if (ok) {
+          for (uint32_t q = 0; q < s.n_queues; ++q) {
+            const double* x = tail.q.data() + 4 * (size_t)q;
+            queues[q].allocated.v[0] += x[0];
+            queues[q].allocated.v[1] += x[1];
+            queues[q].request.v[0] += x[2];
+            queues[q].request.v[1] += x[3];
+          }
+        } else {  // the second half's sums again, in task order after the first half's
+          cq = -1;
+          for (uint32_t t = h; t < s.n_tasks; ++t) {
+            const int st = task_status[t];
+            const bool al = allocated_status(st);
+            if (al || st == KB_ST_PENDING) prop_add(t, s.task_job[t], al);
+          }
+          flush();
+        }
+      }
+    }
+    if (w_pend >= 0) HostPool::get().join(w_pend);
     else build_pend();
     const auto i1 = std::chrono::steady_clock::now();
     for (uint32_t j = 0; j < s.n_jobs; ++j) jobs[j].drf_share = dominant_share(jobs[j].drf_alloc, total);
     const auto i2 = std::chrono::steady_clock::now();
     if (prop) open_proportion();
     if (ctx->issue_trace)
-      fprintf(stderr, "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f\n",
+      fprintf(stderr, "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f split=%d\n",
               std::chrono::duration<double, std::milli>(i1 - i0).count(),
               std::chrono::duration<double, std::milli>(i2 - i1).count(),
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count());
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count(),
+              h < s.n_tasks ? 1 : 0);
     return KB_OK;
   }
 
@@ -506,26 +616,56 @@ struct Driver {
     jorder.resize(s.n_jobs);
     for (uint32_t j = 0; j < s.n_jobs; ++j) jorder[j] = (int)j;
     std::sort(jorder.begin(), jorder.end(), [&](int a, int b) { return s.job_uid_rank[a] < s.job_uid_rank[b]; });
-    pend_off.assign(s.n_jobs + 1, 0);
-    for (uint32_t t = 0; t < s.n_tasks; ++t)
-      if (s.task_status[t] == KB_ST_PENDING) ++pend_off[s.task_job[t] + 1];
-    max_pending = 1;
-    for (uint32_t j = 0; j < s.n_jobs; ++j) {
-      max_pending = std::max<uint32_t>(max_pending, pend_off[j + 1]);
-      pend_off[j + 1] += pend_off[j];
-    }
-    pend.resize(pend_off[s.n_jobs]);
     pend_all = pend_eng = 0;
     jobs_pend = jobs_off = 0;
-    std::vector<uint32_t> cur(pend_off.begin(), pend_off.end() - 1);
-    for (uint32_t t = 0; t < s.n_tasks; ++t)
-      if (s.task_status[t] == KB_ST_PENDING) {
-        pend[cur[s.task_job[t]]++] = (int)t;
-        if (!task_res_empty(t)) {
-          ++pend_all;
-          pend_eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
+    // tasks grouped by job in job order (the exporters' layout): one pass appends each job's pending tasks and closes
+    // its CSR range; otherwise (the pass meets a smaller job index) the count pass and the fill pass
+    pend_off.assign(s.n_jobs + 1, 0);
+    pend.resize(s.n_tasks);
+    bool grouped = true;
+    {
+      uint32_t k = 0;
+      int last = -1;
+      for (uint32_t t = 0; t < s.n_tasks; ++t) {
+        const int j = s.task_job[t];
+        if (j != last) {
+          if (j < last) {
+            grouped = false;
+            break;
+          }
+          for (int jj = last + 1; jj <= j; ++jj) pend_off[jj] = k;
+          last = j;
+        }
+        if (s.task_status[t] == KB_ST_PENDING) {
+          pend[k++] = (int)t;
+          if (!task_res_empty(t)) {
+            ++pend_all;
+            pend_eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
+          }
         }
       }
+      if (grouped)
+        for (uint32_t jj = (uint32_t)(last + 1); jj <= s.n_jobs; ++jj) pend_off[jj] = k;
+    }
+    if (!grouped) {
+      pend_all = pend_eng = 0;
+      pend_off.assign(s.n_jobs + 1, 0);
+      for (uint32_t t = 0; t < s.n_tasks; ++t)
+        if (s.task_status[t] == KB_ST_PENDING) ++pend_off[s.task_job[t] + 1];
+      for (uint32_t j = 0; j < s.n_jobs; ++j) pend_off[j + 1] += pend_off[j];
+      std::vector<uint32_t> cur(pend_off.begin(), pend_off.end() - 1);
+      for (uint32_t t = 0; t < s.n_tasks; ++t)
+        if (s.task_status[t] == KB_ST_PENDING) {
+          pend[cur[s.task_job[t]]++] = (int)t;
+          if (!task_res_empty(t)) {
+            ++pend_all;
+            pend_eng += spec_fed_ok(s.task_spec[t]) ? 1 : 0;
+          }
+        }
+    }
+    pend.resize(pend_off[s.n_jobs]);
+    max_pending = 1;
+    for (uint32_t j = 0; j < s.n_jobs; ++j) max_pending = std::max<uint32_t>(max_pending, pend_off[j + 1] - pend_off[j]);
     for (uint32_t j = 0; j < s.n_jobs; ++j)
       if (pend_off[j + 1] > pend_off[j]) {
         ++jobs_pend;

@@ -1,2 +1,2 @@
 set -u
-TAG=${TAG} TESTS="${TESTS}" LINES="${LINES}" LIBLINES="${LIBLINES:-}" bash scripts/ab_lines.sh || exit $?
+TAG=${TAG} TESTS="${TESTS:-}" LINES="${LINES:-}" LIBLINES="${LIBLINES:-}" bash scripts/ab_lines.sh || exit $?
