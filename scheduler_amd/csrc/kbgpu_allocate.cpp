@@ -5,6 +5,7 @@
 // the job's ordered pending tasks to kb_place_job (device), then replays the placements into the
 // host-side job / share state the ordering reads.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -24,10 +25,13 @@ namespace {
 // Host helper threads (two per process): kb_allocate builds the cycle's pending lists on one and walks the second
 // half of the tasks for the session-open state on the other while its own thread walks the first half (independent
 // passes over the session's task arrays, ~0.2 ms each on C2's 100k tasks, before the first job can be issued). A
-// driver that finds no worker free (another context's cycle in another thread) runs the work itself.
+// driver that finds no worker free (another context's cycle in another thread) runs the work itself. A worker spins
+// for kSpin after its last job before it sleeps, and join() spins before it waits: a futex wake-up costs as much as
+// the work (cycles come every ~16 ms on C2, so a serving loop's workers never sleep).
 class HostPool {
  public:
   static constexpr int kWorkers = 2;
+  static constexpr auto kSpin = std::chrono::milliseconds(40);
   static HostPool& get() {
     static HostPool h;
     return h;
@@ -37,10 +41,11 @@ class HostPool {
     std::lock_guard<std::mutex> lk(mu_);
     for (int i = 0; i < kWorkers; ++i) {
       Worker& w = w_[i];
-      if (w.busy) continue;
+      if (w.busy.load(std::memory_order_relaxed)) continue;
       if (!w.th.joinable()) w.th = std::thread([this, i] { loop(i); });
       w.job = std::move(f);
-      w.busy = true;
+      w.busy.store(true, std::memory_order_relaxed);
+      w.has_job.store(true, std::memory_order_release);
       cv_.notify_all();
       return i;
     }
@@ -48,13 +53,16 @@ class HostPool {
   }
   void join(int i) {
     if (i < 0) return;
+    Worker& w = w_[i];
+    const auto t0 = std::chrono::steady_clock::now();
+    while (w.busy.load(std::memory_order_acquire) && std::chrono::steady_clock::now() - t0 < kSpin) __builtin_ia32_pause();
     std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return !w_[i].busy; });
+    done_.wait(lk, [&] { return !w.busy.load(std::memory_order_acquire); });
   }
   ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+      stop_.store(true);
     }
     cv_.notify_all();
     for (Worker& w : w_)
@@ -65,23 +73,28 @@ class HostPool {
   struct Worker {
     std::thread th;
     std::function<void()> job;
-    bool busy = false;
+    std::atomic<bool> busy{false}, has_job{false};
   };
   void loop(int i) {
     Worker& w = w_[i];
     for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!w.has_job.load(std::memory_order_acquire) && !stop_.load(std::memory_order_relaxed) &&
+             std::chrono::steady_clock::now() - t0 < kSpin)
+        __builtin_ia32_pause();
       std::function<void()> f;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || w.job != nullptr; });
-        if (stop_) return;
+        cv_.wait(lk, [&] { return stop_.load() || w.job != nullptr; });
+        if (stop_.load()) return;
         f = std::move(w.job);
         w.job = nullptr;
+        w.has_job.store(false, std::memory_order_relaxed);
       }
       f();
       {
         std::lock_guard<std::mutex> lk(mu_);
-        w.busy = false;
+        w.busy.store(false, std::memory_order_release);
       }
       done_.notify_all();
     }
@@ -89,7 +102,7 @@ class HostPool {
   std::mutex mu_;
   std::condition_variable cv_, done_;
   Worker w_[kWorkers];
-  bool stop_ = false;
+  std::atomic<bool> stop_{false};
 };
 
 constexpr double kMinMilliCPU = 10, kMinMemory = 10 * 1024 * 1024, kMinMilliScalar = 10;  // resource_info.go:70-72
@@ -354,47 +367,68 @@ struct Driver {
     return queues[q].deserved.less_equal(queues[q].allocated);
   }
 
-  // init()'s task pass over the second half of the tasks, on a helper thread: the jobs' counts, the allocated-status
-  // tasks (their DRF sums and Allocated lists are replayed in task order by init()), and the queues' proportion sums
-  // of this half. exact: every cpu / memory request summed here is a non-negative integer and none has scalars --
-  // then, with the totals below 2^53, every partial sum is exact and first half + second half equals the task-order
-  // sum bit for bit; else init() sums this half again in task order.
-  struct TailPass {
+  // init()'s task pass over a range of the tasks (the first half on init()'s thread, the second on a helper): the
+  // jobs' counts, the allocated-status tasks (their DRF sums and Allocated lists are then replayed in task order), and
+  // the queues' proportion sums of the range (proportion.go:72-81, OnSessionOpen's task walk). Counts and sums stay in
+  // registers while the job stays the same, the sums in two accumulators. exact: every cpu / memory request summed is
+  // a non-negative integer and none has scalars -- then, with the totals below 2^53, every partial sum is exact and
+  // the split sums equal the task-order sums bit for bit; else init() sums every task again in task order.
+  struct TaskPass {
     uint32_t t0 = 0, t1 = 0;
     std::vector<int32_t> ready, waiting, valid;
     std::vector<int> alloc;
     std::vector<double> q;  // per queue: allocated cpu, memory, request cpu, memory
     bool exact = true;
-  } tail;
+  } head, tail;
   static bool exact_int(double x) { return x >= 0 && x < 9007199254740992.0 && x == (double)(int64_t)x; }
-  void tail_pass(bool prop) {
-    TailPass& T = tail;
+  void task_pass(TaskPass& T, bool prop) {
     T.ready.assign(s.n_jobs, 0);
     T.waiting.assign(s.n_jobs, 0);
     T.valid.assign(s.n_jobs, 0);
     T.alloc.clear();
     T.q.assign(4 * (size_t)s.n_queues, 0.0);
-    bool exact = true;
     const uint64_t sc_bits = S >= 64 ? ~0ull : (1ull << S) - 1;  // (add_scalars reads these bits only)
+    bool exact = true;
+    int cj = -1;
+    int32_t r = 0, w = 0, v = 0;
+    double a[2][2] = {}, q[2][2] = {};  // [accumulator][cpu, memory]: allocated, request
+    const auto flush = [&]() {
+      if (cj < 0) return;
+      T.ready[cj] += r;
+      T.waiting[cj] += w;
+      T.valid[cj] += v;
+      double* x = T.q.data() + 4 * (size_t)s.job_queue[cj];
+      x[0] += a[0][0] + a[1][0];
+      x[1] += a[0][1] + a[1][1];
+      x[2] += q[0][0] + q[1][0];
+      x[3] += q[0][1] + q[1][1];
+      r = w = v = 0;
+      a[0][0] = a[0][1] = a[1][0] = a[1][1] = q[0][0] = q[0][1] = q[1][0] = q[1][1] = 0;
+    };
     for (uint32_t t = T.t0; t < T.t1; ++t) {
       const int j = s.task_job[t], st = s.task_status[t];
+      if (j != cj) {
+        flush();
+        cj = j;
+      }
       const bool al = allocated_status(st);
-      T.ready[j] += (al || st == KB_ST_SUCCEEDED) ? 1 : 0;
-      T.waiting[j] += st == KB_ST_PIPELINED ? 1 : 0;
-      T.valid[j] += (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) ? 1 : 0;
+      r += (al || st == KB_ST_SUCCEEDED) ? 1 : 0;
+      w += st == KB_ST_PIPELINED ? 1 : 0;
+      v += (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) ? 1 : 0;
       if (al) T.alloc.push_back((int)t);
       if (prop && (al || st == KB_ST_PENDING)) {
         const double* p = task_req(t);
-        double* q = T.q.data() + 4 * (size_t)s.job_queue[j];
         exact = exact && exact_int(p[0]) && exact_int(p[1]) && (s.task_resreq_mask[t] & sc_bits) == 0;
+        const int k = t & 1;
         if (al) {
-          q[0] += p[0];
-          q[1] += p[1];
+          a[k][0] += p[0];
+          a[k][1] += p[1];
         }
-        q[2] += p[0];
-        q[3] += p[1];
+        q[k][0] += p[0];
+        q[k][1] += p[1];
       }
     }
+    flush();
     T.exact = exact;
   }
 
@@ -409,13 +443,14 @@ struct Driver {
     }
     const bool prop = has[KB_PLUGIN_PROPORTION];
     // the second half of the task pass on the other helper (large sessions: the split pays for the thread hand-off)
-    uint32_t h = s.n_tasks;
+    head.t0 = 0;
+    head.t1 = s.n_tasks;
+    tail.t0 = tail.t1 = s.n_tasks;
     int w_tail = -1;
     if (s.n_tasks >= 32768) {
-      tail.t0 = h = s.n_tasks / 2;
-      tail.t1 = s.n_tasks;
-      w_tail = HostPool::get().post([this, prop] { tail_pass(prop); });
-      if (w_tail < 0) h = s.n_tasks;  // (no worker free: one pass)
+      tail.t0 = head.t1 = s.n_tasks / 2;
+      w_tail = HostPool::get().post([this, prop] { task_pass(tail, prop); });
+      if (w_tail < 0) tail.t0 = head.t1 = s.n_tasks;  // (no worker free: one pass)
     }
     total.S = S;
     for (int i = 0; i < 2 + S; ++i) total.v[i] = s.total_alloc[i];
@@ -428,92 +463,75 @@ struct Driver {
     for (auto& q : queues) {
       q.deserved.S = q.allocated.S = q.request.S = S;
     }
-    // one pass over the tasks: the jobs' counts and DRF allocations, and (proportion) the queues' allocated /
-    // request sums -- the latter in task order with cpu and memory in registers while the queue stays the same (the
-    // same float additions in the same order as one add_raw per task)
-    int cq = -1;
-    double ac = 0, am = 0, rc = 0, rm = 0;
-    bool exact = true;  // (as TailPass::exact, for this half's cpu / memory sums)
-    const auto flush = [&]() {
-      if (cq < 0) return;
-      queues[cq].allocated.v[0] = ac;
-      queues[cq].allocated.v[1] = am;
-      queues[cq].request.v[0] = rc;
-      queues[cq].request.v[1] = rm;
-    };
-    // proportion.go:72-81 (OnSessionOpen's task walk): task t's requests into its queue's sums
-    const auto prop_add = [&](uint32_t t, int j, bool al) {
-      const int qi = s.job_queue[j];
-      if (qi != cq) {
-        flush();
-        cq = qi;
-        ac = queues[qi].allocated.v[0];
-        am = queues[qi].allocated.v[1];
-        rc = queues[qi].request.v[0];
-        rm = queues[qi].request.v[1];
-      }
-      const double* p = task_req(t);
-      const uint64_t m = s.task_resreq_mask[t];
-      exact = exact && exact_int(p[0]) && exact_int(p[1]);
-      if (al) {
-        ac += p[0];
-        am += p[1];
-        queues[qi].allocated.add_scalars(p, m);
-      }
-      rc += p[0];
-      rm += p[1];
-      queues[qi].request.add_scalars(p, m);
-    };
-    for (uint32_t t = 0; t < h; ++t) {
-      int j = s.task_job[t], st = task_status[t];
-      const bool al = allocated_status(st);
-      if (al || st == KB_ST_SUCCEEDED) jobs[j].ready++;
-      if (st == KB_ST_PIPELINED) jobs[j].waiting++;
-      if (al || st == KB_ST_SUCCEEDED || st == KB_ST_PIPELINED || st == KB_ST_PENDING) jobs[j].valid++;
-      if (st == KB_ST_ALLOCATED) job_allocated[j].push_back((int)t);
-      if (al) jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
-      if (prop && (al || st == KB_ST_PENDING)) prop_add(t, j, al);
+    const auto ia = std::chrono::steady_clock::now();
+    task_pass(head, prop);
+    const auto ib = std::chrono::steady_clock::now();
+    if (w_tail >= 0) HostPool::get().join(w_tail);
+    else tail.exact = true, tail.alloc.clear();
+    // the jobs' counts; the allocated-status tasks' DRF sums and Allocated lists in task order
+    for (uint32_t j = 0; j < s.n_jobs; ++j) {
+      jobs[j].ready = head.ready[j] + (w_tail >= 0 ? tail.ready[j] : 0);
+      jobs[j].waiting = head.waiting[j] + (w_tail >= 0 ? tail.waiting[j] : 0);
+      jobs[j].valid = head.valid[j] + (w_tail >= 0 ? tail.valid[j] : 0);
     }
-    flush();
-    if (h < s.n_tasks) {  // the second half's results, in task order where order matters
-      HostPool::get().join(w_tail);
-      for (uint32_t j = 0; j < s.n_jobs; ++j) {
-        jobs[j].ready += tail.ready[j];
-        jobs[j].waiting += tail.waiting[j];
-        jobs[j].valid += tail.valid[j];
-      }
-      for (int t : tail.alloc) {
+    for (const TaskPass* T : {&head, &tail})
+      for (int t : T->alloc) {
         const int j = s.task_job[t];
         if (task_status[t] == KB_ST_ALLOCATED) job_allocated[j].push_back(t);
         jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
       }
-      if (prop) {
-        bool ok = exact && tail.exact;
-        if (ok)
-          for (uint32_t q = 0; q < s.n_queues && ok; ++q) {
-            const double* x = tail.q.data() + 4 * (size_t)q;
-            ok = exact_int(queues[q].allocated.v[0] + x[0]) && exact_int(queues[q].allocated.v[1] + x[1]) &&
-                 exact_int(queues[q].request.v[0] + x[2]) && exact_int(queues[q].request.v[1] + x[3]);
-          }
-        if (ok) {
-          for (uint32_t q = 0; q < s.n_queues; ++q) {
-            const double* x = tail.q.data() + 4 * (size_t)q;
-            queues[q].allocated.v[0] += x[0];
-            queues[q].allocated.v[1] += x[1];
-            queues[q].request.v[0] += x[2];
-            queues[q].request.v[1] += x[3];
-          }
-        } else {  // the second half's sums again, in task order after the first half's
-          cq = -1;
-          for (uint32_t t = h; t < s.n_tasks; ++t) {
-            const int st = task_status[t];
-            const bool al = allocated_status(st);
-            if (al || st == KB_ST_PENDING) prop_add(t, s.task_job[t], al);
-          }
-          flush();
+    if (prop) {  // the queues' allocated / request sums: the split sums when exact, else in task order
+      bool ok = head.exact && tail.exact;
+      std::vector<double> sum(4 * (size_t)s.n_queues);
+      for (size_t i = 0; ok && i < sum.size(); ++i) {
+        sum[i] = head.q[i] + (w_tail >= 0 ? tail.q[i] : 0.0);
+        ok = exact_int(sum[i]);
+      }
+      if (ok) {
+        for (uint32_t q = 0; q < s.n_queues; ++q) {
+          queues[q].allocated.v[0] = sum[4 * q];
+          queues[q].allocated.v[1] = sum[4 * q + 1];
+          queues[q].request.v[0] = sum[4 * q + 2];
+          queues[q].request.v[1] = sum[4 * q + 3];
         }
+      } else {  // one add per task in task order, cpu and memory in registers while the queue stays the same
+        int cq = -1;
+        double ac = 0, am = 0, rc = 0, rm = 0;
+        const auto qflush = [&]() {
+          if (cq < 0) return;
+          queues[cq].allocated.v[0] = ac;
+          queues[cq].allocated.v[1] = am;
+          queues[cq].request.v[0] = rc;
+          queues[cq].request.v[1] = rm;
+        };
+        for (uint32_t t = 0; t < s.n_tasks; ++t) {
+          const int st = task_status[t];
+          const bool al = allocated_status(st);
+          if (!(al || st == KB_ST_PENDING)) continue;
+          const int qi = s.job_queue[s.task_job[t]];
+          if (qi != cq) {
+            qflush();
+            cq = qi;
+            ac = queues[qi].allocated.v[0];
+            am = queues[qi].allocated.v[1];
+            rc = queues[qi].request.v[0];
+            rm = queues[qi].request.v[1];
+          }
+          const double* p = task_req(t);
+          const uint64_t m = s.task_resreq_mask[t];
+          if (al) {
+            ac += p[0];
+            am += p[1];
+            queues[qi].allocated.add_scalars(p, m);
+          }
+          rc += p[0];
+          rm += p[1];
+          queues[qi].request.add_scalars(p, m);
+        }
+        qflush();
       }
     }
+    const auto ic = std::chrono::steady_clock::now();
     if (w_pend >= 0) HostPool::get().join(w_pend);
     else build_pend();
     const auto i1 = std::chrono::steady_clock::now();
@@ -521,11 +539,16 @@ struct Driver {
     const auto i2 = std::chrono::steady_clock::now();
     if (prop) open_proportion();
     if (ctx->issue_trace)
-      fprintf(stderr, "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f split=%d\n",
+      fprintf(stderr,
+              "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f split=%d (setup %.3f first half %.3f "
+              "merge %.3f pending-list join %.3f)\n",
               std::chrono::duration<double, std::milli>(i1 - i0).count(),
               std::chrono::duration<double, std::milli>(i2 - i1).count(),
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count(),
-              h < s.n_tasks ? 1 : 0);
+              w_tail >= 0 ? 1 : 0, std::chrono::duration<double, std::milli>(ia - i0).count(),
+              std::chrono::duration<double, std::milli>(ib - ia).count(),
+              std::chrono::duration<double, std::milli>(ic - ib).count(),
+              std::chrono::duration<double, std::milli>(i1 - ic).count());
     return KB_OK;
   }
 
