@@ -1165,26 +1165,53 @@ int kb_set_shard_peer(kb_ctx* c, const kb_shard* sh, kb_allgather_fn fn, void* u
       return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the inbox handles", rc);
     for (int w = 0; w < W; ++w) start = std::max(start, h[1 + w].epoch);
   }
+  // Each rank opens every peer's inbox; a failure is recorded, not returned at once: every rank's outcome is
+  // all-gathered below, so that every rank fails alike and names the same pair (a rank returning alone would leave
+  // the others blocked in the next all-gather)
+  struct OpenOutcome {
+    int32_t ok, peer, code, pad;  // code: 1 the peer's GPU is not visible, 2 no peer path, 3 the IPC open failed
+  };
+  OpenOutcome mine{1, -1, 0, 0};
   for (int w = 0; w < W; ++w) {
     if (w == sh->rank) {
       c->peer_inbox[w] = c->inbox;
       continue;
     }
+    if (!mine.ok) continue;
     if (strncmp(h[1 + w].bus, h[0].bus, sizeof(h[0].bus)) != 0) {  // another GPU: the xGMI path must be open
       int ord = -1, can = 0;
       if (hipDeviceGetByPCIBusId(&ord, h[1 + w].bus) != hipSuccess || ord < 0) {
         (void)hipGetLastError();
-        return fail(c, KB_E_HIP, "rank %d's GPU (%s) is not visible to rank %d", w, h[1 + w].bus, sh->rank);
+        mine = OpenOutcome{0, w, 1, 0};
+        continue;
       }
-      HIP_OK(c, hipDeviceCanAccessPeer(&can, c->device, ord));
-      if (!can)
-        return fail(c, KB_E_HIP, "rank %d (GPU %s) cannot access rank %d's GPU (%s): no peer path", sh->rank,
-                    h[0].bus, w, h[1 + w].bus);
+      if (hipDeviceCanAccessPeer(&can, c->device, ord) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        mine = OpenOutcome{0, w, 2, 0};
+        continue;
+      }
     }
     void* p = nullptr;
-    const hipError_t e = hipIpcOpenMemHandle(&p, h[1 + w].h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return fail(c, KB_E_HIP, "hipIpcOpenMemHandle (rank %d's inbox): %s", w, hipGetErrorString(e));
+    if (hipIpcOpenMemHandle(&p, h[1 + w].h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      (void)hipGetLastError();
+      mine = OpenOutcome{0, w, 3, 0};
+      continue;
+    }
     c->peer_inbox[w] = p;
+  }
+  if (W > 1) {
+    std::vector<OpenOutcome> all((size_t)W);
+    if (int rc = fn(user, &mine, all.data(), sizeof(OpenOutcome)))
+      return fail(c, KB_E_HIP, "all-gather callback failed (%d) exchanging the inbox opens", rc);
+    for (int w = 0; w < W; ++w)
+      if (!all[w].ok) {
+        const int q = all[w].peer;
+        const char* why = all[w].code == 1   ? "does not see the GPU of"
+                          : all[w].code == 2 ? "has no peer path to the GPU of"
+                                             : "could not open (hipIpcOpenMemHandle) the inbox of";
+        return fail(c, KB_E_HIP, "node-sharded setup: rank %d (GPU %s) %s rank %d (GPU %s)", w,
+                    w == sh->rank ? h[0].bus : h[1 + w].bus, why, q, q == sh->rank ? h[0].bus : h[1 + q].bus);
+      }
   }
   if (W > 1)
     if (int rc = shard_peer_preflight(c, sh, fn, user, start)) return rc;
