@@ -1131,7 +1131,7 @@ struct Driver {
     } engine{ctx};
     clk::time_point pause_t0{};
     uint64_t pause_units = 0;  // off-engine units run since the pause began
-    // A pause ends the engine instead of resuming it once it has gone on too long (the engine's idle exit is 1 s, 10 s
+    // A pause ends the engine instead of resuming it once it has gone on too long (the engine's idle exit is 1 s, 30 s
     // node-sharded). One GPU: 200 ms of wall clock. Node-sharded: every rank must end and relaunch its engine at the
     // same unit (a relaunch bumps the exchange epoch), so the bound is a unit count, which every rank's driver sees
     // alike -- never a rank's own clock.

@@ -1932,8 +1932,9 @@ int kb_fed_begin(kb_ctx* c, uint32_t max_job_tasks) {
     SP.self_inbox = c->shard_self_inbox ? 1 : 0;
     c->stats.fed_sharded++;
   }
-  // node-sharded: 10 s (every rank's engine waits for the slowest rank's host at each exchange)
-  const uint64_t idle = c->sharded ? 10 * c->fed_idle : c->fed_idle;
+  // node-sharded: 30 s (every rank's engine waits for the slowest rank's host at each exchange; eight ranks sharing
+  // one GPU in the tests once left a rank's engine without progress for over 10 s)
+  const uint64_t idle = c->sharded ? 30 * c->fed_idle : c->fed_idle;
   // resident sweepers: the census grid's spare workgroups (split engine, placed on an XCC, plain launch)
   c->fed_sweepers_now = xchg && !c->fed_coop && c->fed_xcc >= 0 && c->fed_xcc < 8 && !c->fed_kernel_sweeps;
   if (c->fed_sweepers_now && !c->fed_hring) {
