@@ -126,12 +126,13 @@ def main():
     seed = synth.SEED + (0 if shard else rank)
     snap, sess = session_snapshot(args, seed)
 
+    exch = {"kind": "peer"}  # node-sharded: the device exchange, or the host-staged one if its pre-flight fails
+
     def make_ctx(every):
-        c = runtime.Context(device, timing=not args.no_timing, timing_every=every, path=args.path,
-                            options=args.options)
-        if shard:
-            c.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
-        return c
+        def fresh():
+            return runtime.Context(device, timing=not args.no_timing, timing_every=every, path=args.path,
+                                   options=args.options)
+        return sharded_context(fresh, dist, rank, world, device, snap.n_nodes, exch) if shard else fresh()
 
     # fed-engine cycles: the engine's one launch per cycle is timed (per-job sweep events would add barrier packets
     # on the sweep queue and host calls to every job); per-job launch paths: every Nth job's launches
@@ -247,7 +248,7 @@ def main():
             "roofline": roofline,
             **({"engine": engine} if engine is not None else {}),
             "cpu_baseline": cpu,
-            **(shard_fields(st, args) if shard else {}),
+            **({**shard_fields(st, args), "shard_exchange": exch} if shard else {}),
             **side,
         }
         print(json.dumps(result), flush=True)
@@ -428,6 +429,38 @@ def tensor_device(dist, device):
     return "cpu" if dist is not None and dist.get_backend() == "gloo" else f"cuda:{device}"
 
 
+def sharded_context(fresh, dist, rank, world, device, n_total, exch):
+    """A node-sharded context (this rank's block of n_total nodes) on the engines' device exchange
+    (kb_set_shard_peer). If a peer mapping or the pre-flight round trip fails on any rank, every rank takes the
+    host-staged exchange (kb_set_shard) instead and `exch` records why -- the line still measures the sharded cycle
+    rather than ending the run. exch["kind"] == "host" on entry skips the peer attempt."""
+    from scheduler_amd import runtime
+    c = fresh()
+    kw = shard_exchange(dist, rank, device)
+    if exch.get("kind", "peer") == "peer":
+        err = None
+        try:
+            c.set_shard(rank, world, n_total, **kw)
+        except runtime.KbError as e:  # (the pre-flight's outcome is all-gathered: every rank fails alike)
+            err = str(e)[:300]
+        if all_ranks_ok(dist, device, err is None):
+            exch["kind"] = "peer"
+            return c
+        exch.update(kind="host", peer_error=err or "the peer pre-flight failed on another rank")
+        c.close()
+        c = fresh()
+    c.set_shard(rank, world, n_total, **{**kw, "peer": False})
+    return c
+
+
+def all_ranks_ok(dist, device, ok):
+    """True on every rank iff `ok` holds on every rank (one MIN all-reduce over the process group)."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=tensor_device(dist, device))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def shard_exchange(dist, rank, device):
     """Context.set_shard keywords: the node-sharded fed engine's device exchange (kb_set_shard_peer), whose inbox
     IPC handles travel once through an all-gather over the torch process group (RCCL, or gloo when the ranks share
@@ -486,8 +519,9 @@ def shard_side(args, dist, rank, world, device, config="C5"):
     try:
         c = CONFIGS[config]
         snap = synth.c2_snapshot(n_nodes=c["nodes"], n_jobs=c["jobs"], tasks_per_job=c["tasks"], seed=synth.SEED)
-        ctx = runtime.Context(device, timing=True, timing_every=1 << 30, options=args.options)
-        ctx.set_shard(rank, world, snap.n_nodes, **shard_exchange(dist, rank, device))
+        exch = {"kind": "peer"}
+        ctx = sharded_context(lambda: runtime.Context(device, timing=True, timing_every=1 << 30, options=args.options),
+                              dist, rank, world, device, snap.n_nodes, exch)
         ctx.upload(snap)
         ctx.allocate(snap)  # warm-up cycle
         ctx.stats(reset=True)
@@ -510,7 +544,7 @@ def shard_side(args, dist, rank, world, device, config="C5"):
         out = {"workload": c["workload"] + f", node table split into {world} blocks",
                "value": round(placed * args.side_steps / elapsed, 1), "unit": "pods/s",
                "steps": args.side_steps, "scaling": "strong", "ms_per_step": round(elapsed / args.side_steps * 1e3, 3),
-               "roofline": roofline_of(st, a, c), **shard_fields(st, a)}
+               "roofline": roofline_of(st, a, c), **shard_fields(st, a), "shard_exchange": exch}
         if st["launches"][runtime.KERNELS.index("fed_engine_kernel")]:
             out["engine"] = engine_of(st)
         return out

@@ -1087,6 +1087,193 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
   }
 }
 
+// eval_plain_kernel with four consecutive nodes per lane (eval_plain4_kernel): the same per-pair arithmetic, but each
+// spec row gets one 16-byte store per lane (reasons; scores: one per 4 B of score) -- a wave writes 1 KB of a row
+// per store instruction instead of 256 B, the streaming-store form (MI355X_MICROARCH.md's HBM section), and the four
+// nodes' f64 chains are independent work for the same wave. An A/B build (-DKB_EVAL_VEC4, `make evalv4`): taken
+// there when N % 4 == 0 (rows start 16-byte aligned and no lane's four nodes straddle two rows) and the output fits
+// buffer offsets (launch_eval_t). Measured 36.2 us against 34.2-41.0 us for eval_plain_kernel at 256 x 50k (r06v):
+// 214 VGPRs leave two waves per SIMD, and the VALU work per pair is unchanged, so it stays the default's bound.
+struct PlainNode {  // a node's side of eval_plain_kernel's fast loop
+  uint32_t after, post_be;
+  double num_c, num_m, cap_c, cap_m, lc_inv, lm_inv, ic10, im10, t_ic, t_im, t_rc, t_rm, d_nc, d_nm, d_ac, d_am;
+  bool pos;
+};
+// false when some operand leaves the exact-double range (the lane then takes the int64 loop for its four nodes)
+__device__ __forceinline__ bool plain_node_init(PlainNode& p, const Row& r, const DevCfg& C) {
+  p.after = 0;
+  p.post_be = 0;
+  if (C.predicates) {
+    const uint32_t f = r.flags;
+    const uint32_t pre = f & ((1u << KB_R_NOT_READY) | (1u << KB_R_OUT_OF_DISK) | (1u << KB_R_NETWORK_UNAVAILABLE) |
+                              (1u << KB_R_UNSCHEDULABLE));
+    uint32_t post = 0;
+    if (C.disk_pressure && (f & KB_NODE_DISK_PRESSURE)) post = 1u << KB_R_DISK_PRESSURE;
+    else if (C.pid_pressure && (f & KB_NODE_PID_PRESSURE)) post = 1u << KB_R_PID_PRESSURE;
+    p.post_be = (C.mem_pressure && (f & KB_NODE_MEM_PRESSURE)) ? 1u << KB_R_MEMORY_PRESSURE : post;
+    p.after = r.max_pods <= r.pod_count ? 1u << KB_R_POD_NUMBER : (pre ? pre : post);
+    if (r.max_pods <= r.pod_count || pre) p.post_be = p.after;
+  }
+  const double d_ic = (double)r.idle_cpu, d_im = (double)r.idle_mem, d_rc = (double)r.rel_cpu,
+               d_rm = (double)r.rel_mem;
+  p.d_nc = (double)r.nz_cpu;
+  p.d_nm = (double)r.nz_mem;
+  p.d_ac = (double)r.alloc_cpu;
+  p.d_am = (double)r.alloc_mem;
+  const bool fast = fabs(d_ic) < kPlainMax && fabs(d_im) < kPlainMax && fabs(d_rc) < kPlainMax &&
+                    fabs(d_rm) < kPlainMax && fabs(p.d_nc) < kPlainMax && fabs(p.d_nm) < kPlainMax &&
+                    fabs(p.d_ac) < kPlainMax && fabs(p.d_am) < kPlainMax;
+  p.t_ic = d_ic + 10.0;
+  p.t_im = d_im + 10485760.0;
+  p.t_rc = d_rc + 10.0;
+  p.t_rm = d_rm + 10485760.0;
+  p.pos = p.d_ac > 0.0 && p.d_am > 0.0;
+  const bool zc = p.d_ac == 0.0, zm = p.d_am == 0.0;
+  p.num_c = zc ? -1.0 : (p.d_ac - p.d_nc) * 10.0;
+  p.num_m = zm ? -1.0 : (p.d_am - p.d_nm) * 10.0;
+  p.cap_c = zc ? 1.0 : p.d_ac;
+  p.cap_m = zm ? 1.0 : p.d_am;
+  p.lc_inv = zc ? 1.0 : 1.0 / p.d_ac;
+  p.lm_inv = zm ? 1.0 : 1.0 / p.d_am;
+  p.ic10 = p.pos ? 10.0 / p.d_ac : 0.0;
+  p.im10 = p.pos ? 10.0 / p.d_am : 0.0;
+  return fast;
+}
+// one (spec, node) pair of the fast loop: eval_plain_kernel's body; fb = Balanced's IEEE fallback is due
+template <class SCORE>
+__device__ __forceinline__ void plain_pair(const PlainNode& p, double icpu, double imem, double nzc10, double nzm10,
+                                           double nzc, double nzm, uint32_t bem, const SCORE* s_tab, uint32_t& rs,
+                                           SCORE& score, bool& fb) {
+  const bool fit = ((icpu < p.t_ic) & (imem < p.t_im)) | ((icpu < p.t_rc) & (imem < p.t_rm));
+  const uint32_t fm = 0u - (uint32_t)fit;
+  rs = (((p.post_be & bem) | (p.after & ~bem)) & fm) | ((1u << KB_R_RESOURCE_FIT) & ~fm);
+  const int lc = lr_score_f64(p.num_c - nzc10, p.cap_c, p.lc_inv);
+  const int lm = lr_score_f64(p.num_m - nzm10, p.cap_m, p.lm_inv);
+  const double rc = nzc + p.d_nc, rm = nzm + p.d_nm;
+  const bool over = (rc >= p.d_ac) | (rm >= p.d_am);
+  const double f = 10.0 - fabs(fma(rc, p.ic10, -(rm * p.im10)));
+  const double fr = f - floor(f);
+  const bool po = p.pos & over;
+  const bool est = p.pos & !over & (fr > 1e-9) & (fr < 1.0 - 1e-9);
+  fb = !est & !po;
+  score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
+}
+template <class SCORE>
+__global__ __launch_bounds__(256) void eval_plain4_kernel(DevNodes N, DevSpecs P, DevCfg C, const int32_t* spec_ids,
+                                                          int t, int spb, uint32_t* reasons, SCORE* scores) {
+  __shared__ int64_t s_req[4][kEvalPlainSpecs];
+  __shared__ double s_dreq[4][kEvalPlainSpecs];
+  __shared__ double s_dnz[2][kEvalPlainSpecs];
+  __shared__ uint32_t s_bem[kEvalPlainSpecs];
+  __shared__ SCORE s_tab[11 * 11];
+  const int j0 = blockIdx.y * spb;
+  const int nj = t - j0 < spb ? t - j0 : spb;
+  const int n0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;  // (N % 4 == 0: all four nodes or none)
+  Row r[4];
+  if (n0 < N.n) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = load_row(N, n0 + k);
+  }
+  if ((int)threadIdx.x < nj) {
+    const kb_spec sp = P.specs[spec_ids[j0 + threadIdx.x]];
+    s_req[0][threadIdx.x] = sp.init_cpu;
+    s_req[1][threadIdx.x] = sp.init_mem;
+    s_req[2][threadIdx.x] = sp.nz_cpu;
+    s_req[3][threadIdx.x] = sp.nz_mem;
+    s_dreq[0][threadIdx.x] = (double)sp.init_cpu;
+    s_dreq[1][threadIdx.x] = (double)sp.init_mem;
+    s_dreq[2][threadIdx.x] = (double)sp.nz_cpu * 10.0;
+    s_dreq[3][threadIdx.x] = (double)sp.nz_mem * 10.0;
+    s_dnz[0][threadIdx.x] = (double)sp.nz_cpu;
+    s_dnz[1][threadIdx.x] = (double)sp.nz_mem;
+    s_bem[threadIdx.x] = (sp.flags & KB_SPEC_BEST_EFFORT) ? ~0u : 0u;
+  }
+  if (threadIdx.x >= 128 && threadIdx.x < 128 + 121) {
+    const int q = (int)threadIdx.x - 128;
+    s_tab[q] = C.nodeorder ? (SCORE)(q / 11) * (SCORE)C.w_lr + (SCORE)(q % 11) * (SCORE)C.w_bra : (SCORE)0;
+  }
+  __syncthreads();
+  if (n0 >= N.n) return;
+  const uint32_t stride = (uint32_t)N.n;
+  PlainNode p[4];
+  bool fast = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fast &= plain_node_init(p[k], r[k], C);
+  if (fast) {
+    const uint32_t out_pairs = (uint32_t)t * stride;
+    const __amdgpu_buffer_rsrc_t rbuf = __builtin_amdgcn_make_buffer_rsrc(reasons, (short)0, (int)(out_pairs * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t sbuf =
+        __builtin_amdgcn_make_buffer_rsrc(scores, (short)0, (int)(out_pairs * (uint32_t)sizeof(SCORE)), 0x00020000);
+    uint64_t fb[4] = {0, 0, 0, 0};
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll 1
+    for (int j = 0; j < nj; ++j) {
+      const double icpu = s_dreq[0][j], imem = s_dreq[1][j], nzc10 = s_dreq[2][j], nzm10 = s_dreq[3][j];
+      const double nzc = s_dnz[0][j], nzm = s_dnz[1][j];
+      const uint32_t bem = s_bem[j];
+      uint32_t rs[4];
+      SCORE sc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        bool b;
+        plain_pair<SCORE>(p[k], icpu, imem, nzc10, nzm10, nzc, nzm, bem, s_tab, rs[k], sc[k], b);
+        fb[k] |= (uint64_t)b << j;
+      }
+      const uint32_t orow = (uint32_t)(j0 + j) * stride;  // (uniform: scalar)
+      const v4u rv = {rs[0], rs[1], rs[2], rs[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(rv, rbuf, n0 * 4, (int)(orow * 4u), kEvalAux);
+      if constexpr (sizeof(SCORE) == 4) {
+        const v4u sv = {(unsigned)sc[0], (unsigned)sc[1], (unsigned)sc[2], (unsigned)sc[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(sv, sbuf, n0 * 4, (int)(orow * 4u), kEvalAux);
+      } else {
+        const v4u s01 = {(unsigned)(uint64_t)sc[0], (unsigned)((uint64_t)sc[0] >> 32), (unsigned)(uint64_t)sc[1],
+                         (unsigned)((uint64_t)sc[1] >> 32)};
+        const v4u s23 = {(unsigned)(uint64_t)sc[2], (unsigned)((uint64_t)sc[2] >> 32), (unsigned)(uint64_t)sc[3],
+                         (unsigned)((uint64_t)sc[3] >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(s01, sbuf, n0 * 8, (int)(orow * 8u), kEvalAux);
+        __builtin_amdgcn_raw_buffer_store_b128(s23, sbuf, n0 * 8 + 16, (int)(orow * 8u), kEvalAux);
+      }
+    }
+    if (!C.nodeorder) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint64_t m = fb[k];
+      while (m) {  // the deferred Balanced fallbacks (this thread's later store to the same word)
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        const int lc = lr_score_f64(p[k].num_c - s_dreq[2][j], p[k].cap_c, p[k].lc_inv);
+        const int lm = lr_score_f64(p[k].num_m - s_dreq[3][j], p[k].cap_m, p[k].lm_inv);
+        const double rc = s_dnz[0][j] + p[k].d_nc, rm = s_dnz[1][j] + p[k].d_nm;
+        scores[(size_t)(j0 + j) * stride + n0 + k] =
+            s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, p[k].d_ac, rm, p[k].d_am, 0.0, 0.0, false)];
+      }
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {  // the int64 forms (eval_plain_kernel's tail loop), node by node
+    const int n = n0 + k;
+    const Row rk = load_row(N, n);  // (reloaded: no dynamic index into the register arrays)
+    PlainNode pk;
+    plain_node_init(pk, rk, C);
+    const double inv_c = 1.0 / (double)rk.alloc_cpu, inv_m = 1.0 / (double)rk.alloc_mem;
+    for (int j = 0; j < nj; ++j) {
+      const int64_t icpu = s_req[0][j], imem = s_req[1][j];
+      const bool fit = (le_tol(icpu, rk.idle_cpu, 10) && le_tol(imem, rk.idle_mem, 10ll * 1024 * 1024)) ||
+                       (le_tol(icpu, rk.rel_cpu, 10) && le_tol(imem, rk.rel_mem, 10ll * 1024 * 1024));
+      const uint32_t rs = !fit ? 1u << KB_R_RESOURCE_FIT : (s_bem[j] ? pk.post_be : pk.after);
+      int64_t score = 0;
+      if (C.nodeorder) {
+        const int64_t rc = s_req[2][j] + rk.nz_cpu, rm = s_req[3][j] + rk.nz_mem;
+        const int64_t lr = (lr_score_inv(rc, rk.alloc_cpu, inv_c) + lr_score_inv(rm, rk.alloc_mem, inv_m)) / 2;
+        score = lr * C.w_lr + bra_score_inv(rc, rk.alloc_cpu, rm, rk.alloc_mem, inv_c, inv_m) * C.w_bra;
+      }
+      reasons[(size_t)(j0 + j) * stride + n] = rs;
+      scores[(size_t)(j0 + j) * stride + n] = (SCORE)score;
+    }
+  }
+}
+
 // ===========================================================================
 // Trajectory path (N <= kTrajMaxNodes, scores that fit a 32-bit key).
 //
@@ -7013,6 +7200,22 @@ template <class SCORE>
 static void launch_eval_t(const DevNodes& N, const DevSpecs& P, const DevCfg& C, const int32_t* spec_ids, int t,
                           uint32_t* reasons, SCORE* scores, const int64_t* mm, bool plain, int cus, int spb_opt,
                           void* stream) {
+  const bool buf = (uint64_t)t * (uint64_t)N.n * sizeof(SCORE) < (1ull << 31);
+#if defined(KB_EVAL_VEC4)  // (A/B build: measured slower than one node per lane)
+  if (plain && buf && N.n % 4 == 0) {  // four nodes per lane, 16-byte stores (eval_plain4_kernel)
+    static int bpc4 = 0;  // (its own occupancy, once per instance)
+    if (bpc4 == 0) {
+      int nb = 0;
+      bpc4 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_plain4_kernel<SCORE>, 256, 0) == hipSuccess && nb > 0
+                 ? nb : 1;
+    }
+    const int spb = eval_plain_spb((N.n + 3) / 4, t, cus & 0xffff, bpc4, spb_opt);
+    dim3 grid((N.n / 4 + 255) / 256, (t + spb - 1) / spb);
+    hipLaunchKernelGGL((eval_plain4_kernel<SCORE>), grid, dim3(256), 0, (hipStream_t)stream, N, P, C, spec_ids, t,
+                       spb, reasons, scores);
+    return;
+  }
+#endif
   if (plain) {
     const int spb = eval_plain_spb(N.n, t, cus & 0xffff, cus >> 16, spb_opt);
 #ifdef KB_EVAL_NPT2

@@ -4,6 +4,8 @@ Bar: bit-exact. Masks (first-fail reason sets) and scores for every (spec, node)
 allocate outcomes (placement sequence, binds, statuses, FitErrors histograms) under the lowest-index
 tie-break applied to both.
 """
+import copy
+
 import numpy as np
 import pytest
 
@@ -98,10 +100,17 @@ def _plain_spec(snap):
         (snap.tolerates.shape[1] == 1)
 
 
-def test_eval_plain_matches_oracle():
+@pytest.mark.parametrize("extra", [0, 1, 2, 3])
+def test_eval_plain_matches_oracle(extra):
     """kb_eval's row-only kernel (plain specs: resource fit, pod count, conditions, memory / disk / PID pressure,
-    BestEffort, LeastRequested + Balanced) against the oracle on every (spec, node) pair."""
+    BestEffort, LeastRequested + Balanced) against the oracle on every (spec, node) pair. `extra` copies of the first
+    nodes make every residue of N mod 4: N % 4 == 0 takes the four-nodes-per-lane kernel (eval_plain4_kernel), the
+    others the one-node-per-lane kernel."""
     cl = plain_edge_cluster()
+    for k in range(extra):
+        nd = copy.deepcopy(cl.nodes[k])
+        nd.name += f"-x{k}"
+        cl.nodes.append(nd)
     snap = E.Snapshot(cl)
     reps = {}
     for t in snap.session_tasks:
@@ -126,7 +135,7 @@ def test_eval_plain_matches_oracle():
     assert np.array_equal(r32, reasons) and np.array_equal(s32.astype(np.int64), scores)
 
 
-@pytest.mark.parametrize("name,cfg", [("plain-edge", None), ("C2-2000", None), ("C1-parity", None),
+@pytest.mark.parametrize("name,cfg", [("plain-edge", None), ("C2-2000", None), ("C2-2002", None), ("C1-parity", None),
                                       ("plain-edge", {"nodeorder_enabled": 0}),
                                       ("plain-edge", {"predicates_enabled": 0})])
 def test_eval_plain_equals_general(name, cfg):
@@ -134,6 +143,7 @@ def test_eval_plain_equals_general(name, cfg):
     the nodeorder or predicates plugin off (the score table all 0; no post reasons)."""
     cl = {"plain-edge": plain_edge_cluster, "C2-2000": lambda: synth.c2(n_nodes=2000, n_jobs=64, tasks_per_job=1,
                                                                         seed=9),
+          "C2-2002": lambda: synth.c2(n_nodes=2002, n_jobs=64, tasks_per_job=1, seed=9),
           "C1-parity": lambda: synth.c1(n_nodes=120, n_jobs=24, tasks_per_job=25, seed=1)}[name]()
     snap = E.Snapshot(cl)
     if cfg:
