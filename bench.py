@@ -154,8 +154,25 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
+    def warm():
+        for _ in range(args.warmup):
+            step()
+    if shard and exch["kind"] == "peer" and args.warmup:
+        # a cycle on the device exchange that fails on any rank (a peer that stops answering: the engines' idle
+        # bound) moves every rank to the host-staged exchange before the timed region, and the line says so
+        err = None
+        try:
+            warm()
+        except runtime.KbError as e:
+            err = str(e)[:300]
+        if not all_ranks_ok(dist, device, err is None):
+            exch.update(kind="host", peer_error=err or "a warm-up cycle on the peer exchange failed on another rank")
+            ctx.close()
+            ctx = make_ctx(1 << 30)
+            ctx.upload(snap)
+            warm()
+    else:
+        warm()
     if args.warmup and not ctx.stats()["fed_cycles"] and not args.no_timing and not shard:
         ctx.close()  # per-job launch paths: time every Nth job's launches
         ctx = make_ctx(args.timing_every)

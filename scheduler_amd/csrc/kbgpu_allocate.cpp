@@ -22,15 +22,16 @@
 
 namespace {
 
-// Host helper threads (two per process): kb_allocate builds the cycle's pending lists on one and walks the second
-// half of the tasks for the session-open state on the other while its own thread walks the first half (independent
-// passes over the session's task arrays, ~0.2 ms each on C2's 100k tasks, before the first job can be issued). A
+// Host helper threads (four per process): kb_allocate builds the cycle's pending lists on one and walks the last three
+// quarters of the tasks for the session-open state on the others while its own thread walks the first quarter
+// (independent passes over the session's task arrays, ~0.3 ms in one piece on C2's 100k tasks, before the first job
+// can be issued). A
 // driver that finds no worker free (another context's cycle in another thread) runs the work itself. A worker spins
 // for kSpin after its last job before it sleeps, and join() spins before it waits: a futex wake-up costs as much as
 // the work (cycles come every ~16 ms on C2, so a serving loop's workers never sleep).
 class HostPool {
  public:
-  static constexpr int kWorkers = 2;
+  static constexpr int kWorkers = 4;
   static constexpr auto kSpin = std::chrono::milliseconds(40);
   static HostPool& get() {
     static HostPool h;
@@ -367,19 +368,22 @@ struct Driver {
     return queues[q].deserved.less_equal(queues[q].allocated);
   }
 
-  // init()'s task pass over a range of the tasks (the first half on init()'s thread, the second on a helper): the
+  // init()'s task pass over a range of the tasks (the first part on init()'s thread, the others on helpers): the
   // jobs' counts, the allocated-status tasks (their DRF sums and Allocated lists are then replayed in task order), and
   // the queues' proportion sums of the range (proportion.go:72-81, OnSessionOpen's task walk). Counts and sums stay in
   // registers while the job stays the same, the sums in two accumulators. exact: every cpu / memory request summed is
   // a non-negative integer and none has scalars -- then, with the totals below 2^53, every partial sum is exact and
-  // the split sums equal the task-order sums bit for bit; else init() sums every task again in task order.
+  // the split sums equal the task-order sums bit for bit; else init() sums every task again in task order. The parts
+  // are contiguous and ascending, so replaying their allocated-status lists part by part is task order.
   struct TaskPass {
     uint32_t t0 = 0, t1 = 0;
     std::vector<int32_t> ready, waiting, valid;
     std::vector<int> alloc;
     std::vector<double> q;  // per queue: allocated cpu, memory, request cpu, memory
     bool exact = true;
-  } head, tail;
+  };
+  static constexpr int kTaskParts = 4;
+  TaskPass part[kTaskParts];
   static bool exact_int(double x) { return x >= 0 && x < 9007199254740992.0 && x == (double)(int64_t)x; }
   void task_pass(TaskPass& T, bool prop) {
     T.ready.assign(s.n_jobs, 0);
@@ -442,15 +446,17 @@ struct Driver {
       if (p == KB_PLUGIN_PRIORITY && (s.tier_plugins[i].enable & KB_EN_TASK_ORDER)) task_prio = true;
     }
     const bool prop = has[KB_PLUGIN_PROPORTION];
-    // the second half of the task pass on the other helper (large sessions: the split pays for the thread hand-off)
-    head.t0 = 0;
-    head.t1 = s.n_tasks;
-    tail.t0 = tail.t1 = s.n_tasks;
-    int w_tail = -1;
-    if (s.n_tasks >= 32768) {
-      tail.t0 = head.t1 = s.n_tasks / 2;
-      w_tail = HostPool::get().post([this, prop] { task_pass(tail, prop); });
-      if (w_tail < 0) tail.t0 = head.t1 = s.n_tasks;  // (no worker free: one pass)
+    // parts 1.. of the task pass on the other helpers (large sessions: the split pays for the thread hand-off; a part
+    // no worker takes runs on init()'s thread after part 0)
+    const int np = s.n_tasks >= 32768 ? kTaskParts : 1;
+    int w_part[kTaskParts] = {-1, -1, -1, -1};
+    for (int i = 0; i < np; ++i) {
+      part[i].t0 = (uint32_t)((uint64_t)s.n_tasks * i / np);
+      part[i].t1 = (uint32_t)((uint64_t)s.n_tasks * (i + 1) / np);
+    }
+    for (int i = 1; i < np; ++i) {
+      TaskPass* T = &part[i];
+      w_part[i] = HostPool::get().post([this, prop, T] { task_pass(*T, prop); });
     }
     total.S = S;
     for (int i = 0; i < 2 + S; ++i) total.v[i] = s.total_alloc[i];
@@ -464,28 +470,34 @@ struct Driver {
       q.deserved.S = q.allocated.S = q.request.S = S;
     }
     const auto ia = std::chrono::steady_clock::now();
-    task_pass(head, prop);
+    task_pass(part[0], prop);
+    for (int i = 1; i < np; ++i)
+      if (w_part[i] < 0) task_pass(part[i], prop);
     const auto ib = std::chrono::steady_clock::now();
-    if (w_tail >= 0) HostPool::get().join(w_tail);
-    else tail.exact = true, tail.alloc.clear();
+    for (int i = 1; i < np; ++i) HostPool::get().join(w_part[i]);
     // the jobs' counts; the allocated-status tasks' DRF sums and Allocated lists in task order
     for (uint32_t j = 0; j < s.n_jobs; ++j) {
-      jobs[j].ready = head.ready[j] + (w_tail >= 0 ? tail.ready[j] : 0);
-      jobs[j].waiting = head.waiting[j] + (w_tail >= 0 ? tail.waiting[j] : 0);
-      jobs[j].valid = head.valid[j] + (w_tail >= 0 ? tail.valid[j] : 0);
+      int32_t r = 0, w = 0, v = 0;
+      for (int i = 0; i < np; ++i) r += part[i].ready[j], w += part[i].waiting[j], v += part[i].valid[j];
+      jobs[j].ready = r;
+      jobs[j].waiting = w;
+      jobs[j].valid = v;
     }
-    for (const TaskPass* T : {&head, &tail})
-      for (int t : T->alloc) {
+    for (int i = 0; i < np; ++i)
+      for (int t : part[i].alloc) {
         const int j = s.task_job[t];
         if (task_status[t] == KB_ST_ALLOCATED) job_allocated[j].push_back(t);
         jobs[j].drf_alloc.add_raw(task_req(t), s.task_resreq_mask[t]);
       }
     if (prop) {  // the queues' allocated / request sums: the split sums when exact, else in task order
-      bool ok = head.exact && tail.exact;
+      bool ok = true;
+      for (int i = 0; i < np; ++i) ok = ok && part[i].exact;
       std::vector<double> sum(4 * (size_t)s.n_queues);
-      for (size_t i = 0; ok && i < sum.size(); ++i) {
-        sum[i] = head.q[i] + (w_tail >= 0 ? tail.q[i] : 0.0);
-        ok = exact_int(sum[i]);
+      for (size_t k = 0; ok && k < sum.size(); ++k) {
+        double x = 0;
+        for (int i = 0; i < np; ++i) x += part[i].q[k];
+        sum[k] = x;
+        ok = exact_int(sum[k]);
       }
       if (ok) {
         for (uint32_t q = 0; q < s.n_queues; ++q) {
@@ -540,12 +552,12 @@ struct Driver {
     if (prop) open_proportion();
     if (ctx->issue_trace)
       fprintf(stderr,
-              "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f split=%d (setup %.3f first half %.3f "
+              "kb_host_trace init tasks_ms=%.3f drf_ms=%.3f proportion_ms=%.3f parts=%d (setup %.3f first part %.3f "
               "merge %.3f pending-list join %.3f)\n",
               std::chrono::duration<double, std::milli>(i1 - i0).count(),
               std::chrono::duration<double, std::milli>(i2 - i1).count(),
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i2).count(),
-              w_tail >= 0 ? 1 : 0, std::chrono::duration<double, std::milli>(ia - i0).count(),
+              np, std::chrono::duration<double, std::milli>(ia - i0).count(),
               std::chrono::duration<double, std::milli>(ib - ia).count(),
               std::chrono::duration<double, std::milli>(ic - ib).count(),
               std::chrono::duration<double, std::milli>(i1 - ic).count());

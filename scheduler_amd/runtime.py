@@ -489,7 +489,6 @@ class Context:
             self._ssn_cache = (key, ssn, self._ssn_keep)
         if out is not None and len(out["task_node"]) == max(nt, 1) and len(out["job_fail_task"]) == max(nj, 1):
             out = {k: out[k] for k in ("task_node", "task_status", "job_fail_task", "job_reason_hist", "event_task")}
-            out["event_task"][:] = 0  # (kb_allocate writes the first n_events entries)
         else:
             out = {"task_node": np.zeros(max(nt, 1), np.int32), "task_status": np.zeros(max(nt, 1), np.int32),
                    "job_fail_task": np.zeros(max(nj, 1), np.int32),
@@ -506,6 +505,7 @@ class Context:
         out["nofit"] = dict(self._nofit)
         out["overlay_reason"] = dict(self.overlay_reason)
         out["overlay_fail"] = dict(self.overlay_fail)
+        out["event_task"][res.n_events:] = 0  # (kb_allocate writes the first n_events entries; a reused array's tail)
         out["n_events"] = res.n_events
         out["elapsed_ms"] = res.elapsed_ms
         out["device_ms"] = res.device_ms
