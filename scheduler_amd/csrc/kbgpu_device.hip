@@ -877,6 +877,18 @@ __device__ __forceinline__ int lr_score_f64(double num, double cap, double inv) 
   const int q = qe + (rem >= cap ? 1 : 0) - (rem < 0.0 ? 1 : 0);
   return num < 0.0 ? 0 : q;
 }
+// The same quotient from a reciprocal biased up by 2^-50 (inv_up = RN(RN(1/cap) * (1 + 2^-50))): num * inv_up then
+// exceeds num / cap for num > 0 (the three roundings lose less than 3 * 2^-53 relative) by less than 10 * 2^-49
+// (num / cap <= 10), so its truncation is the floor or one above it, and the one exact remainder test corrects it
+// (num < 0, req > cap: score 0, as in lr_score_f64; the quotient there may saturate the conversion, hence the
+// unsigned step). Two VALU instructions fewer per call than lr_score_f64 (eval_plain_kernel's loop).
+__device__ __forceinline__ int lr_score_up(double num, double cap, double inv_up) {
+  const int qe = (int)(num * inv_up);
+  const double rem = fma(-(double)qe, cap, num);
+  const int q = (int)((uint32_t)qe - (rem < 0.0 ? 1u : 0u));
+  return num < 0.0 ? 0 : q;
+}
+constexpr double kInvUp = 1.0 + 0x1p-50;
 // BalancedResourceAllocation (balanced_resource_allocation.go:41-77) as bra_score_inv, on such doubles: with
 // positive capacities (pos) f = 10 - |rc * 10/ac - rm * 10/am| estimates (1 - |cf - mf|) * 10 within 1e-14, which
 // decides the truncation unless f lies within 1e-9 of an integer; then (and for other capacities) the IEEE
@@ -967,12 +979,11 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
     const double num_c = zc ? -1.0 : (d_ac - d_nc) * 10.0, num_m = zm ? -1.0 : (d_am - d_nm) * 10.0;
     const double cap_c = zc ? 1.0 : d_ac, cap_m = zm ? 1.0 : d_am;
     const double lc_inv = zc ? 1.0 : inv_c, lm_inv = zm ? 1.0 : inv_m;
+    const double lc_up = lc_inv * kInvUp, lm_up = lm_inv * kInvUp;  // (lr_score_up)
     // Balanced's estimate on positive capacities only (elsewhere every spec takes the fallback)
     const double ic10 = pos ? 10.0 / d_ac : 0.0, im10 = pos ? 10.0 / d_am : 0.0;
-    // The loop body is branch-free, so the unrolled iterations' LDS reads and f64 chains interleave. Balanced's
-    // IEEE-division fallback (f within 1e-9 of an integer, or a capacity <= 0) is deferred: the spec's bit in fb,
-    // and the score is rewritten after the loop (the same thread's later store to the same word)
-    uint64_t fb = 0;
+    // The unrolled iterations' LDS reads and f64 chains interleave; Balanced's IEEE-division fallback (f within 1e-9
+    // of an integer, or a capacity <= 0) is a branch the wave skips unless one of its lanes needs it
     // (BUF) the output arrays as buffer resources: raw, whole-array record counts (< 4 GiB: launch_eval_t)
     const uint32_t out_pairs = (uint32_t)t * (uint32_t)stride;
     const __amdgpu_buffer_rsrc_t rbuf = __builtin_amdgcn_make_buffer_rsrc(reasons, (short)0, (int)(out_pairs * 4u), 0x00020000);
@@ -987,17 +998,21 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       const uint32_t fm = 0u - (uint32_t)fit;
       const uint32_t rs = (((post_be & bem) | (after & ~bem)) & fm) | ((1u << KB_R_RESOURCE_FIT) & ~fm);
       // row_score_inv with no NodeAffinity, overlay or InterPodAffinity term (the table is 0 without nodeorder)
-      const int lc = lr_score_f64(num_c - nzc10, cap_c, lc_inv);
-      const int lm = lr_score_f64(num_m - nzm10, cap_m, lm_inv);
+      const int lc = lr_score_up(num_c - nzc10, cap_c, lc_up);
+      const int lm = lr_score_up(num_m - nzm10, cap_m, lm_up);
       const double rc = nzc + d_nc, rm = nzm + d_nm;
       const bool over = (rc >= d_ac) | (rm >= d_am);
       const double f = 10.0 - fabs(fma(rc, ic10, -(rm * im10)));  // in [0, 10]
       const double fr = f - floor(f);
       const bool po = pos & over;
       const bool est = pos & !over & (fr > 1e-9) & (fr < 1.0 - 1e-9);
-      fb |= (uint64_t)(!est & !po) << j;
+      const bool fbit = !est & !po;
       // (kb_eval32's host check bounds the int32 sum; kb_eval sums in int64)
-      const SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
+      SCORE score = s_tab[((lc + lm) >> 1) * 11 + (po ? 0 : (int)f)];
+      // Balanced's IEEE-division fallback (f within 1e-9 of an integer, or a capacity <= 0): rare, in place -- a
+      // branch the wave skips when no lane takes it (a deferred bit per spec cost more VALU per pair than it saved)
+      if (fbit && C.nodeorder) [[unlikely]]
+        score = s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, d_ac, rm, d_am, 0.0, 0.0, false)];
       // uniform row bases: the stores take a scalar base and the lane's offset; non-temporal (the output is
       // streamed once, never read back by this kernel: no point keeping it in the caches)
       if constexpr (BUF) {
@@ -1058,16 +1073,6 @@ __global__ __launch_bounds__(256) void eval_plain_kernel(DevNodes N, DevSpecs P,
       rrow[n] = rs;
       srow[n] = score;
 #endif
-    }
-    if (!C.nodeorder) fb = 0;
-    while (fb) {  // the deferred Balanced fallbacks
-      const int j = __builtin_ctzll(fb);
-      fb &= fb - 1;
-      const int lc = lr_score_f64(num_c - s_dreq[2][j], cap_c, lc_inv);
-      const int lm = lr_score_f64(num_m - s_dreq[3][j], cap_m, lm_inv);
-      const double rc = s_dnz[0][j] + d_nc, rm = s_dnz[1][j] + d_nm;
-      scores[(size_t)(j0 + j) * stride + n] =
-          s_tab[((lc + lm) >> 1) * 11 + bra_score_f64(rc, d_ac, rm, d_am, 0.0, 0.0, false)];
     }
     return;
   }
